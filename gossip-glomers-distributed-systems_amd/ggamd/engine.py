@@ -1,0 +1,266 @@
+"""ctypes binding of the engine C ABI (include/gossip.h).
+
+`Engine` drives any library exporting the gossip.h symbols. The product is
+``libgossip_hip.so`` (HIP kernels for gfx950, built in-tree by ``make``);
+tests may hand in the CPU oracle library explicitly. `Engine()` without a
+library path loads the HIP library and raises if it is missing — there is no
+silent CPU fallback on the product path.
+
+The handler surface mirrors the reference node (``broadcast/main.go:22-40``):
+``topology`` (HandleTopology), ``broadcast`` (client HandleBroadcast), ``read``
+(HandleRead) and ``step`` (the passing of lockstep 100 ms rounds, during which
+every node-to-node broadcast, broadcast_ok, read and read_ok happens).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIP_LIB = os.path.join(PKG_DIR, "libgossip_hip.so")
+HOST_LIB = os.path.join(PKG_DIR, "libgossip_host.so")
+
+GG_TRACK_DELIVERY = 1
+ERRNO = {-5: "EIO", -12: "ENOMEM", -22: "EINVAL", -28: "ENOSPC", -38: "ENOSYS"}
+
+
+class GGConfig(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_uint64),
+        ("n_lanes", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("seed", C.c_uint64),
+        ("sync_base_ticks", C.c_uint32),
+        ("sync_jitter_ticks", C.c_uint32),
+        ("enable_sync", C.c_int32),
+        ("device", C.c_int32),
+        ("rank", C.c_uint32),
+        ("world", C.c_uint32),
+    ]
+
+
+class GGRoundStats(C.Structure):
+    _fields_ = [
+        ("round", C.c_int64),
+        ("new_bits", C.c_uint64),
+        ("fwd_sent", C.c_uint64),
+        ("fwd_delivered", C.c_uint64),
+        ("pushes", C.c_uint64),
+        ("push_delivered", C.c_uint64),
+        ("acks", C.c_uint64),
+        ("reads", C.c_uint64),
+        ("read_oks", C.c_uint64),
+        ("dropped", C.c_uint64),
+        ("syncs_fired", C.c_uint64),
+        ("seen_hash", C.c_uint64),
+        ("kernel_ms", C.c_double),
+    ]
+
+
+class GGExchange(C.Structure):
+    _fields_ = [
+        ("node_lo", C.c_uint64),
+        ("node_hi", C.c_uint64),
+        ("slice_rows", C.c_uint64),
+        ("frontier", C.c_void_p),
+        ("seen", C.c_void_p),
+        ("fired", C.c_void_p),
+        ("frontier_bytes", C.c_uint64),
+        ("seen_bytes", C.c_uint64),
+        ("fired_bytes", C.c_uint64),
+        ("need_seen", C.c_int32),
+    ]
+
+
+STAT_FIELDS = [f for f, _ in GGRoundStats._fields_]
+COUNT_FIELDS = [f for f in STAT_FIELDS if f not in ("round", "kernel_ms")]
+
+GG_SYMBOLS = [
+    "gg_abi_version", "gg_create", "gg_destroy", "gg_last_error", "gg_topology",
+    "gg_partition_seeded", "gg_partition_groups", "gg_broadcast", "gg_lane_of", "gg_step",
+    "gg_current_round", "gg_read", "gg_read_bits", "gg_delivery_rounds", "gg_reset",
+    "gg_dist_round_begin", "gg_dist_round_end", "gg_dist_range",
+]
+
+_LIBS: dict[str, C.CDLL] = {}
+
+
+def load_library(path: str) -> C.CDLL:
+    path = os.path.abspath(path)
+    if path in _LIBS:
+        return _LIBS[path]
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"engine library {path} is not built (run `make` in {PKG_DIR})")
+    lib = C.CDLL(path)
+    P = C.POINTER
+    lib.gg_abi_version.restype = C.c_int
+    lib.gg_create.argtypes = [P(GGConfig), P(C.c_void_p)]
+    lib.gg_destroy.argtypes = [C.c_void_p]
+    lib.gg_destroy.restype = None
+    lib.gg_last_error.argtypes = [C.c_void_p]
+    lib.gg_last_error.restype = C.c_char_p
+    lib.gg_topology.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
+    lib.gg_partition_seeded.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_uint64]
+    lib.gg_partition_groups.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]
+    lib.gg_broadcast.argtypes = [C.c_void_p, C.c_uint32, C.c_int64, C.c_int64]
+    lib.gg_lane_of.argtypes = [C.c_void_p, C.c_int64]
+    lib.gg_step.argtypes = [C.c_void_p, C.c_uint32, P(GGRoundStats)]
+    lib.gg_current_round.argtypes = [C.c_void_p]
+    lib.gg_current_round.restype = C.c_int64
+    lib.gg_read.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, P(C.c_uint64)]
+    lib.gg_read_bits.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
+    lib.gg_delivery_rounds.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64]
+    lib.gg_reset.argtypes = [C.c_void_p]
+    lib.gg_dist_round_begin.argtypes = [C.c_void_p, P(GGExchange)]
+    lib.gg_dist_round_end.argtypes = [C.c_void_p, P(GGRoundStats)]
+    lib.gg_dist_range.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint64)]
+    _LIBS[path] = lib
+    return lib
+
+
+class GGError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRNO.get(code, code)}: {msg}")
+        self.code = code
+
+
+@dataclass
+class Topology:
+    n_nodes: int
+    row_ptr: np.ndarray  # int64 [V+1]
+    col: np.ndarray  # int32 [nnz]
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.size)
+
+    def rows(self) -> list[list[int]]:
+        return [self.col[self.row_ptr[v]:self.row_ptr[v + 1]].tolist() for v in range(self.n_nodes)]
+
+    @staticmethod
+    def from_rows(rows: list[list[int]]) -> "Topology":
+        rp = np.zeros(len(rows) + 1, np.int64)
+        for v, r in enumerate(rows):
+            rp[v + 1] = rp[v] + len(r)
+        col = np.array([x for r in rows for x in r], np.int32)
+        return Topology(len(rows), rp, col)
+
+
+def stats_dict(s: GGRoundStats) -> dict:
+    return {f: getattr(s, f) for f in STAT_FIELDS}
+
+
+class Engine:
+    """One engine = every simulated node of one topology (or one shard of it)."""
+
+    def __init__(self, n_nodes: int, n_lanes: int, *, seed: int = 0, sync_base: int = 20,
+                 sync_jitter: int = 10, enable_sync: bool = True, track_delivery: bool = False,
+                 device: int = -1, rank: int = 0, world: int = 1, library: str | None = None):
+        self.lib = load_library(library or HIP_LIB)
+        self.library = os.path.abspath(library or HIP_LIB)
+        cfg = GGConfig(n_nodes, n_lanes, GG_TRACK_DELIVERY if track_delivery else 0, seed,
+                       sync_base, sync_jitter, 1 if enable_sync else 0, device, rank, world)
+        h = C.c_void_p()
+        rc = self.lib.gg_create(C.byref(cfg), C.byref(h))
+        if rc != 0:
+            raise GGError(rc, "gg_create failed")
+        self.h = h
+        self.V, self.W, self.nw = n_nodes, n_lanes, n_lanes // 64
+        self.rank, self.world = rank, world
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _ok(self, rc: int):
+        if rc != 0:
+            raise GGError(rc, self.lib.gg_last_error(self.h).decode())
+        return rc
+
+    # ---- handler surface ---------------------------------------------------
+
+    def topology(self, topo: Topology):
+        rp = np.ascontiguousarray(topo.row_ptr, np.int64)
+        col = np.ascontiguousarray(topo.col, np.int32)
+        self._ok(self.lib.gg_topology(self.h, rp.ctypes.data, col.ctypes.data, col.size))
+
+    def partition_seeded(self, r0: int, r1: int, epoch_seed: int):
+        self._ok(self.lib.gg_partition_seeded(self.h, r0, r1, epoch_seed))
+
+    def partition_groups(self, r0: int, r1: int, groups):
+        g = np.ascontiguousarray(groups, np.uint8)
+        assert g.size == self.V
+        self._ok(self.lib.gg_partition_groups(self.h, r0, r1, g.ctypes.data))
+
+    def broadcast(self, node: int, value: int, rnd: int):
+        self._ok(self.lib.gg_broadcast(self.h, node, value, rnd))
+
+    def broadcast_many(self, nodes, values, rnd: int):
+        for n, v in zip(nodes, values):
+            self._ok(self.lib.gg_broadcast(self.h, int(n), int(v), rnd))
+
+    def lane_of(self, value: int) -> int:
+        return self.lib.gg_lane_of(self.h, value)
+
+    def step(self, n_rounds: int = 1) -> list[dict]:
+        arr = (GGRoundStats * max(1, n_rounds))()
+        self._ok(self.lib.gg_step(self.h, n_rounds, arr))
+        return [stats_dict(arr[i]) for i in range(n_rounds)]
+
+    @property
+    def round(self) -> int:
+        return self.lib.gg_current_round(self.h)
+
+    def read(self, node: int) -> list[int]:
+        n = C.c_uint64(0)
+        self._ok(self.lib.gg_read(self.h, node, None, 0, C.byref(n)))
+        out = np.zeros(max(1, n.value), np.int64)
+        self._ok(self.lib.gg_read(self.h, node, out.ctypes.data, out.size, C.byref(n)))
+        return out[: n.value].tolist()
+
+    def read_bits(self, lo: int = 0, hi: int | None = None) -> np.ndarray:
+        hi = self.V if hi is None else hi
+        out = np.zeros((hi - lo, self.nw), np.uint64)
+        self._ok(self.lib.gg_read_bits(self.h, lo, hi, out.ctypes.data))
+        return out
+
+    def delivery_rounds(self, lo: int = 0, hi: int | None = None) -> np.ndarray:
+        hi = self.V if hi is None else hi
+        out = np.zeros((hi - lo, self.W), np.int32)
+        self._ok(self.lib.gg_delivery_rounds(self.h, lo, hi, out.ctypes.data, out.size))
+        return out
+
+    def reset(self):
+        self._ok(self.lib.gg_reset(self.h))
+
+    # ---- sharded rounds ------------------------------------------------------
+
+    def dist_range(self) -> tuple[int, int]:
+        lo, hi = C.c_uint64(0), C.c_uint64(0)
+        self._ok(self.lib.gg_dist_range(self.h, C.byref(lo), C.byref(hi)))
+        return lo.value, hi.value
+
+    def dist_round_begin(self) -> GGExchange:
+        x = GGExchange()
+        self._ok(self.lib.gg_dist_round_begin(self.h, C.byref(x)))
+        return x
+
+    def dist_round_end(self) -> dict:
+        s = GGRoundStats()
+        self._ok(self.lib.gg_dist_round_end(self.h, C.byref(s)))
+        return stats_dict(s)
+
+
+def missing_symbols(path: str) -> list[str]:
+    lib = C.CDLL(os.path.abspath(path))
+    return [s for s in GG_SYMBOLS if not hasattr(lib, s)]

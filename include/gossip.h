@@ -1,0 +1,161 @@
+/*
+ * gossip.h — C ABI of the MI355X gossip-propagation engine.
+ *
+ * Drop-in boundary for the hot path of dshebib/gossip-glomers-distributed-systems
+ * `broadcast/` (the Gossip Glomers "broadcast" challenge solution). The reference
+ * registers five maelstrom handlers per node (`broadcast/main.go:22-40`) and runs
+ * one OS process per node; this engine runs every node of a topology in lockstep
+ * 100 ms rounds (one round = one simulated latency tick) on one or more GPUs.
+ *
+ * Entry point                 replaces (reference file:line)
+ * ---------------------------------------------------------------------------
+ * gg_create                   maelstrom.NewNode + Context{} + handler table
+ *                             `broadcast/main.go:17-40`; sync timer `main.go:42-51`
+ * gg_topology                 HandleTopology `broadcast/broadcast.go:36-48`
+ *                             (every node keeps its own row; here: all rows at once)
+ * gg_partition_seeded /       Maelstrom `--nemesis partition` (external harness,
+ * gg_partition_groups         `README.md:18`): messages across groups are dropped
+ * gg_broadcast                client `broadcast` -> HandleBroadcast `broadcast.go:59-79`
+ * gg_step                     n lockstep rounds: every HandleBroadcast /
+ *                             rebroadcastAllExcept (`:50-57`) / SyncBroadcast
+ *                             (`:81-122`) / HandleRead (`:124-132`) / broadcast_ok
+ *                             (`main.go:38-40`) event of those rounds
+ * gg_read / gg_read_bits      client `read` -> HandleRead `broadcast.go:124-132`
+ * gg_delivery_rounds          observation only (first round each value was seen)
+ * gg_dist_*                   one-engine-per-GPU vertex-range sharding (new)
+ *
+ * Determinization contract (restated in DESIGN.md §2):
+ * one round per 100 ms tick; every message sent in round r is delivered in
+ * round r+1 unless the partition plan drops it (evaluated at the send round);
+ * within a round a node handles client broadcasts, then node broadcasts in
+ * ascending sender id, then sync read_ok callbacks in ascending peer id, then
+ * read requests (answered with the end-of-round set), then its sync timer.
+ *
+ * Conventions: 0 = success; negative errno on failure (GG_EINVAL, GG_ENOMEM,
+ * GG_EIO for HIP/driver failures, GG_ENOSPC when more distinct message values
+ * than lanes were broadcast) and gg_last_error() describes it — the analogue of a
+ * handler returning an error. All inputs are caller-owned and copied; outputs go
+ * to caller buffers. One engine is driven by one host thread.
+ *
+ * Two libraries export exactly these symbols: libgossip_hip.so (the product,
+ * HIP kernels for gfx950) and oracle/_build/libgossip_cpu.so (the CPU bitset
+ * restatement, used only by tests and the CPU baseline).
+ */
+#ifndef GOSSIP_H_
+#define GOSSIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GG_ABI_VERSION 1
+
+#define GG_OK 0
+#define GG_EIO (-5)
+#define GG_ENOMEM (-12)
+#define GG_EINVAL (-22)
+#define GG_ENOSPC (-28)
+#define GG_ENOSYS (-38)
+
+/* gg_config.flags */
+#define GG_TRACK_DELIVERY 1u /* keep the first-seen round of every (node,lane) */
+
+typedef struct gg_engine gg_engine; /* opaque; owns all device memory */
+
+typedef struct {
+    uint64_t n_nodes;           /* V: node ids 0..V-1 ("n0".."n<V-1>") */
+    uint32_t n_lanes;           /* W: message lanes, multiple of 64, 64..8192 */
+    uint32_t flags;             /* GG_TRACK_DELIVERY */
+    uint64_t seed;              /* sync schedule + seeded partitions */
+    uint32_t sync_base_ticks;   /* 20  (= 2 s,  `main.go:47`) */
+    uint32_t sync_jitter_ticks; /* 10  (= rand.Intn(1000) ms, `main.go:46`) */
+    int32_t enable_sync;        /* 1 = run SyncBroadcast timers */
+    int32_t device;             /* HIP device ordinal; -1 = current device */
+    uint32_t rank;              /* sharded mode: this engine's rank (0 if single) */
+    uint32_t world;             /* sharded mode: number of engines (1 = single) */
+} gg_config;
+
+typedef struct {
+    int64_t round;           /* round these counters belong to */
+    uint64_t new_bits;       /* (node,msg) deliveries in this round */
+    uint64_t fwd_sent;       /* node->node `broadcast` forwards sent (:55, :99) */
+    uint64_t fwd_delivered;  /* ... of which not dropped */
+    uint64_t pushes;         /* sync pushes sent (:106) */
+    uint64_t push_delivered; /* ... of which not dropped */
+    uint64_t acks;           /* broadcast_ok replies to nodes sent (:69, :78) */
+    uint64_t reads;          /* sync `read` RPCs sent (:120) */
+    uint64_t read_oks;       /* `read_ok` replies to nodes sent (:131) */
+    uint64_t dropped;        /* messages of every kind sent this round and dropped */
+    uint64_t syncs_fired;    /* sync timers that fired this round */
+    uint64_t seen_hash;      /* order-free hash of every node's set */
+    double kernel_ms;        /* device time of the round (0 for the CPU oracle) */
+} gg_round_stats;
+
+/* Inter-node messages of a round = fwd_sent + pushes + acks + reads + read_oks. */
+
+int gg_create(const gg_config* cfg, gg_engine** out);
+void gg_destroy(gg_engine* e);
+const char* gg_last_error(const gg_engine* e);
+int gg_abi_version(void);
+
+/* Adjacency: row v lists topology[v] = the nodes v sends to, ascending and
+ * unique (HandleTopology keeps topology[own id], missing row = empty list).
+ * Directed lists are allowed; symmetric ones take a faster path. */
+int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64_t nnz);
+
+/* Partition windows [round_from, round_to): a message sent in such a round
+ * between nodes of different groups is dropped. Windows must not overlap.
+ * Seeded: group(v) = bisection bit from (seed, epoch_seed, v). */
+int gg_partition_seeded(gg_engine* e, int64_t round_from, int64_t round_to, uint64_t epoch_seed);
+int gg_partition_groups(gg_engine* e, int64_t round_from, int64_t round_to, const uint8_t* group);
+
+/* Client broadcast of `message` to `node`, delivered in `round` (>= current
+ * round). The first broadcast of a value assigns it the next free lane. */
+int gg_broadcast(gg_engine* e, uint32_t node, int64_t message, int64_t round);
+int gg_lane_of(const gg_engine* e, int64_t message); /* lane or GG_EINVAL */
+
+/* Run n_rounds lockstep rounds; out[i] (may be NULL) receives round i's stats. */
+int gg_step(gg_engine* e, uint32_t n_rounds, gg_round_stats* out);
+int64_t gg_current_round(const gg_engine* e);
+
+/* HandleRead: the values node holds, ascending. n_out = count (even if > cap). */
+int gg_read(gg_engine* e, uint32_t node, int64_t* out, uint64_t cap, uint64_t* n_out);
+/* Raw sets of nodes [lo,hi): (hi-lo) * W/64 words, lane l = bit l%64 of word l/64. */
+int gg_read_bits(gg_engine* e, uint32_t node_lo, uint32_t node_hi, uint64_t* out);
+/* First round each lane was seen, -1 if never: (hi-lo) * W int32 (GG_TRACK_DELIVERY). */
+int gg_delivery_rounds(gg_engine* e, uint32_t node_lo, uint32_t node_hi, int32_t* out, uint64_t cap);
+
+/* Back to round 0 with empty sets, no queued broadcasts, no lanes assigned;
+ * topology and partition windows are kept. */
+int gg_reset(gg_engine* e);
+
+/* ---- sharded mode (cfg.world > 1): one engine per GPU, vertex-range shards ----
+ * Every rank gives gg_topology the whole graph and keeps the rows of its own
+ * range (edge-balanced cut points, identical on every rank). A round is
+ *   gg_dist_round_begin -> caller all-gathers the exchange slices ->
+ *   gg_dist_round_end   -> caller sums the per-rank stats.
+ * The exchange buffers are laid out [world][slice_rows][...]; each rank writes
+ * its own slice and the all-gather fills the rest (equal-size slices). */
+typedef struct {
+    uint64_t node_lo, node_hi; /* owned node range */
+    uint64_t slice_rows;       /* rows per rank slice (>= node_hi - node_lo) */
+    void* frontier;            /* [world][slice_rows][W/64] u64 new-bit buffer */
+    void* seen;                /* [world][slice_rows][W/64] u64 set buffer */
+    void* fired;               /* [world][slice_rows/64] u64 sync-fired bitmap */
+    uint64_t frontier_bytes;   /* bytes per rank slice of each buffer */
+    uint64_t seen_bytes;
+    uint64_t fired_bytes;
+    int32_t need_seen;         /* 1 if this round's seen slices must be exchanged */
+} gg_exchange;
+
+int gg_dist_round_begin(gg_engine* e, gg_exchange* xch);
+int gg_dist_round_end(gg_engine* e, gg_round_stats* out);
+int gg_dist_range(const gg_engine* e, uint64_t* node_lo, uint64_t* node_hi);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GOSSIP_H_ */

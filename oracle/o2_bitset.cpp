@@ -1,0 +1,603 @@
+// O2 — bitset CPU restatement of the reference broadcast handlers.
+//
+// TEST INFRASTRUCTURE ONLY: built into oracle/_build/libgossip_cpu.so and loaded
+// by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg. It exports
+// the same C ABI (include/gossip.h) as the product library libgossip_hip.so so a
+// parity test can drive both with identical calls. Nothing in the product links it.
+//
+// Parity status: parity unpinned by reference tests (there are none: SURVEY.md §4,
+// §8c). O2 is checked against the message-level literal restatement O1
+// (oracle/o1_literal.py) on randomized small graphs, partitions and sync
+// schedules, and against the analytic KATs of SURVEY.md §8c (tests/).
+//
+// Semantics, per node v in round r:
+//   S  = seen_prev(v) | client broadcasts of round r          HandleBroadcast :59-79
+//   for in-neighbour u ascending whose message was not dropped in round r-1:
+//        contrib = seen_prev(u) if u pushed to v in r-1 else F_prev(u)
+//        claim_u = contrib & ~S ;  S |= claim_u                first deliverer = u
+//   if v's sync fired in r-2: for out-neighbour w ascending whose read (r-2) and
+//        read_ok (r-1) both arrived:  R = seen_prev(w)         SyncBroadcast :82-117
+//        new = R & ~S (forwarded to all but w, :97-100); push = S & ~R (to w,
+//        :104-108); S |= R (:110-114)
+//   seen_cur(v) = S ; F_cur(v) = S & ~seen_prev(v)             rebroadcastAllExcept :50-57
+// Message counts use per-claimer popcounts (forward exclusion, :52) and the
+// partition masks at the send round. Acks of round r are the broadcasts
+// delivered in round r; they are counted by the sender in round r-1.
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "gossip.h"
+#include "gossip_spec.h"
+
+namespace {
+
+struct Window {
+    int64_t from, to;
+    bool seeded;
+    uint64_t epoch_seed;
+    std::vector<uint8_t> group;  // global node -> group (explicit windows)
+};
+
+struct Injection {
+    uint32_t node;  // global id
+    uint32_t lane;
+};
+
+struct Acc {  // per-thread counters
+    uint64_t new_bits = 0, fwd_sent = 0, fwd_deliv = 0, pushes = 0, push_deliv = 0;
+    uint64_t reads = 0, read_oks = 0, dropped = 0, fired = 0, hash = 0;
+    uint64_t next_acks = 0, next_ackdrop = 0;
+    void add(const Acc& o) {
+        new_bits += o.new_bits; fwd_sent += o.fwd_sent; fwd_deliv += o.fwd_deliv;
+        pushes += o.pushes; push_deliv += o.push_deliv; reads += o.reads;
+        read_oks += o.read_oks; dropped += o.dropped; fired += o.fired; hash += o.hash;
+        next_acks += o.next_acks; next_ackdrop += o.next_ackdrop;
+    }
+};
+
+inline int popc(uint64_t x) { return __builtin_popcountll(x); }
+
+}  // namespace
+
+struct gg_engine {
+    gg_config cfg{};
+    std::string err;
+    uint64_t V = 0, nw = 0;
+    uint32_t rank = 0, world = 1;
+    uint64_t lo = 0, hi = 0, slice = 0;    // owned range, rows per rank slice
+    std::vector<uint64_t> rank_lo;         // [world+1]
+    bool have_topo = false, symmetric = true;
+    // owned rows; columns are replica indices (rank * slice + offset)
+    std::vector<int64_t> in_ptr, out_ptr;
+    std::vector<uint32_t> in_col, out_col;
+    std::vector<uint8_t> in_recip;
+    // replicas [world*slice][nw]
+    std::vector<uint64_t> seen[2], F[2];
+    std::vector<uint64_t> fired[4];        // [world*slice/64]
+    std::vector<int64_t> sync_next;        // owned
+    std::vector<uint32_t> sync_k;
+    std::vector<int32_t> dr;               // owned rows * W
+    std::vector<Window> windows;
+    std::unordered_map<int64_t, uint32_t> lanes;
+    std::vector<int64_t> lane_value;
+    std::map<int64_t, std::vector<Injection>> inj;
+    int64_t round = 0;
+    uint64_t pend_acks = 0, pend_ackdrop = 0;
+    int threads = 1;
+    bool dist_open = false;
+    Acc dist_acc;
+
+    int fail(int code, const std::string& m) { err = m; return code; }
+
+    uint64_t global_of(uint64_t rep) const {
+        uint64_t r = rep / slice;
+        return rank_lo[r] + (rep - r * slice);
+    }
+    uint64_t rep_of(uint64_t g) const {
+        uint32_t r = (uint32_t)(std::upper_bound(rank_lo.begin(), rank_lo.end(), g) - rank_lo.begin()) - 1;
+        return (uint64_t)r * slice + (g - rank_lo[r]);
+    }
+    const Window* window_at(int64_t r) const {
+        for (const auto& w : windows)
+            if (w.from <= r && r < w.to) return &w;
+        return nullptr;
+    }
+    int group_of(const Window* w, uint64_t g) const {
+        return w->seeded ? (int)gg_part_group(cfg.seed, w->epoch_seed, g) : (int)w->group[g];
+    }
+    // message from global a to global b sent in round r dropped?
+    bool masked(int64_t r, uint64_t a, uint64_t b) const {
+        const Window* w = window_at(r);
+        return w && group_of(w, a) != group_of(w, b);
+    }
+    bool fired_at(int64_t r, uint64_t rep) const {
+        if (r < 0) return false;
+        return (fired[r & 3][rep >> 6] >> (rep & 63)) & 1ull;
+    }
+    void reset_state() {
+        for (int b = 0; b < 2; ++b) {
+            std::fill(seen[b].begin(), seen[b].end(), 0ull);
+            std::fill(F[b].begin(), F[b].end(), 0ull);
+        }
+        for (int b = 0; b < 4; ++b) std::fill(fired[b].begin(), fired[b].end(), 0ull);
+        for (uint64_t i = 0; i < hi - lo; ++i) {
+            sync_k[i] = 0;
+            sync_next[i] = gg_sync_interval(cfg.seed, lo + i, 0, cfg.sync_base_ticks, cfg.sync_jitter_ticks);
+        }
+        std::fill(dr.begin(), dr.end(), -1);
+        lanes.clear();
+        lane_value.clear();
+        inj.clear();
+        round = 0;
+        pend_acks = pend_ackdrop = 0;
+        dist_open = false;
+    }
+    void compute_round(Acc& total);
+};
+
+void gg_engine::compute_round(Acc& total) {
+    const int64_t r = round;
+    const uint64_t n_own = hi - lo;
+    const uint64_t own0 = (uint64_t)rank * slice;
+    const bool sync = cfg.enable_sync != 0;
+    const uint32_t W = cfg.n_lanes;
+    std::vector<uint64_t>& sp_all = seen[(r + 1) & 1];  // seen_prev (round r-1)
+    std::vector<uint64_t>& sc_all = seen[r & 1];        // seen_cur
+    std::vector<uint64_t>& Fp_all = F[(r + 1) & 1];
+    std::vector<uint64_t>& Fc_all = F[r & 1];
+    // fired slot of round r: owned words cleared here (world slices are refreshed by the exchange)
+    {
+        auto& fr = fired[r & 3];
+        std::fill(fr.begin() + own0 / 64, fr.begin() + (own0 + slice) / 64, 0ull);
+    }
+    // injections of round r for owned nodes, grouped per node (call order kept)
+    std::unordered_map<uint32_t, std::vector<uint32_t>> inj_by_node;
+    {
+        auto it = inj.find(r);
+        if (it != inj.end()) {
+            for (const auto& x : it->second)
+                if (x.node >= lo && x.node < hi) inj_by_node[x.node].push_back(x.lane);
+            inj.erase(it);
+        }
+    }
+    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads, n_own / 256 + 1));
+    std::vector<Acc> accs(T);
+    std::vector<std::vector<uint64_t>> firedw(T);
+    auto work = [&](int t) {
+        Acc& a = accs[t];
+        std::vector<uint64_t> S(nw), sp(nw);
+        const uint64_t b0 = n_own * t / T, b1 = n_own * (t + 1) / T;
+        for (uint64_t i = b0; i < b1; ++i) {
+            const uint64_t g = lo + i, rep = own0 + i;
+            const uint64_t* spv = &sp_all[rep * nw];
+            for (uint64_t j = 0; j < nw; ++j) sp[j] = S[j] = spv[j];
+            // (1) client broadcasts
+            auto ij = inj_by_node.find((uint32_t)g);
+            if (ij != inj_by_node.end())
+                for (uint32_t lane : ij->second) S[lane >> 6] |= 1ull << (lane & 63);
+            // (2) node broadcasts, ascending sender
+            uint64_t cl_recip = 0, cl_deliv = 0, cl_ackdrop = 0;
+            for (int64_t e = in_ptr[i]; e < in_ptr[i + 1]; ++e) {
+                const uint64_t urep = in_col[e];
+                const uint64_t u = global_of(urep);
+                if (sync && fired_at(r - 1, urep) && !masked(r - 1, u, g)) {  // read arrives
+                    a.read_oks++;                                             // HandleRead :131
+                    if (masked(r, g, u)) a.dropped++;
+                }
+                if (masked(r - 1, u, g)) continue;                            // dropped in flight
+                const bool push = sync && fired_at(r - 3, urep) && !masked(r - 3, u, g) &&
+                                  !masked(r - 2, g, u);
+                const uint64_t* src = push ? &sp_all[urep * nw] : &Fp_all[urep * nw];
+                uint64_t pc = 0;
+                for (uint64_t j = 0; j < nw; ++j) {
+                    uint64_t c = src[j] & ~S[j];
+                    S[j] |= c;
+                    pc += popc(c);
+                }
+                if (pc && in_recip[e]) {
+                    cl_recip += pc;
+                    if (!masked(r, g, u)) {
+                        cl_deliv += pc;
+                        if (masked(r + 1, u, g)) cl_ackdrop += pc;
+                    }
+                }
+            }
+            // (3) sync callback: fired in r-2, peers ascending
+            uint64_t cb_new = 0, cb_new_deliv = 0, cb_new_ackdrop = 0;
+            uint64_t push_sent = 0, push_deliv = 0, push_ackdrop = 0;
+            if (sync && fired_at(r - 2, rep)) {
+                for (int64_t e = out_ptr[i]; e < out_ptr[i + 1]; ++e) {
+                    const uint64_t wrep = out_col[e];
+                    const uint64_t w = global_of(wrep);
+                    if (masked(r - 2, g, w) || masked(r - 1, w, g)) continue;
+                    const uint64_t* R = &sp_all[wrep * nw];
+                    uint64_t pn = 0, pp = 0;
+                    for (uint64_t j = 0; j < nw; ++j) {
+                        pn += popc(R[j] & ~S[j]);
+                        pp += popc(S[j] & ~R[j]);
+                        S[j] |= R[j];
+                    }
+                    cb_new += pn;
+                    push_sent += pp;
+                    if (!masked(r, g, w)) {
+                        cb_new_deliv += pn;
+                        push_deliv += pp;
+                        if (masked(r + 1, w, g)) {
+                            cb_new_ackdrop += pn;
+                            push_ackdrop += pp;
+                        }
+                    }
+                }
+            }
+            // state
+            uint64_t* sc = &sc_all[rep * nw];
+            uint64_t* fc = &Fc_all[rep * nw];
+            uint64_t Tn = 0;
+            for (uint64_t j = 0; j < nw; ++j) {
+                sc[j] = S[j];
+                uint64_t f = S[j] & ~sp[j];
+                fc[j] = f;
+                Tn += popc(f);
+                if (S[j]) a.hash += gg_word_hash(g * nw + j, S[j]);
+                if (f && !dr.empty()) {
+                    uint64_t x = f;
+                    while (x) {
+                        int b = __builtin_ctzll(x);
+                        x &= x - 1;
+                        dr[i * W + j * 64 + b] = (int32_t)r;
+                    }
+                }
+            }
+            a.new_bits += Tn;
+            // counts of what v sends in round r
+            const uint64_t deg = (uint64_t)(out_ptr[i + 1] - out_ptr[i]);
+            uint64_t U = deg, AD = 0, mdrop = 0;
+            const bool mr = window_at(r) != nullptr, mr1 = window_at(r + 1) != nullptr;
+            if (mr || mr1) {
+                U = 0;
+                for (int64_t e = out_ptr[i]; e < out_ptr[i + 1]; ++e) {
+                    const uint64_t w = global_of(out_col[e]);
+                    if (!masked(r, g, w)) {
+                        U++;
+                        if (masked(r + 1, w, g)) AD++;
+                    } else {
+                        mdrop++;
+                    }
+                }
+            }
+            const uint64_t fs = deg * Tn - cl_recip - cb_new;
+            const uint64_t fd = U * Tn - cl_deliv - cb_new_deliv;
+            a.fwd_sent += fs;
+            a.fwd_deliv += fd;
+            a.pushes += push_sent;
+            a.push_deliv += push_deliv;
+            a.dropped += (fs - fd) + (push_sent - push_deliv);
+            a.next_acks += fd + push_deliv;
+            a.next_ackdrop += AD * Tn - cl_ackdrop - cb_new_ackdrop + push_ackdrop;
+            // (5) sync timer
+            if (sync && r == sync_next[i]) {
+                a.fired++;
+                a.reads += deg;                                          // RPC read :120
+                a.dropped += mdrop;
+                firedw[t].push_back(rep);
+                sync_k[i]++;
+                sync_next[i] = r + gg_sync_interval(cfg.seed, g, sync_k[i], cfg.sync_base_ticks,
+                                                    cfg.sync_jitter_ticks);
+            }
+        }
+    };
+    if (T == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t) th.emplace_back(work, t);
+        for (auto& x : th) x.join();
+    }
+    for (int t = 0; t < T; ++t) {
+        total.add(accs[t]);
+        for (uint64_t rep : firedw[t]) fired[r & 3][rep >> 6] |= 1ull << (rep & 63);
+    }
+}
+
+// --------------------------------------------------------------------------
+
+extern "C" {
+
+int gg_abi_version(void) { return GG_ABI_VERSION; }
+
+int gg_create(const gg_config* cfg, gg_engine** out) {
+    if (!cfg || !out) return GG_EINVAL;
+    *out = nullptr;
+    if (cfg->n_nodes == 0 || cfg->n_nodes > 0x7fffffffull) return GG_EINVAL;
+    if (cfg->n_lanes == 0 || cfg->n_lanes % 64 || cfg->n_lanes > 8192) return GG_EINVAL;
+    if (cfg->enable_sync && cfg->sync_base_ticks == 0) return GG_EINVAL;
+    if (cfg->world == 0 || cfg->rank >= cfg->world) return GG_EINVAL;
+    auto* e = new gg_engine();
+    e->cfg = *cfg;
+    e->V = cfg->n_nodes;
+    e->nw = cfg->n_lanes / 64;
+    e->rank = cfg->rank;
+    e->world = cfg->world;
+    unsigned hc = std::thread::hardware_concurrency();
+    e->threads = hc ? (int)hc : 1;
+    if (const char* s = getenv("GG_CPU_THREADS")) e->threads = std::max(1, atoi(s));
+    *out = e;
+    return GG_OK;
+}
+
+void gg_destroy(gg_engine* e) { delete e; }
+
+const char* gg_last_error(const gg_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64_t nnz) {
+    if (!e || !row_ptr || (nnz && !col)) return GG_EINVAL;
+    const uint64_t V = e->V;
+    if (row_ptr[0] != 0 || (uint64_t)row_ptr[V] != nnz) return e->fail(GG_EINVAL, "row_ptr[0]/row_ptr[V] mismatch");
+    for (uint64_t v = 0; v < V; ++v) {
+        if (row_ptr[v + 1] < row_ptr[v]) return e->fail(GG_EINVAL, "row_ptr not monotone");
+        for (int64_t k = row_ptr[v]; k < row_ptr[v + 1]; ++k) {
+            if (col[k] < 0 || (uint64_t)col[k] >= V) return e->fail(GG_EINVAL, "neighbour id out of range");
+            if (k > row_ptr[v] && col[k] <= col[k - 1])
+                return e->fail(GG_EINVAL, "neighbour list not ascending/unique");
+        }
+    }
+    // transpose: in-lists ascending by sender
+    std::vector<int64_t> tin(V + 1, 0);
+    for (uint64_t k = 0; k < nnz; ++k) tin[col[k] + 1]++;
+    for (uint64_t v = 0; v < V; ++v) tin[v + 1] += tin[v];
+    std::vector<uint32_t> tcol(nnz);
+    {
+        std::vector<int64_t> pos(tin.begin(), tin.end() - 1);
+        for (uint64_t u = 0; u < V; ++u)
+            for (int64_t k = row_ptr[u]; k < row_ptr[u + 1]; ++k) tcol[pos[col[k]]++] = (uint32_t)u;
+    }
+    bool sym = true;
+    for (uint64_t v = 0; v < V && sym; ++v) {
+        if (tin[v + 1] - tin[v] != row_ptr[v + 1] - row_ptr[v]) sym = false;
+        else
+            for (int64_t k = 0; k < tin[v + 1] - tin[v]; ++k)
+                if ((int64_t)tcol[tin[v] + k] != col[row_ptr[v] + k]) { sym = false; break; }
+    }
+    e->symmetric = sym;
+    // edge-balanced vertex ranges over the in-lists (pull work)
+    const uint32_t Wd = e->world;
+    e->rank_lo.assign(Wd + 1, V);
+    e->rank_lo[0] = 0;
+    {
+        const uint64_t total = nnz + V;
+        uint32_t p = 1;
+        for (uint64_t v = 0; v < V && p < Wd; ++v) {
+            uint64_t cum = (uint64_t)tin[v + 1] + v + 1;
+            while (p < Wd && cum >= total * p / Wd) e->rank_lo[p++] = v + 1;
+        }
+        while (p < Wd) e->rank_lo[p++] = V;
+    }
+    uint64_t maxrows = 0;
+    for (uint32_t p = 0; p < Wd; ++p) maxrows = std::max<uint64_t>(maxrows, e->rank_lo[p + 1] - e->rank_lo[p]);
+    e->slice = std::max<uint64_t>(64, (maxrows + 63) / 64 * 64);
+    e->lo = e->rank_lo[e->rank];
+    e->hi = e->rank_lo[e->rank + 1];
+    const uint64_t n_own = e->hi - e->lo;
+    // owned rows with replica column ids
+    e->in_ptr.assign(n_own + 1, 0);
+    e->out_ptr.assign(n_own + 1, 0);
+    for (uint64_t i = 0; i < n_own; ++i) {
+        e->in_ptr[i + 1] = e->in_ptr[i] + (tin[e->lo + i + 1] - tin[e->lo + i]);
+        e->out_ptr[i + 1] = e->out_ptr[i] + (row_ptr[e->lo + i + 1] - row_ptr[e->lo + i]);
+    }
+    e->in_col.resize(e->in_ptr[n_own]);
+    e->in_recip.resize(e->in_ptr[n_own]);
+    e->out_col.resize(e->out_ptr[n_own]);
+    for (uint64_t i = 0; i < n_own; ++i) {
+        const uint64_t v = e->lo + i;
+        const int32_t* ob = col + row_ptr[v];
+        const int32_t* oe = col + row_ptr[v + 1];
+        for (int64_t k = 0; k < tin[v + 1] - tin[v]; ++k) {
+            uint32_t u = tcol[tin[v] + k];
+            e->in_col[e->in_ptr[i] + k] = (uint32_t)e->rep_of(u);
+            e->in_recip[e->in_ptr[i] + k] = std::binary_search(ob, oe, (int32_t)u) ? 1 : 0;
+        }
+        for (int64_t k = 0; k < row_ptr[v + 1] - row_ptr[v]; ++k)
+            e->out_col[e->out_ptr[i] + k] = (uint32_t)e->rep_of((uint64_t)ob[k]);
+    }
+    const uint64_t rows = (uint64_t)Wd * e->slice;
+    for (int b = 0; b < 2; ++b) {
+        e->seen[b].assign(rows * e->nw, 0);
+        e->F[b].assign(rows * e->nw, 0);
+    }
+    for (int b = 0; b < 4; ++b) e->fired[b].assign(rows / 64, 0);
+    e->sync_next.assign(n_own, 0);
+    e->sync_k.assign(n_own, 0);
+    if (e->cfg.flags & GG_TRACK_DELIVERY) e->dr.assign(n_own * e->cfg.n_lanes, -1);
+    else e->dr.clear();
+    e->have_topo = true;
+    e->reset_state();
+    return GG_OK;
+}
+
+static int add_window(gg_engine* e, int64_t a, int64_t b, Window&& w) {
+    if (!e) return GG_EINVAL;
+    if (a >= b) return e->fail(GG_EINVAL, "empty partition window");
+    for (const auto& x : e->windows)
+        if (a < x.to && x.from < b) return e->fail(GG_EINVAL, "overlapping partition windows");
+    w.from = a;
+    w.to = b;
+    e->windows.push_back(std::move(w));
+    return GG_OK;
+}
+
+int gg_partition_seeded(gg_engine* e, int64_t a, int64_t b, uint64_t epoch_seed) {
+    Window w;
+    w.seeded = true;
+    w.epoch_seed = epoch_seed;
+    return add_window(e, a, b, std::move(w));
+}
+
+int gg_partition_groups(gg_engine* e, int64_t a, int64_t b, const uint8_t* group) {
+    if (!e || !group) return GG_EINVAL;
+    Window w;
+    w.seeded = false;
+    w.epoch_seed = 0;
+    w.group.assign(group, group + e->V);
+    return add_window(e, a, b, std::move(w));
+}
+
+int gg_broadcast(gg_engine* e, uint32_t node, int64_t message, int64_t round) {
+    if (!e) return GG_EINVAL;
+    if (node >= e->V) return e->fail(GG_EINVAL, "node out of range");
+    if (round < e->round) return e->fail(GG_EINVAL, "broadcast scheduled in the past");
+    auto it = e->lanes.find(message);
+    uint32_t lane;
+    if (it == e->lanes.end()) {
+        if (e->lane_value.size() >= e->cfg.n_lanes) return e->fail(GG_ENOSPC, "all message lanes in use");
+        lane = (uint32_t)e->lane_value.size();
+        e->lanes.emplace(message, lane);
+        e->lane_value.push_back(message);
+    } else {
+        lane = it->second;
+    }
+    e->inj[round].push_back({node, lane});
+    return GG_OK;
+}
+
+int gg_lane_of(const gg_engine* e, int64_t message) {
+    if (!e) return GG_EINVAL;
+    auto it = e->lanes.find(message);
+    return it == e->lanes.end() ? GG_EINVAL : (int)it->second;
+}
+
+int64_t gg_current_round(const gg_engine* e) { return e ? e->round : -1; }
+
+static void fill_stats(gg_engine* e, const Acc& a, gg_round_stats* s) {
+    s->round = e->round;
+    s->new_bits = a.new_bits;
+    s->fwd_sent = a.fwd_sent;
+    s->fwd_delivered = a.fwd_deliv;
+    s->pushes = a.pushes;
+    s->push_delivered = a.push_deliv;
+    s->acks = e->pend_acks;
+    s->reads = a.reads;
+    s->read_oks = a.read_oks;
+    s->dropped = a.dropped + e->pend_ackdrop;
+    s->syncs_fired = a.fired;
+    s->seen_hash = a.hash;
+    s->kernel_ms = 0.0;
+}
+
+int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
+    if (!e) return GG_EINVAL;
+    if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
+    if (e->world != 1) return e->fail(GG_EINVAL, "sharded engine: use gg_dist_round_begin/end");
+    for (uint32_t k = 0; k < n; ++k) {
+        Acc a;
+        e->compute_round(a);
+        gg_round_stats s;
+        fill_stats(e, a, &s);
+        if (out) out[k] = s;
+        e->pend_acks = a.next_acks;
+        e->pend_ackdrop = a.next_ackdrop;
+        e->round++;
+    }
+    return GG_OK;
+}
+
+int gg_dist_range(const gg_engine* e, uint64_t* lo, uint64_t* hi) {
+    if (!e || !e->have_topo) return GG_EINVAL;
+    if (lo) *lo = e->lo;
+    if (hi) *hi = e->hi;
+    return GG_OK;
+}
+
+int gg_dist_round_begin(gg_engine* e, gg_exchange* x) {
+    if (!e || !x) return GG_EINVAL;
+    if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
+    if (e->dist_open) return e->fail(GG_EINVAL, "round already open");
+    e->dist_acc = Acc();
+    e->compute_round(e->dist_acc);
+    const int64_t r = e->round;
+    x->node_lo = e->lo;
+    x->node_hi = e->hi;
+    x->slice_rows = e->slice;
+    x->frontier = e->F[r & 1].data();
+    x->seen = e->seen[r & 1].data();
+    x->fired = e->fired[r & 3].data();
+    x->frontier_bytes = e->slice * e->nw * 8;
+    x->seen_bytes = e->slice * e->nw * 8;
+    x->fired_bytes = e->slice / 8;
+    // remote seen_prev is read in round r+1 by callbacks (fired r-1) and push
+    // edges (fired r-2); fires start at round >= sync_base.
+    x->need_seen = (e->cfg.enable_sync && r + 1 >= (int64_t)e->cfg.sync_base_ticks + 1) ? 1 : 0;
+    e->dist_open = true;
+    return GG_OK;
+}
+
+int gg_dist_round_end(gg_engine* e, gg_round_stats* out) {
+    if (!e || !e->dist_open) return GG_EINVAL;
+    gg_round_stats s;
+    fill_stats(e, e->dist_acc, &s);
+    if (out) *out = s;
+    e->pend_acks = e->dist_acc.next_acks;
+    e->pend_ackdrop = e->dist_acc.next_ackdrop;
+    e->round++;
+    e->dist_open = false;
+    return GG_OK;
+}
+
+static bool owned(const gg_engine* e, uint64_t a, uint64_t b) { return a <= b && a >= e->lo && b <= e->hi; }
+
+int gg_read(gg_engine* e, uint32_t node, int64_t* out, uint64_t cap, uint64_t* n_out) {
+    if (!e || !e->have_topo) return GG_EINVAL;
+    if (!owned(e, node, (uint64_t)node + 1)) return e->fail(GG_EINVAL, "node not owned by this engine");
+    const uint64_t rep = (uint64_t)e->rank * e->slice + (node - e->lo);
+    const auto& sc = e->seen[(e->round + 1) & 1];  // last completed round
+    std::vector<int64_t> vals;
+    for (uint64_t j = 0; j < e->nw; ++j) {
+        uint64_t x = sc[rep * e->nw + j];
+        while (x) {
+            int b = __builtin_ctzll(x);
+            x &= x - 1;
+            uint64_t lane = j * 64 + b;
+            if (lane < e->lane_value.size()) vals.push_back(e->lane_value[lane]);
+        }
+    }
+    std::sort(vals.begin(), vals.end());
+    if (n_out) *n_out = vals.size();
+    if (out)
+        for (uint64_t i = 0; i < vals.size() && i < cap; ++i) out[i] = vals[i];
+    return GG_OK;
+}
+
+int gg_read_bits(gg_engine* e, uint32_t a, uint32_t b, uint64_t* out) {
+    if (!e || !e->have_topo || !out) return GG_EINVAL;
+    if (!owned(e, a, b)) return e->fail(GG_EINVAL, "range not owned by this engine");
+    const auto& sc = e->seen[(e->round + 1) & 1];
+    const uint64_t rep = (uint64_t)e->rank * e->slice + (a - e->lo);
+    std::memcpy(out, &sc[rep * e->nw], (uint64_t)(b - a) * e->nw * 8);
+    return GG_OK;
+}
+
+int gg_delivery_rounds(gg_engine* e, uint32_t a, uint32_t b, int32_t* out, uint64_t cap) {
+    if (!e || !e->have_topo || !out) return GG_EINVAL;
+    if (e->dr.empty()) return e->fail(GG_EINVAL, "GG_TRACK_DELIVERY not enabled");
+    if (!owned(e, a, b)) return e->fail(GG_EINVAL, "range not owned by this engine");
+    const uint64_t n = (uint64_t)(b - a) * e->cfg.n_lanes;
+    if (cap < n) return e->fail(GG_EINVAL, "output buffer too small");
+    std::memcpy(out, &e->dr[(a - e->lo) * e->cfg.n_lanes], n * 4);
+    return GG_OK;
+}
+
+int gg_reset(gg_engine* e) {
+    if (!e) return GG_EINVAL;
+    if (e->have_topo) e->reset_state();
+    return GG_OK;
+}
+
+}  // extern "C"
