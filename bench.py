@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""Benchmark: (node,msg) deliveries/s of the gossip-propagation engine.
+
+One *step* = one full propagation episode of config C2 (BASELINE.json
+configs[1]): a 4-ary tree (Maelstrom `tree4`) of 2^20 nodes per GPU, K = 1024
+fresh messages broadcast by clients at seeded uniform nodes in round 0, sync
+timers on, no partitions; the episode is reset -> inject -> lockstep rounds
+until the round after the last delivery (quiescence, fixed during warmup).
+`value` = all (node,msg) deliveries of the timed episodes on all ranks / the
+max-over-ranks wall time. On N GPUs the tree has N * 2^20 nodes, vertex-range
+sharded, with one RCCL all-gather of frontier slices per round ("scaling":
+"weak").
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+For N > 1 launch under torch.distributed.run (one process per GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "gossip-glomers-distributed-systems_amd")
+sys.path.insert(0, PKG)
+
+import numpy as np  # noqa: E402
+
+METRIC = "(node,msg) deliveries/sec at 1/2/4/8 GPUs; % of HBM roofline; msgs/op"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes_per_round(V: int, E: int, nwp: int) -> int:
+    """SURVEY.md §8d dense-pull bytes of one expand launch (no partitions):
+    row_ptr 8(V+1) + col 4E + gathered frontier rows E*w + seen_prev read,
+    seen_cur write, F_cur write 3*V*w, with w = bytes per node set."""
+    w = 8 * nwp
+    return 8 * (V + 1) + 4 * E + E * w + 3 * V * w
+
+
+def next_pow2(x: int) -> int:
+    p = 1
+    while p < x:
+        p <<= 1
+    return p
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--nodes-per-gpu", type=int, default=1 << 20)
+    ap.add_argument("--lanes", type=int, default=1024)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-episodes", type=int, default=2)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from ggamd import topology as T
+    from ggamd.engine import Engine
+    from ggamd.workload import BASE_SEED, inject, uniform_injections
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    V = args.nodes_per_gpu * world
+    K = args.lanes
+    seed = BASE_SEED + 2
+    topo = T.tree(V, 4)
+    inj = uniform_injections(V, K, seed)
+    eng = Engine(V, K, seed=seed, enable_sync=True, device=local, rank=rank, world=world)
+    eng.topology(topo)
+    runner = None
+    if world > 1:
+        from ggamd.dist import ShardedRunner
+        runner = ShardedRunner(eng, device)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+        torch.cuda.synchronize()
+
+    def run_rounds(n):
+        if runner is None:
+            return eng.step(n)
+        return runner.step(n, reduce=False)
+
+    # warmup 0: find the quiescence round with per-round global counts
+    eng.reset()
+    inject(eng, inj)
+    R = 0
+    while True:
+        st = runner.step(1)[0] if runner else eng.step(1)[0]
+        R += 1
+        if st["new_bits"] == 0 and R > 1:
+            break
+        if R > 400:
+            raise RuntimeError("no quiescence within 400 rounds")
+
+    def episode():
+        eng.reset()
+        inject(eng, inj)
+        return run_rounds(R)
+
+    for _ in range(max(0, args.warmup - 1)):
+        episode()
+
+    barrier()
+    t0 = time.perf_counter()
+    local_stats = []
+    for _ in range(args.steps):
+        local_stats.append(episode())
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        per_ep = [runner.reduce(s) for s in local_stats]
+    else:
+        per_ep = local_stats
+    deliveries = sum(s["new_bits"] for ep in per_ep for s in ep)
+    msgs = sum(s["fwd_sent"] + s["pushes"] + s["acks"] + s["reads"] + s["read_oks"]
+               for s in per_ep[-1])
+    # roofline of the dominant kernel (expand_round) from the engine's HIP events
+    lo, hi = eng.dist_range() if world > 1 else (0, V)
+    E_own = int(topo.row_ptr[hi] - topo.row_ptr[lo])
+    nwp = next_pow2(K // 64)
+    B = algorithmic_bytes_per_round(hi - lo, E_own, nwp)
+    ms_local = [s["kernel_ms"] for ep in local_stats for s in ep]
+    avg_ms = float(np.mean(ms_local))
+    achieved = B / (avg_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        value = deliveries / elapsed
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "deliveries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (seeded tree4 topology, seeded client broadcasts)",
+            "config": {
+                "workload": "C2: tree4 of 2^20 nodes per GPU, 1024 messages broadcast in round 0 "
+                            "at seeded uniform nodes, sync on, no partitions; one step = one "
+                            "episode to quiescence",
+                "nodes": V, "edges": int(topo.nnz), "lanes": K, "rounds_per_step": R,
+                "deliveries_per_step": deliveries // args.steps,
+                "inter_node_msgs_per_step": msgs,
+                "msgs_per_op": msgs / K,
+                "parallelism": f"vertex-range x{world}" if world > 1 else "single GPU",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "expand_round",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "algorithmic_bytes_per_launch": B,
+                "avg_launch_ms": avg_ms,
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(topo, inj, V, K, seed, R, args.cpu_episodes)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier(device_ids=[local])
+        dist.destroy_process_group()
+
+
+def cpu_baseline(topo, inj, V, K, seed, R, episodes):
+    """The O2 bitset oracle (same semantics, CPU restatement of the reference
+    handlers) timed on this host's cores over `episodes` full C2 episodes."""
+    from ggamd.engine import Engine
+    from ggamd.workload import inject
+    lib = os.path.join(REPO, "oracle", "_build", "libgossip_cpu.so")
+    if not os.path.exists(lib):
+        return None
+    threads = min(16, os.cpu_count() or 1)
+    os.environ["GG_CPU_THREADS"] = str(threads)
+    e = Engine(V, K, seed=seed, enable_sync=True, library=lib)
+    e.topology(topo)
+    dl = 0
+    t0 = time.perf_counter()
+    for _ in range(episodes):
+        e.reset()
+        inject(e, inj)
+        dl += sum(s["new_bits"] for s in e.step(R))
+    dt = time.perf_counter() - t0
+    return {"value": dl / dt, "unit": "deliveries/s", "cores": threads, "kind": "port",
+            "sample": f"{episodes} full C2 episodes ({R} rounds each) of the O2 bitset oracle"}
+
+
+if __name__ == "__main__":
+    main()

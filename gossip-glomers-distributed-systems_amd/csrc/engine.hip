@@ -1,0 +1,739 @@
+// engine.hip — libgossip_hip.so: the C ABI of include/gossip.h on MI355X.
+//
+// Host side of the engine: input validation and CSR transposition
+// (HandleTopology, `broadcast/broadcast.go:36-48`, for every node at once),
+// message-value <-> lane bookkeeping (`BroadcastMsgBody.Message`, `:22-25`),
+// the client broadcast queue, partition windows, device memory, and the
+// per-round launch sequence of csrc/expand_kernels.hpp on one HIP stream.
+//
+// Device layout: node sets are rows of nwp u64 words (nwp =
+// W/64 rounded up to a power of two), node-major, in four ping-pong buffers
+// seen[2], F[2] (F = new bits of a round = what the node forwards next round);
+// fired[4] is a ring of per-round sync-timer bitmaps; CSR in-lists carry the
+// sender's row with bit 31 set when the sender is also in the receiver's
+// out-list (forward exclusion, `:52`). In sharded mode every buffer is a
+// replica laid out [world][slice_rows], columns index replica rows, and the
+// caller all-gathers each rank's slices between gg_dist_round_begin/end.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "expand_kernels.hpp"
+#include "gossip.h"
+
+namespace {
+
+constexpr uint32_t kMaxBatch = 256;  // rounds per counter readback
+constexpr int kMaxBlocks = 2048;
+
+struct Window {
+    int64_t from, to;
+    bool seeded;
+    uint64_t epoch_seed;
+    std::vector<uint8_t> group;  // explicit: global node -> group
+    uint8_t* d_grp = nullptr;    // replica-row groups on device
+};
+
+struct Injection {
+    uint32_t node;
+    uint32_t lane;
+};
+
+uint32_t next_pow2(uint32_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+}  // namespace
+
+struct gg_engine {
+    gg_config cfg{};
+    std::string err;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint64_t V = 0, nw = 0, nwp = 0;
+    uint32_t rank = 0, world = 1;
+    uint64_t lo = 0, hi = 0, slice = 0, rows = 0;
+    std::vector<uint64_t> rank_lo;
+    bool have_topo = false, symmetric = true;
+
+    int64_t* d_in_ptr = nullptr;
+    uint32_t* d_in_col = nullptr;
+    int64_t* d_out_ptr = nullptr;
+    uint32_t* d_out_col = nullptr;
+    uint64_t* d_seen[2] = {nullptr, nullptr};
+    uint64_t* d_F[2] = {nullptr, nullptr};
+    uint64_t* d_fired[4] = {nullptr, nullptr, nullptr, nullptr};
+    int32_t* d_sync_next = nullptr;
+    uint32_t* d_sync_k = nullptr;
+    int32_t* d_dr = nullptr;
+    uint64_t* d_rank_lo = nullptr;
+    unsigned long long* d_counters = nullptr;
+    unsigned long long* h_counters = nullptr;  // pinned
+    uint32_t* d_inj = nullptr;
+    uint32_t* h_inj = nullptr;  // pinned
+    size_t inj_cap = 0;         // pairs
+    std::vector<hipEvent_t> ev;  // 2 per batched round
+
+    std::vector<Window> windows;
+    std::unordered_map<int64_t, uint32_t> lanes;
+    std::vector<int64_t> lane_value;
+    std::map<int64_t, std::vector<Injection>> inj;
+    int64_t round = 0;
+    unsigned long long pend_acks = 0, pend_ackdrop = 0;
+    bool dist_open = false;
+
+    int fail(int code, const std::string& m) {
+        err = m;
+        return code;
+    }
+    void free_topology();
+    ~gg_engine();
+};
+
+#define HIPCHK(x)                                                                          \
+    do {                                                                                   \
+        hipError_t err_ = (x);                                                             \
+        if (err_ != hipSuccess)                                                            \
+            return e->fail(GG_EIO, std::string(#x) + ": " + hipGetErrorString(err_));      \
+    } while (0)
+
+template <class T>
+static void dfree(T*& p) {
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+void gg_engine::free_topology() {
+    if (d_out_col == d_in_col) d_out_col = nullptr;
+    if (d_out_ptr == d_in_ptr) d_out_ptr = nullptr;
+    dfree(d_out_col);
+    dfree(d_out_ptr);
+    dfree(d_in_ptr);
+    dfree(d_in_col);
+    for (auto& p : d_seen) dfree(p);
+    for (auto& p : d_F) dfree(p);
+    for (auto& p : d_fired) dfree(p);
+    dfree(d_sync_next);
+    dfree(d_sync_k);
+    dfree(d_dr);
+    dfree(d_rank_lo);
+    for (auto& w : windows) dfree(w.d_grp);
+    have_topo = false;
+}
+
+gg_engine::~gg_engine() {
+    (void)hipSetDevice(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    free_topology();
+    dfree(d_counters);
+    dfree(d_inj);
+    if (h_counters) (void)hipHostFree(h_counters);
+    if (h_inj) (void)hipHostFree(h_inj);
+    for (auto& x : ev) (void)hipEventDestroy(x);
+    if (stream) (void)hipStreamDestroy(stream);
+}
+
+// ---------------------------------------------------------------------------
+
+namespace {
+
+int reset_device_state(gg_engine* e) {
+    const size_t rowbytes = e->rows * e->nwp * 8;
+    for (int b = 0; b < 2; ++b) {
+        HIPCHK(hipMemsetAsync(e->d_seen[b], 0, rowbytes, e->stream));
+        HIPCHK(hipMemsetAsync(e->d_F[b], 0, rowbytes, e->stream));
+    }
+    for (int b = 0; b < 4; ++b) HIPCHK(hipMemsetAsync(e->d_fired[b], 0, e->rows / 8, e->stream));
+    const uint64_t n_own = e->hi - e->lo;
+    if (n_own) {
+        hipLaunchKernelGGL(gg::sync_init, dim3((unsigned)((n_own + 255) / 256)), dim3(256), 0, e->stream,
+                           e->d_sync_next, e->d_sync_k, n_own, e->lo, e->cfg.seed,
+                           e->cfg.sync_base_ticks, e->cfg.sync_jitter_ticks);
+        HIPCHK(hipGetLastError());
+    }
+    if (e->d_dr) HIPCHK(hipMemsetAsync(e->d_dr, 0xff, n_own * e->cfg.n_lanes * 4, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return GG_OK;
+}
+
+int materialize_windows(gg_engine* e) {
+    for (auto& w : e->windows) {
+        if (w.d_grp) continue;
+        HIPCHK(hipMalloc(&w.d_grp, e->rows));
+        if (w.seeded) {
+            hipLaunchKernelGGL(gg::fill_seeded_groups, dim3((unsigned)((e->rows + 255) / 256)), dim3(256), 0,
+                               e->stream, w.d_grp, e->rows, e->slice, e->d_rank_lo, e->world,
+                               e->cfg.seed, w.epoch_seed);
+            HIPCHK(hipGetLastError());
+        } else {
+            std::vector<uint8_t> h(e->rows, 0);
+            for (uint32_t p = 0; p < e->world; ++p)
+                for (uint64_t g = e->rank_lo[p]; g < e->rank_lo[p + 1]; ++g)
+                    h[(uint64_t)p * e->slice + (g - e->rank_lo[p])] = w.group[g];
+            HIPCHK(hipMemcpy(w.d_grp, h.data(), e->rows, hipMemcpyHostToDevice));
+        }
+    }
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return GG_OK;
+}
+
+const uint8_t* group_at(const gg_engine* e, int64_t r) {
+    for (const auto& w : e->windows)
+        if (w.from <= r && r < w.to) return w.d_grp;
+    return nullptr;
+}
+
+template <int G, int WPL>
+void launch_t(const gg::RoundArgs& a, bool syncw, bool maskw, hipStream_t s) {
+    const uint64_t groups = gg::kBlock / G;
+    uint64_t blocks = (a.n_own + groups - 1) / groups;
+    blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, kMaxBlocks));
+    dim3 grid((unsigned)blocks), block(gg::kBlock);
+    if (syncw) {
+        if (maskw) hipLaunchKernelGGL((gg::expand_round<G, WPL, true, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((gg::expand_round<G, WPL, true, false>), grid, block, 0, s, a);
+    } else {
+        if (maskw) hipLaunchKernelGGL((gg::expand_round<G, WPL, false, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((gg::expand_round<G, WPL, false, false>), grid, block, 0, s, a);
+    }
+}
+
+void launch_expand(const gg::RoundArgs& a, bool syncw, bool maskw, hipStream_t s) {
+    switch (a.nwp) {
+        case 1: launch_t<1, 1>(a, syncw, maskw, s); break;
+        case 2: launch_t<1, 2>(a, syncw, maskw, s); break;
+        case 4: launch_t<2, 2>(a, syncw, maskw, s); break;
+        case 8: launch_t<4, 2>(a, syncw, maskw, s); break;
+        case 16: launch_t<8, 2>(a, syncw, maskw, s); break;
+        case 32: launch_t<16, 2>(a, syncw, maskw, s); break;
+        case 64: launch_t<32, 2>(a, syncw, maskw, s); break;
+        case 128: launch_t<64, 2>(a, syncw, maskw, s); break;
+        default: break;
+    }
+}
+
+// Enqueue round e->round (kernels only). inj: device pairs for this round.
+int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned long long* d_ctr,
+                  hipEvent_t ev0, hipEvent_t ev1) {
+    const int64_t r = e->round;
+    gg::RoundArgs a{};
+    a.in_ptr = e->d_in_ptr;
+    a.in_col = e->d_in_col;
+    a.out_ptr = e->d_out_ptr;
+    a.out_col = e->d_out_col;
+    a.seen_prev = e->d_seen[(r + 1) & 1];
+    a.seen_cur = e->d_seen[r & 1];
+    a.F_prev = e->d_F[(r + 1) & 1];
+    a.F_cur = e->d_F[r & 1];
+    a.fired_m1 = e->d_fired[(r - 1) & 3];
+    a.fired_m2 = e->d_fired[(r - 2) & 3];
+    a.fired_m3 = e->d_fired[(r - 3) & 3];
+    a.fired_cur = e->d_fired[r & 3];
+    a.sync_next = e->d_sync_next;
+    a.sync_k = e->d_sync_k;
+    bool maskw = false;
+    for (int k = 0; k < 5; ++k) {
+        a.grp[k] = group_at(e, r - 3 + k);
+        maskw |= a.grp[k] != nullptr;
+    }
+    a.inj = d_inj;
+    a.n_inj = n_inj;
+    a.counters = d_ctr;
+    a.n_own = e->hi - e->lo;
+    a.own0 = (uint64_t)e->rank * e->slice;
+    a.lo = e->lo;
+    a.nwp = (uint32_t)e->nwp;
+    a.nw = (uint32_t)e->nw;
+    a.round = r;
+    a.seed = e->cfg.seed;
+    a.sync_base = e->cfg.sync_base_ticks;
+    a.sync_jitter = e->cfg.sync_jitter_ticks;
+    a.enable_sync = e->cfg.enable_sync;
+    const bool syncw = e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks + 1;
+
+    HIPCHK(hipMemsetAsync(a.fired_cur, 0, e->rows / 8, e->stream));
+    HIPCHK(hipEventRecord(ev0, e->stream));
+    if (a.n_own) {
+        launch_expand(a, syncw, maskw, e->stream);
+        HIPCHK(hipGetLastError());
+        if (e->d_dr) {
+            const uint64_t n = a.n_own * e->nw;
+            hipLaunchKernelGGL(gg::track_delivery, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream,
+                               a.F_cur, e->d_dr, a.n_own, a.own0, (uint32_t)e->nwp, (uint32_t)e->nw,
+                               e->cfg.n_lanes, (int32_t)r);
+            HIPCHK(hipGetLastError());
+        }
+    }
+    HIPCHK(hipEventRecord(ev1, e->stream));
+    return GG_OK;
+}
+
+// Host-side stats of one round from its 64 counter slots.
+void fold_stats(gg_engine* e, const unsigned long long* slots, float ms, gg_round_stats* s) {
+    unsigned long long c[gg::kCounters] = {0};
+    for (int k = 0; k < gg::kSlots; ++k)
+        for (int j = 0; j < gg::C_NUM; ++j) c[j] += slots[k * gg::kCounters + j];
+    s->round = e->round;
+    s->new_bits = c[gg::C_NEW];
+    s->fwd_sent = c[gg::C_FWD_SENT];
+    s->fwd_delivered = c[gg::C_FWD_DELIV];
+    s->pushes = c[gg::C_PUSH];
+    s->push_delivered = c[gg::C_PUSH_DELIV];
+    s->acks = e->pend_acks;
+    s->reads = c[gg::C_READS];
+    s->read_oks = c[gg::C_READ_OKS];
+    s->dropped = c[gg::C_DROPPED] + e->pend_ackdrop;
+    s->syncs_fired = c[gg::C_FIRED];
+    s->seen_hash = c[gg::C_HASH];
+    s->kernel_ms = ms;
+    e->pend_acks = c[gg::C_NEXT_ACKS];
+    e->pend_ackdrop = c[gg::C_NEXT_ACKDROP];
+}
+
+int ensure_events(gg_engine* e, size_t n) {
+    while (e->ev.size() < n) {
+        hipEvent_t x;
+        HIPCHK(hipEventCreate(&x));
+        e->ev.push_back(x);
+    }
+    return GG_OK;
+}
+
+int ensure_inj(gg_engine* e, size_t pairs) {
+    if (pairs <= e->inj_cap) return GG_OK;
+    size_t cap = std::max<size_t>(pairs, 2 * e->inj_cap + 1024);
+    HIPCHK(hipStreamSynchronize(e->stream));
+    dfree(e->d_inj);
+    if (e->h_inj) (void)hipHostFree(e->h_inj);
+    e->h_inj = nullptr;
+    HIPCHK(hipMalloc(&e->d_inj, cap * 8));
+    HIPCHK(hipHostMalloc(&e->h_inj, cap * 8));
+    e->inj_cap = cap;
+    return GG_OK;
+}
+
+// Pack the owned injections of rounds [r0, r0+n) into h_inj; off[k] = first pair of round r0+k.
+size_t pack_injections(gg_engine* e, int64_t r0, uint32_t n, std::vector<size_t>& off) {
+    off.assign(n + 1, 0);
+    std::vector<std::pair<uint32_t, uint32_t>> tmp;
+    for (uint32_t k = 0; k < n; ++k) {
+        off[k] = tmp.size();
+        auto it = e->inj.find(r0 + k);
+        if (it == e->inj.end()) continue;
+        const size_t b = tmp.size();
+        for (const auto& x : it->second)
+            if (x.node >= e->lo && x.node < e->hi) tmp.emplace_back((uint32_t)(x.node - e->lo), x.lane);
+        std::stable_sort(tmp.begin() + b, tmp.end(),
+                         [](const auto& p, const auto& q) { return p.first < q.first; });
+    }
+    off[n] = tmp.size();
+    if (ensure_inj(e, tmp.size()) != GG_OK) return (size_t)-1;
+    for (size_t t = 0; t < tmp.size(); ++t) {
+        e->h_inj[2 * t] = tmp[t].first;
+        e->h_inj[2 * t + 1] = tmp[t].second;
+    }
+    return tmp.size();
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+
+extern "C" {
+
+int gg_abi_version(void) { return GG_ABI_VERSION; }
+
+int gg_create(const gg_config* cfg, gg_engine** out) {
+    if (!cfg || !out) return GG_EINVAL;
+    *out = nullptr;
+    if (cfg->n_nodes == 0 || cfg->n_nodes > 0x7fffffffull) return GG_EINVAL;
+    if (cfg->n_lanes == 0 || cfg->n_lanes % 64 || cfg->n_lanes > 8192) return GG_EINVAL;
+    if (cfg->enable_sync && cfg->sync_base_ticks == 0) return GG_EINVAL;
+    if (cfg->world == 0 || cfg->rank >= cfg->world) return GG_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GG_EIO;
+    auto* e = new gg_engine();
+    e->cfg = *cfg;
+    e->V = cfg->n_nodes;
+    e->nw = cfg->n_lanes / 64;
+    e->nwp = next_pow2((uint32_t)e->nw);
+    e->rank = cfg->rank;
+    e->world = cfg->world;
+    if (cfg->device >= 0) {
+        e->device = cfg->device;
+        if (hipSetDevice(e->device) != hipSuccess) { delete e; return GG_EIO; }
+    } else if (hipGetDevice(&e->device) != hipSuccess) {
+        delete e;
+        return GG_EIO;
+    }
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&e->d_counters, (size_t)kMaxBatch * gg::kSlots * gg::kCounters * 8) != hipSuccess ||
+        hipHostMalloc(&e->h_counters, (size_t)kMaxBatch * gg::kSlots * gg::kCounters * 8) != hipSuccess) {
+        delete e;
+        return GG_EIO;
+    }
+    *out = e;
+    return GG_OK;
+}
+
+void gg_destroy(gg_engine* e) { delete e; }
+
+const char* gg_last_error(const gg_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64_t nnz) {
+    if (!e || !row_ptr || (nnz && !col)) return GG_EINVAL;
+    HIPCHK(hipSetDevice(e->device));
+    const uint64_t V = e->V;
+    if (row_ptr[0] != 0 || (uint64_t)row_ptr[V] != nnz) return e->fail(GG_EINVAL, "row_ptr[0]/row_ptr[V] mismatch");
+    for (uint64_t v = 0; v < V; ++v) {
+        if (row_ptr[v + 1] < row_ptr[v]) return e->fail(GG_EINVAL, "row_ptr not monotone");
+        for (int64_t k = row_ptr[v]; k < row_ptr[v + 1]; ++k) {
+            if (col[k] < 0 || (uint64_t)col[k] >= V) return e->fail(GG_EINVAL, "neighbour id out of range");
+            if (k > row_ptr[v] && col[k] <= col[k - 1])
+                return e->fail(GG_EINVAL, "neighbour list not ascending/unique");
+        }
+    }
+    if (nnz >= (1ull << 32)) return e->fail(GG_EINVAL, "more than 2^32 edges per engine not supported yet");
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->free_topology();
+    // transpose: in-lists ascending by sender
+    std::vector<int64_t> tin(V + 1, 0);
+    for (uint64_t k = 0; k < nnz; ++k) tin[col[k] + 1]++;
+    for (uint64_t v = 0; v < V; ++v) tin[v + 1] += tin[v];
+    std::vector<uint32_t> tcol(nnz);
+    {
+        std::vector<int64_t> pos(tin.begin(), tin.end() - 1);
+        for (uint64_t u = 0; u < V; ++u)
+            for (int64_t k = row_ptr[u]; k < row_ptr[u + 1]; ++k) tcol[pos[col[k]]++] = (uint32_t)u;
+    }
+    bool sym = true;
+    for (uint64_t v = 0; v < V && sym; ++v) {
+        if (tin[v + 1] - tin[v] != row_ptr[v + 1] - row_ptr[v]) {
+            sym = false;
+            break;
+        }
+        for (int64_t k = 0; k < tin[v + 1] - tin[v]; ++k)
+            if ((int64_t)tcol[tin[v] + k] != col[row_ptr[v] + k]) { sym = false; break; }
+    }
+    e->symmetric = sym;
+    // edge-balanced vertex ranges over the in-lists
+    const uint32_t Wd = e->world;
+    e->rank_lo.assign(Wd + 1, V);
+    e->rank_lo[0] = 0;
+    {
+        const uint64_t total = nnz + V;
+        uint32_t p = 1;
+        for (uint64_t v = 0; v < V && p < Wd; ++v) {
+            uint64_t cum = (uint64_t)tin[v + 1] + v + 1;
+            while (p < Wd && cum >= total * p / Wd) e->rank_lo[p++] = v + 1;
+        }
+        while (p < Wd) e->rank_lo[p++] = V;
+    }
+    uint64_t maxrows = 0;
+    for (uint32_t p = 0; p < Wd; ++p) maxrows = std::max<uint64_t>(maxrows, e->rank_lo[p + 1] - e->rank_lo[p]);
+    e->slice = std::max<uint64_t>(64, (maxrows + 63) / 64 * 64);
+    e->rows = (uint64_t)Wd * e->slice;
+    e->lo = e->rank_lo[e->rank];
+    e->hi = e->rank_lo[e->rank + 1];
+    const uint64_t n_own = e->hi - e->lo;
+    auto rep_of = [&](uint64_t g) -> uint32_t {
+        uint32_t p = (uint32_t)(std::upper_bound(e->rank_lo.begin(), e->rank_lo.end(), g) - e->rank_lo.begin()) - 1;
+        return (uint32_t)((uint64_t)p * e->slice + (g - e->rank_lo[p]));
+    };
+    if (e->rows > 0x7fffffffull) return e->fail(GG_EINVAL, "replica rows exceed 2^31");
+    std::vector<int64_t> iptr(n_own + 1, 0), optr(n_own + 1, 0);
+    for (uint64_t i = 0; i < n_own; ++i) {
+        iptr[i + 1] = iptr[i] + (tin[e->lo + i + 1] - tin[e->lo + i]);
+        optr[i + 1] = optr[i] + (row_ptr[e->lo + i + 1] - row_ptr[e->lo + i]);
+    }
+    std::vector<uint32_t> icol(iptr[n_own]), ocol(optr[n_own]);
+    for (uint64_t i = 0; i < n_own; ++i) {
+        const uint64_t v = e->lo + i;
+        const int32_t* ob = col + row_ptr[v];
+        const int32_t* oe = col + row_ptr[v + 1];
+        for (int64_t k = 0; k < tin[v + 1] - tin[v]; ++k) {
+            const uint32_t u = tcol[tin[v] + k];
+            const bool recip = sym || std::binary_search(ob, oe, (int32_t)u);
+            icol[iptr[i] + k] = rep_of(u) | (recip ? gg::kRecipBit : 0u);
+        }
+        for (int64_t k = 0; k < row_ptr[v + 1] - row_ptr[v]; ++k) ocol[optr[i] + k] = rep_of((uint64_t)ob[k]);
+    }
+    // device buffers
+    HIPCHK(hipMalloc(&e->d_in_ptr, (n_own + 1) * 8));
+    HIPCHK(hipMalloc(&e->d_in_col, std::max<size_t>(1, icol.size()) * 4));
+    HIPCHK(hipMemcpy(e->d_in_ptr, iptr.data(), (n_own + 1) * 8, hipMemcpyHostToDevice));
+    if (!icol.empty()) HIPCHK(hipMemcpy(e->d_in_col, icol.data(), icol.size() * 4, hipMemcpyHostToDevice));
+    if (sym) {
+        // out-lists equal in-lists; readers of out_col mask off the recip bit
+        e->d_out_ptr = e->d_in_ptr;
+        e->d_out_col = e->d_in_col;
+    } else {
+        HIPCHK(hipMalloc(&e->d_out_ptr, (n_own + 1) * 8));
+        HIPCHK(hipMalloc(&e->d_out_col, std::max<size_t>(1, ocol.size()) * 4));
+        HIPCHK(hipMemcpy(e->d_out_ptr, optr.data(), (n_own + 1) * 8, hipMemcpyHostToDevice));
+        if (!ocol.empty()) HIPCHK(hipMemcpy(e->d_out_col, ocol.data(), ocol.size() * 4, hipMemcpyHostToDevice));
+    }
+    const size_t rowbytes = e->rows * e->nwp * 8;
+    for (int b = 0; b < 2; ++b) {
+        HIPCHK(hipMalloc(&e->d_seen[b], rowbytes));
+        HIPCHK(hipMalloc(&e->d_F[b], rowbytes));
+    }
+    for (int b = 0; b < 4; ++b) HIPCHK(hipMalloc(&e->d_fired[b], e->rows / 8));
+    HIPCHK(hipMalloc(&e->d_sync_next, std::max<uint64_t>(1, n_own) * 4));
+    HIPCHK(hipMalloc(&e->d_sync_k, std::max<uint64_t>(1, n_own) * 4));
+    HIPCHK(hipMalloc(&e->d_rank_lo, (Wd + 1) * 8));
+    HIPCHK(hipMemcpy(e->d_rank_lo, e->rank_lo.data(), (Wd + 1) * 8, hipMemcpyHostToDevice));
+    if (e->cfg.flags & GG_TRACK_DELIVERY) HIPCHK(hipMalloc(&e->d_dr, std::max<uint64_t>(1, n_own) * e->cfg.n_lanes * 4));
+    e->have_topo = true;
+    e->lanes.clear();
+    e->lane_value.clear();
+    e->inj.clear();
+    e->round = 0;
+    e->pend_acks = e->pend_ackdrop = 0;
+    e->dist_open = false;
+    return reset_device_state(e);
+}
+
+static int add_window(gg_engine* e, int64_t a, int64_t b, Window&& w) {
+    if (a >= b) return e->fail(GG_EINVAL, "empty partition window");
+    for (const auto& x : e->windows)
+        if (a < x.to && x.from < b) return e->fail(GG_EINVAL, "overlapping partition windows");
+    w.from = a;
+    w.to = b;
+    e->windows.push_back(std::move(w));
+    return GG_OK;
+}
+
+int gg_partition_seeded(gg_engine* e, int64_t a, int64_t b, uint64_t epoch_seed) {
+    if (!e) return GG_EINVAL;
+    Window w;
+    w.seeded = true;
+    w.epoch_seed = epoch_seed;
+    return add_window(e, a, b, std::move(w));
+}
+
+int gg_partition_groups(gg_engine* e, int64_t a, int64_t b, const uint8_t* group) {
+    if (!e || !group) return GG_EINVAL;
+    Window w;
+    w.seeded = false;
+    w.epoch_seed = 0;
+    w.group.assign(group, group + e->V);
+    return add_window(e, a, b, std::move(w));
+}
+
+int gg_broadcast(gg_engine* e, uint32_t node, int64_t message, int64_t round) {
+    if (!e) return GG_EINVAL;
+    if (node >= e->V) return e->fail(GG_EINVAL, "node out of range");
+    if (round < e->round) return e->fail(GG_EINVAL, "broadcast scheduled in the past");
+    auto it = e->lanes.find(message);
+    uint32_t lane;
+    if (it == e->lanes.end()) {
+        if (e->lane_value.size() >= e->cfg.n_lanes) return e->fail(GG_ENOSPC, "all message lanes in use");
+        lane = (uint32_t)e->lane_value.size();
+        e->lanes.emplace(message, lane);
+        e->lane_value.push_back(message);
+    } else {
+        lane = it->second;
+    }
+    e->inj[round].push_back({node, lane});
+    return GG_OK;
+}
+
+int gg_broadcast_many(gg_engine* e, const uint32_t* nodes, const int64_t* messages,
+                      const int64_t* rounds, uint64_t n) {
+    if (!e || (n && (!nodes || !messages || !rounds))) return GG_EINVAL;
+    for (uint64_t k = 0; k < n; ++k) {
+        int rc = gg_broadcast(e, nodes[k], messages[k], rounds[k]);
+        if (rc) return rc;
+    }
+    return GG_OK;
+}
+
+int gg_lane_of(const gg_engine* e, int64_t message) {
+    if (!e) return GG_EINVAL;
+    auto it = e->lanes.find(message);
+    return it == e->lanes.end() ? GG_EINVAL : (int)it->second;
+}
+
+int64_t gg_current_round(const gg_engine* e) { return e ? e->round : -1; }
+
+int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
+    if (!e) return GG_EINVAL;
+    if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
+    if (e->world != 1) return e->fail(GG_EINVAL, "sharded engine: use gg_dist_round_begin/end");
+    HIPCHK(hipSetDevice(e->device));
+    int rc = materialize_windows(e);
+    if (rc) return rc;
+    uint32_t done = 0;
+    std::vector<size_t> off;
+    while (done < n) {
+        const uint32_t m = std::min<uint32_t>(kMaxBatch, n - done);
+        const int64_t r0 = e->round;
+        if ((rc = ensure_events(e, 2 * (size_t)m))) return rc;
+        HIPCHK(hipStreamSynchronize(e->stream));  // h_inj reuse
+        const size_t total = pack_injections(e, r0, m, off);
+        if (total == (size_t)-1) return GG_EIO;
+        if (total) HIPCHK(hipMemcpyAsync(e->d_inj, e->h_inj, total * 8, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(hipMemsetAsync(e->d_counters, 0, (size_t)m * gg::kSlots * gg::kCounters * 8, e->stream));
+        for (uint32_t k = 0; k < m; ++k) {
+            const uint32_t ni = (uint32_t)(off[k + 1] - off[k]);
+            rc = enqueue_round(e, ni ? e->d_inj + 2 * off[k] : nullptr, ni,
+                               e->d_counters + (size_t)k * gg::kSlots * gg::kCounters, e->ev[2 * k],
+                               e->ev[2 * k + 1]);
+            if (rc) return rc;
+            e->round++;
+        }
+        HIPCHK(hipMemcpyAsync(e->h_counters, e->d_counters, (size_t)m * gg::kSlots * gg::kCounters * 8,
+                              hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        for (uint32_t k = 0; k < m; ++k) {
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, e->ev[2 * k], e->ev[2 * k + 1]));
+            gg_round_stats s;
+            const int64_t save = e->round;
+            e->round = r0 + k;
+            fold_stats(e, e->h_counters + (size_t)k * gg::kSlots * gg::kCounters, ms, &s);
+            e->round = save;
+            if (out) out[done + k] = s;
+            e->inj.erase(r0 + k);
+        }
+        done += m;
+    }
+    return GG_OK;
+}
+
+int gg_dist_range(const gg_engine* e, uint64_t* lo, uint64_t* hi) {
+    if (!e || !e->have_topo) return GG_EINVAL;
+    if (lo) *lo = e->lo;
+    if (hi) *hi = e->hi;
+    return GG_OK;
+}
+
+int gg_dist_round_begin(gg_engine* e, gg_exchange* x) {
+    if (!e || !x) return GG_EINVAL;
+    if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
+    if (e->dist_open) return e->fail(GG_EINVAL, "round already open");
+    HIPCHK(hipSetDevice(e->device));
+    int rc = materialize_windows(e);
+    if (rc) return rc;
+    if ((rc = ensure_events(e, 2))) return rc;
+    std::vector<size_t> off;
+    const size_t total = pack_injections(e, e->round, 1, off);
+    if (total == (size_t)-1) return GG_EIO;
+    if (total) HIPCHK(hipMemcpyAsync(e->d_inj, e->h_inj, total * 8, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemsetAsync(e->d_counters, 0, (size_t)gg::kSlots * gg::kCounters * 8, e->stream));
+    rc = enqueue_round(e, total ? e->d_inj : nullptr, (uint32_t)total, e->d_counters, e->ev[0], e->ev[1]);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(e->h_counters, e->d_counters, (size_t)gg::kSlots * gg::kCounters * 8,
+                          hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    const int64_t r = e->round;
+    x->node_lo = e->lo;
+    x->node_hi = e->hi;
+    x->slice_rows = e->slice;
+    x->frontier = e->d_F[r & 1];
+    x->seen = e->d_seen[r & 1];
+    x->fired = e->d_fired[r & 3];
+    x->frontier_bytes = e->slice * e->nwp * 8;
+    x->seen_bytes = e->slice * e->nwp * 8;
+    x->fired_bytes = e->slice / 8;
+    x->need_seen = (e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks) ? 1 : 0;
+    e->dist_open = true;
+    return GG_OK;
+}
+
+int gg_dist_round_end(gg_engine* e, gg_round_stats* out) {
+    if (!e || !e->dist_open) return GG_EINVAL;
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
+    gg_round_stats s;
+    fold_stats(e, e->h_counters, ms, &s);
+    if (out) *out = s;
+    e->inj.erase(e->round);
+    e->round++;
+    e->dist_open = false;
+    return GG_OK;
+}
+
+static bool owned(const gg_engine* e, uint64_t a, uint64_t b) { return a <= b && a >= e->lo && b <= e->hi; }
+
+static int copy_rows(gg_engine* e, uint64_t a, uint64_t b, std::vector<uint64_t>& h) {
+    const uint64_t rep = (uint64_t)e->rank * e->slice + (a - e->lo);
+    h.resize((b - a) * e->nwp);
+    if (b > a) {
+        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipMemcpy(h.data(), e->d_seen[(e->round + 1) & 1] + rep * e->nwp, h.size() * 8, hipMemcpyDeviceToHost));
+    }
+    return GG_OK;
+}
+
+int gg_read(gg_engine* e, uint32_t node, int64_t* out, uint64_t cap, uint64_t* n_out) {
+    if (!e || !e->have_topo) return GG_EINVAL;
+    if (!owned(e, node, (uint64_t)node + 1)) return e->fail(GG_EINVAL, "node not owned by this engine");
+    HIPCHK(hipSetDevice(e->device));
+    std::vector<uint64_t> h;
+    int rc = copy_rows(e, node, (uint64_t)node + 1, h);
+    if (rc) return rc;
+    std::vector<int64_t> vals;
+    for (uint64_t j = 0; j < e->nw; ++j) {
+        uint64_t x = h[j];
+        while (x) {
+            const int b = __builtin_ctzll(x);
+            x &= x - 1;
+            const uint64_t lane = j * 64 + b;
+            if (lane < e->lane_value.size()) vals.push_back(e->lane_value[lane]);
+        }
+    }
+    std::sort(vals.begin(), vals.end());
+    if (n_out) *n_out = vals.size();
+    if (out)
+        for (uint64_t i = 0; i < vals.size() && i < cap; ++i) out[i] = vals[i];
+    return GG_OK;
+}
+
+int gg_read_bits(gg_engine* e, uint32_t a, uint32_t b, uint64_t* out) {
+    if (!e || !e->have_topo || !out) return GG_EINVAL;
+    if (!owned(e, a, b)) return e->fail(GG_EINVAL, "range not owned by this engine");
+    HIPCHK(hipSetDevice(e->device));
+    std::vector<uint64_t> h;
+    int rc = copy_rows(e, a, b, h);
+    if (rc) return rc;
+    for (uint64_t i = 0; i < (uint64_t)(b - a); ++i)
+        std::memcpy(out + i * e->nw, h.data() + i * e->nwp, e->nw * 8);
+    return GG_OK;
+}
+
+int gg_delivery_rounds(gg_engine* e, uint32_t a, uint32_t b, int32_t* out, uint64_t cap) {
+    if (!e || !e->have_topo || !out) return GG_EINVAL;
+    if (!e->d_dr) return e->fail(GG_EINVAL, "GG_TRACK_DELIVERY not enabled");
+    if (!owned(e, a, b)) return e->fail(GG_EINVAL, "range not owned by this engine");
+    const uint64_t n = (uint64_t)(b - a) * e->cfg.n_lanes;
+    if (cap < n) return e->fail(GG_EINVAL, "output buffer too small");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (n) HIPCHK(hipMemcpy(out, e->d_dr + (a - e->lo) * e->cfg.n_lanes, n * 4, hipMemcpyDeviceToHost));
+    return GG_OK;
+}
+
+int gg_reset(gg_engine* e) {
+    if (!e) return GG_EINVAL;
+    e->lanes.clear();
+    e->lane_value.clear();
+    e->inj.clear();
+    e->round = 0;
+    e->pend_acks = e->pend_ackdrop = 0;
+    e->dist_open = false;
+    if (!e->have_topo) return GG_OK;
+    HIPCHK(hipSetDevice(e->device));
+    return reset_device_state(e);
+}
+
+}  // extern "C"

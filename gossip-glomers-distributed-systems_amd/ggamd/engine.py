@@ -80,7 +80,8 @@ COUNT_FIELDS = [f for f in STAT_FIELDS if f not in ("round", "kernel_ms")]
 
 GG_SYMBOLS = [
     "gg_abi_version", "gg_create", "gg_destroy", "gg_last_error", "gg_topology",
-    "gg_partition_seeded", "gg_partition_groups", "gg_broadcast", "gg_lane_of", "gg_step",
+    "gg_partition_seeded", "gg_partition_groups", "gg_broadcast", "gg_broadcast_many",
+    "gg_lane_of", "gg_step",
     "gg_current_round", "gg_read", "gg_read_bits", "gg_delivery_rounds", "gg_reset",
     "gg_dist_round_begin", "gg_dist_round_end", "gg_dist_range",
 ]
@@ -106,6 +107,7 @@ def load_library(path: str) -> C.CDLL:
     lib.gg_partition_seeded.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_uint64]
     lib.gg_partition_groups.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]
     lib.gg_broadcast.argtypes = [C.c_void_p, C.c_uint32, C.c_int64, C.c_int64]
+    lib.gg_broadcast_many.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
     lib.gg_lane_of.argtypes = [C.c_void_p, C.c_int64]
     lib.gg_step.argtypes = [C.c_void_p, C.c_uint32, P(GGRoundStats)]
     lib.gg_current_round.argtypes = [C.c_void_p]
@@ -205,9 +207,12 @@ class Engine:
     def broadcast(self, node: int, value: int, rnd: int):
         self._ok(self.lib.gg_broadcast(self.h, node, value, rnd))
 
-    def broadcast_many(self, nodes, values, rnd: int):
-        for n, v in zip(nodes, values):
-            self._ok(self.lib.gg_broadcast(self.h, int(n), int(v), rnd))
+    def broadcast_many(self, nodes, values, rounds):
+        nodes = np.ascontiguousarray(nodes, np.uint32)
+        values = np.ascontiguousarray(values, np.int64)
+        rounds = np.ascontiguousarray(np.broadcast_to(rounds, nodes.shape), np.int64)
+        self._ok(self.lib.gg_broadcast_many(self.h, nodes.ctypes.data, values.ctypes.data,
+                                            rounds.ctypes.data, nodes.size))
 
     def lane_of(self, value: int) -> int:
         return self.lib.gg_lane_of(self.h, value)

@@ -1,0 +1,87 @@
+"""Synthetic workloads of SURVEY.md §8d (seeded; base seed 0x6A09E667F3BCC909 + config#).
+
+A workload = topology + message injections + partition windows + sync
+settings. C1 is the reference's own challenge setting (Maelstrom
+`--node-count 25 --topology tree4 --rate 100 --latency 100`); C2..C5 are the
+scale-up configs of BASELINE.json.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import topology as T
+from .engine import Topology
+
+BASE_SEED = 0x6A09E667F3BCC909
+
+
+@dataclass
+class Workload:
+    name: str
+    topo: Topology
+    n_lanes: int
+    injections: list  # (node, value, round)
+    seed: int
+    sync_base: int = 20
+    sync_jitter: int = 10
+    enable_sync: bool = True
+    windows: list = field(default_factory=list)  # ("seeded", r0, r1, epoch_seed)
+    max_rounds: int = 400
+
+    def apply(self, eng):
+        eng.topology(self.topo)
+        self.apply_events(eng)
+
+    def apply_events(self, eng):
+        for w in self.windows:
+            if w[0] == "seeded":
+                eng.partition_seeded(w[1], w[2], w[3])
+            else:
+                eng.partition_groups(w[1], w[2], w[3])
+        inject(eng, self.injections)
+
+
+def inject(eng, injections):
+    if not injections:
+        return
+    a = np.asarray(injections, dtype=np.int64)
+    eng.broadcast_many(a[:, 0], a[:, 1], a[:, 2])
+
+
+def uniform_injections(V: int, K: int, seed: int, rnd: int = 0) -> list:
+    """K fresh values 0..K-1 broadcast by clients at uniform seeded nodes in round `rnd`."""
+    rng = np.random.Generator(np.random.PCG64(seed & ((1 << 63) - 1)))
+    nodes = rng.integers(0, V, size=K)
+    return [(int(nodes[k]), k, rnd) for k in range(K)]
+
+
+def c2(V: int = 1 << 20, K: int = 1024) -> Workload:
+    """1M-node tree4, 1024 concurrent messages (1 Kbit sets), sync on, no partitions."""
+    seed = BASE_SEED + 2
+    return Workload("C2", T.tree(V, 4), K, uniform_injections(V, K, seed), seed)
+
+
+def c3(V: int = 10_000_000, K: int = 1024) -> Workload:
+    """Random 8-regular, seeded random bisection in rounds [2,12) then healed, sync on."""
+    seed = BASE_SEED + 3
+    return Workload("C3", T.random_regular(V, 8, seed), K, uniform_injections(V, K, seed), seed,
+                    windows=[("seeded", 2, 12, seed ^ 0x5EED)])
+
+
+def c4(V: int = 100_000_000, K: int = 4096) -> Workload:
+    """R-MAT (.57,.19,.19,.05) edge factor 16, symmetrized; 4096 messages."""
+    seed = BASE_SEED + 4
+    return Workload("C4", T.rmat(V, 16, seed=seed), K, uniform_injections(V, K, seed), seed)
+
+
+def c5(side: int = 32768, K: int = 64) -> Workload:
+    """side^2 grid + 1 long-range link per node (small world); 64 messages."""
+    seed = BASE_SEED + 5
+    V = side * side
+    return Workload("C5", T.grid_links(side, seed), K, uniform_injections(V, K, seed), seed)
+
+
+def by_name(name: str, **kw) -> Workload:
+    return {"C2": c2, "C3": c3, "C4": c4, "C5": c5}[name.upper()](**kw)

@@ -114,6 +114,9 @@ int gg_partition_groups(gg_engine* e, int64_t round_from, int64_t round_to, cons
 /* Client broadcast of `message` to `node`, delivered in `round` (>= current
  * round). The first broadcast of a value assigns it the next free lane. */
 int gg_broadcast(gg_engine* e, uint32_t node, int64_t message, int64_t round);
+/* n client broadcasts at once (same rules, applied in array order). */
+int gg_broadcast_many(gg_engine* e, const uint32_t* nodes, const int64_t* messages,
+                      const int64_t* rounds, uint64_t n);
 int gg_lane_of(const gg_engine* e, int64_t message); /* lane or GG_EINVAL */
 
 /* Run n_rounds lockstep rounds; out[i] (may be NULL) receives round i's stats. */

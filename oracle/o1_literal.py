@@ -256,8 +256,9 @@ class O1Network:
                 if not snapshot.get(m, False):  # :98
                     self.rebroadcast_all_except(node, full_msg.src, m)  # :99
                 missing.append(m)  # :101 (every m, unconditionally)
+            in_resp = set(resp)  # :105 slices.Contains, as a set lookup (same answer)
             for m in sorted(snapshot):  # :104 (map order; all sends land in one round)
-                if m not in resp:  # :105 slices.Contains
+                if m not in in_resp:
                     self._send(node.nid, full_msg.src,
                                {"type": "broadcast", "message": m}, "push")  # :106
             for m in missing:  # :110-114

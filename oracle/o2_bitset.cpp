@@ -468,6 +468,16 @@ int gg_broadcast(gg_engine* e, uint32_t node, int64_t message, int64_t round) {
     return GG_OK;
 }
 
+int gg_broadcast_many(gg_engine* e, const uint32_t* nodes, const int64_t* messages,
+                      const int64_t* rounds, uint64_t n) {
+    if (!e || (n && (!nodes || !messages || !rounds))) return GG_EINVAL;
+    for (uint64_t k = 0; k < n; ++k) {
+        int rc = gg_broadcast(e, nodes[k], messages[k], rounds[k]);
+        if (rc) return rc;
+    }
+    return GG_OK;
+}
+
 int gg_lane_of(const gg_engine* e, int64_t message) {
     if (!e) return GG_EINVAL;
     auto it = e->lanes.find(message);

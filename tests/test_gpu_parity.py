@@ -1,0 +1,146 @@
+"""GPU parity: the HIP engine (libgossip_hip.so, via the C ABI) against the
+oracles on identical seeded inputs.
+
+Bit-exact on every round's counters (deliveries, forwards sent/delivered,
+pushes, acks, reads, read_oks, drops, sync firings, set hash), every node's
+read set and every (node, message) delivery round. Small cases are also
+compared with the message-level O1; 4K-node variants of C2..C5 and the full
+C2 config are compared with O2, plus size-independent properties (delivery
+round = hop distance, total deliveries = V*K on a connected graph).
+"""
+import random
+
+import numpy as np
+import pytest
+
+from ggamd import topology as T
+from ggamd.workload import uniform_injections
+from helpers import (Scenario, bfs_dist, c1_scenario, diff_stats, make_engine, make_o1,
+                     random_scenario)
+
+pytestmark = pytest.mark.gpu
+
+
+def _compare(sc, hip_lib, ref_lib, full=True):
+    g = make_engine(hip_lib, sc, track=full)
+    c = make_engine(ref_lib, sc, track=full)
+    sg = g.step(sc.rounds)
+    scpu = c.step(sc.rounds)
+    d = diff_stats(sg, scpu)
+    assert not d, d[:10]
+    assert np.array_equal(g.read_bits(), c.read_bits())
+    if full:
+        assert np.array_equal(g.delivery_rounds(), c.delivery_rounds())
+    return sg, g
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_small_vs_o2(hip_lib, cpu_lib, seed):
+    rnd = random.Random(7000 + seed)
+    for _ in range(10):
+        _compare(random_scenario(rnd), hip_lib, cpu_lib)
+
+
+@pytest.mark.parametrize("W", [64, 128, 192, 256, 512, 1024, 2048, 4096, 8192])
+def test_lane_widths(hip_lib, cpu_lib, W):
+    """Every (lanes-per-node, words-per-lane) kernel instantiation."""
+    rnd = random.Random(W)
+    for _ in range(3):
+        _compare(random_scenario(rnd, max_v=120, W=W, rounds=40), hip_lib, cpu_lib)
+
+
+def test_random_small_vs_o1(hip_lib):
+    rnd = random.Random(99)
+    for _ in range(6):
+        sc = random_scenario(rnd)
+        o1 = make_o1(sc)
+        g = make_engine(hip_lib, sc)
+        d = diff_stats(o1.step(sc.rounds), g.step(sc.rounds))
+        assert not d, d[:10]
+        for v in range(sc.topo.n_nodes):
+            assert o1.read(v) == g.read(v)
+
+
+@pytest.mark.parametrize("partition", [False, True])
+def test_c1_vs_o1(hip_lib, partition):
+    sc = c1_scenario(partition=partition)
+    o1 = make_o1(sc)
+    g = make_engine(hip_lib, sc)
+    d = diff_stats(o1.step(sc.rounds), g.step(sc.rounds))
+    assert not d, d[:10]
+    dr = g.delivery_rounds()
+    for v in range(25):
+        assert o1.read(v) == g.read(v)
+        assert o1.delivery_rounds(v) == dr[v].tolist()
+
+
+def _c_small(name):
+    V = 4096
+    if name == "C2":
+        topo, W, win = T.tree(V, 4), 1024, []
+    elif name == "C3":
+        topo, W, win = T.random_regular(V, 8, seed=3), 1024, [("seeded", 2, 12, 0x5EED)]
+    elif name == "C4":
+        topo, W, win = T.rmat(V, 16, seed=4), 4096, []
+    else:
+        topo, W, win = T.grid_links(64, seed=5), 64, []
+    inj = uniform_injections(V, W, seed={"C2": 2, "C3": 3, "C4": 4, "C5": 5}[name])
+    return Scenario(topo, W, 60, inj, seed=11, windows=win)
+
+
+@pytest.mark.parametrize("name", ["C2", "C3", "C4", "C5"])
+def test_config_4k_vs_o2(hip_lib, cpu_lib, name):
+    sg, _ = _compare(_c_small(name), hip_lib, cpu_lib)
+    assert sum(s["new_bits"] for s in sg) > 0
+
+
+def test_c2_full_vs_o2(hip_lib, cpu_lib):
+    """Config C2 at full size: 2^20-node tree4, 1024 messages in round 0."""
+    V, W = 1 << 20, 1024
+    topo = T.tree(V, 4)
+    inj = uniform_injections(V, W, seed=0x6A09E667F3BCC909 + 2)
+    sc = Scenario(topo, W, 26, inj, seed=0x6A09E667F3BCC909 + 2)
+    g = make_engine(hip_lib, sc, track=False)
+    c = make_engine(cpu_lib, sc, track=False)
+    sg, scpu = g.step(sc.rounds), c.step(sc.rounds)
+    d = diff_stats(sg, scpu)
+    assert not d, d[:10]
+    assert sum(s["new_bits"] for s in sg) == V * W  # connected: everyone gets everything
+    assert np.array_equal(g.read_bits(0, 4096), c.read_bits(0, 4096))
+    assert np.array_equal(g.read_bits(V - 4096, V), c.read_bits(V - 4096, V))
+
+
+def test_c2_delivery_round_is_hop_distance(hip_lib):
+    """KAT-1 at scale: with sync after propagation and no partitions, the round
+    message m reaches v is hop_dist(src_m, v) (size-independent property)."""
+    V, W = 1 << 16, 256
+    topo = T.tree(V, 4)
+    inj = uniform_injections(V, W, seed=77)
+    sc = Scenario(topo, W, 40, inj, seed=5)
+    g = make_engine(hip_lib, sc, track=True)
+    g.step(sc.rounds)
+    dr = g.delivery_rounds()
+    for k in (0, 1, 17, 100, 255):
+        src = inj[k][0]
+        assert np.array_equal(dr[:, g.lane_of(k)], bfs_dist(topo, src))
+
+
+def test_reset_repeatable(hip_lib):
+    rnd = random.Random(3)
+    sc = random_scenario(rnd, max_v=200, W=256, rounds=40)
+    g = make_engine(hip_lib, sc)
+    a = g.step(sc.rounds)
+    g.reset()
+    for n, v, r in sc.injections:
+        g.broadcast(n, v, r)
+    b = g.step(sc.rounds)
+    assert not diff_stats(a, b)
+
+
+def test_batched_steps_equal_single_steps(hip_lib):
+    rnd = random.Random(4)
+    sc = random_scenario(rnd, max_v=300, W=512, rounds=45)
+    a = make_engine(hip_lib, sc).step(sc.rounds)
+    e = make_engine(hip_lib, sc)
+    b = [e.step(1)[0] for _ in range(sc.rounds)]
+    assert not diff_stats(a, b)
