@@ -1,0 +1,88 @@
+"""Sharded (N > 1) path on CPU: world_size-2 gloo runs of the sharded round
+protocol (ggamd.dist.ShardedRunner over gg_dist_round_begin/end) against the
+same scenario on one unsharded engine. Counters summed over ranks, node sets
+and delivery rounds of every rank's range must equal the single-engine run.
+The engine here is the CPU oracle library; the GPU run of the same
+orchestration uses the HIP library with the nccl (RCCL) backend.
+"""
+import os
+import random
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from helpers import c1_scenario, diff_stats, make_engine, random_scenario
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, lib, sc, q):
+    import torch.distributed as dist
+
+    from ggamd.dist import ShardedRunner
+    os.environ["GG_CPU_THREADS"] = "2"
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        import torch
+        e = make_engine(lib, sc, rank=rank, world=world)
+        r = ShardedRunner(e, torch.device("cpu"))
+        stats = r.step(sc.rounds)
+        lo, hi = e.dist_range()
+        bits = e.read_bits(lo, hi)
+        dr = e.delivery_rounds(lo, hi)
+        q.put((rank, stats, lo, hi, bits, dr))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_dist(lib, sc, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, lib, sc, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(res, key=lambda x: x[0])
+
+
+def _check(lib, sc, world=2):
+    single = make_engine(lib, sc)
+    s1 = single.step(sc.rounds)
+    res = _run_dist(lib, sc, world)
+    for rank, stats, lo, hi, bits, dr in res:
+        d = diff_stats(s1, stats)
+        assert not d, (rank, d[:10])
+        assert np.array_equal(bits, single.read_bits(lo, hi))
+        assert np.array_equal(dr, single.delivery_rounds(lo, hi))
+    assert res[0][2] == 0 and res[-1][3] == sc.topo.n_nodes
+    assert all(res[k][3] == res[k + 1][2] for k in range(world - 1))
+
+
+def test_c1_two_ranks(cpu_lib):
+    _check(cpu_lib, c1_scenario(partition=True, rounds=120))
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_random_two_ranks(cpu_lib, seed):
+    rnd = random.Random(seed)
+    sc = random_scenario(rnd, max_v=300, W=128, rounds=50)
+    _check(cpu_lib, sc)
+
+
+def test_random_three_ranks(cpu_lib):
+    rnd = random.Random(11)
+    sc = random_scenario(rnd, max_v=200, W=64, rounds=45)
+    _check(cpu_lib, sc, world=3)
