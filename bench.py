@@ -32,12 +32,21 @@ METRIC = "(node,msg) deliveries/sec at 1/2/4/8 GPUs; % of HBM roofline; msgs/op"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def algorithmic_bytes_per_round(V: int, E: int, nwp: int) -> int:
-    """SURVEY.md §8d dense-pull bytes of one expand launch (no partitions):
-    row_ptr 8(V+1) + col 4E + gathered frontier rows E*w + seen_prev read,
-    seen_cur write, F_cur write 3*V*w, with w = bytes per node set."""
+def dense_bytes_per_round(V: int, E: int, nwp: int) -> int:
+    """SURVEY.md §8d dense-pull bytes of one round: row_ptr 8(V+1) + col 4E +
+    every sender row gathered E*w + read seen, write seen, write F 3*V*w."""
     w = 8 * nwp
     return 8 * (V + 1) + 4 * E + E * w + 3 * V * w
+
+
+def algorithmic_bytes(V: int, E: int, nwp: int, work_rows: int, work_gathers: int) -> int:
+    """Bytes the activity-skipping kernel must move in one round (§8d with the
+    frontier gathers replaced by the kernel-counted active-row gathers):
+    row_ptr 8(V+1), col 4E, flags read V + per-edge sender flags E, flags
+    write V, gathered active sender rows work_gathers*w, and for each node
+    that does work: read base, write base, write F (3w)."""
+    w = 8 * nwp
+    return 8 * (V + 1) + 4 * E + 2 * V + E + work_gathers * w + 3 * work_rows * w
 
 
 def next_pow2(x: int) -> int:
@@ -140,10 +149,13 @@ def main():
     lo, hi = eng.dist_range() if world > 1 else (0, V)
     E_own = int(topo.row_ptr[hi] - topo.row_ptr[lo])
     nwp = next_pow2(K // 64)
-    B = algorithmic_bytes_per_round(hi - lo, E_own, nwp)
-    ms_local = [s["kernel_ms"] for ep in local_stats for s in ep]
-    avg_ms = float(np.mean(ms_local))
-    achieved = B / (avg_ms * 1e-3) / 1e9
+    rounds_local = [s for ep in local_stats for s in ep]
+    B_tot = sum(algorithmic_bytes(hi - lo, E_own, nwp, s["work_rows"], s["work_gathers"])
+                for s in rounds_local)
+    ms_tot = sum(s["kernel_ms"] for s in rounds_local)
+    avg_ms = ms_tot / len(rounds_local)
+    B = B_tot / len(rounds_local)
+    achieved = B_tot / (ms_tot * 1e-3) / 1e9
 
     if rank == 0:
         value = deliveries / elapsed
@@ -179,6 +191,7 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None,
                 "algorithmic_bytes_per_launch": B,
+                "dense_bytes_per_launch": dense_bytes_per_round(hi - lo, E_own, nwp),
                 "avg_launch_ms": avg_ms,
             },
             "cpu_baseline": None,

@@ -7,9 +7,10 @@
 // per-round launch sequence of csrc/expand_kernels.hpp on one HIP stream.
 //
 // Device layout: node sets are rows of nwp u64 words (nwp =
-// W/64 rounded up to a power of two), node-major, in four ping-pong buffers
-// seen[2], F[2] (F = new bits of a round = what the node forwards next round);
-// fired[4] is a ring of per-round sync-timer bitmaps; CSR in-lists carry the
+// W/64 rounded up to a power of two), node-major: `base` (sets, updated in
+// place), F[2] (new bits of a round = what the node forwards next round) and
+// flags[2] (ACT: F row valid; LAG: set = base | F); fired[4] is a ring of
+// per-round sync-timer bitmaps; CSR in-lists carry the
 // sender's row with bit 31 set when the sender is also in the receiver's
 // out-list (forward exclusion, `:52`). In sharded mode every buffer is a
 // replica laid out [world][slice_rows], columns index replica rows, and the
@@ -51,6 +52,10 @@ uint32_t next_pow2(uint32_t x) {
     return p;
 }
 
+// Lanes per node group of the expand kernel for a row of nwp words
+// (two 8-byte words per lane; see launch_expand).
+uint32_t lanes_per_node(uint32_t nwp) { return nwp <= 2 ? 1u : nwp / 2; }
+
 }  // namespace
 
 struct gg_engine {
@@ -68,8 +73,12 @@ struct gg_engine {
     uint32_t* d_in_col = nullptr;
     int64_t* d_out_ptr = nullptr;
     uint32_t* d_out_col = nullptr;
-    uint64_t* d_seen[2] = {nullptr, nullptr};
+    uint64_t* d_base = nullptr;
     uint64_t* d_F[2] = {nullptr, nullptr};
+    uint8_t* d_flg[2] = {nullptr, nullptr};
+    uint8_t* d_cand = nullptr;       // [rows] candidate bytes
+    uint8_t* d_tile_cand = nullptr;  // [tile_bytes]
+    uint64_t tile_nodes = 0, tile_bytes = 0;
     uint64_t* d_fired[4] = {nullptr, nullptr, nullptr, nullptr};
     int32_t* d_sync_next = nullptr;
     uint32_t* d_sync_k = nullptr;
@@ -88,6 +97,7 @@ struct gg_engine {
     std::map<int64_t, std::vector<Injection>> inj;
     int64_t round = 0;
     unsigned long long pend_acks = 0, pend_ackdrop = 0;
+    unsigned long long hash_total = 0;
     bool dist_open = false;
 
     int fail(int code, const std::string& m) {
@@ -118,8 +128,11 @@ void gg_engine::free_topology() {
     dfree(d_out_ptr);
     dfree(d_in_ptr);
     dfree(d_in_col);
-    for (auto& p : d_seen) dfree(p);
+    dfree(d_base);
     for (auto& p : d_F) dfree(p);
+    for (auto& p : d_flg) dfree(p);
+    dfree(d_cand);
+    dfree(d_tile_cand);
     for (auto& p : d_fired) dfree(p);
     dfree(d_sync_next);
     dfree(d_sync_k);
@@ -147,11 +160,11 @@ namespace {
 
 int reset_device_state(gg_engine* e) {
     const size_t rowbytes = e->rows * e->nwp * 8;
-    for (int b = 0; b < 2; ++b) {
-        HIPCHK(hipMemsetAsync(e->d_seen[b], 0, rowbytes, e->stream));
-        HIPCHK(hipMemsetAsync(e->d_F[b], 0, rowbytes, e->stream));
-    }
+    HIPCHK(hipMemsetAsync(e->d_base, 0, rowbytes, e->stream));
+    for (int b = 0; b < 2; ++b) HIPCHK(hipMemsetAsync(e->d_flg[b], 0, e->rows, e->stream));  // F rows: read only where ACT
     for (int b = 0; b < 4; ++b) HIPCHK(hipMemsetAsync(e->d_fired[b], 0, e->rows / 8, e->stream));
+    HIPCHK(hipMemsetAsync(e->d_cand, 0, e->rows, e->stream));
+    HIPCHK(hipMemsetAsync(e->d_tile_cand, 0, e->tile_bytes, e->stream));
     const uint64_t n_own = e->hi - e->lo;
     if (n_own) {
         hipLaunchKernelGGL(gg::sync_init, dim3((unsigned)((n_own + 255) / 256)), dim3(256), 0, e->stream,
@@ -202,7 +215,7 @@ void launch_t(const gg::RoundArgs& a, bool syncw, bool maskw, hipStream_t s) {
         else hipLaunchKernelGGL((gg::expand_round<G, WPL, true, false>), grid, block, 0, s, a);
     } else {
         if (maskw) hipLaunchKernelGGL((gg::expand_round<G, WPL, false, true>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((gg::expand_round<G, WPL, false, false>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((gg::expand_round_lean<G, WPL>), grid, block, 0, s, a);
     }
 }
 
@@ -229,10 +242,15 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.in_col = e->d_in_col;
     a.out_ptr = e->d_out_ptr;
     a.out_col = e->d_out_col;
-    a.seen_prev = e->d_seen[(r + 1) & 1];
-    a.seen_cur = e->d_seen[r & 1];
+    a.base = e->d_base;
     a.F_prev = e->d_F[(r + 1) & 1];
     a.F_cur = e->d_F[r & 1];
+    a.flg_prev = e->d_flg[(r + 1) & 1];
+    a.flg_cur = e->d_flg[r & 1];
+    a.cand = e->d_cand;
+    a.tile_cand = e->d_tile_cand;
+    a.tile_nodes = (uint32_t)e->tile_nodes;
+    a.mark_all = e->world > 1;
     a.fired_m1 = e->d_fired[(r - 1) & 3];
     a.fired_m2 = e->d_fired[(r - 2) & 3];
     a.fired_m3 = e->d_fired[(r - 3) & 3];
@@ -257,17 +275,33 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.sync_base = e->cfg.sync_base_ticks;
     a.sync_jitter = e->cfg.sync_jitter_ticks;
     a.enable_sync = e->cfg.enable_sync;
-    const bool syncw = e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks + 1;
+    // timers fire from round sync_base on; their reads/callbacks/pushes follow
+    const bool syncw = e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks;
 
-    HIPCHK(hipMemsetAsync(a.fired_cur, 0, e->rows / 8, e->stream));
     HIPCHK(hipEventRecord(ev0, e->stream));
     if (a.n_own) {
+        {
+            const uint64_t blocks = std::min<uint64_t>((a.n_own + gg::kBlock - 1) / gg::kBlock, 4096);
+            dim3 grid((unsigned)blocks), block(gg::kBlock);
+            if (syncw) {
+                if (maskw) hipLaunchKernelGGL((gg::round_prep<true, true>), grid, block, 0, e->stream, a);
+                else hipLaunchKernelGGL((gg::round_prep<true, false>), grid, block, 0, e->stream, a);
+            } else {
+                if (maskw) hipLaunchKernelGGL((gg::round_prep<false, true>), grid, block, 0, e->stream, a);
+                else hipLaunchKernelGGL((gg::round_prep<false, false>), grid, block, 0, e->stream, a);
+            }
+            HIPCHK(hipGetLastError());
+        }
+        if (n_inj) {
+            hipLaunchKernelGGL(gg::mark_injections, dim3((n_inj + 255) / 256), dim3(256), 0, e->stream, a);
+            HIPCHK(hipGetLastError());
+        }
         launch_expand(a, syncw, maskw, e->stream);
         HIPCHK(hipGetLastError());
         if (e->d_dr) {
             const uint64_t n = a.n_own * e->nw;
             hipLaunchKernelGGL(gg::track_delivery, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream,
-                               a.F_cur, e->d_dr, a.n_own, a.own0, (uint32_t)e->nwp, (uint32_t)e->nw,
+                               a.F_cur, a.flg_cur, e->d_dr, a.n_own, a.own0, (uint32_t)e->nwp, (uint32_t)e->nw,
                                e->cfg.n_lanes, (int32_t)r);
             HIPCHK(hipGetLastError());
         }
@@ -292,8 +326,11 @@ void fold_stats(gg_engine* e, const unsigned long long* slots, float ms, gg_roun
     s->read_oks = c[gg::C_READ_OKS];
     s->dropped = c[gg::C_DROPPED] + e->pend_ackdrop;
     s->syncs_fired = c[gg::C_FIRED];
-    s->seen_hash = c[gg::C_HASH];
+    e->hash_total += c[gg::C_HASH];
+    s->seen_hash = e->hash_total;
     s->kernel_ms = ms;
+    s->work_rows = c[gg::C_ACTIVE];
+    s->work_gathers = c[gg::C_GATHERS];
     e->pend_acks = c[gg::C_NEXT_ACKS];
     e->pend_ackdrop = c[gg::C_NEXT_ACKDROP];
 }
@@ -482,9 +519,15 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
         if (!ocol.empty()) HIPCHK(hipMemcpy(e->d_out_col, ocol.data(), ocol.size() * 4, hipMemcpyHostToDevice));
     }
     const size_t rowbytes = e->rows * e->nwp * 8;
+    e->tile_nodes = gg::kBlock / lanes_per_node((uint32_t)e->nwp);
+    e->tile_bytes = ((n_own + e->tile_nodes - 1) / e->tile_nodes + gg::kTilesPerProbe) / gg::kTilesPerProbe *
+                    gg::kTilesPerProbe;
+    HIPCHK(hipMalloc(&e->d_cand, e->rows));
+    HIPCHK(hipMalloc(&e->d_tile_cand, e->tile_bytes));
+    HIPCHK(hipMalloc(&e->d_base, rowbytes));
     for (int b = 0; b < 2; ++b) {
-        HIPCHK(hipMalloc(&e->d_seen[b], rowbytes));
         HIPCHK(hipMalloc(&e->d_F[b], rowbytes));
+        HIPCHK(hipMalloc(&e->d_flg[b], e->rows));
     }
     for (int b = 0; b < 4; ++b) HIPCHK(hipMalloc(&e->d_fired[b], e->rows / 8));
     HIPCHK(hipMalloc(&e->d_sync_next, std::max<uint64_t>(1, n_own) * 4));
@@ -498,6 +541,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     e->inj.clear();
     e->round = 0;
     e->pend_acks = e->pend_ackdrop = 0;
+    e->hash_total = 0;
     e->dist_open = false;
     return reset_device_state(e);
 }
@@ -640,11 +684,13 @@ int gg_dist_round_begin(gg_engine* e, gg_exchange* x) {
     x->node_hi = e->hi;
     x->slice_rows = e->slice;
     x->frontier = e->d_F[r & 1];
-    x->seen = e->d_seen[r & 1];
+    x->seen = e->d_base;
     x->fired = e->d_fired[r & 3];
+    x->flags = e->d_flg[r & 1];
     x->frontier_bytes = e->slice * e->nwp * 8;
     x->seen_bytes = e->slice * e->nwp * 8;
     x->fired_bytes = e->slice / 8;
+    x->flags_bytes = e->slice;
     x->need_seen = (e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks) ? 1 : 0;
     e->dist_open = true;
     return GG_OK;
@@ -665,12 +711,24 @@ int gg_dist_round_end(gg_engine* e, gg_round_stats* out) {
 
 static bool owned(const gg_engine* e, uint64_t a, uint64_t b) { return a <= b && a >= e->lo && b <= e->hi; }
 
+// Node sets of owned nodes [a, b) after the last completed round:
+// base | F_last where the node's flag says LAG.
 static int copy_rows(gg_engine* e, uint64_t a, uint64_t b, std::vector<uint64_t>& h) {
     const uint64_t rep = (uint64_t)e->rank * e->slice + (a - e->lo);
-    h.resize((b - a) * e->nwp);
-    if (b > a) {
-        HIPCHK(hipStreamSynchronize(e->stream));
-        HIPCHK(hipMemcpy(h.data(), e->d_seen[(e->round + 1) & 1] + rep * e->nwp, h.size() * 8, hipMemcpyDeviceToHost));
+    const uint64_t n = b - a;
+    h.resize(n * e->nwp);
+    if (!n) return GG_OK;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipMemcpy(h.data(), e->d_base + rep * e->nwp, h.size() * 8, hipMemcpyDeviceToHost));
+    if (e->round == 0) return GG_OK;
+    const int last = (int)((e->round - 1) & 1);
+    std::vector<uint8_t> fl(n);
+    HIPCHK(hipMemcpy(fl.data(), e->d_flg[last] + rep, n, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> f(e->nwp);
+    for (uint64_t i = 0; i < n; ++i) {
+        if (!(fl[i] & gg::FL_LAG)) continue;
+        HIPCHK(hipMemcpy(f.data(), e->d_F[last] + (rep + i) * e->nwp, e->nwp * 8, hipMemcpyDeviceToHost));
+        for (uint64_t j = 0; j < e->nwp; ++j) h[i * e->nwp + j] |= f[j];
     }
     return GG_OK;
 }
@@ -730,6 +788,7 @@ int gg_reset(gg_engine* e) {
     e->inj.clear();
     e->round = 0;
     e->pend_acks = e->pend_ackdrop = 0;
+    e->hash_total = 0;
     e->dist_open = false;
     if (!e->have_topo) return GG_OK;
     HIPCHK(hipSetDevice(e->device));

@@ -1,24 +1,39 @@
 // expand_kernels.hpp — the per-round gossip kernels for gfx950 (CDNA4).
 //
-// One launch of `expand_round` executes one lockstep round for every owned
-// node: it is the device form of HandleBroadcast (`broadcast/broadcast.go:59-79`)
-// + rebroadcastAllExcept (`:50-57`) + the SyncBroadcast callback (`:82-117`) +
-// the sync timer (`broadcast/main.go:42-51`), in the determinized order of
-// DESIGN.md §2 (client broadcasts, node broadcasts by ascending sender, read_ok
-// callbacks by ascending peer, reads, timer).
+// One lockstep round is two launches:
+//   round_prep   — one thread per node: the sync timer (`broadcast/main.go:42-51`,
+//                  `SyncBroadcast` reads, `broadcast.go:119-121`), the read_oks
+//                  that answer last round's reads (`HandleRead`, `:124-132`), and
+//                  *candidate marking*: a node can change this round only if a
+//                  sender of its in-list was active (or pushed) last round, it has
+//                  a deferred fold (LAG), a sync callback, or a client broadcast;
+//                  active senders mark their out-lists (single-engine mode).
+//   expand_round — the device form of HandleBroadcast (`:59-79`) +
+//                  rebroadcastAllExcept (`:50-57`) + the SyncBroadcast callback
+//                  (`:82-117`) for every candidate node, in the determinized order
+//                  of DESIGN.md §2 (client broadcasts, node broadcasts by ascending
+//                  sender, read_ok callbacks by ascending peer).
 //
-// Work mapping: a node's set is nwp 64-bit words; a *node group*
-// of G lanes owns one node, lane l holding words [l*WPL, l*WPL+WPL) (16-byte
-// loads for WPL = 2), so one wave64 streams 64/G rows per instruction. Every
-// bitwise step (claim = src & ~S, S |= claim, callback new/push) is lane-local;
-// the sequential semantics (first deliverer claims, callbacks in peer order)
-// are a loop over the CSR list inside the group, so no cross-lane reduction is
-// needed on the hot path. Message counts are linear in per-lane popcounts and
-// are summed per lane, reduced once per block, and added into one of 64 counter
-// slots (64 x 16 u64) to keep atomic contention low.
+// State: `base` holds every node's set *in place*; F[r&1] holds
+// the bits a node learned in round r (what it forwards in r+1), valid only
+// where flags[r&1] has ACT. A node whose set is read by a sync peer in round r
+// (a read_ok payload or a push) keeps base = its round r-1 set and marks LAG;
+// then its true set is base | F. So every reader computes
+//     set(u) = base[u] | (LAG(u) ? F_prev[u] : 0)
+// and idle nodes move no row.
 //
-// Memory-bound, no MFMA: per round it streams row_ptr, col, seen_prev, the
-// gathered neighbour frontier rows, and writes seen_cur and F_cur.
+// Work mapping of expand_round: a block owns tiles of NG = 256/G consecutive
+// nodes, skipping tiles with no candidate (8 tile flags per probe). For a live
+// tile the CSR slice (row_ptr, col) and per-sender flags are staged in LDS with
+// coalesced loads; a *node group* of G lanes owns one node, lane l holding
+// words [l*WPL, l*WPL+WPL) of its set (16-byte accesses for WPL = 2). Pass 1
+// compacts the node's contributing senders in LDS; pass 2 gathers their rows 4
+// at a time and runs the claim chain (first deliverer, ascending sender) in
+// registers. Counters are linear in per-lane popcounts: summed per lane,
+// reduced once per block, added to one of 64 counter slots.
+//
+// Memory-bound, no MFMA: HBM traffic per round is the active senders' rows,
+// the changed nodes' base/F rows, and the CSR of candidate tiles.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -28,38 +43,59 @@
 
 namespace gg {
 
+// Occupancy target of the lean round kernel (no sync events, no partition
+// masks: the propagation phase): 5 waves/SIMD fits its registers unspilled.
+#ifndef GG_LEAN_WAVES_PER_EU
+#define GG_LEAN_WAVES_PER_EU 5
+#endif
+
 constexpr int kBlock = 256;
-constexpr int kSlots = 64;     // counter slots
-constexpr int kCounters = 16;  // per slot
+constexpr int kSlots = 64;       // counter slots
+constexpr int kCounters = 16;    // per slot
+constexpr int kEdgeStage = 2048; // in-edges staged in LDS per tile
+constexpr int kTilesPerProbe = 8;
 constexpr uint32_t kColMask = 0x7fffffffu;
 constexpr uint32_t kRecipBit = 0x80000000u;
 
+// node flags (flags[r&1][row])
+constexpr uint8_t FL_ACT = 1;  // F row of this round is valid and non-zero
+constexpr uint8_t FL_LAG = 2;  // base lacks this round's F (set = base | F)
+// staged per-sender flags
+constexpr uint8_t SE_ACT = 1, SE_LAG = 2, SE_FM2 = 8, SE_FM3 = 16;
+// candidate bytes
+constexpr uint8_t CA_NODE = 1, CA_INJ = 2;
+
 enum Counter : int {
     C_NEW = 0, C_FWD_SENT, C_FWD_DELIV, C_PUSH, C_PUSH_DELIV, C_READS, C_READ_OKS,
-    C_DROPPED, C_FIRED, C_HASH, C_NEXT_ACKS, C_NEXT_ACKDROP, C_NUM
+    C_DROPPED, C_FIRED, C_HASH, C_NEXT_ACKS, C_NEXT_ACKDROP, C_ACTIVE, C_GATHERS, C_NUM
 };
 
 struct RoundArgs {
-    const int64_t* in_ptr;     // [n_own+1]
-    const uint32_t* in_col;    // replica row of the sender | kRecipBit if sender in out(v)
-    const int64_t* out_ptr;    // [n_own+1]
-    const uint32_t* out_col;   // replica rows
-    const uint64_t* seen_prev; // [rows][nwp]
-    uint64_t* seen_cur;
-    const uint64_t* F_prev;
+    const int64_t* in_ptr;      // [n_own+1]
+    const uint32_t* in_col;     // replica row of the sender | kRecipBit if sender in out(v)
+    const int64_t* out_ptr;     // [n_own+1]
+    const uint32_t* out_col;    // replica rows (| kRecipBit when shared with in_col)
+    uint64_t* base;             // [rows][nwp] node sets, in place
+    const uint64_t* F_prev;     // [rows][nwp] new bits of round r-1 (valid where ACT)
     uint64_t* F_cur;
-    const uint64_t* fired_m1;  // fired bitmaps of rounds r-1, r-2, r-3 (replica rows)
+    const uint8_t* flg_prev;    // [rows] FL_* of round r-1
+    uint8_t* flg_cur;
+    uint8_t* cand;              // [rows] candidate bytes of this round (cleared by expand)
+    uint8_t* tile_cand;         // [n_tiles rounded to 8] tile has a candidate
+    const uint64_t* fired_m1;   // sync-fired bitmaps of rounds r-1, r-2, r-3
     const uint64_t* fired_m2;
     const uint64_t* fired_m3;
-    uint64_t* fired_cur;       // round r (cleared before launch)
-    int32_t* sync_next;        // [n_own]
+    uint64_t* fired_cur;        // round r (written whole by round_prep)
+    int32_t* sync_next;         // [n_own]
     uint32_t* sync_k;
-    const uint8_t* grp[5];     // partition groups of rounds r-3..r+1 (nullptr: no window)
-    const uint32_t* inj;       // (local node, lane) pairs sorted by node
+    const uint8_t* grp[5];      // partition groups of rounds r-3..r+1 (nullptr: no window)
+    const uint32_t* inj;        // (local node, lane) pairs sorted by node
     uint32_t n_inj;
     unsigned long long* counters;  // [kSlots][kCounters]
     uint64_t n_own, own0, lo;
     uint32_t nwp, nw;
+    uint32_t tile_nodes;        // NG of the expand kernel
+    int32_t mark_all;           // sharded engines: every owned node is a candidate
     int64_t round;
     uint64_t seed;
     uint32_t sync_base, sync_jitter;
@@ -99,7 +135,7 @@ __device__ __forceinline__ bool bit_at(const uint64_t* bm, uint64_t row) {
     return (bm[row >> 6] >> (row & 63)) & 1ull;
 }
 
-// message from replica row a to replica row b in round (r-3+k) dropped?
+// message from replica row ra to replica row rb in round (r-3+k) dropped?
 template <bool MASKW>
 __device__ __forceinline__ bool masked(const RoundArgs& a, int k, uint64_t ra, uint64_t rb) {
     if constexpr (!MASKW) {
@@ -110,208 +146,443 @@ __device__ __forceinline__ bool masked(const RoundArgs& a, int k, uint64_t ra, u
     }
 }
 
+template <bool SYNCW>
+__device__ __forceinline__ uint8_t sender_flags(const RoundArgs& a, uint64_t u) {
+    uint8_t f = a.flg_prev[u] & (FL_ACT | FL_LAG);
+    if constexpr (SYNCW) {
+        f |= (bit_at(a.fired_m2, u) ? SE_FM2 : 0) | (bit_at(a.fired_m3, u) ? SE_FM3 : 0);
+    }
+    return f;
+}
+
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
     return x;
 }
 
-// One round. G lanes per node, WPL words per lane; SYNCW: sync events possible
-// in r-3..r-1; MASKW: some partition window covers r-3..r+1.
-template <int G, int WPL, bool SYNCW, bool MASKW>
-__global__ __launch_bounds__(kBlock) void expand_round(RoundArgs a) {
-    constexpr int kGroups = kBlock / G;
-    constexpr int kUnroll = 4;
-    const int lg = threadIdx.x % G;
-    const uint64_t stride = (uint64_t)gridDim.x * kGroups;
-    unsigned long long acc[C_NUM];
-#pragma unroll
-    for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
-
-    for (uint64_t i = (uint64_t)blockIdx.x * kGroups + threadIdx.x / G; i < a.n_own; i += stride) {
-        const uint64_t rep = a.own0 + i;
-        const uint64_t off = (uint64_t)lg * WPL;
-        const Row<WPL> sp = load_row<WPL>(a.seen_prev + rep * a.nwp + off);
-        Row<WPL> S = sp;
-
-        // (1) client broadcasts of this round (HandleBroadcast from a client)
-        if (a.n_inj) {
-            uint32_t lo = 0, hi = a.n_inj;
-            while (lo < hi) {
-                uint32_t mid = (lo + hi) >> 1;
-                if (a.inj[2 * mid] < (uint32_t)i) lo = mid + 1;
-                else hi = mid;
-            }
-            for (uint32_t k = lo; k < a.n_inj && a.inj[2 * k] == (uint32_t)i; ++k) {
-                const uint32_t lane = a.inj[2 * k + 1];
-                const uint32_t word = lane >> 6;
-                if (word / WPL == (uint32_t)lg) S.w[word % WPL] |= 1ull << (lane & 63);
-            }
-        }
-
-        // (2) node broadcasts, ascending sender: first deliverer claims
-        unsigned long long cl_recip = 0, cl_deliv = 0, cl_ackdrop = 0, n_readok = 0, d_readok = 0;
-        const int64_t e0 = a.in_ptr[i], e1 = a.in_ptr[i + 1];
-        for (int64_t e = e0; e < e1; e += kUnroll) {
-            uint32_t c[kUnroll];
-            bool live[kUnroll];
-            Row<WPL> src[kUnroll];
-#pragma unroll
-            for (int k = 0; k < kUnroll; ++k) {
-                const bool valid = e + k < e1;
-                c[k] = valid ? a.in_col[e + k] : 0u;
-                const uint64_t u = c[k] & kColMask;
-                bool drop = masked<MASKW>(a, 2, u, rep);  // sent in r-1
-                bool push = false;
-                if constexpr (SYNCW) {
-                    if (valid && bit_at(a.fired_m1, u) && !drop) {  // u's read arrives now
-                        n_readok++;
-                        if (masked<MASKW>(a, 3, rep, u)) d_readok++;
-                    }
-                    push = bit_at(a.fired_m3, u) && !masked<MASKW>(a, 0, u, rep) &&
-                           !masked<MASKW>(a, 1, rep, u);
-                }
-                live[k] = valid && !drop;
-                const uint64_t* base = push ? a.seen_prev : a.F_prev;
-                if (live[k]) {
-                    src[k] = load_row<WPL>(base + u * a.nwp + off);
-                } else {
-#pragma unroll
-                    for (int w = 0; w < WPL; ++w) src[k].w[w] = 0;
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < kUnroll; ++k) {
-                unsigned long long pc = 0;
-#pragma unroll
-                for (int w = 0; w < WPL; ++w) {
-                    const uint64_t claim = src[k].w[w] & ~S.w[w];
-                    S.w[w] |= claim;
-                    pc += __popcll(claim);
-                }
-                if (live[k] && (c[k] & kRecipBit)) {
-                    cl_recip += pc;
-                    const uint64_t u = c[k] & kColMask;
-                    if (!masked<MASKW>(a, 3, rep, u)) {
-                        cl_deliv += pc;
-                        if (masked<MASKW>(a, 4, u, rep)) cl_ackdrop += pc;
-                    }
-                }
-            }
-        }
-
-        // (3) sync callback: v fired in r-2, read_oks of peers in ascending order
-        unsigned long long cb_new = 0, cb_new_deliv = 0, cb_new_ackdrop = 0;
-        unsigned long long push_sent = 0, push_deliv = 0, push_ackdrop = 0;
-        const int64_t o0 = a.out_ptr[i], o1 = a.out_ptr[i + 1];
-        if constexpr (SYNCW) {
-            if (bit_at(a.fired_m2, rep)) {
-                for (int64_t e = o0; e < o1; ++e) {
-                    const uint64_t w = a.out_col[e] & kColMask;
-                    if (masked<MASKW>(a, 1, rep, w) || masked<MASKW>(a, 2, w, rep)) continue;
-                    const Row<WPL> R = load_row<WPL>(a.seen_prev + w * a.nwp + off);
-                    unsigned long long pn = 0, pp = 0;
-#pragma unroll
-                    for (int k = 0; k < WPL; ++k) {
-                        pn += __popcll(R.w[k] & ~S.w[k]);
-                        pp += __popcll(S.w[k] & ~R.w[k]);
-                        S.w[k] |= R.w[k];
-                    }
-                    cb_new += pn;
-                    push_sent += pp;
-                    if (!masked<MASKW>(a, 3, rep, w)) {
-                        cb_new_deliv += pn;
-                        push_deliv += pp;
-                        if (masked<MASKW>(a, 4, w, rep)) {
-                            cb_new_ackdrop += pn;
-                            push_ackdrop += pp;
-                        }
-                    }
-                }
-            }
-        }
-
-        // new state
-        Row<WPL> F;
-        unsigned long long T = 0;
-        const uint64_t g = a.lo + i;
-#pragma unroll
-        for (int k = 0; k < WPL; ++k) {
-            F.w[k] = S.w[k] & ~sp.w[k];
-            T += __popcll(F.w[k]);
-            if (S.w[k]) acc[C_HASH] += gg_word_hash(g * a.nw + off + k, S.w[k]);
-        }
-        store_row<WPL>(a.seen_cur + rep * a.nwp + off, S);
-        store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
-
-        // messages v sends in round r (rebroadcastAllExcept :50-57, pushes :106)
-        const unsigned long long deg = (unsigned long long)(o1 - o0);
-        unsigned long long U = deg, AD = 0, mdrop = 0;
-        if constexpr (MASKW) {
-            if (a.grp[3] != nullptr || a.grp[4] != nullptr) {
-                U = 0;
-                for (int64_t e = o0; e < o1; ++e) {
-                    const uint64_t w = a.out_col[e] & kColMask;
-                    if (!masked<MASKW>(a, 3, rep, w)) {
-                        U++;
-                        if (masked<MASKW>(a, 4, w, rep)) AD++;
-                    } else {
-                        mdrop++;
-                    }
-                }
-            }
-        }
-        const unsigned long long fs = deg * T - cl_recip - cb_new;
-        const unsigned long long fd = U * T - cl_deliv - cb_new_deliv;
-        acc[C_NEW] += T;
-        acc[C_FWD_SENT] += fs;
-        acc[C_FWD_DELIV] += fd;
-        acc[C_PUSH] += push_sent;
-        acc[C_PUSH_DELIV] += push_deliv;
-        acc[C_DROPPED] += (fs - fd) + (push_sent - push_deliv);
-        acc[C_NEXT_ACKS] += fd + push_deliv;
-        acc[C_NEXT_ACKDROP] += AD * T - cl_ackdrop - cb_new_ackdrop + push_ackdrop;
-
-        if (lg == 0) {  // node-uniform events, counted once per node
-            acc[C_READ_OKS] += n_readok;
-            acc[C_DROPPED] += d_readok;
-            // (5) sync timer (main.go:42-51)
-            if (a.enable_sync && (int64_t)a.sync_next[i] == a.round) {
-                atomicOr((unsigned long long*)&a.fired_cur[rep >> 6], 1ull << (rep & 63));
-                acc[C_FIRED] += 1;
-                acc[C_READS] += deg;
-                acc[C_DROPPED] += mdrop;
-                const uint32_t k = a.sync_k[i] + 1;
-                a.sync_k[i] = k;
-                a.sync_next[i] = (int32_t)(a.round + gg_sync_interval(a.seed, g, k, a.sync_base,
-                                                                      a.sync_jitter));
-            }
-        }
+// Push edge: u's sync callback of round r-1 pushed to v (u fired in r-3, its
+// read reached v in r-3 and v's read_ok reached u in r-2), so v receives u's
+// whole round r-1 set.
+template <bool SYNCW, bool MASKW>
+__device__ __forceinline__ bool is_push(const RoundArgs& a, uint8_t ef, uint64_t u, uint64_t v) {
+    if constexpr (!SYNCW) {
+        return false;
+    } else {
+        return (ef & SE_FM3) && !masked<MASKW>(a, 0, u, v) && !masked<MASKW>(a, 1, v, u);
     }
+}
 
-    // block reduction -> one atomic per counter per block into slot blockIdx % 64
-    __shared__ unsigned long long red[kBlock / 64][C_NUM];
+// Block reduction of C_NUM per-thread counters -> one atomic per counter per
+// block into slot blockIdx % 64.
+__device__ __forceinline__ void flush_counters(const RoundArgs& a, unsigned long long (&acc)[C_NUM],
+                                               unsigned long long (*s_red)[C_NUM]) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
     for (int k = 0; k < C_NUM; ++k) {
         const unsigned long long s = wave_sum(acc[k]);
-        if (lane == 0) red[wave][k] = s;
+        if (lane == 0) s_red[wave][k] = s;
     }
     __syncthreads();
     if (threadIdx.x < C_NUM) {
         unsigned long long s = 0;
 #pragma unroll
-        for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
+        for (int w = 0; w < kBlock / 64; ++w) s += s_red[w][threadIdx.x];
         if (s) atomicAdd(&a.counters[(blockIdx.x % kSlots) * kCounters + threadIdx.x], s);
     }
 }
 
+// ---------------------------------------------------------------------------
+// round_prep: one thread per owned node (64 consecutive nodes per wave, so a
+// wave owns whole words of the fired bitmap).
+template <bool SYNCW, bool MASKW>
+__global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
+    __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
+    unsigned long long c_reads = 0, c_read_oks = 0, c_dropped = 0, c_fired = 0;
+    const uint64_t nwords = (a.n_own + 63) / 64;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < nwords * 64; t += stride) {
+        const uint64_t i = t;
+        const bool valid = i < a.n_own;
+        const uint64_t rep = a.own0 + i;
+        bool fire = false;
+        if (valid) {
+            const uint8_t f = a.flg_prev[rep];
+            a.flg_cur[rep] = 0;  // expand_round sets the flags of changed nodes
+            const int64_t o0 = a.out_ptr[i], o1 = a.out_ptr[i + 1];
+            bool fm1 = false, fm2 = false, fm3 = false;
+            if constexpr (SYNCW) {
+                fm1 = bit_at(a.fired_m1, rep);
+                fm2 = bit_at(a.fired_m2, rep);
+                fm3 = bit_at(a.fired_m3, rep);
+            }
+            // candidates of this round
+            if (a.mark_all || (f & FL_LAG) || fm2) {
+                a.cand[rep] = CA_NODE;
+                a.tile_cand[i / a.tile_nodes] = 1;
+            }
+            if (!a.mark_all && ((f & FL_ACT) || fm3)) {  // senders mark their receivers
+                for (int64_t e = o0; e < o1; ++e) {
+                    const uint64_t w = a.out_col[e] & kColMask;  // single engine: w == local row
+                    a.cand[w] = CA_NODE;
+                    a.tile_cand[(w - a.own0) / a.tile_nodes] = 1;
+                }
+            }
+            if constexpr (SYNCW) {
+                // reads v sent in r-1 arrive now; each answered by a read_ok (:131)
+                if (fm1) {
+                    for (int64_t e = o0; e < o1; ++e) {
+                        const uint64_t w = a.out_col[e] & kColMask;
+                        if (masked<MASKW>(a, 2, rep, w)) continue;
+                        c_read_oks++;
+                        if (masked<MASKW>(a, 3, w, rep)) c_dropped++;
+                    }
+                }
+                // (5) the sync timer (main.go:42-51): read RPC to every neighbour (:119-121)
+                if ((int64_t)a.sync_next[i] == a.round) {
+                    fire = true;
+                    c_fired++;
+                    c_reads += (unsigned long long)(o1 - o0);
+                    if constexpr (MASKW) {
+                        for (int64_t e = o0; e < o1; ++e)
+                            c_dropped += masked<MASKW>(a, 3, rep, a.out_col[e] & kColMask) ? 1 : 0;
+                    }
+                    const uint32_t kk = a.sync_k[i] + 1;
+                    a.sync_k[i] = kk;
+                    a.sync_next[i] = (int32_t)(a.round + gg_sync_interval(a.seed, a.lo + i, kk,
+                                                                          a.sync_base, a.sync_jitter));
+                }
+            }
+        }
+        const unsigned long long word = __ballot(fire);
+        if ((threadIdx.x & 63) == 0) a.fired_cur[(a.own0 + (i & ~63ull)) >> 6] = word;
+    }
+    unsigned long long acc[C_NUM];
+#pragma unroll
+    for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
+    acc[C_READS] = c_reads;
+    acc[C_READ_OKS] = c_read_oks;
+    acc[C_DROPPED] = c_dropped;
+    acc[C_FIRED] = c_fired;
+    flush_counters(a, acc, s_red);
+}
+
+// Client broadcasts of this round mark their nodes (after round_prep).
+__global__ void mark_injections(RoundArgs a) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.n_inj) return;
+    const uint64_t i = a.inj[2 * k];
+    a.cand[a.own0 + i] = CA_NODE | CA_INJ;
+    a.tile_cand[i / a.tile_nodes] = 1;
+}
+
+// ---------------------------------------------------------------------------
+// expand_round. G lanes per node, WPL words per lane; SYNCW: sync events
+// possible in r-3..r (timers fire from r >= sync_base); MASKW: some partition
+// window covers r-3..r+1.
+template <int G, int WPL, bool SYNCW, bool MASKW>
+__device__ __forceinline__ void expand_body(const RoundArgs& a) {
+    constexpr int NG = kBlock / G;  // nodes per tile
+    constexpr int kBatch = 4;
+    constexpr uint8_t L_PUSH = 1, L_LAG = 2;  // compacted-list flags
+    __shared__ int64_t s_ptr[NG + 1];
+    __shared__ uint32_t s_col[kEdgeStage];
+    __shared__ uint8_t s_ef[kEdgeStage];
+    __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
+
+    const int j = threadIdx.x / G;
+    const int lg = threadIdx.x % G;
+    const uint64_t off = (uint64_t)lg * WPL;
+    const int gshift = (threadIdx.x & 63) / G * G;
+    const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+    // always-live counters
+    unsigned long long c_new = 0, c_fwd = 0, c_hash = 0, c_active = 0, c_gathers = 0;
+    // MASKW-only
+    unsigned long long c_fwd_deliv = 0, c_push_deliv = 0, c_dropped = 0, c_next_ackdrop = 0;
+    // SYNCW-only
+    unsigned long long c_push = 0;
+
+    const uint64_t ntiles = (a.n_own + NG - 1) / NG;
+    const uint64_t nprobes = (ntiles + kTilesPerProbe - 1) / kTilesPerProbe;
+    for (uint64_t probe = blockIdx.x; probe < nprobes; probe += gridDim.x) {
+        unsigned long long tb = *reinterpret_cast<const unsigned long long*>(a.tile_cand + probe * kTilesPerProbe);
+        if (tb == 0) continue;  // block-uniform
+        for (int tt = 0; tt < kTilesPerProbe; ++tt, tb >>= 8) {
+            if ((tb & 0xff) == 0) continue;
+            const uint64_t t0 = (probe * kTilesPerProbe + tt) * NG;
+            // ---- stage the tile's CSR slice and sender flags (coalesced, shared)
+            for (int t = threadIdx.x; t <= NG; t += kBlock) {  // NG + 1 entries (NG may be kBlock)
+                const uint64_t idx = t0 + t < a.n_own ? t0 + t : a.n_own;
+                s_ptr[t] = a.in_ptr[idx];
+            }
+            __syncthreads();
+            const int64_t eb = s_ptr[0];
+            const int64_t ne = s_ptr[NG] - eb;
+            const int ns = ne < kEdgeStage ? (int)ne : kEdgeStage;
+            for (int k = threadIdx.x; k < ns; k += kBlock) {
+                const uint32_t c = a.in_col[eb + k];
+                s_col[k] = c;
+                s_ef[k] = sender_flags<SYNCW>(a, c & kColMask);
+            }
+            __syncthreads();
+
+            const uint64_t i = t0 + j;
+            const uint64_t rep = a.own0 + i;
+            const uint8_t ca = i < a.n_own ? a.cand[rep] : 0;
+            if (ca) {
+                const int64_t k0 = s_ptr[j] - eb, k1 = s_ptr[j + 1] - eb;
+                const bool staged = k1 <= ns;  // else: hub slow path straight from global
+                const uint8_t own = a.flg_prev[rep];
+                const bool lag = own & FL_LAG;
+                bool callback = false, keep = false;
+                if constexpr (SYNCW) {
+                    callback = bit_at(a.fired_m2, rep);
+                    keep = bit_at(a.fired_m3, rep);  // v pushed in r-1: its set is read now
+                }
+                // ---- pass 1: who reaches v this round (no row traffic); compact the
+                // contributing senders of a staged node in place in LDS.
+                int m = 0;
+                bool need = false;
+                for (int64_t k = k0; k < k1; ++k) {
+                    uint32_t c;
+                    uint8_t ef;
+                    if (staged) {
+                        c = s_col[k];
+                        ef = s_ef[k];
+                    } else {
+                        c = a.in_col[eb + k];
+                        ef = sender_flags<SYNCW>(a, c & kColMask);
+                    }
+                    const uint64_t u = c & kColMask;
+                    const bool drop = masked<MASKW>(a, 2, u, rep);  // sent in r-1
+                    if constexpr (SYNCW) keep |= (ef & SE_FM2) != 0;  // u's callback reads v now
+                    const bool p = !drop && is_push<SYNCW, MASKW>(a, ef, u, rep);
+                    if (!drop && ((ef & SE_ACT) || p)) {
+                        need = true;
+                        if (staged) {  // every lane of the group writes the same entry
+                            s_col[k0 + m] = c;
+                            s_ef[k0 + m] = (p ? L_PUSH : 0) | ((ef & SE_LAG) ? L_LAG : 0);
+                            ++m;
+                        }
+                    }
+                }
+                const bool has_inj = (ca & CA_INJ) != 0;
+                if (lg == 0) a.cand[rep] = 0;
+                if (need || lag || callback || has_inj) {
+                    const unsigned long long deg = (unsigned long long)(a.out_ptr[i + 1] - a.out_ptr[i]);
+                    // ---- pass 2: the round for node v
+                    Row<WPL> sp = load_row<WPL>(a.base + rep * a.nwp + off);
+                    if (lag) {
+                        const Row<WPL> f = load_row<WPL>(a.F_prev + rep * a.nwp + off);
+#pragma unroll
+                        for (int w = 0; w < WPL; ++w) sp.w[w] |= f.w[w];
+                    }
+                    Row<WPL> S = sp;
+                    // (1) client broadcasts of this round
+                    if (has_inj) {
+                        uint32_t lo = 0, hi = a.n_inj;
+                        while (lo < hi) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (a.inj[2 * mid] < (uint32_t)i) lo = mid + 1;
+                            else hi = mid;
+                        }
+                        for (uint32_t k = lo; k < a.n_inj && a.inj[2 * k] == (uint32_t)i; ++k) {
+                            const uint32_t lane = a.inj[2 * k + 1];
+                            const uint32_t word = lane >> 6;
+                            if (word / WPL == (uint32_t)lg) S.w[word % WPL] |= 1ull << (lane & 63);
+                        }
+                    }
+                    // (2) node broadcasts, ascending sender: first deliverer claims
+                    unsigned long long cl_recip = 0, cl_deliv = 0, cl_ackdrop = 0;
+                    auto claim = [&](const Row<WPL>& src, uint32_t c) {
+                        unsigned long long pc = 0;
+#pragma unroll
+                        for (int w = 0; w < WPL; ++w) {
+                            const uint64_t cw = src.w[w] & ~S.w[w];
+                            S.w[w] |= cw;
+                            pc += __popcll(cw);
+                        }
+                        if (c & kRecipBit) {
+                            cl_recip += pc;
+                            if constexpr (MASKW) {
+                                const uint64_t u = c & kColMask;
+                                if (!masked<MASKW>(a, 3, rep, u)) {
+                                    cl_deliv += pc;
+                                    if (masked<MASKW>(a, 4, u, rep)) cl_ackdrop += pc;
+                                }
+                            }
+                        }
+                    };
+                    auto sender_row = [&](uint32_t c, bool push, bool slag) {
+                        const uint64_t u = c & kColMask;
+                        if (SYNCW && push) {  // push edge: u's whole set of round r-1
+                            Row<WPL> r = load_row<WPL>(a.base + u * a.nwp + off);
+                            if (slag) {
+                                const Row<WPL> f = load_row<WPL>(a.F_prev + u * a.nwp + off);
+#pragma unroll
+                                for (int w = 0; w < WPL; ++w) r.w[w] |= f.w[w];
+                            }
+                            return r;
+                        }
+                        return load_row<WPL>(a.F_prev + u * a.nwp + off);
+                    };
+                    if (staged) {
+                        c_gathers += (lg == 0) ? (unsigned long long)m : 0ull;
+                        for (int b0 = 0; b0 < m; b0 += kBatch) {
+                            uint32_t cb[kBatch];
+                            Row<WPL> src[kBatch];
+#pragma unroll
+                            for (int b = 0; b < kBatch; ++b) {
+                                const bool v = b0 + b < m;
+                                cb[b] = v ? s_col[k0 + b0 + b] : 0u;
+                                const uint8_t lf = v ? s_ef[k0 + b0 + b] : 0;
+                                if (v) {
+                                    src[b] = sender_row(cb[b], lf & L_PUSH, lf & L_LAG);
+                                } else {
+#pragma unroll
+                                    for (int w = 0; w < WPL; ++w) src[b].w[w] = 0;
+                                }
+                            }
+#pragma unroll
+                            for (int b = 0; b < kBatch; ++b) claim(src[b], cb[b]);
+                        }
+                    } else {
+                        for (int64_t k = k0; k < k1; ++k) {  // hub slow path
+                            const uint32_t c = a.in_col[eb + k];
+                            const uint64_t u = c & kColMask;
+                            const uint8_t ef = sender_flags<SYNCW>(a, u);
+                            if (masked<MASKW>(a, 2, u, rep)) continue;
+                            const bool p = is_push<SYNCW, MASKW>(a, ef, u, rep);
+                            if (!(ef & SE_ACT) && !p) continue;
+                            c_gathers += (lg == 0) ? 1ull : 0ull;
+                            claim(sender_row(c, p, (ef & SE_LAG) != 0), c);
+                        }
+                    }
+                    // (3) sync callback: v fired in r-2, read_oks of peers in ascending order
+                    unsigned long long cb_new = 0, cb_new_deliv = 0, cb_new_ackdrop = 0;
+                    unsigned long long push_sent = 0, push_deliv = 0, push_ackdrop = 0;
+                    if constexpr (SYNCW) {
+                        if (callback) {
+                            const int64_t o0 = a.out_ptr[i], o1 = a.out_ptr[i + 1];
+                            for (int64_t e = o0; e < o1; ++e) {
+                                const uint64_t w = a.out_col[e] & kColMask;
+                                if (masked<MASKW>(a, 1, rep, w) || masked<MASKW>(a, 2, w, rep)) continue;
+                                const Row<WPL> R = sender_row((uint32_t)w, true, (a.flg_prev[w] & FL_LAG) != 0);
+                                unsigned long long pn = 0, pp = 0;
+#pragma unroll
+                                for (int q = 0; q < WPL; ++q) {
+                                    pn += __popcll(R.w[q] & ~S.w[q]);
+                                    pp += __popcll(S.w[q] & ~R.w[q]);
+                                    S.w[q] |= R.w[q];
+                                }
+                                cb_new += pn;
+                                push_sent += pp;
+                                if (!masked<MASKW>(a, 3, rep, w)) {
+                                    cb_new_deliv += pn;
+                                    push_deliv += pp;
+                                    if (masked<MASKW>(a, 4, w, rep)) {
+                                        cb_new_ackdrop += pn;
+                                        push_ackdrop += pp;
+                                    }
+                                }
+                            }
+                        }
+                    }
+                    // ---- new state
+                    Row<WPL> F;
+                    unsigned long long T = 0;
+                    const uint64_t g = a.lo + i;
+#pragma unroll
+                    for (int w = 0; w < WPL; ++w) {
+                        F.w[w] = S.w[w] & ~sp.w[w];
+                        T += __popcll(F.w[w]);
+                        if (F.w[w]) {  // seen_hash delta of a changed word
+                            const uint64_t idx = g * a.nw + off + w;
+                            c_hash += gg_word_hash(idx, S.w[w]) - (sp.w[w] ? gg_word_hash(idx, sp.w[w]) : 0ull);
+                        }
+                    }
+                    const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
+                    if (any) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
+                    if (keep) {
+                        if (lag) store_row<WPL>(a.base + rep * a.nwp + off, sp);
+                    } else if (any || lag) {
+                        store_row<WPL>(a.base + rep * a.nwp + off, S);
+                    }
+                    if (lg == 0 && any) a.flg_cur[rep] = (uint8_t)(FL_ACT | (keep ? FL_LAG : 0));
+
+                    // messages v sends in round r (rebroadcastAllExcept :50-57, pushes :106)
+                    const unsigned long long fs = deg * T - cl_recip - cb_new;
+                    c_new += T;
+                    c_fwd += fs;
+                    c_active += (lg == 0) ? 1ull : 0ull;
+                    if constexpr (SYNCW) c_push += push_sent;
+                    if constexpr (MASKW) {
+                        unsigned long long U = deg, AD = 0;
+                        if (a.grp[3] != nullptr || a.grp[4] != nullptr) {
+                            U = 0;
+                            for (int64_t e = a.out_ptr[i]; e < a.out_ptr[i + 1]; ++e) {
+                                const uint64_t w = a.out_col[e] & kColMask;
+                                if (!masked<MASKW>(a, 3, rep, w)) {
+                                    U++;
+                                    if (masked<MASKW>(a, 4, w, rep)) AD++;
+                                }
+                            }
+                        }
+                        const unsigned long long fd = U * T - cl_deliv - cb_new_deliv;
+                        c_fwd_deliv += fd;
+                        c_push_deliv += push_deliv;
+                        c_dropped += (fs - fd) + (push_sent - push_deliv);
+                        c_next_ackdrop += AD * T - cl_ackdrop - cb_new_ackdrop + push_ackdrop;
+                    }
+                }
+            }
+            __syncthreads();  // LDS reuse by the next tile
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            *reinterpret_cast<unsigned long long*>(a.tile_cand + probe * kTilesPerProbe) = 0ull;
+    }
+
+    // without partition masks nothing is dropped: delivered = sent
+    if constexpr (!MASKW) {
+        c_fwd_deliv = c_fwd;
+        c_push_deliv = c_push;
+    }
+    unsigned long long acc[C_NUM];
+#pragma unroll
+    for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
+    acc[C_NEW] = c_new;
+    acc[C_FWD_SENT] = c_fwd;
+    acc[C_FWD_DELIV] = c_fwd_deliv;
+    acc[C_PUSH] = c_push;
+    acc[C_PUSH_DELIV] = c_push_deliv;
+    acc[C_DROPPED] = c_dropped;
+    acc[C_HASH] = c_hash;
+    acc[C_NEXT_ACKS] = c_fwd_deliv + c_push_deliv;
+    acc[C_NEXT_ACKDROP] = c_next_ackdrop;
+    acc[C_ACTIVE] = c_active;
+    acc[C_GATHERS] = c_gathers;
+    flush_counters(a, acc, s_red);
+}
+
+template <int G, int WPL, bool SYNCW, bool MASKW>
+__global__ __launch_bounds__(kBlock) void expand_round(RoundArgs a) {
+    expand_body<G, WPL, SYNCW, MASKW>(a);
+}
+
+template <int G, int WPL>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GG_LEAN_WAVES_PER_EU)))
+void expand_round_lean(RoundArgs a) {
+    expand_body<G, WPL, false, false>(a);
+}
+
 // First-seen round of every new bit (GG_TRACK_DELIVERY only; observation).
-__global__ void track_delivery(const uint64_t* F_cur, int32_t* dr, uint64_t n_own, uint64_t own0,
-                               uint32_t nwp, uint32_t nw, uint32_t W, int32_t round) {
+__global__ void track_delivery(const uint64_t* F_cur, const uint8_t* flg_cur, int32_t* dr, uint64_t n_own,
+                               uint64_t own0, uint32_t nwp, uint32_t nw, uint32_t W, int32_t round) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_own * nw) return;
     const uint64_t i = t / nw, j = t % nw;
+    if (!(flg_cur[own0 + i] & FL_ACT)) return;
     uint64_t x = F_cur[(own0 + i) * nwp + j];
     while (x) {
         const int b = __builtin_ctzll(x);

@@ -64,6 +64,8 @@ class ShardedRunner:
         x = self.eng.dist_round_begin()
         self._gather(x.frontier, x.frontier_bytes)
         self._gather(x.fired, x.fired_bytes)
+        if x.flags_bytes:
+            self._gather(x.flags, x.flags_bytes)
         if x.need_seen:
             self._gather(x.seen, x.seen_bytes)
         if self.device.type == "cuda":
@@ -89,7 +91,8 @@ class ShardedRunner:
         tot = t.cpu().numpy().view(np.uint64)
         out = []
         for k, s in enumerate(local):
-            d = {"round": s["round"], "kernel_ms": float(ms[k])}
+            d = {"round": s["round"], "kernel_ms": float(ms[k]),
+                 "work_rows": s["work_rows"], "work_gathers": s["work_gathers"]}
             for j, f in enumerate(COUNT_FIELDS):
                 d[f] = int(tot[k, j]) & M64
             out.append(d)

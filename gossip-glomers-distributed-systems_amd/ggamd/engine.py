@@ -20,7 +20,7 @@ from dataclasses import dataclass
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HIP_LIB = os.path.join(PKG_DIR, "libgossip_hip.so")
+HIP_LIB = os.environ.get("GG_HIP_LIB") or os.path.join(PKG_DIR, "libgossip_hip.so")
 HOST_LIB = os.path.join(PKG_DIR, "libgossip_host.so")
 
 GG_TRACK_DELIVERY = 1
@@ -57,6 +57,8 @@ class GGRoundStats(C.Structure):
         ("syncs_fired", C.c_uint64),
         ("seen_hash", C.c_uint64),
         ("kernel_ms", C.c_double),
+        ("work_rows", C.c_uint64),
+        ("work_gathers", C.c_uint64),
     ]
 
 
@@ -68,15 +70,18 @@ class GGExchange(C.Structure):
         ("frontier", C.c_void_p),
         ("seen", C.c_void_p),
         ("fired", C.c_void_p),
+        ("flags", C.c_void_p),
         ("frontier_bytes", C.c_uint64),
         ("seen_bytes", C.c_uint64),
         ("fired_bytes", C.c_uint64),
+        ("flags_bytes", C.c_uint64),
         ("need_seen", C.c_int32),
     ]
 
 
 STAT_FIELDS = [f for f, _ in GGRoundStats._fields_]
-COUNT_FIELDS = [f for f in STAT_FIELDS if f not in ("round", "kernel_ms")]
+DIAG_FIELDS = ("round", "kernel_ms", "work_rows", "work_gathers")
+COUNT_FIELDS = [f for f in STAT_FIELDS if f not in DIAG_FIELDS]
 
 GG_SYMBOLS = [
     "gg_abi_version", "gg_create", "gg_destroy", "gg_last_error", "gg_topology",

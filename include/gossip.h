@@ -91,6 +91,8 @@ typedef struct {
     uint64_t syncs_fired;    /* sync timers that fired this round */
     uint64_t seen_hash;      /* order-free hash of every node's set */
     double kernel_ms;        /* device time of the round (0 for the CPU oracle) */
+    uint64_t work_rows;      /* diagnostics, engine-specific (not part of parity): */
+    uint64_t work_gathers;   /*   nodes that moved rows, sender rows gathered */
 } gg_round_stats;
 
 /* Inter-node messages of a round = fwd_sent + pushes + acks + reads + read_oks. */
@@ -147,9 +149,11 @@ typedef struct {
     void* frontier;            /* [world][slice_rows][W/64] u64 new-bit buffer */
     void* seen;                /* [world][slice_rows][W/64] u64 set buffer */
     void* fired;               /* [world][slice_rows/64] u64 sync-fired bitmap */
+    void* flags;               /* [world][slice_rows] u8 per-node row flags (may be NULL) */
     uint64_t frontier_bytes;   /* bytes per rank slice of each buffer */
     uint64_t seen_bytes;
     uint64_t fired_bytes;
+    uint64_t flags_bytes;      /* 0 when the engine has no flags buffer */
     int32_t need_seen;         /* 1 if this round's seen slices must be exchanged */
 } gg_exchange;
 

@@ -500,6 +500,8 @@ static void fill_stats(gg_engine* e, const Acc& a, gg_round_stats* s) {
     s->syncs_fired = a.fired;
     s->seen_hash = a.hash;
     s->kernel_ms = 0.0;
+    s->work_rows = 0;
+    s->work_gathers = 0;
 }
 
 int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
@@ -542,6 +544,8 @@ int gg_dist_round_begin(gg_engine* e, gg_exchange* x) {
     x->frontier_bytes = e->slice * e->nw * 8;
     x->seen_bytes = e->slice * e->nw * 8;
     x->fired_bytes = e->slice / 8;
+    x->flags = nullptr;
+    x->flags_bytes = 0;
     // remote seen_prev is read in round r+1 by callbacks (fired r-1) and push
     // edges (fired r-2); fires start at round >= sync_base.
     x->need_seen = (e->cfg.enable_sync && r + 1 >= (int64_t)e->cfg.sync_base_ticks + 1) ? 1 : 0;
