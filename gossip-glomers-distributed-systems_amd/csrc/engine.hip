@@ -56,6 +56,19 @@ uint32_t next_pow2(uint32_t x) {
 // (two 8-byte words per lane; see launch_expand).
 uint32_t lanes_per_node(uint32_t nwp) { return nwp <= 2 ? 1u : nwp / 2; }
 
+struct BatchKey {
+    int64_t r0 = -1;
+    uint32_t m = 0;
+    uint64_t inj_hash = 0;
+    size_t windows = 0;
+    const void* inj_buf = nullptr;
+    bool operator==(const BatchKey& o) const {
+        return r0 == o.r0 && m == o.m && inj_hash == o.inj_hash && windows == o.windows && inj_buf == o.inj_buf;
+    }
+};
+
+
+
 }  // namespace
 
 struct gg_engine {
@@ -99,6 +112,9 @@ struct gg_engine {
     unsigned long long pend_acks = 0, pend_ackdrop = 0;
     unsigned long long hash_total = 0;
     bool dist_open = false;
+    hipGraphExec_t graph_exec = nullptr;  // launch cache (run_batch)
+    BatchKey graph_key;
+    bool graph_broken = false;
 
     int fail(int code, const std::string& m) {
         err = m;
@@ -122,6 +138,8 @@ static void dfree(T*& p) {
 }
 
 void gg_engine::free_topology() {
+    if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
+    graph_exec = nullptr;
     if (d_out_col == d_in_col) d_out_col = nullptr;
     if (d_out_ptr == d_in_ptr) d_out_ptr = nullptr;
     dfree(d_out_col);
@@ -380,6 +398,57 @@ size_t pack_injections(gg_engine* e, int64_t r0, uint32_t n, std::vector<size_t>
     return tmp.size();
 }
 
+
+// ---- launch cache: a multi-round batch is captured once into a hipGraph and
+// replayed while (first round, length, injections, partition windows, buffers)
+// are unchanged — e.g. every episode after gg_reset in a benchmark loop. The
+// replayed kernels are exactly the captured launches; only host launch cost is
+// saved. GG_NO_GRAPH=1 disables it.
+template <class F>
+int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& off, size_t total, F&& enqueue) {
+    static const bool no_graph = getenv("GG_NO_GRAPH") != nullptr;
+    if (total) HIPCHK(hipMemcpyAsync(e->d_inj, e->h_inj, total * 8, hipMemcpyHostToDevice, e->stream));
+    if (no_graph || m < 4 || e->graph_broken) {
+        int rc = enqueue();
+        if (rc) return rc;
+        HIPCHK(hipStreamSynchronize(e->stream));
+        return GG_OK;
+    }
+    BatchKey key;
+    key.r0 = r0;
+    key.m = m;
+    key.windows = e->windows.size();
+    key.inj_buf = e->d_inj;
+    uint64_t h = gg_mix64(total);
+    for (size_t t = 0; t < 2 * total; ++t) h = gg_mix64(h ^ e->h_inj[t]);
+    for (size_t k = 0; k <= m; ++k) h = gg_mix64(h ^ off[k]);
+    key.inj_hash = h;
+    if (!(e->graph_exec && key == e->graph_key)) {
+        if (e->graph_exec) (void)hipGraphExecDestroy(e->graph_exec);
+        e->graph_exec = nullptr;
+        hipGraph_t g = nullptr;
+        if (hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+            e->graph_broken = true;
+            return run_batch(e, r0, m, off, 0, enqueue);
+        }
+        const int rc = enqueue();
+        const hipError_t ec = hipStreamEndCapture(e->stream, &g);
+        hipGraphExec_t ge = nullptr;
+        if (rc || ec != hipSuccess || !g || hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) != hipSuccess) {
+            if (g) (void)hipGraphDestroy(g);
+            (void)hipGetLastError();
+            e->graph_broken = true;  // fall back to direct launches for good
+            return run_batch(e, r0, m, off, 0, enqueue);
+        }
+        (void)hipGraphDestroy(g);
+        e->graph_exec = ge;
+        e->graph_key = key;
+    }
+    HIPCHK(hipGraphLaunch(e->graph_exec, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return GG_OK;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -626,17 +695,24 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
         const size_t total = pack_injections(e, r0, m, off);
         if (total == (size_t)-1) return GG_EIO;
         if (total) HIPCHK(hipMemcpyAsync(e->d_inj, e->h_inj, total * 8, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(hipMemsetAsync(e->d_counters, 0, (size_t)m * gg::kSlots * gg::kCounters * 8, e->stream));
-        for (uint32_t k = 0; k < m; ++k) {
-            const uint32_t ni = (uint32_t)(off[k + 1] - off[k]);
-            rc = enqueue_round(e, ni ? e->d_inj + 2 * off[k] : nullptr, ni,
-                               e->d_counters + (size_t)k * gg::kSlots * gg::kCounters, e->ev[2 * k],
-                               e->ev[2 * k + 1]);
-            if (rc) return rc;
-            e->round++;
-        }
-        HIPCHK(hipMemcpyAsync(e->h_counters, e->d_counters, (size_t)m * gg::kSlots * gg::kCounters * 8,
-                              hipMemcpyDeviceToHost, e->stream));
+        const int64_t save_round = e->round;
+        auto enqueue_batch = [&]() -> int {
+            HIPCHK(hipMemsetAsync(e->d_counters, 0, (size_t)m * gg::kSlots * gg::kCounters * 8, e->stream));
+            for (uint32_t k = 0; k < m; ++k) {
+                const uint32_t ni = (uint32_t)(off[k + 1] - off[k]);
+                e->round = r0 + k;
+                int rc2 = enqueue_round(e, ni ? e->d_inj + 2 * off[k] : nullptr, ni,
+                                        e->d_counters + (size_t)k * gg::kSlots * gg::kCounters, e->ev[2 * k],
+                                        e->ev[2 * k + 1]);
+                if (rc2) return rc2;
+            }
+            HIPCHK(hipMemcpyAsync(e->h_counters, e->d_counters, (size_t)m * gg::kSlots * gg::kCounters * 8,
+                                  hipMemcpyDeviceToHost, e->stream));
+            return GG_OK;
+        };
+        rc = run_batch(e, r0, m, off, total, enqueue_batch);
+        e->round = save_round + m;
+        if (rc) return rc;
         HIPCHK(hipStreamSynchronize(e->stream));
         for (uint32_t k = 0; k < m; ++k) {
             float ms = 0.f;

@@ -144,3 +144,27 @@ def test_batched_steps_equal_single_steps(hip_lib):
     e = make_engine(hip_lib, sc)
     b = [e.step(1)[0] for _ in range(sc.rounds)]
     assert not diff_stats(a, b)
+
+
+def test_launch_cache_replay_and_invalidation(hip_lib, cpu_lib):
+    """Episodes replayed from the captured launch sequence match fresh runs; a
+    changed injection set or partition window must not reuse the cache."""
+    rnd = random.Random(12)
+    sc = random_scenario(rnd, max_v=400, W=256, rounds=30)
+    g = make_engine(hip_lib, sc)
+    c = make_engine(cpu_lib, sc)
+    ref = c.step(sc.rounds)
+    assert not diff_stats(ref, g.step(sc.rounds))
+    for _ in range(2):  # replays
+        g.reset()
+        for n, v, r in sc.injections:
+            g.broadcast(n, v, r)
+        assert not diff_stats(ref, g.step(sc.rounds))
+    # different injections -> must recompute
+    g.reset()
+    c.reset()
+    inj2 = [(n, v + 7, r) for n, v, r in sc.injections[::2]]
+    for eng in (g, c):
+        for n, v, r in inj2:
+            eng.broadcast(n, v, r)
+    assert not diff_stats(c.step(sc.rounds), g.step(sc.rounds))
