@@ -119,13 +119,19 @@ def main():
         if R > 400:
             raise RuntimeError("no quiescence within 400 rounds")
 
+    event_ms = []
+
     def episode():
         eng.reset()
         inject(eng, inj)
-        return run_rounds(R)
+        st = run_rounds(R)
+        if runner is None:
+            event_ms.append(eng.step_device_ms())
+        return st
 
     for _ in range(max(0, args.warmup - 1)):
         episode()
+    event_ms.clear()
 
     barrier()
     t0 = time.perf_counter()
@@ -193,6 +199,11 @@ def main():
                 "algorithmic_bytes_per_launch": B,
                 "dense_bytes_per_launch": dense_bytes_per_round(hi - lo, E_own, nwp),
                 "avg_launch_ms": avg_ms,
+                "timing": "per round: device clock (s_memrealtime) from the first block start of "
+                          "round_prep to the last block end of expand_round; cross-check: HIP "
+                          "events around each step's launch sequence on the engine stream",
+                "event_ms_per_step": (sum(event_ms) / len(event_ms)) if event_ms else None,
+                "stamp_ms_per_step": ms_tot / args.steps,
             },
             "cpu_baseline": None,
         }

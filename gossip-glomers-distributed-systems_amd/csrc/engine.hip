@@ -113,6 +113,7 @@ struct gg_engine {
     unsigned long long hash_total = 0;
     bool dist_open = false;
     hipGraphExec_t graph_exec = nullptr;  // launch cache (run_batch)
+    double step_event_ms = 0.0;           // HIP-event time of the last gg_step (device)
     BatchKey graph_key;
     bool graph_broken = false;
 
@@ -252,8 +253,7 @@ void launch_expand(const gg::RoundArgs& a, bool syncw, bool maskw, hipStream_t s
 }
 
 // Enqueue round e->round (kernels only). inj: device pairs for this round.
-int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned long long* d_ctr,
-                  hipEvent_t ev0, hipEvent_t ev1) {
+int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned long long* d_ctr) {
     const int64_t r = e->round;
     gg::RoundArgs a{};
     a.in_ptr = e->d_in_ptr;
@@ -296,7 +296,6 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     // timers fire from round sync_base on; their reads/callbacks/pushes follow
     const bool syncw = e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks;
 
-    HIPCHK(hipEventRecord(ev0, e->stream));
     if (a.n_own) {
         {
             const uint64_t blocks = std::min<uint64_t>((a.n_own + gg::kBlock - 1) / gg::kBlock, 4096);
@@ -324,15 +323,21 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             HIPCHK(hipGetLastError());
         }
     }
-    HIPCHK(hipEventRecord(ev1, e->stream));
     return GG_OK;
 }
 
-// Host-side stats of one round from its 64 counter slots.
-void fold_stats(gg_engine* e, const unsigned long long* slots, float ms, gg_round_stats* s) {
+// Host-side stats of one round from its 64 counter slots; kernel_ms from the
+// device clock stamps (first block start .. last block end, 100 MHz).
+void fold_stats(gg_engine* e, const unsigned long long* slots, gg_round_stats* s) {
     unsigned long long c[gg::kCounters] = {0};
-    for (int k = 0; k < gg::kSlots; ++k)
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (int k = 0; k < gg::kSlots; ++k) {
         for (int j = 0; j < gg::C_NUM; ++j) c[j] += slots[k * gg::kCounters + j];
+        const unsigned long long si = slots[k * gg::kCounters + gg::C_TSTART_INV];
+        if (si) t0 = std::min(t0, ~si);
+        t1 = std::max(t1, slots[k * gg::kCounters + gg::C_TEND]);
+    }
+    const double ms = (t1 > t0 && t0 != ~0ull) ? (double)(t1 - t0) / 1.0e5 : 0.0;
     s->round = e->round;
     s->new_bits = c[gg::C_NEW];
     s->fwd_sent = c[gg::C_FWD_SENT];
@@ -409,9 +414,14 @@ int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& o
     static const bool no_graph = getenv("GG_NO_GRAPH") != nullptr;
     if (total) HIPCHK(hipMemcpyAsync(e->d_inj, e->h_inj, total * 8, hipMemcpyHostToDevice, e->stream));
     if (no_graph || m < 4 || e->graph_broken) {
+        HIPCHK(hipEventRecord(e->ev[0], e->stream));
         int rc = enqueue();
         if (rc) return rc;
+        HIPCHK(hipEventRecord(e->ev[1], e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
+        e->step_event_ms += ms;
         return GG_OK;
     }
     BatchKey key;
@@ -444,8 +454,13 @@ int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& o
         e->graph_exec = ge;
         e->graph_key = key;
     }
+    HIPCHK(hipEventRecord(e->ev[0], e->stream));
     HIPCHK(hipGraphLaunch(e->graph_exec, e->stream));
+    HIPCHK(hipEventRecord(e->ev[1], e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
+    e->step_event_ms += ms;
     return GG_OK;
 }
 
@@ -687,10 +702,11 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
     if (rc) return rc;
     uint32_t done = 0;
     std::vector<size_t> off;
+    e->step_event_ms = 0.0;
     while (done < n) {
         const uint32_t m = std::min<uint32_t>(kMaxBatch, n - done);
         const int64_t r0 = e->round;
-        if ((rc = ensure_events(e, 2 * (size_t)m))) return rc;
+        if ((rc = ensure_events(e, 2))) return rc;
         HIPCHK(hipStreamSynchronize(e->stream));  // h_inj reuse
         const size_t total = pack_injections(e, r0, m, off);
         if (total == (size_t)-1) return GG_EIO;
@@ -702,8 +718,7 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
                 const uint32_t ni = (uint32_t)(off[k + 1] - off[k]);
                 e->round = r0 + k;
                 int rc2 = enqueue_round(e, ni ? e->d_inj + 2 * off[k] : nullptr, ni,
-                                        e->d_counters + (size_t)k * gg::kSlots * gg::kCounters, e->ev[2 * k],
-                                        e->ev[2 * k + 1]);
+                                        e->d_counters + (size_t)k * gg::kSlots * gg::kCounters);
                 if (rc2) return rc2;
             }
             HIPCHK(hipMemcpyAsync(e->h_counters, e->d_counters, (size_t)m * gg::kSlots * gg::kCounters * 8,
@@ -715,18 +730,22 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
         if (rc) return rc;
         HIPCHK(hipStreamSynchronize(e->stream));
         for (uint32_t k = 0; k < m; ++k) {
-            float ms = 0.f;
-            HIPCHK(hipEventElapsedTime(&ms, e->ev[2 * k], e->ev[2 * k + 1]));
             gg_round_stats s;
             const int64_t save = e->round;
             e->round = r0 + k;
-            fold_stats(e, e->h_counters + (size_t)k * gg::kSlots * gg::kCounters, ms, &s);
+            fold_stats(e, e->h_counters + (size_t)k * gg::kSlots * gg::kCounters, &s);
             e->round = save;
             if (out) out[done + k] = s;
             e->inj.erase(r0 + k);
         }
         done += m;
     }
+    return GG_OK;
+}
+
+int gg_step_device_ms(const gg_engine* e, double* ms) {
+    if (!e || !ms) return GG_EINVAL;
+    *ms = e->step_event_ms;
     return GG_OK;
 }
 
@@ -750,7 +769,7 @@ int gg_dist_round_begin(gg_engine* e, gg_exchange* x) {
     if (total == (size_t)-1) return GG_EIO;
     if (total) HIPCHK(hipMemcpyAsync(e->d_inj, e->h_inj, total * 8, hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipMemsetAsync(e->d_counters, 0, (size_t)gg::kSlots * gg::kCounters * 8, e->stream));
-    rc = enqueue_round(e, total ? e->d_inj : nullptr, (uint32_t)total, e->d_counters, e->ev[0], e->ev[1]);
+    rc = enqueue_round(e, total ? e->d_inj : nullptr, (uint32_t)total, e->d_counters);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(e->h_counters, e->d_counters, (size_t)gg::kSlots * gg::kCounters * 8,
                           hipMemcpyDeviceToHost, e->stream));
@@ -774,10 +793,8 @@ int gg_dist_round_begin(gg_engine* e, gg_exchange* x) {
 
 int gg_dist_round_end(gg_engine* e, gg_round_stats* out) {
     if (!e || !e->dist_open) return GG_EINVAL;
-    float ms = 0.f;
-    HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
     gg_round_stats s;
-    fold_stats(e, e->h_counters, ms, &s);
+    fold_stats(e, e->h_counters, &s);
     if (out) *out = s;
     e->inj.erase(e->round);
     e->round++;

@@ -69,6 +69,12 @@ enum Counter : int {
     C_NEW = 0, C_FWD_SENT, C_FWD_DELIV, C_PUSH, C_PUSH_DELIV, C_READS, C_READ_OKS,
     C_DROPPED, C_FIRED, C_HASH, C_NEXT_ACKS, C_NEXT_ACKDROP, C_ACTIVE, C_GATHERS, C_NUM
 };
+// per-slot device clock stamps (s_memrealtime, 100 MHz): ~first block start
+// (stored complemented, so a max of zero-initialised slots gives the min) and
+// last block end of the round's kernels
+constexpr int C_TSTART_INV = 14, C_TEND = 15;
+
+__device__ __forceinline__ unsigned long long clock100() { return __builtin_amdgcn_s_memrealtime(); }
 
 struct RoundArgs {
     const int64_t* in_ptr;      // [n_own+1]
@@ -176,7 +182,7 @@ __device__ __forceinline__ bool is_push(const RoundArgs& a, uint8_t ef, uint64_t
 // Block reduction of C_NUM per-thread counters -> one atomic per counter per
 // block into slot blockIdx % 64.
 __device__ __forceinline__ void flush_counters(const RoundArgs& a, unsigned long long (&acc)[C_NUM],
-                                               unsigned long long (*s_red)[C_NUM]) {
+                                               unsigned long long (*s_red)[C_NUM], unsigned long long t_start) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
     for (int k = 0; k < C_NUM; ++k) {
@@ -190,6 +196,11 @@ __device__ __forceinline__ void flush_counters(const RoundArgs& a, unsigned long
         for (int w = 0; w < kBlock / 64; ++w) s += s_red[w][threadIdx.x];
         if (s) atomicAdd(&a.counters[(blockIdx.x % kSlots) * kCounters + threadIdx.x], s);
     }
+    if (threadIdx.x == 0) {
+        unsigned long long* slot = a.counters + (blockIdx.x % kSlots) * kCounters;
+        atomicMax(slot + C_TSTART_INV, ~t_start);
+        atomicMax(slot + C_TEND, clock100());
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -198,6 +209,7 @@ __device__ __forceinline__ void flush_counters(const RoundArgs& a, unsigned long
 template <bool SYNCW, bool MASKW>
 __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
     __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
+    const unsigned long long t_start = clock100();
     unsigned long long c_reads = 0, c_read_oks = 0, c_dropped = 0, c_fired = 0;
     const uint64_t nwords = (a.n_own + 63) / 64;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
@@ -264,7 +276,7 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
     acc[C_READ_OKS] = c_read_oks;
     acc[C_DROPPED] = c_dropped;
     acc[C_FIRED] = c_fired;
-    flush_counters(a, acc, s_red);
+    flush_counters(a, acc, s_red, t_start);
 }
 
 // Client broadcasts of this round mark their nodes (after round_prep).
@@ -295,6 +307,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
     const uint64_t off = (uint64_t)lg * WPL;
     const int gshift = (threadIdx.x & 63) / G * G;
     const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+    const unsigned long long t_start = clock100();
     // always-live counters
     unsigned long long c_new = 0, c_fwd = 0, c_hash = 0, c_active = 0, c_gathers = 0;
     // MASKW-only
@@ -562,7 +575,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
     acc[C_NEXT_ACKDROP] = c_next_ackdrop;
     acc[C_ACTIVE] = c_active;
     acc[C_GATHERS] = c_gathers;
-    flush_counters(a, acc, s_red);
+    flush_counters(a, acc, s_red, t_start);
 }
 
 template <int G, int WPL, bool SYNCW, bool MASKW>

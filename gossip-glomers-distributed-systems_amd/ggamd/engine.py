@@ -87,7 +87,7 @@ GG_SYMBOLS = [
     "gg_abi_version", "gg_create", "gg_destroy", "gg_last_error", "gg_topology",
     "gg_partition_seeded", "gg_partition_groups", "gg_broadcast", "gg_broadcast_many",
     "gg_lane_of", "gg_step",
-    "gg_current_round", "gg_read", "gg_read_bits", "gg_delivery_rounds", "gg_reset",
+    "gg_current_round", "gg_step_device_ms", "gg_read", "gg_read_bits", "gg_delivery_rounds", "gg_reset",
     "gg_dist_round_begin", "gg_dist_round_end", "gg_dist_range",
 ]
 
@@ -115,6 +115,7 @@ def load_library(path: str) -> C.CDLL:
     lib.gg_broadcast_many.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
     lib.gg_lane_of.argtypes = [C.c_void_p, C.c_int64]
     lib.gg_step.argtypes = [C.c_void_p, C.c_uint32, P(GGRoundStats)]
+    lib.gg_step_device_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
     lib.gg_current_round.argtypes = [C.c_void_p]
     lib.gg_current_round.restype = C.c_int64
     lib.gg_read.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, P(C.c_uint64)]
@@ -226,6 +227,12 @@ class Engine:
         arr = (GGRoundStats * max(1, n_rounds))()
         self._ok(self.lib.gg_step(self.h, n_rounds, arr))
         return [stats_dict(arr[i]) for i in range(n_rounds)]
+
+    def step_device_ms(self) -> float:
+        """HIP-event device time of the last step() call (whole launch sequence)."""
+        x = C.c_double(0.0)
+        self._ok(self.lib.gg_step_device_ms(self.h, C.byref(x)))
+        return x.value
 
     @property
     def round(self) -> int:

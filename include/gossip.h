@@ -124,6 +124,9 @@ int gg_lane_of(const gg_engine* e, int64_t message); /* lane or GG_EINVAL */
 /* Run n_rounds lockstep rounds; out[i] (may be NULL) receives round i's stats. */
 int gg_step(gg_engine* e, uint32_t n_rounds, gg_round_stats* out);
 int64_t gg_current_round(const gg_engine* e);
+/* Device time of the last gg_step measured with HIP events on the engine's
+ * stream around the whole launch sequence (0 for the CPU oracle). */
+int gg_step_device_ms(const gg_engine* e, double* ms);
 
 /* HandleRead: the values node holds, ascending. n_out = count (even if > cap). */
 int gg_read(gg_engine* e, uint32_t node, int64_t* out, uint64_t cap, uint64_t* n_out);

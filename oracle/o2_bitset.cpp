@@ -521,6 +521,12 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
     return GG_OK;
 }
 
+int gg_step_device_ms(const gg_engine* e, double* ms) {
+    if (!e || !ms) return GG_EINVAL;
+    *ms = 0.0;  // no device
+    return GG_OK;
+}
+
 int gg_dist_range(const gg_engine* e, uint64_t* lo, uint64_t* hi) {
     if (!e || !e->have_topo) return GG_EINVAL;
     if (lo) *lo = e->lo;
