@@ -91,6 +91,8 @@ struct gg_engine {
     uint8_t* d_flg[2] = {nullptr, nullptr};
     uint8_t* d_cand = nullptr;       // [rows] candidate bytes
     uint8_t* d_tile_cand = nullptr;  // [tile_bytes]
+    gg::TileWork* d_work = nullptr;  // [tiles] live-tile worklist
+    uint32_t* d_n_work = nullptr;
     uint64_t tile_nodes = 0, tile_bytes = 0;
     uint64_t* d_fired[4] = {nullptr, nullptr, nullptr, nullptr};
     int32_t* d_sync_next = nullptr;
@@ -152,6 +154,8 @@ void gg_engine::free_topology() {
     for (auto& p : d_flg) dfree(p);
     dfree(d_cand);
     dfree(d_tile_cand);
+    dfree(d_work);
+    dfree(d_n_work);
     for (auto& p : d_fired) dfree(p);
     dfree(d_sync_next);
     dfree(d_sync_k);
@@ -267,6 +271,8 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.flg_cur = e->d_flg[r & 1];
     a.cand = e->d_cand;
     a.tile_cand = e->d_tile_cand;
+    a.work = e->d_work;
+    a.n_work = e->d_n_work;
     a.tile_nodes = (uint32_t)e->tile_nodes;
     a.mark_all = e->world > 1;
     a.fired_m1 = e->d_fired[(r - 1) & 3];
@@ -311,6 +317,13 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         }
         if (n_inj) {
             hipLaunchKernelGGL(gg::mark_injections, dim3((n_inj + 255) / 256), dim3(256), 0, e->stream, a);
+            HIPCHK(hipGetLastError());
+        }
+        {
+            const uint64_t ntiles = (a.n_own + e->tile_nodes - 1) / e->tile_nodes;
+            const uint64_t groups = (ntiles + 7) / 8;
+            hipLaunchKernelGGL(gg::compact_tiles, dim3((unsigned)((groups + gg::kBlock - 1) / gg::kBlock)),
+                               dim3(gg::kBlock), 0, e->stream, a);
             HIPCHK(hipGetLastError());
         }
         launch_expand(a, syncw, maskw, e->stream);
@@ -604,10 +617,12 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     }
     const size_t rowbytes = e->rows * e->nwp * 8;
     e->tile_nodes = gg::kBlock / lanes_per_node((uint32_t)e->nwp);
-    e->tile_bytes = ((n_own + e->tile_nodes - 1) / e->tile_nodes + gg::kTilesPerProbe) / gg::kTilesPerProbe *
-                    gg::kTilesPerProbe;
+    const uint64_t ntiles = (n_own + e->tile_nodes - 1) / e->tile_nodes;
+    e->tile_bytes = (ntiles + 8) / 8 * 8;
     HIPCHK(hipMalloc(&e->d_cand, e->rows));
     HIPCHK(hipMalloc(&e->d_tile_cand, e->tile_bytes));
+    HIPCHK(hipMalloc(&e->d_work, std::max<uint64_t>(1, ntiles) * sizeof(gg::TileWork)));
+    HIPCHK(hipMalloc(&e->d_n_work, 4));
     HIPCHK(hipMalloc(&e->d_base, rowbytes));
     for (int b = 0; b < 2; ++b) {
         HIPCHK(hipMalloc(&e->d_F[b], rowbytes));

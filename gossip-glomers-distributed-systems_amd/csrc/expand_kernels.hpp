@@ -22,10 +22,12 @@
 //     set(u) = base[u] | (LAG(u) ? F_prev[u] : 0)
 // and idle nodes move no row.
 //
-// Work mapping of expand_round: a block owns tiles of NG = 256/G consecutive
-// nodes, skipping tiles with no candidate (8 tile flags per probe). For a live
-// tile the CSR slice (row_ptr, col) and per-sender flags are staged in LDS with
-// coalesced loads; a *node group* of G lanes owns one node, lane l holding
+// Work mapping of expand_round: the live tiles (NG = 256/G consecutive nodes
+// with at least one candidate) are compacted into a worklist (compact_tiles)
+// and dealt round-robin to blocks. For a live tile the CSR slice (row_ptr, col)
+// is staged in LDS with coalesced loads in one round trip (the worklist entry
+// carries the tile's edge range), plus per-sender flags unless the round is
+// dense and lean (then flags and rows are gathered together); a *node group* of G lanes owns one node, lane l holding
 // words [l*WPL, l*WPL+WPL) of its set (16-byte accesses for WPL = 2). Pass 1
 // compacts the node's contributing senders in LDS; pass 2 gathers their rows 4
 // at a time and runs the claim chain (first deliverer, ascending sender) in
@@ -49,11 +51,15 @@ namespace gg {
 #define GG_LEAN_WAVES_PER_EU 5
 #endif
 
+// Sender (flag, row) pairs a lane keeps in flight in dense lean rounds.
+#ifndef GG_SPEC_BATCH
+#define GG_SPEC_BATCH 4
+#endif
+
 constexpr int kBlock = 256;
 constexpr int kSlots = 64;       // counter slots
 constexpr int kCounters = 16;    // per slot
 constexpr int kEdgeStage = 2048; // in-edges staged in LDS per tile
-constexpr int kTilesPerProbe = 8;
 constexpr uint32_t kColMask = 0x7fffffffu;
 constexpr uint32_t kRecipBit = 0x80000000u;
 
@@ -76,6 +82,12 @@ constexpr int C_TSTART_INV = 14, C_TEND = 15;
 
 __device__ __forceinline__ unsigned long long clock100() { return __builtin_amdgcn_s_memrealtime(); }
 
+struct TileWork {
+    uint32_t tile;   // tile index (nodes tile*NG ..)
+    uint32_t ne;     // in-edges of the tile
+    int64_t eb;      // in_ptr of the tile's first node
+};
+
 struct RoundArgs {
     const int64_t* in_ptr;      // [n_own+1]
     const uint32_t* in_col;     // replica row of the sender | kRecipBit if sender in out(v)
@@ -88,6 +100,8 @@ struct RoundArgs {
     uint8_t* flg_cur;
     uint8_t* cand;              // [rows] candidate bytes of this round (cleared by expand)
     uint8_t* tile_cand;         // [n_tiles rounded to 8] tile has a candidate
+    struct TileWork* work;      // live tiles of the round (compact_tiles)
+    uint32_t* n_work;           // number of live tiles
     const uint64_t* fired_m1;   // sync-fired bitmaps of rounds r-1, r-2, r-3
     const uint64_t* fired_m2;
     const uint64_t* fired_m3;
@@ -213,6 +227,7 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
     unsigned long long c_reads = 0, c_read_oks = 0, c_dropped = 0, c_fired = 0;
     const uint64_t nwords = (a.n_own + 63) / 64;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.n_work = 0;  // compact_tiles runs after this kernel
     for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < nwords * 64; t += stride) {
         const uint64_t i = t;
         const bool valid = i < a.n_own;
@@ -288,6 +303,54 @@ __global__ void mark_injections(RoundArgs a) {
     a.tile_cand[i / a.tile_nodes] = 1;
 }
 
+// Live tiles -> worklist (order irrelevant: tiles are independent and counters
+// are sums). 8 tile flags per thread; clears the flags for the next round.
+__global__ __launch_bounds__(kBlock) void compact_tiles(RoundArgs a) {
+    __shared__ uint32_t s_cnt[kBlock / 64];
+    __shared__ uint32_t s_base;
+    const uint64_t ntiles = (a.n_own + a.tile_nodes - 1) / a.tile_nodes;
+    const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;  // 8-tile group
+    unsigned long long tb = 0;
+    if (q * 8 < ntiles) {
+        tb = *reinterpret_cast<const unsigned long long*>(a.tile_cand + q * 8);
+        if (tb) *reinterpret_cast<unsigned long long*>(a.tile_cand + q * 8) = 0ull;
+    }
+    uint32_t c = 0;
+    for (int t = 0; t < 8; ++t) c += ((tb >> (8 * t)) & 0xff) ? 1u : 0u;
+    // block exclusive scan of c
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_cnt[wave] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            const uint32_t x = s_cnt[w];
+            s_cnt[w] = tot;
+            tot += x;
+        }
+        s_base = tot ? atomicAdd(a.n_work, tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t pos = s_base + s_cnt[wave] + incl - c;
+    for (int t = 0; t < 8; ++t) {
+        if (!((tb >> (8 * t)) & 0xff)) continue;
+        const uint64_t tile = q * 8 + t;
+        const uint64_t n0 = tile * a.tile_nodes;
+        const uint64_t n1 = n0 + a.tile_nodes < a.n_own ? n0 + a.tile_nodes : a.n_own;
+        TileWork w;
+        w.tile = (uint32_t)tile;
+        w.eb = a.in_ptr[n0];
+        w.ne = (uint32_t)(a.in_ptr[n1] - w.eb);
+        a.work[pos++] = w;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // expand_round. G lanes per node, WPL words per lane; SYNCW: sync events
 // possible in r-3..r (timers fire from r >= sync_base); MASKW: some partition
@@ -295,11 +358,15 @@ __global__ void mark_injections(RoundArgs a) {
 template <int G, int WPL, bool SYNCW, bool MASKW>
 __device__ __forceinline__ void expand_body(const RoundArgs& a) {
     constexpr int NG = kBlock / G;  // nodes per tile
-    constexpr int kBatch = 4;
+    constexpr int kBatch = 4;       // flags-first: contributing rows in flight per lane
+    constexpr int kSpec = GG_SPEC_BATCH;  // dense lean rounds: (flag, row) pairs in flight per lane
+    constexpr int kPre = 64;        // worklist entries preloaded per chunk
+    constexpr bool LEAN = !SYNCW && !MASKW;
     constexpr uint8_t L_PUSH = 1, L_LAG = 2;  // compacted-list flags
     __shared__ int64_t s_ptr[NG + 1];
     __shared__ uint32_t s_col[kEdgeStage];
     __shared__ uint8_t s_ef[kEdgeStage];
+    __shared__ TileWork s_work[kPre];
     __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
 
     const int j = threadIdx.x / G;
@@ -315,27 +382,33 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
     // SYNCW-only
     unsigned long long c_push = 0;
 
+    const uint64_t n_work = *a.n_work;
     const uint64_t ntiles = (a.n_own + NG - 1) / NG;
-    const uint64_t nprobes = (ntiles + kTilesPerProbe - 1) / kTilesPerProbe;
-    for (uint64_t probe = blockIdx.x; probe < nprobes; probe += gridDim.x) {
-        unsigned long long tb = *reinterpret_cast<const unsigned long long*>(a.tile_cand + probe * kTilesPerProbe);
-        if (tb == 0) continue;  // block-uniform
-        for (int tt = 0; tt < kTilesPerProbe; ++tt, tb >>= 8) {
-            if ((tb & 0xff) == 0) continue;
-            const uint64_t t0 = (probe * kTilesPerProbe + tt) * NG;
-            // ---- stage the tile's CSR slice and sender flags (coalesced, shared)
+    // most tiles live: load sender flags together with their rows (speculative
+    // gathers; a row of an inactive sender is ignored) instead of flags first
+    const bool dense = LEAN && n_work * 2 > ntiles;
+
+    for (uint64_t base = blockIdx.x; base < n_work; base += (uint64_t)kPre * gridDim.x) {
+        if (threadIdx.x < kPre) {
+            const uint64_t idx = base + (uint64_t)threadIdx.x * gridDim.x;
+            if (idx < n_work) s_work[threadIdx.x] = a.work[idx];
+        }
+        __syncthreads();
+        for (int q = 0; q < kPre; ++q) {
+            if (base + (uint64_t)q * gridDim.x >= n_work) break;  // block-uniform
+            const TileWork tw = s_work[q];
+            const uint64_t t0 = (uint64_t)tw.tile * NG;
+            const int64_t eb = tw.eb;
+            const int ns = tw.ne < (uint32_t)kEdgeStage ? (int)tw.ne : kEdgeStage;
+            // ---- stage the tile's row_ptr and col slices (one round trip)
             for (int t = threadIdx.x; t <= NG; t += kBlock) {  // NG + 1 entries (NG may be kBlock)
                 const uint64_t idx = t0 + t < a.n_own ? t0 + t : a.n_own;
                 s_ptr[t] = a.in_ptr[idx];
             }
-            __syncthreads();
-            const int64_t eb = s_ptr[0];
-            const int64_t ne = s_ptr[NG] - eb;
-            const int ns = ne < kEdgeStage ? (int)ne : kEdgeStage;
             for (int k = threadIdx.x; k < ns; k += kBlock) {
                 const uint32_t c = a.in_col[eb + k];
                 s_col[k] = c;
-                s_ef[k] = sender_flags<SYNCW>(a, c & kColMask);
+                if (!dense) s_ef[k] = sender_flags<SYNCW>(a, c & kColMask);
             }
             __syncthreads();
 
@@ -343,54 +416,29 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
             const uint64_t rep = a.own0 + i;
             const uint8_t ca = i < a.n_own ? a.cand[rep] : 0;
             if (ca) {
+                if (lg == 0) a.cand[rep] = 0;
                 const int64_t k0 = s_ptr[j] - eb, k1 = s_ptr[j + 1] - eb;
                 const bool staged = k1 <= ns;  // else: hub slow path straight from global
                 const uint8_t own = a.flg_prev[rep];
                 const bool lag = own & FL_LAG;
+                const bool has_inj = (ca & CA_INJ) != 0;
                 bool callback = false, keep = false;
                 if constexpr (SYNCW) {
                     callback = bit_at(a.fired_m2, rep);
                     keep = bit_at(a.fired_m3, rep);  // v pushed in r-1: its set is read now
                 }
-                // ---- pass 1: who reaches v this round (no row traffic); compact the
-                // contributing senders of a staged node in place in LDS.
-                int m = 0;
-                bool need = false;
-                for (int64_t k = k0; k < k1; ++k) {
-                    uint32_t c;
-                    uint8_t ef;
-                    if (staged) {
-                        c = s_col[k];
-                        ef = s_ef[k];
-                    } else {
-                        c = a.in_col[eb + k];
-                        ef = sender_flags<SYNCW>(a, c & kColMask);
-                    }
-                    const uint64_t u = c & kColMask;
-                    const bool drop = masked<MASKW>(a, 2, u, rep);  // sent in r-1
-                    if constexpr (SYNCW) keep |= (ef & SE_FM2) != 0;  // u's callback reads v now
-                    const bool p = !drop && is_push<SYNCW, MASKW>(a, ef, u, rep);
-                    if (!drop && ((ef & SE_ACT) || p)) {
-                        need = true;
-                        if (staged) {  // every lane of the group writes the same entry
-                            s_col[k0 + m] = c;
-                            s_ef[k0 + m] = (p ? L_PUSH : 0) | ((ef & SE_LAG) ? L_LAG : 0);
-                            ++m;
-                        }
-                    }
-                }
-                const bool has_inj = (ca & CA_INJ) != 0;
-                if (lg == 0) a.cand[rep] = 0;
-                if (need || lag || callback || has_inj) {
-                    const unsigned long long deg = (unsigned long long)(a.out_ptr[i + 1] - a.out_ptr[i]);
-                    // ---- pass 2: the round for node v
-                    Row<WPL> sp = load_row<WPL>(a.base + rep * a.nwp + off);
+                Row<WPL> sp, S;
+                unsigned long long cl_recip = 0, cl_deliv = 0, cl_ackdrop = 0;
+                unsigned long long cb_new = 0, cb_new_deliv = 0, cb_new_ackdrop = 0;
+                unsigned long long push_sent = 0, push_deliv = 0, push_ackdrop = 0;
+                auto load_own = [&]() {
+                    sp = load_row<WPL>(a.base + rep * a.nwp + off);
                     if (lag) {
                         const Row<WPL> f = load_row<WPL>(a.F_prev + rep * a.nwp + off);
 #pragma unroll
                         for (int w = 0; w < WPL; ++w) sp.w[w] |= f.w[w];
                     }
-                    Row<WPL> S = sp;
+                    S = sp;
                     // (1) client broadcasts of this round
                     if (has_inj) {
                         uint32_t lo = 0, hi = a.n_inj;
@@ -405,102 +453,166 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                             if (word / WPL == (uint32_t)lg) S.w[word % WPL] |= 1ull << (lane & 63);
                         }
                     }
-                    // (2) node broadcasts, ascending sender: first deliverer claims
-                    unsigned long long cl_recip = 0, cl_deliv = 0, cl_ackdrop = 0;
-                    auto claim = [&](const Row<WPL>& src, uint32_t c) {
-                        unsigned long long pc = 0;
+                };
+                // (2) first deliverer claims, ascending sender
+                auto claim = [&](const Row<WPL>& src, uint32_t c) {
+                    unsigned long long pc = 0;
 #pragma unroll
-                        for (int w = 0; w < WPL; ++w) {
-                            const uint64_t cw = src.w[w] & ~S.w[w];
-                            S.w[w] |= cw;
-                            pc += __popcll(cw);
-                        }
-                        if (c & kRecipBit) {
-                            cl_recip += pc;
-                            if constexpr (MASKW) {
-                                const uint64_t u = c & kColMask;
-                                if (!masked<MASKW>(a, 3, rep, u)) {
-                                    cl_deliv += pc;
-                                    if (masked<MASKW>(a, 4, u, rep)) cl_ackdrop += pc;
-                                }
-                            }
-                        }
-                    };
-                    auto sender_row = [&](uint32_t c, bool push, bool slag) {
-                        const uint64_t u = c & kColMask;
-                        if (SYNCW && push) {  // push edge: u's whole set of round r-1
-                            Row<WPL> r = load_row<WPL>(a.base + u * a.nwp + off);
-                            if (slag) {
-                                const Row<WPL> f = load_row<WPL>(a.F_prev + u * a.nwp + off);
-#pragma unroll
-                                for (int w = 0; w < WPL; ++w) r.w[w] |= f.w[w];
-                            }
-                            return r;
-                        }
-                        return load_row<WPL>(a.F_prev + u * a.nwp + off);
-                    };
-                    if (staged) {
-                        c_gathers += (lg == 0) ? (unsigned long long)m : 0ull;
-                        for (int b0 = 0; b0 < m; b0 += kBatch) {
-                            uint32_t cb[kBatch];
-                            Row<WPL> src[kBatch];
-#pragma unroll
-                            for (int b = 0; b < kBatch; ++b) {
-                                const bool v = b0 + b < m;
-                                cb[b] = v ? s_col[k0 + b0 + b] : 0u;
-                                const uint8_t lf = v ? s_ef[k0 + b0 + b] : 0;
-                                if (v) {
-                                    src[b] = sender_row(cb[b], lf & L_PUSH, lf & L_LAG);
-                                } else {
-#pragma unroll
-                                    for (int w = 0; w < WPL; ++w) src[b].w[w] = 0;
-                                }
-                            }
-#pragma unroll
-                            for (int b = 0; b < kBatch; ++b) claim(src[b], cb[b]);
-                        }
-                    } else {
-                        for (int64_t k = k0; k < k1; ++k) {  // hub slow path
-                            const uint32_t c = a.in_col[eb + k];
+                    for (int w = 0; w < WPL; ++w) {
+                        const uint64_t cw = src.w[w] & ~S.w[w];
+                        S.w[w] |= cw;
+                        pc += __popcll(cw);
+                    }
+                    if (c & kRecipBit) {
+                        cl_recip += pc;
+                        if constexpr (MASKW) {
                             const uint64_t u = c & kColMask;
-                            const uint8_t ef = sender_flags<SYNCW>(a, u);
-                            if (masked<MASKW>(a, 2, u, rep)) continue;
-                            const bool p = is_push<SYNCW, MASKW>(a, ef, u, rep);
-                            if (!(ef & SE_ACT) && !p) continue;
-                            c_gathers += (lg == 0) ? 1ull : 0ull;
-                            claim(sender_row(c, p, (ef & SE_LAG) != 0), c);
+                            if (!masked<MASKW>(a, 3, rep, u)) {
+                                cl_deliv += pc;
+                                if (masked<MASKW>(a, 4, u, rep)) cl_ackdrop += pc;
+                            }
                         }
                     }
-                    // (3) sync callback: v fired in r-2, read_oks of peers in ascending order
-                    unsigned long long cb_new = 0, cb_new_deliv = 0, cb_new_ackdrop = 0;
-                    unsigned long long push_sent = 0, push_deliv = 0, push_ackdrop = 0;
-                    if constexpr (SYNCW) {
-                        if (callback) {
-                            const int64_t o0 = a.out_ptr[i], o1 = a.out_ptr[i + 1];
-                            for (int64_t e = o0; e < o1; ++e) {
-                                const uint64_t w = a.out_col[e] & kColMask;
-                                if (masked<MASKW>(a, 1, rep, w) || masked<MASKW>(a, 2, w, rep)) continue;
-                                const Row<WPL> R = sender_row((uint32_t)w, true, (a.flg_prev[w] & FL_LAG) != 0);
-                                unsigned long long pn = 0, pp = 0;
+                };
+                auto sender_row = [&](uint32_t c, bool push, bool slag) {
+                    const uint64_t u = c & kColMask;
+                    if (SYNCW && push) {  // push edge: u's whole set of round r-1
+                        Row<WPL> r = load_row<WPL>(a.base + u * a.nwp + off);
+                        if (slag) {
+                            const Row<WPL> f = load_row<WPL>(a.F_prev + u * a.nwp + off);
 #pragma unroll
-                                for (int q = 0; q < WPL; ++q) {
-                                    pn += __popcll(R.w[q] & ~S.w[q]);
-                                    pp += __popcll(S.w[q] & ~R.w[q]);
-                                    S.w[q] |= R.w[q];
+                            for (int w = 0; w < WPL; ++w) r.w[w] |= f.w[w];
+                        }
+                        return r;
+                    }
+                    return load_row<WPL>(a.F_prev + u * a.nwp + off);
+                };
+                bool work = true;
+                if (dense) {
+                    // ---- lean dense path: own row + (flag, row) of every sender, kSpec at a time
+                    load_own();
+                    for (int64_t k = k0; k < k1; k += kSpec) {
+                        uint32_t cb[kSpec];
+                        uint8_t fb[kSpec];
+                        Row<WPL> src[kSpec];
+#pragma unroll
+                        for (int b = 0; b < kSpec; ++b) {
+                            const bool v = k + b < k1;
+                            cb[b] = v ? (k + b < ns ? s_col[k + b] : a.in_col[eb + k + b]) : 0u;
+                            const uint64_t u = cb[b] & kColMask;
+                            fb[b] = v ? a.flg_prev[u] : (uint8_t)0;
+                            if (v) {
+                                src[b] = load_row<WPL>(a.F_prev + u * a.nwp + off);
+                            } else {
+#pragma unroll
+                                for (int w = 0; w < WPL; ++w) src[b].w[w] = 0;
+                            }
+                        }
+#pragma unroll
+                        for (int b = 0; b < kSpec; ++b) {
+                            if (fb[b] & FL_ACT) {
+                                claim(src[b], cb[b]);
+                                c_gathers += (lg == 0) ? 1ull : 0ull;
+                            }
+                        }
+                    }
+                } else {
+                    // ---- pass 1: who reaches v this round (no row traffic); compact the
+                    // contributing senders of a staged node in place in LDS.
+                    int m = 0;
+                    bool need = false;
+                    for (int64_t k = k0; k < k1; ++k) {
+                        uint32_t c;
+                        uint8_t ef;
+                        if (staged) {
+                            c = s_col[k];
+                            ef = s_ef[k];
+                        } else {
+                            c = a.in_col[eb + k];
+                            ef = sender_flags<SYNCW>(a, c & kColMask);
+                        }
+                        const uint64_t u = c & kColMask;
+                        const bool drop = masked<MASKW>(a, 2, u, rep);  // sent in r-1
+                        if constexpr (SYNCW) keep |= (ef & SE_FM2) != 0;  // u's callback reads v now
+                        const bool p = !drop && is_push<SYNCW, MASKW>(a, ef, u, rep);
+                        if (!drop && ((ef & SE_ACT) || p)) {
+                            need = true;
+                            if (staged) {  // every lane of the group writes the same entry
+                                s_col[k0 + m] = c;
+                                s_ef[k0 + m] = (p ? L_PUSH : 0) | ((ef & SE_LAG) ? L_LAG : 0);
+                                ++m;
+                            }
+                        }
+                    }
+                    work = need || lag || callback || has_inj;
+                    if (work) {
+                        // ---- pass 2: gather the contributing senders' rows
+                        load_own();
+                        if (staged) {
+                            c_gathers += (lg == 0) ? (unsigned long long)m : 0ull;
+                            for (int b0 = 0; b0 < m; b0 += kBatch) {
+                                uint32_t cb[kBatch];
+                                Row<WPL> src[kBatch];
+#pragma unroll
+                                for (int b = 0; b < kBatch; ++b) {
+                                    const bool v = b0 + b < m;
+                                    cb[b] = v ? s_col[k0 + b0 + b] : 0u;
+                                    const uint8_t lf = v ? s_ef[k0 + b0 + b] : 0;
+                                    if (v) {
+                                        src[b] = sender_row(cb[b], lf & L_PUSH, lf & L_LAG);
+                                    } else {
+#pragma unroll
+                                        for (int w = 0; w < WPL; ++w) src[b].w[w] = 0;
+                                    }
                                 }
-                                cb_new += pn;
-                                push_sent += pp;
-                                if (!masked<MASKW>(a, 3, rep, w)) {
-                                    cb_new_deliv += pn;
-                                    push_deliv += pp;
-                                    if (masked<MASKW>(a, 4, w, rep)) {
-                                        cb_new_ackdrop += pn;
-                                        push_ackdrop += pp;
+#pragma unroll
+                                for (int b = 0; b < kBatch; ++b) claim(src[b], cb[b]);
+                            }
+                        } else {
+                            for (int64_t k = k0; k < k1; ++k) {  // hub slow path
+                                const uint32_t c = a.in_col[eb + k];
+                                const uint64_t u = c & kColMask;
+                                const uint8_t ef = sender_flags<SYNCW>(a, u);
+                                if (masked<MASKW>(a, 2, u, rep)) continue;
+                                const bool p = is_push<SYNCW, MASKW>(a, ef, u, rep);
+                                if (!(ef & SE_ACT) && !p) continue;
+                                c_gathers += (lg == 0) ? 1ull : 0ull;
+                                claim(sender_row(c, p, (ef & SE_LAG) != 0), c);
+                            }
+                        }
+                        // (3) sync callback: v fired in r-2, read_oks of peers in ascending order
+                        if constexpr (SYNCW) {
+                            if (callback) {
+                                const int64_t o0 = a.out_ptr[i], o1 = a.out_ptr[i + 1];
+                                for (int64_t e = o0; e < o1; ++e) {
+                                    const uint64_t w = a.out_col[e] & kColMask;
+                                    if (masked<MASKW>(a, 1, rep, w) || masked<MASKW>(a, 2, w, rep)) continue;
+                                    const Row<WPL> R =
+                                        sender_row((uint32_t)w, true, (a.flg_prev[w] & FL_LAG) != 0);
+                                    unsigned long long pn = 0, pp = 0;
+#pragma unroll
+                                    for (int q2 = 0; q2 < WPL; ++q2) {
+                                        pn += __popcll(R.w[q2] & ~S.w[q2]);
+                                        pp += __popcll(S.w[q2] & ~R.w[q2]);
+                                        S.w[q2] |= R.w[q2];
+                                    }
+                                    cb_new += pn;
+                                    push_sent += pp;
+                                    if (!masked<MASKW>(a, 3, rep, w)) {
+                                        cb_new_deliv += pn;
+                                        push_deliv += pp;
+                                        if (masked<MASKW>(a, 4, w, rep)) {
+                                            cb_new_ackdrop += pn;
+                                            push_ackdrop += pp;
+                                        }
                                     }
                                 }
                             }
                         }
                     }
+                }
+                if (work) {
+                    const unsigned long long deg = (unsigned long long)(a.out_ptr[i + 1] - a.out_ptr[i]);
                     // ---- new state
                     Row<WPL> F;
                     unsigned long long T = 0;
@@ -551,9 +663,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
             }
             __syncthreads();  // LDS reuse by the next tile
         }
-        __syncthreads();
-        if (threadIdx.x == 0)
-            *reinterpret_cast<unsigned long long*>(a.tile_cand + probe * kTilesPerProbe) = 0ull;
+        __syncthreads();  // s_work reuse
     }
 
     // without partition masks nothing is dropped: delivered = sent
