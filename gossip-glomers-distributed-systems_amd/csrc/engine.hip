@@ -94,6 +94,7 @@ struct gg_engine {
     gg::TileWork* d_work = nullptr;  // [tiles] live-tile worklist
     uint32_t* d_n_work = nullptr;
     uint64_t tile_nodes = 0, tile_bytes = 0;
+    uint64_t n_in_edges = 0;
     uint64_t* d_fired[4] = {nullptr, nullptr, nullptr, nullptr};
     int32_t* d_sync_next = nullptr;
     uint32_t* d_sync_k = nullptr;
@@ -274,6 +275,9 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.work = e->d_work;
     a.n_work = e->d_n_work;
     a.tile_nodes = (uint32_t)e->tile_nodes;
+    a.symmetric = e->symmetric ? 1 : 0;
+    a.n_edges = e->n_in_edges;
+    a.rows = e->rows;
     a.mark_all = e->world > 1;
     a.fired_m1 = e->d_fired[(r - 1) & 3];
     a.fired_m2 = e->d_fired[(r - 2) & 3];
@@ -601,6 +605,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
         for (int64_t k = 0; k < row_ptr[v + 1] - row_ptr[v]; ++k) ocol[optr[i] + k] = rep_of((uint64_t)ob[k]);
     }
     // device buffers
+    e->n_in_edges = icol.size();
     HIPCHK(hipMalloc(&e->d_in_ptr, (n_own + 1) * 8));
     HIPCHK(hipMalloc(&e->d_in_col, std::max<size_t>(1, icol.size()) * 4));
     HIPCHK(hipMemcpy(e->d_in_ptr, iptr.data(), (n_own + 1) * 8, hipMemcpyHostToDevice));

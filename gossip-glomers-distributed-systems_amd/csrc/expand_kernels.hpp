@@ -115,6 +115,9 @@ struct RoundArgs {
     uint64_t n_own, own0, lo;
     uint32_t nwp, nw;
     uint32_t tile_nodes;        // NG of the expand kernel
+    int32_t symmetric;          // out-lists == in-lists
+    uint64_t n_edges;           // in_col entries of this engine
+    uint64_t rows;              // replica rows
     int32_t mark_all;           // sharded engines: every owned node is a candidate
     int64_t round;
     uint64_t seed;
