@@ -90,6 +90,7 @@ struct gg_engine {
     uint64_t* d_F[2] = {nullptr, nullptr};
     uint8_t* d_flg[2] = {nullptr, nullptr};
     uint8_t* d_cand = nullptr;       // [rows] candidate bytes
+    uint8_t* d_zmark = nullptr;      // [rows] stale-F-row marks
     uint8_t* d_tile_cand = nullptr;  // [tile_bytes]
     gg::TileWork* d_work = nullptr;  // [tiles] live-tile worklist
     uint32_t* d_n_work = nullptr;
@@ -154,6 +155,7 @@ void gg_engine::free_topology() {
     for (auto& p : d_F) dfree(p);
     for (auto& p : d_flg) dfree(p);
     dfree(d_cand);
+    dfree(d_zmark);
     dfree(d_tile_cand);
     dfree(d_work);
     dfree(d_n_work);
@@ -185,9 +187,13 @@ namespace {
 int reset_device_state(gg_engine* e) {
     const size_t rowbytes = e->rows * e->nwp * 8;
     HIPCHK(hipMemsetAsync(e->d_base, 0, rowbytes, e->stream));
-    for (int b = 0; b < 2; ++b) HIPCHK(hipMemsetAsync(e->d_flg[b], 0, e->rows, e->stream));  // F rows: read only where ACT
+    for (int b = 0; b < 2; ++b) {
+        HIPCHK(hipMemsetAsync(e->d_F[b], 0, rowbytes, e->stream));  // F rows are zero unless ACT
+        HIPCHK(hipMemsetAsync(e->d_flg[b], 0, e->rows, e->stream));
+    }
     for (int b = 0; b < 4; ++b) HIPCHK(hipMemsetAsync(e->d_fired[b], 0, e->rows / 8, e->stream));
     HIPCHK(hipMemsetAsync(e->d_cand, 0, e->rows, e->stream));
+    HIPCHK(hipMemsetAsync(e->d_zmark, 0, e->rows, e->stream));
     HIPCHK(hipMemsetAsync(e->d_tile_cand, 0, e->tile_bytes, e->stream));
     const uint64_t n_own = e->hi - e->lo;
     if (n_own) {
@@ -257,6 +263,24 @@ void launch_expand(const gg::RoundArgs& a, bool syncw, bool maskw, hipStream_t s
     }
 }
 
+void launch_stream(const gg::RoundArgs& a, hipStream_t s) {
+    const uint32_t G = std::max<uint32_t>(1, a.nwp / 2);
+    const uint64_t ngb = gg::kBlock / G;
+    uint64_t blocks = (a.n_own + ngb - 1) / ngb;
+    blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, kMaxBlocks));
+    dim3 grid((unsigned)blocks), block(gg::kBlock);
+    switch (a.nwp) {
+        case 2: hipLaunchKernelGGL((gg::expand_stream<1, 2>), grid, block, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((gg::expand_stream<2, 2>), grid, block, 0, s, a); break;
+        case 8: hipLaunchKernelGGL((gg::expand_stream<4, 2>), grid, block, 0, s, a); break;
+        case 16: hipLaunchKernelGGL((gg::expand_stream<8, 2>), grid, block, 0, s, a); break;
+        case 32: hipLaunchKernelGGL((gg::expand_stream<16, 2>), grid, block, 0, s, a); break;
+        case 64: hipLaunchKernelGGL((gg::expand_stream<32, 2>), grid, block, 0, s, a); break;
+        case 128: hipLaunchKernelGGL((gg::expand_stream<64, 2>), grid, block, 0, s, a); break;
+        default: break;
+    }
+}
+
 // Enqueue round e->round (kernels only). inj: device pairs for this round.
 int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned long long* d_ctr) {
     const int64_t r = e->round;
@@ -271,6 +295,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.flg_prev = e->d_flg[(r + 1) & 1];
     a.flg_cur = e->d_flg[r & 1];
     a.cand = e->d_cand;
+    a.zmark = e->d_zmark;
     a.tile_cand = e->d_tile_cand;
     a.work = e->d_work;
     a.n_work = e->d_n_work;
@@ -279,6 +304,10 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.n_edges = e->n_in_edges;
     a.rows = e->rows;
     a.mark_all = e->world > 1;
+    {
+        static const uint32_t ablate = getenv("GG_ABLATE") ? (uint32_t)atoi(getenv("GG_ABLATE")) : 0u;
+        a.ablate = ablate;  // diagnostic timing only
+    }
     a.fired_m1 = e->d_fired[(r - 1) & 3];
     a.fired_m2 = e->d_fired[(r - 2) & 3];
     a.fired_m3 = e->d_fired[(r - 3) & 3];
@@ -332,6 +361,10 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         }
         launch_expand(a, syncw, maskw, e->stream);
         HIPCHK(hipGetLastError());
+        if (!syncw && !maskw && e->nwp >= 2) {  // dense propagation rounds (decided on device)
+            launch_stream(a, e->stream);
+            HIPCHK(hipGetLastError());
+        }
         if (e->d_dr) {
             const uint64_t n = a.n_own * e->nw;
             hipLaunchKernelGGL(gg::track_delivery, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream,
@@ -625,6 +658,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     const uint64_t ntiles = (n_own + e->tile_nodes - 1) / e->tile_nodes;
     e->tile_bytes = (ntiles + 8) / 8 * 8;
     HIPCHK(hipMalloc(&e->d_cand, e->rows));
+    HIPCHK(hipMalloc(&e->d_zmark, e->rows));
     HIPCHK(hipMalloc(&e->d_tile_cand, e->tile_bytes));
     HIPCHK(hipMalloc(&e->d_work, std::max<uint64_t>(1, ntiles) * sizeof(gg::TileWork)));
     HIPCHK(hipMalloc(&e->d_n_work, 4));

@@ -46,10 +46,19 @@
 namespace gg {
 
 // Occupancy target of the lean round kernel (no sync events, no partition
-// masks: the propagation phase): 5 waves/SIMD fits its registers unspilled.
+// masks: the propagation phase): 4 blocks/CU, the LDS budget of its DMA landing slots.
 #ifndef GG_LEAN_WAVES_PER_EU
-#define GG_LEAN_WAVES_PER_EU 5
+#define GG_LEAN_WAVES_PER_EU 4
 #endif
+
+// Sender rows a lane keeps in flight (LDS slots) in expand_stream, and its occupancy.
+#ifndef GG_STREAM_ROWS
+#define GG_STREAM_ROWS 6
+#endif
+#ifndef GG_STREAM_WAVES_PER_EU
+#define GG_STREAM_WAVES_PER_EU 6
+#endif
+constexpr int kStreamRows = GG_STREAM_ROWS;
 
 // Sender (flag, row) pairs a lane keeps in flight in dense lean rounds.
 #ifndef GG_SPEC_BATCH
@@ -99,6 +108,7 @@ struct RoundArgs {
     const uint8_t* flg_prev;    // [rows] FL_* of round r-1
     uint8_t* flg_cur;
     uint8_t* cand;              // [rows] candidate bytes of this round (cleared by expand)
+    uint8_t* zmark;             // [rows] F row of this parity is stale (node active 2 rounds ago)
     uint8_t* tile_cand;         // [n_tiles rounded to 8] tile has a candidate
     struct TileWork* work;      // live tiles of the round (compact_tiles)
     uint32_t* n_work;           // number of live tiles
@@ -119,6 +129,8 @@ struct RoundArgs {
     uint64_t n_edges;           // in_col entries of this engine
     uint64_t rows;              // replica rows
     int32_t mark_all;           // sharded engines: every owned node is a candidate
+    uint32_t ablate;            // DIAGNOSTIC timing builds only (GG_ABLATE): 1 no row stores,
+                                // 2 no sender-row gathers, 4 no own-row loads, 8 no hash; results invalid
     int64_t round;
     uint64_t seed;
     uint32_t sync_base, sync_jitter;
@@ -129,6 +141,15 @@ template <int WPL>
 struct Row {
     uint64_t w[WPL];
 };
+
+// S.w[w] |= bit b, with w a runtime value: selects, not a runtime-indexed
+// register array (which would live in scratch).
+template <int WPL>
+__device__ __forceinline__ void set_lane_bit(Row<WPL>& S, uint32_t w, uint32_t b) {
+#pragma unroll
+    for (int q = 0; q < WPL; ++q)
+        if ((uint32_t)q == w) S.w[q] |= 1ull << b;
+}
 
 template <int WPL>
 __device__ __forceinline__ Row<WPL> load_row(const uint64_t* p) {
@@ -178,6 +199,15 @@ __device__ __forceinline__ uint8_t sender_flags(const RoundArgs& a, uint64_t u) 
     return f;
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
+// (lgkmcnt), not for its global stores/loads (vmcnt counts stores on CDNA, so
+// __syncthreads() would stall every tile on the previous tile's row stores).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
@@ -198,6 +228,28 @@ __device__ __forceinline__ bool is_push(const RoundArgs& a, uint8_t ef, uint64_t
 
 // Block reduction of C_NUM per-thread counters -> one atomic per counter per
 // block into slot blockIdx % 64.
+// Wait until every vector-memory op of this wave (loads, stores, LDS-DMA) is
+// done: s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15). Issued through the builtin
+// so the compiler's waitcnt pass sees it and does not add drains of its own
+// for loads this wait already covers.
+__device__ __forceinline__ void vm_drain() {
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    asm volatile("" ::: "memory");
+}
+
+// 16-byte LDS-DMA (global_load_lds_dwordx4): LDS destination = M0 (wave-uniform
+// base) + lane * 16. Issued from inline asm because the compiler's waitcnt
+// pass cannot tell one wave's DMA slots apart and puts a full vmcnt(0) drain
+// in front of every builtin DMA, serialising them; callers wait themselves
+// (s_waitcnt vmcnt(0)) before reading the slots. Extra vector-memory ops the
+// compiler does not see only make its own vmcnt(N) waits stricter.
+__device__ __forceinline__ void dma16(const void* src, const void* lds_wave_base) {
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)lds_wave_base);
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0)
+                 : "memory");
+}
+
 __device__ __forceinline__ void flush_counters(const RoundArgs& a, unsigned long long (&acc)[C_NUM],
                                                unsigned long long (*s_red)[C_NUM], unsigned long long t_start) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -238,6 +290,13 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
         bool fire = false;
         if (valid) {
             const uint8_t f = a.flg_prev[rep];
+            // flg_cur still holds round r-2's flags: an F row written then is
+            // stale in this round's F buffer; expand zeroes it unless the node
+            // writes a new one, so F rows stay zero for inactive nodes.
+            if (a.flg_cur[rep] & FL_ACT) {
+                a.zmark[rep] = 1;
+                a.tile_cand[i / a.tile_nodes] = 1;
+            }
             a.flg_cur[rep] = 0;  // expand_round sets the flags of changed nodes
             const int64_t o0 = a.out_ptr[i], o1 = a.out_ptr[i + 1];
             bool fm1 = false, fm2 = false, fm3 = false;
@@ -365,7 +424,10 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
     constexpr int kSpec = GG_SPEC_BATCH;  // dense lean rounds: (flag, row) pairs in flight per lane
     constexpr int kPre = 64;        // worklist entries preloaded per chunk
     constexpr bool LEAN = !SYNCW && !MASKW;
+    constexpr int kDmaRows = 6;     // dense lean rounds: sender rows in flight per lane (via LDS)
     constexpr uint8_t L_PUSH = 1, L_LAG = 2;  // compacted-list flags
+    // per-wave LDS landing slots of the dense lean path (kDmaRows x 1 KiB per wave)
+    __shared__ __attribute__((aligned(16))) uint8_t s_rows[(LEAN && WPL == 2) ? 4 * kDmaRows * 1024 : 16];
     __shared__ int64_t s_ptr[NG + 1];
     __shared__ uint32_t s_col[kEdgeStage];
     __shared__ uint8_t s_ef[kEdgeStage];
@@ -390,19 +452,34 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
     // most tiles live: load sender flags together with their rows (speculative
     // gathers; a row of an inactive sender is ignored) instead of flags first
     const bool dense = LEAN && n_work * 2 > ntiles;
+    if constexpr (LEAN && WPL == 2) {
+        if (dense) {  // expand_stream runs this round
+            unsigned long long acc[C_NUM];
+#pragma unroll
+            for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
+            flush_counters(a, acc, s_red, t_start);
+            return;
+        }
+    }
 
     for (uint64_t base = blockIdx.x; base < n_work; base += (uint64_t)kPre * gridDim.x) {
         if (threadIdx.x < kPre) {
             const uint64_t idx = base + (uint64_t)threadIdx.x * gridDim.x;
             if (idx < n_work) s_work[threadIdx.x] = a.work[idx];
         }
-        __syncthreads();
+        lds_barrier();
         for (int q = 0; q < kPre; ++q) {
             if (base + (uint64_t)q * gridDim.x >= n_work) break;  // block-uniform
             const TileWork tw = s_work[q];
             const uint64_t t0 = (uint64_t)tw.tile * NG;
             const int64_t eb = tw.eb;
             const int ns = tw.ne < (uint32_t)kEdgeStage ? (int)tw.ne : kEdgeStage;
+            const uint64_t i = t0 + j;
+            const uint64_t rep = a.own0 + i;
+            // per-node bytes, issued with the staging loads (same round trip)
+            const uint8_t ca = i < a.n_own ? a.cand[rep] : 0;
+            const uint8_t zm = i < a.n_own ? a.zmark[rep] : 0;
+            const uint8_t own = i < a.n_own ? a.flg_prev[rep] : 0;
             // ---- stage the tile's row_ptr and col slices (one round trip)
             for (int t = threadIdx.x; t <= NG; t += kBlock) {  // NG + 1 entries (NG may be kBlock)
                 const uint64_t idx = t0 + t < a.n_own ? t0 + t : a.n_own;
@@ -413,16 +490,21 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                 s_col[k] = c;
                 if (!dense) s_ef[k] = sender_flags<SYNCW>(a, c & kColMask);
             }
-            __syncthreads();
+            lds_barrier();
 
-            const uint64_t i = t0 + j;
-            const uint64_t rep = a.own0 + i;
-            const uint8_t ca = i < a.n_own ? a.cand[rep] : 0;
+            if (zm && !ca) {  // only the stale F row to clear
+                if (!(a.ablate & 1)) {
+                    Row<WPL> z;
+#pragma unroll
+                    for (int w = 0; w < WPL; ++w) z.w[w] = 0;
+                    store_row<WPL>(a.F_cur + rep * a.nwp + off, z);
+                }
+                if (lg == 0) a.zmark[rep] = 0;
+            }
             if (ca) {
                 if (lg == 0) a.cand[rep] = 0;
                 const int64_t k0 = s_ptr[j] - eb, k1 = s_ptr[j + 1] - eb;
                 const bool staged = k1 <= ns;  // else: hub slow path straight from global
-                const uint8_t own = a.flg_prev[rep];
                 const bool lag = own & FL_LAG;
                 const bool has_inj = (ca & CA_INJ) != 0;
                 bool callback = false, keep = false;
@@ -435,7 +517,12 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                 unsigned long long cb_new = 0, cb_new_deliv = 0, cb_new_ackdrop = 0;
                 unsigned long long push_sent = 0, push_deliv = 0, push_ackdrop = 0;
                 auto load_own = [&]() {
-                    sp = load_row<WPL>(a.base + rep * a.nwp + off);
+                    if (a.ablate & 4) {
+#pragma unroll
+                        for (int w = 0; w < WPL; ++w) sp.w[w] = 0;
+                    } else {
+                        sp = load_row<WPL>(a.base + rep * a.nwp + off);
+                    }
                     if (lag) {
                         const Row<WPL> f = load_row<WPL>(a.F_prev + rep * a.nwp + off);
 #pragma unroll
@@ -453,7 +540,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                         for (uint32_t k = lo; k < a.n_inj && a.inj[2 * k] == (uint32_t)i; ++k) {
                             const uint32_t lane = a.inj[2 * k + 1];
                             const uint32_t word = lane >> 6;
-                            if (word / WPL == (uint32_t)lg) S.w[word % WPL] |= 1ull << (lane & 63);
+                            if (word / WPL == (uint32_t)lg) set_lane_bit<WPL>(S, word % WPL, lane & 63);
                         }
                     }
                 };
@@ -492,30 +579,64 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                 };
                 bool work = true;
                 if (dense) {
-                    // ---- lean dense path: own row + (flag, row) of every sender, kSpec at a time
+                    // ---- lean dense path: own row + (flag, row) of every sender.
                     load_own();
-                    for (int64_t k = k0; k < k1; k += kSpec) {
-                        uint32_t cb[kSpec];
-                        uint8_t fb[kSpec];
-                        Row<WPL> src[kSpec];
+                    if constexpr (WPL == 2) {
+                        // Each lane DMAs its own 16-byte chunk of kDmaRows sender rows
+                        // into its wave's LDS slots (global_load_lds_dwordx4: LDS
+                        // address = wave-uniform base + lane*16), waits vmcnt, and
+                        // reads back exactly what it loaded: in-flight rows cost
+                        // LDS, not VGPRs, and no other wave touches the slots.
+                        uint8_t* const my = &s_rows[(threadIdx.x >> 6) * kDmaRows * 1024];
+                        const uint32_t lane16 = (threadIdx.x & 63) * 16;
+                        for (int64_t k = k0; k < k1; k += kDmaRows) {
+                            uint32_t cb[kDmaRows];
 #pragma unroll
-                        for (int b = 0; b < kSpec; ++b) {
-                            const bool v = k + b < k1;
-                            cb[b] = v ? (k + b < ns ? s_col[k + b] : a.in_col[eb + k + b]) : 0u;
-                            const uint64_t u = cb[b] & kColMask;
-                            fb[b] = v ? a.flg_prev[u] : (uint8_t)0;
-                            if (v) {
-                                src[b] = load_row<WPL>(a.F_prev + u * a.nwp + off);
-                            } else {
+                            for (int b = 0; b < kDmaRows; ++b) {
+                                const bool v = k + b < k1;
+                                cb[b] = v ? (k + b < ns ? s_col[k + b] : a.in_col[eb + k + b]) : 0u;
+                                const uint64_t u = cb[b] & kColMask;
+                                if (v && !(a.ablate & 2))
+                                    dma16((const void*)(a.F_prev + u * a.nwp + off), my + b * 1024);
+                            }
+                            vm_drain();
+                            // F rows of inactive senders are zero: claim every row
 #pragma unroll
-                                for (int w = 0; w < WPL; ++w) src[b].w[w] = 0;
+                            for (int b = 0; b < kDmaRows; ++b) {
+                                if (k + b < k1) {
+                                    const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(my + b * 1024 + lane16);
+                                    Row<WPL> src;
+                                    src.w[0] = x.x;
+                                    src.w[1 % WPL] = x.y;
+                                    claim(src, cb[b]);
+                                    c_gathers += (lg == 0) ? 1ull : 0ull;
+                                }
                             }
                         }
+                    } else {
+                        for (int64_t k = k0; k < k1; k += kSpec) {
+                            uint32_t cb[kSpec];
+                            uint8_t fb[kSpec];
+                            Row<WPL> src[kSpec];
 #pragma unroll
-                        for (int b = 0; b < kSpec; ++b) {
-                            if (fb[b] & FL_ACT) {
-                                claim(src[b], cb[b]);
-                                c_gathers += (lg == 0) ? 1ull : 0ull;
+                            for (int b = 0; b < kSpec; ++b) {
+                                const bool v = k + b < k1;
+                                cb[b] = v ? (k + b < ns ? s_col[k + b] : a.in_col[eb + k + b]) : 0u;
+                                const uint64_t u = cb[b] & kColMask;
+                                fb[b] = v ? a.flg_prev[u] : (uint8_t)0;
+                                if (v) {
+                                    src[b] = load_row<WPL>(a.F_prev + u * a.nwp + off);
+                                } else {
+#pragma unroll
+                                    for (int w = 0; w < WPL; ++w) src[b].w[w] = 0;
+                                }
+                            }
+#pragma unroll
+                            for (int b = 0; b < kSpec; ++b) {
+                                if (fb[b] & FL_ACT) {
+                                    claim(src[b], cb[b]);
+                                    c_gathers += (lg == 0) ? 1ull : 0ull;
+                                }
                             }
                         }
                     }
@@ -624,14 +745,16 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                     for (int w = 0; w < WPL; ++w) {
                         F.w[w] = S.w[w] & ~sp.w[w];
                         T += __popcll(F.w[w]);
-                        if (F.w[w]) {  // seen_hash delta of a changed word
+                        if (F.w[w] && !(a.ablate & 8)) {  // seen_hash delta of a changed word
                             const uint64_t idx = g * a.nw + off + w;
                             c_hash += gg_word_hash(idx, S.w[w]) - (sp.w[w] ? gg_word_hash(idx, sp.w[w]) : 0ull);
                         }
                     }
                     const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
-                    if (any) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
-                    if (keep) {
+                    if ((any || zm) && !(a.ablate & 1)) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
+                    if (zm && lg == 0) a.zmark[rep] = 0;
+                    if (a.ablate & 1) {
+                    } else if (keep) {
                         if (lag) store_row<WPL>(a.base + rep * a.nwp + off, sp);
                     } else if (any || lag) {
                         store_row<WPL>(a.base + rep * a.nwp + off, S);
@@ -664,9 +787,9 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                     }
                 }
             }
-            __syncthreads();  // LDS reuse by the next tile
+            lds_barrier();  // LDS reuse by the next tile
         }
-        __syncthreads();  // s_work reuse
+        lds_barrier();  // s_work reuse
     }
 
     // without partition masks nothing is dropped: delivered = sent
@@ -700,6 +823,198 @@ template <int G, int WPL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GG_LEAN_WAVES_PER_EU)))
 void expand_round_lean(RoundArgs a) {
     expand_body<G, WPL, false, false>(a);
+}
+
+
+// ---------------------------------------------------------------------------
+// expand_stream: the dense propagation round (no sync events, no masks, most
+// tiles live). No tiles, no barriers: node group q (G lanes) walks nodes
+// q, q + n_groups, ... with a software pipeline — while node i's own row and
+// sender rows land in its wave's LDS slots by DMA, node i+1's column list and
+// node i+2's row pointers and bytes are already in flight — so each node
+// costs about one memory round trip. F rows of inactive senders are zero, so
+// every sender row is claimed without looking at sender flags.
+template <int G, int WPL>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GG_STREAM_WAVES_PER_EU)))
+void expand_stream(RoundArgs a) {
+    static_assert(WPL == 2, "DMA slots hold 16 bytes per lane");
+    constexpr int NGB = kBlock / G;  // node groups per block
+    constexpr int D = kStreamRows;   // sender rows per DMA batch
+    __shared__ __attribute__((aligned(16))) uint8_t s_slots[(kBlock / 64) * (D + 1) * 1024];
+    __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
+    const unsigned long long t_start = clock100();
+    unsigned long long c_new = 0, c_fwd = 0, c_hash = 0, c_active = 0, c_gathers = 0;
+
+    const uint64_t n_work = *a.n_work;
+    const uint64_t ntiles = (a.n_own + a.tile_nodes - 1) / a.tile_nodes;
+    if (n_work * 2 > ntiles) {
+        const int lg = threadIdx.x % G;
+        const uint64_t off = (uint64_t)lg * WPL;
+        const int gshift = (threadIdx.x & 63) / G * G;
+        const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+        uint8_t* const my = &s_slots[(threadIdx.x >> 6) * (D + 1) * 1024];
+        const uint32_t lane16 = (threadIdx.x & 63) * 16;
+        const uint64_t stride = (uint64_t)gridDim.x * NGB;
+
+        struct Meta {
+            int64_t p0, p1;
+            uint8_t ca, zm;
+        };
+        auto fetch_meta = [&](uint64_t n, Meta& m) {
+            if (n < a.n_own && (a.ablate & 64)) {  // diagnostic: synthetic metadata
+                m.p0 = 2 * n;
+                m.p1 = 2 * n + 2;
+                m.ca = CA_NODE;
+                m.zm = 0;
+            } else if (n < a.n_own) {
+                m.p0 = a.in_ptr[n];
+                m.p1 = a.in_ptr[n + 1];
+                m.ca = a.cand[a.own0 + n];
+                m.zm = a.zmark[a.own0 + n];
+            } else {
+                m.p0 = m.p1 = 0;
+                m.ca = m.zm = 0;
+            }
+        };
+        auto fetch_cols = [&](const Meta& m, uint32_t (&c)[D]) {
+#pragma unroll
+            for (int b = 0; b < D; ++b)
+                c[b] = (m.ca && m.p0 + b < m.p1) ? ((a.ablate & 32) ? (uint32_t)((m.p0 + b) / 2) : a.in_col[m.p0 + b])
+                                                 : 0u;
+        };
+
+        uint64_t i = (uint64_t)blockIdx.x * NGB + threadIdx.x / G;
+        Meta m0, m1;
+        uint32_t c0[D], c1[D];
+        fetch_meta(i, m0);
+        fetch_cols(m0, c0);
+        fetch_meta(i + stride, m1);
+        vm_drain();  // nothing pending at the loop head: no compiler drains inside
+        for (; i < a.n_own; i += stride) {
+            const uint64_t rep = a.own0 + i;
+            const bool work = m0.ca != 0;
+            // (a) DMA node i's own row and its first D sender rows
+            if (work) {
+                if (!(a.ablate & 4))
+                    dma16((const void*)(a.base + rep * a.nwp + off), my + D * 1024);
+#pragma unroll
+                for (int b = 0; b < D; ++b) {
+                    if (m0.p0 + b < m0.p1 && !(a.ablate & 2))
+                        dma16((const void*)(a.F_prev + (uint64_t)(c0[b] & kColMask) * a.nwp + off), my + b * 1024);
+                }
+            }
+            // (b) prefetch: columns of node i+stride, row pointers of node i+2*stride
+            Meta m2;
+            fetch_cols(m1, c1);
+            fetch_meta(i + 2 * stride, m2);
+            vm_drain();
+            if (work) {
+                const bool lag = false;  // lean rounds precede every sync timer: no LAG
+                (void)lag;
+                const ulonglong2 o = *reinterpret_cast<const ulonglong2*>(my + D * 1024 + lane16);
+                Row<WPL> sp, S;
+                sp.w[0] = o.x;
+                sp.w[1] = o.y;
+                S = sp;
+                if (m0.ca & CA_INJ) {  // (1) client broadcasts of this round
+                    uint32_t lo = 0, hi = a.n_inj;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (a.inj[2 * mid] < (uint32_t)i) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    for (uint32_t k = lo; k < a.n_inj && a.inj[2 * k] == (uint32_t)i; ++k) {
+                        const uint32_t lane = a.inj[2 * k + 1];
+                        const uint32_t word = lane >> 6;
+                        if (word / WPL == (uint32_t)lg) set_lane_bit<WPL>(S, word % WPL, lane & 63);
+                    }
+                }
+                // (2) node broadcasts, ascending sender: first deliverer claims
+                unsigned long long cl_recip = 0;
+                auto claim = [&](uint64_t x0, uint64_t x1, uint32_t c) {
+                    const uint64_t w0 = x0 & ~S.w[0], w1 = x1 & ~S.w[1];
+                    S.w[0] |= w0;
+                    S.w[1] |= w1;
+                    if (c & kRecipBit) cl_recip += __popcll(w0) + __popcll(w1);
+                };
+#pragma unroll
+                for (int b = 0; b < D; ++b) {
+                    if (m0.p0 + b < m0.p1) {
+                        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(my + b * 1024 + lane16);
+                        claim(x.x, x.y, c0[b]);
+                    }
+                }
+                for (int64_t k = m0.p0 + D; k < m0.p1; k += D) {  // more than D senders
+                    uint32_t cb[D];
+#pragma unroll
+                    for (int b = 0; b < D; ++b) {
+                        cb[b] = k + b < m0.p1 ? a.in_col[k + b] : 0u;
+                        if (k + b < m0.p1)
+                            dma16((const void*)(a.F_prev + (uint64_t)(cb[b] & kColMask) * a.nwp + off), my + b * 1024);
+                    }
+                    vm_drain();
+#pragma unroll
+                    for (int b = 0; b < D; ++b) {
+                        if (k + b < m0.p1) {
+                            const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(my + b * 1024 + lane16);
+                            claim(x.x, x.y, cb[b]);
+                        }
+                    }
+                }
+                c_gathers += (lg == 0) ? (unsigned long long)(m0.p1 - m0.p0) : 0ull;
+                // new state
+                Row<WPL> F;
+                unsigned long long T = 0;
+                const uint64_t g = a.lo + i;
+#pragma unroll
+                for (int w = 0; w < WPL; ++w) {
+                    F.w[w] = S.w[w] & ~sp.w[w];
+                    T += __popcll(F.w[w]);
+                    if (F.w[w] && !(a.ablate & 8)) {
+                        const uint64_t idx = g * a.nw + off + w;
+                        c_hash += gg_word_hash(idx, S.w[w]) - (sp.w[w] ? gg_word_hash(idx, sp.w[w]) : 0ull);
+                    }
+                }
+                const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
+                if (!(a.ablate & 1)) {
+                    if (any || m0.zm) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
+                    if (any) store_row<WPL>(a.base + rep * a.nwp + off, S);
+                }
+                if (lg == 0 && !(a.ablate & 16)) {
+                    if (any) a.flg_cur[rep] = FL_ACT;
+                    a.cand[rep] = 0;
+                    if (m0.zm) a.zmark[rep] = 0;
+                }
+                const unsigned long long deg = a.symmetric ? (unsigned long long)(m0.p1 - m0.p0)
+                                                           : (unsigned long long)(a.out_ptr[i + 1] - a.out_ptr[i]);
+                c_new += T;
+                c_fwd += deg * T - cl_recip;
+                c_active += (lg == 0) ? 1ull : 0ull;
+            } else if (m0.zm) {  // only a stale F row to clear
+                if (!(a.ablate & 1)) {
+                    Row<WPL> z;
+                    z.w[0] = z.w[1] = 0;
+                    store_row<WPL>(a.F_cur + rep * a.nwp + off, z);
+                }
+                if (lg == 0) a.zmark[rep] = 0;
+            }
+            m0 = m1;
+            m1 = m2;
+#pragma unroll
+            for (int b = 0; b < D; ++b) c0[b] = c1[b];
+        }
+    }
+    unsigned long long acc[C_NUM];
+#pragma unroll
+    for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
+    acc[C_NEW] = c_new;
+    acc[C_FWD_SENT] = c_fwd;
+    acc[C_FWD_DELIV] = c_fwd;
+    acc[C_HASH] = c_hash;
+    acc[C_NEXT_ACKS] = c_fwd;
+    acc[C_ACTIVE] = c_active;
+    acc[C_GATHERS] = c_gathers;
+    flush_counters(a, acc, s_red, t_start);
 }
 
 // First-seen round of every new bit (GG_TRACK_DELIVERY only; observation).
