@@ -32,21 +32,30 @@ METRIC = "(node,msg) deliveries/sec at 1/2/4/8 GPUs; % of HBM roofline; msgs/op"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+KERNELS = {"prep": "round_prep", "expand": "expand_round", "stream": "expand_stream"}
+TRAFFIC_JSON = os.path.join(REPO, "profiles", "traffic.json")
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (tools/traffic.py: FETCH_SIZE and WRITE_SIZE in separate passes over this
+    same bench command, FETCH_SIZE doubled for gfx950). None if not profiled."""
+    try:
+        import json as _j
+        d = _j.load(open(TRAFFIC_JSON))
+    except (OSError, ValueError):
+        return None, None
+    for name, ent in d.get("kernels", {}).items():
+        if name.split("(")[0].split("<")[0].split("::")[-1] == kernel:
+            return ent["traffic_bytes_per_dispatch"], f'{os.path.relpath(TRAFFIC_JSON, REPO)} ({d.get("source", "")})'
+    return None, None
+
+
 def dense_bytes_per_round(V: int, E: int, nwp: int) -> int:
     """SURVEY.md §8d dense-pull bytes of one round: row_ptr 8(V+1) + col 4E +
     every sender row gathered E*w + read seen, write seen, write F 3*V*w."""
     w = 8 * nwp
     return 8 * (V + 1) + 4 * E + E * w + 3 * V * w
-
-
-def algorithmic_bytes(V: int, E: int, nwp: int, work_rows: int, work_gathers: int) -> int:
-    """Bytes the activity-skipping kernel must move in one round (§8d with the
-    frontier gathers replaced by the kernel-counted active-row gathers):
-    row_ptr 8(V+1), col 4E, flags read V + per-edge sender flags E, flags
-    write V, gathered active sender rows work_gathers*w, and for each node
-    that does work: read base, write base, write F (3w)."""
-    w = 8 * nwp
-    return 8 * (V + 1) + 4 * E + 2 * V + E + work_gathers * w + 3 * work_rows * w
 
 
 def next_pow2(x: int) -> int:
@@ -151,17 +160,26 @@ def main():
     deliveries = sum(s["new_bits"] for ep in per_ep for s in ep)
     msgs = sum(s["fwd_sent"] + s["pushes"] + s["acks"] + s["reads"] + s["read_oks"]
                for s in per_ep[-1])
-    # roofline of the dominant kernel (expand_round) from the engine's HIP events
+    # roofline of the dominant kernel: per-kind device times (first block start
+    # to last block end of each launch, stamped by the kernels) and the bytes
+    # each launch had to move (counted by the kernels)
     lo, hi = eng.dist_range() if world > 1 else (0, V)
     E_own = int(topo.row_ptr[hi] - topo.row_ptr[lo])
     nwp = next_pow2(K // 64)
     rounds_local = [s for ep in local_stats for s in ep]
-    B_tot = sum(algorithmic_bytes(hi - lo, E_own, nwp, s["work_rows"], s["work_gathers"])
-                for s in rounds_local)
-    ms_tot = sum(s["kernel_ms"] for s in rounds_local)
-    avg_ms = ms_tot / len(rounds_local)
-    B = B_tot / len(rounds_local)
-    achieved = B_tot / (ms_tot * 1e-3) / 1e9
+    kinds = {}
+    for kind, name in KERNELS.items():
+        ms = sum(s[kind + "_ms"] for s in rounds_local)
+        by = sum(s[kind + "_bytes"] for s in rounds_local)
+        kinds[kind] = {"kernel": name, "launches": len(rounds_local), "total_ms": ms, "bytes": by,
+                       "avg_launch_ms": ms / len(rounds_local),
+                       "GBps": by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0}
+    dom = max(kinds, key=lambda k: kinds[k]["total_ms"])
+    D = kinds[dom]
+    achieved = D["GBps"]
+    traffic, traffic_src = pmc_traffic(D["kernel"])
+    round_ms = sum(s["kernel_ms"] for s in rounds_local)
+    round_bytes = sum(s["prep_bytes"] + s["expand_bytes"] + s["stream_bytes"] for s in rounds_local)
 
     if rank == 0:
         value = deliveries / elapsed
@@ -190,20 +208,25 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "expand_round",
+                "kernel": D["kernel"],
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
-                "algorithmic_bytes_per_launch": B,
-                "dense_bytes_per_launch": dense_bytes_per_round(hi - lo, E_own, nwp),
-                "avg_launch_ms": avg_ms,
-                "timing": "per round: device clock (s_memrealtime) from the first block start of "
-                          "round_prep to the last block end of expand_round; cross-check: HIP "
-                          "events around each step's launch sequence on the engine stream",
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": D["bytes"] / D["launches"],
+                "avg_launch_ms": D["avg_launch_ms"],
+                "launches": D["launches"],
+                "dense_bytes_per_round": dense_bytes_per_round(hi - lo, E_own, nwp),
+                "timing": "per launch: device clock (s_memrealtime) from the first block start to the last "
+                          "block end of that kernel, stamped by every block (no-op launches included, as in "
+                          "rocprofv3's average); cross-check: HIP events around each step's launch sequence "
+                          "on the engine stream",
+                "kernels": {k: {kk: v for kk, v in d.items()} for k, d in kinds.items()},
+                "round_GBps": round_bytes / (round_ms * 1e-3) / 1e9 if round_ms > 0 else 0.0,
                 "event_ms_per_step": (sum(event_ms) / len(event_ms)) if event_ms else None,
-                "stamp_ms_per_step": ms_tot / args.steps,
+                "stamp_ms_per_step": round_ms / args.steps,
             },
             "cpu_baseline": None,
         }

@@ -92,8 +92,10 @@ struct gg_engine {
     uint8_t* d_cand = nullptr;       // [rows] candidate bytes
     uint8_t* d_zmark = nullptr;      // [rows] stale-F-row marks
     uint8_t* d_tile_cand = nullptr;  // [tile_bytes]
-    gg::TileWork* d_work = nullptr;  // [tiles] live-tile worklist
-    uint32_t* d_n_work = nullptr;
+    gg::TileWork* d_work = nullptr;  // [tiles] live-tile worklist (sparse sync/mask rounds)
+    uint32_t* d_n_work = nullptr;    // [2] live tiles, candidate nodes
+    uint32_t* d_nodes = nullptr;     // [n_own] candidate-node list (sparse lean rounds)
+    uint32_t* d_act = nullptr;       // [4] ring: nodes that became active per round
     uint64_t tile_nodes = 0, tile_bytes = 0;
     uint64_t n_in_edges = 0;
     uint64_t* d_fired[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -159,6 +161,8 @@ void gg_engine::free_topology() {
     dfree(d_tile_cand);
     dfree(d_work);
     dfree(d_n_work);
+    dfree(d_nodes);
+    dfree(d_act);
     for (auto& p : d_fired) dfree(p);
     dfree(d_sync_next);
     dfree(d_sync_k);
@@ -195,6 +199,7 @@ int reset_device_state(gg_engine* e) {
     HIPCHK(hipMemsetAsync(e->d_cand, 0, e->rows, e->stream));
     HIPCHK(hipMemsetAsync(e->d_zmark, 0, e->rows, e->stream));
     HIPCHK(hipMemsetAsync(e->d_tile_cand, 0, e->tile_bytes, e->stream));
+    HIPCHK(hipMemsetAsync(e->d_act, 0, 4 * sizeof(uint32_t), e->stream));
     const uint64_t n_own = e->hi - e->lo;
     if (n_own) {
         hipLaunchKernelGGL(gg::sync_init, dim3((unsigned)((n_own + 255) / 256)), dim3(256), 0, e->stream,
@@ -263,20 +268,33 @@ void launch_expand(const gg::RoundArgs& a, bool syncw, bool maskw, hipStream_t s
     }
 }
 
-void launch_stream(const gg::RoundArgs& a, hipStream_t s) {
-    const uint32_t G = std::max<uint32_t>(1, a.nwp / 2);
+// expand_stream grid: one resident wave of blocks (node groups walk their
+// items grid-stride), so no partial second wave of blocks trails the round.
+template <int G>
+void launch_stream_t(const gg::RoundArgs& a, hipStream_t s) {
+    static int resident = 0;
+    if (!resident) {
+        int dev = 0, cus = 0, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gg::expand_stream<G, 2>, gg::kBlock, 0);
+        resident = std::max(1, cus) * std::max(1, per_cu);
+    }
     const uint64_t ngb = gg::kBlock / G;
     uint64_t blocks = (a.n_own + ngb - 1) / ngb;
-    blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, kMaxBlocks));
-    dim3 grid((unsigned)blocks), block(gg::kBlock);
+    blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)resident));
+    hipLaunchKernelGGL((gg::expand_stream<G, 2>), dim3((unsigned)blocks), dim3(gg::kBlock), 0, s, a);
+}
+
+void launch_stream(const gg::RoundArgs& a, hipStream_t s) {
     switch (a.nwp) {
-        case 2: hipLaunchKernelGGL((gg::expand_stream<1, 2>), grid, block, 0, s, a); break;
-        case 4: hipLaunchKernelGGL((gg::expand_stream<2, 2>), grid, block, 0, s, a); break;
-        case 8: hipLaunchKernelGGL((gg::expand_stream<4, 2>), grid, block, 0, s, a); break;
-        case 16: hipLaunchKernelGGL((gg::expand_stream<8, 2>), grid, block, 0, s, a); break;
-        case 32: hipLaunchKernelGGL((gg::expand_stream<16, 2>), grid, block, 0, s, a); break;
-        case 64: hipLaunchKernelGGL((gg::expand_stream<32, 2>), grid, block, 0, s, a); break;
-        case 128: hipLaunchKernelGGL((gg::expand_stream<64, 2>), grid, block, 0, s, a); break;
+        case 2: launch_stream_t<1>(a, s); break;
+        case 4: launch_stream_t<2>(a, s); break;
+        case 8: launch_stream_t<4>(a, s); break;
+        case 16: launch_stream_t<8>(a, s); break;
+        case 32: launch_stream_t<16>(a, s); break;
+        case 64: launch_stream_t<32>(a, s); break;
+        case 128: launch_stream_t<64>(a, s); break;
         default: break;
     }
 }
@@ -299,6 +317,8 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.tile_cand = e->d_tile_cand;
     a.work = e->d_work;
     a.n_work = e->d_n_work;
+    a.nodes = e->d_nodes;
+    a.act = e->d_act;
     a.tile_nodes = (uint32_t)e->tile_nodes;
     a.symmetric = e->symmetric ? 1 : 0;
     a.n_edges = e->n_in_edges;
@@ -332,14 +352,18 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.sync_base = e->cfg.sync_base_ticks;
     a.sync_jitter = e->cfg.sync_jitter_ticks;
     a.enable_sync = e->cfg.enable_sync;
-    // timers fire from round sync_base on; their reads/callbacks/pushes follow
-    const bool syncw = e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks;
+    // timers fire from round sync_base on (round_prep: timers, read_ok counts);
+    // the first callbacks and pushes reach the expand kernels two rounds later
+    const int64_t base = (int64_t)e->cfg.sync_base_ticks;
+    const bool syncw_prep = e->cfg.enable_sync && r >= base;
+    const bool syncw = e->cfg.enable_sync && r >= base + 2;
+    a.stream_ok = (!syncw && !maskw && e->nwp >= 2) ? 1 : 0;
 
     if (a.n_own) {
         {
             const uint64_t blocks = std::min<uint64_t>((a.n_own + gg::kBlock - 1) / gg::kBlock, 4096);
             dim3 grid((unsigned)blocks), block(gg::kBlock);
-            if (syncw) {
+            if (syncw_prep) {
                 if (maskw) hipLaunchKernelGGL((gg::round_prep<true, true>), grid, block, 0, e->stream, a);
                 else hipLaunchKernelGGL((gg::round_prep<true, false>), grid, block, 0, e->stream, a);
             } else {
@@ -353,18 +377,17 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             HIPCHK(hipGetLastError());
         }
         {
-            const uint64_t ntiles = (a.n_own + e->tile_nodes - 1) / e->tile_nodes;
-            const uint64_t groups = (ntiles + 7) / 8;
-            hipLaunchKernelGGL(gg::compact_tiles, dim3((unsigned)((groups + gg::kBlock - 1) / gg::kBlock)),
+            const uint64_t groups = (a.n_own + 7) / 8;  // >= tile groups
+            hipLaunchKernelGGL(gg::compact_round, dim3((unsigned)((groups + gg::kBlock - 1) / gg::kBlock)),
                                dim3(gg::kBlock), 0, e->stream, a);
             HIPCHK(hipGetLastError());
         }
-        launch_expand(a, syncw, maskw, e->stream);
-        HIPCHK(hipGetLastError());
-        if (!syncw && !maskw && e->nwp >= 2) {  // dense propagation rounds (decided on device)
+        if (a.stream_ok) {  // lean rounds: all nodes (dense) or the candidate list (sparse)
             launch_stream(a, e->stream);
-            HIPCHK(hipGetLastError());
+        } else {
+            launch_expand(a, syncw, maskw, e->stream);
         }
+        HIPCHK(hipGetLastError());
         if (e->d_dr) {
             const uint64_t n = a.n_own * e->nw;
             hipLaunchKernelGGL(gg::track_delivery, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream,
@@ -376,18 +399,32 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     return GG_OK;
 }
 
-// Host-side stats of one round from its 64 counter slots; kernel_ms from the
-// device clock stamps (first block start .. last block end, 100 MHz).
+// Host-side stats of one round from its 64 counter slots; per-kind times from
+// the device clock stamps (first block start .. last block end, 100 MHz).
 void fold_stats(gg_engine* e, const unsigned long long* slots, gg_round_stats* s) {
     unsigned long long c[gg::kCounters] = {0};
-    unsigned long long t0 = ~0ull, t1 = 0;
+    unsigned long long t0[gg::K_NKIND], t1[gg::K_NKIND];
+    for (int q = 0; q < gg::K_NKIND; ++q) t0[q] = ~0ull, t1[q] = 0;
     for (int k = 0; k < gg::kSlots; ++k) {
-        for (int j = 0; j < gg::C_NUM; ++j) c[j] += slots[k * gg::kCounters + j];
-        const unsigned long long si = slots[k * gg::kCounters + gg::C_TSTART_INV];
-        if (si) t0 = std::min(t0, ~si);
-        t1 = std::max(t1, slots[k * gg::kCounters + gg::C_TEND]);
+        for (int j = 0; j < gg::kCounters; ++j) c[j] += slots[k * gg::kCounters + j];
+        for (int q = 0; q < gg::K_NKIND; ++q) {
+            const unsigned long long si = slots[k * gg::kCounters + gg::kStamp0 + 2 * q];
+            if (si) t0[q] = std::min(t0[q], ~si);
+            t1[q] = std::max(t1[q], slots[k * gg::kCounters + gg::kStamp0 + 2 * q + 1]);
+        }
     }
-    const double ms = (t1 > t0 && t0 != ~0ull) ? (double)(t1 - t0) / 1.0e5 : 0.0;
+    auto span = [](unsigned long long a, unsigned long long b) {
+        return (b > a && a != ~0ull) ? (double)(b - a) / 1.0e5 : 0.0;
+    };
+    const unsigned long long ta = std::min(t0[gg::K_PREP], std::min(t0[gg::K_EXPAND], t0[gg::K_STREAM]));
+    const unsigned long long tb = std::max(t1[gg::K_PREP], std::max(t1[gg::K_EXPAND], t1[gg::K_STREAM]));
+    const double ms = span(ta, tb);
+    s->prep_ms = span(t0[gg::K_PREP], t1[gg::K_PREP]);
+    s->expand_ms = span(t0[gg::K_EXPAND], t1[gg::K_EXPAND]);
+    s->stream_ms = span(t0[gg::K_STREAM], t1[gg::K_STREAM]);
+    s->prep_bytes = c[gg::kBytes0 + gg::K_PREP];
+    s->expand_bytes = c[gg::kBytes0 + gg::K_EXPAND];
+    s->stream_bytes = c[gg::kBytes0 + gg::K_STREAM];
     s->round = e->round;
     s->new_bits = c[gg::C_NEW];
     s->fwd_sent = c[gg::C_FWD_SENT];
@@ -661,7 +698,9 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     HIPCHK(hipMalloc(&e->d_zmark, e->rows));
     HIPCHK(hipMalloc(&e->d_tile_cand, e->tile_bytes));
     HIPCHK(hipMalloc(&e->d_work, std::max<uint64_t>(1, ntiles) * sizeof(gg::TileWork)));
-    HIPCHK(hipMalloc(&e->d_n_work, 4));
+    HIPCHK(hipMalloc(&e->d_n_work, 2 * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&e->d_nodes, std::max<uint64_t>(1, n_own) * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&e->d_act, 4 * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->d_base, rowbytes));
     for (int b = 0; b < 2; ++b) {
         HIPCHK(hipMalloc(&e->d_F[b], rowbytes));

@@ -1,18 +1,23 @@
 // expand_kernels.hpp — the per-round gossip kernels for gfx950 (CDNA4).
 //
-// One lockstep round is two launches:
-//   round_prep   — one thread per node: the sync timer (`broadcast/main.go:42-51`,
-//                  `SyncBroadcast` reads, `broadcast.go:119-121`), the read_oks
-//                  that answer last round's reads (`HandleRead`, `:124-132`), and
-//                  *candidate marking*: a node can change this round only if a
-//                  sender of its in-list was active (or pushed) last round, it has
-//                  a deferred fold (LAG), a sync callback, or a client broadcast;
-//                  active senders mark their out-lists (single-engine mode).
-//   expand_round — the device form of HandleBroadcast (`:59-79`) +
-//                  rebroadcastAllExcept (`:50-57`) + the SyncBroadcast callback
-//                  (`:82-117`) for every candidate node, in the determinized order
-//                  of DESIGN.md §2 (client broadcasts, node broadcasts by ascending
-//                  sender, read_ok callbacks by ascending peer).
+// One lockstep round is three launches on one stream (captured in a hipGraph):
+//   round_prep    — one thread per node: the sync timer (`broadcast/main.go:42-51`,
+//                   `SyncBroadcast` reads, `broadcast.go:119-121`), the read_oks
+//                   that answer last round's reads (`HandleRead`, `:124-132`), and
+//                   in sparse rounds *candidate marking*: a node can change this
+//                   round only if a sender of its in-list was active (or pushed)
+//                   last round, it has a deferred fold (LAG), a sync callback, or a
+//                   client broadcast; active senders mark their out-lists.
+//   expand_round  — the device form of HandleBroadcast (`:59-79`) +
+//                   rebroadcastAllExcept (`:50-57`) + the SyncBroadcast callback
+//                   (`:82-117`) for every candidate node, in the determinized
+//                   order of DESIGN.md §2 (client broadcasts, node broadcasts by
+//                   ascending sender, read_ok callbacks by ascending peer).
+//   expand_stream — the same for *dense* lean rounds, over every node.
+// Which of expand_round / expand_stream works (the other exits at once) is
+// decided on the device from the number of nodes that became active in the
+// previous round (dense_round), so one captured launch sequence serves every
+// round shape.
 //
 // State: `base` holds every node's set *in place*; F[r&1] holds
 // the bits a node learned in round r (what it forwards in r+1), valid only
@@ -22,17 +27,17 @@
 //     set(u) = base[u] | (LAG(u) ? F_prev[u] : 0)
 // and idle nodes move no row.
 //
-// Work mapping of expand_round: the live tiles (NG = 256/G consecutive nodes
-// with at least one candidate) are compacted into a worklist (compact_tiles)
-// and dealt round-robin to blocks. For a live tile the CSR slice (row_ptr, col)
-// is staged in LDS with coalesced loads in one round trip (the worklist entry
-// carries the tile's edge range), plus per-sender flags unless the round is
-// dense and lean (then flags and rows are gathered together); a *node group* of G lanes owns one node, lane l holding
-// words [l*WPL, l*WPL+WPL) of its set (16-byte accesses for WPL = 2). Pass 1
-// compacts the node's contributing senders in LDS; pass 2 gathers their rows 4
-// at a time and runs the claim chain (first deliverer, ascending sender) in
-// registers. Counters are linear in per-lane popcounts: summed per lane,
-// reduced once per block, added to one of 64 counter slots.
+// Work mapping of expand_round: tiles of NG = 256/G consecutive nodes; each
+// block examines tiles blockIdx.x + k*gridDim.x 64 at a time (their candidate
+// flags, set by round_prep / mark_injections), compacts the live ones with
+// their edge ranges in LDS, and for each stages the CSR slice (row_ptr, col)
+// plus per-sender flags in LDS with coalesced loads; a *node group* of G lanes
+// owns one node, lane l holding words [l*WPL, l*WPL+WPL) of its set (16-byte
+// accesses for WPL = 2). Pass 1 compacts the node's contributing senders in
+// LDS; pass 2 gathers their rows 4 at a time and runs the claim chain (first
+// deliverer, ascending sender) in registers. Counters are linear in per-lane
+// popcounts: summed per lane, reduced once per block, added to one of 64
+// counter slots.
 //
 // Memory-bound, no MFMA: HBM traffic per round is the active senders' rows,
 // the changed nodes' base/F rows, and the CSR of candidate tiles.
@@ -56,7 +61,7 @@ namespace gg {
 #define GG_STREAM_ROWS 6
 #endif
 #ifndef GG_STREAM_WAVES_PER_EU
-#define GG_STREAM_WAVES_PER_EU 6
+#define GG_STREAM_WAVES_PER_EU 5
 #endif
 constexpr int kStreamRows = GG_STREAM_ROWS;
 
@@ -67,7 +72,7 @@ constexpr int kStreamRows = GG_STREAM_ROWS;
 
 constexpr int kBlock = 256;
 constexpr int kSlots = 64;       // counter slots
-constexpr int kCounters = 16;    // per slot
+constexpr int kCounters = 32;    // per slot
 constexpr int kEdgeStage = 2048; // in-edges staged in LDS per tile
 constexpr uint32_t kColMask = 0x7fffffffu;
 constexpr uint32_t kRecipBit = 0x80000000u;
@@ -82,12 +87,20 @@ constexpr uint8_t CA_NODE = 1, CA_INJ = 2;
 
 enum Counter : int {
     C_NEW = 0, C_FWD_SENT, C_FWD_DELIV, C_PUSH, C_PUSH_DELIV, C_READS, C_READ_OKS,
-    C_DROPPED, C_FIRED, C_HASH, C_NEXT_ACKS, C_NEXT_ACKDROP, C_ACTIVE, C_GATHERS, C_NUM
+    C_DROPPED, C_FIRED, C_HASH, C_NEXT_ACKS, C_NEXT_ACKDROP, C_ACTIVE, C_GATHERS,
+    C_NACT,   // nodes that became active (ACT) this round: next round's dense/sparse choice
+    C_BYTES,  // algorithmic bytes the launch had to move, per kernel kind
+    C_NUM
 };
-// per-slot device clock stamps (s_memrealtime, 100 MHz): ~first block start
-// (stored complemented, so a max of zero-initialised slots gives the min) and
-// last block end of the round's kernels
-constexpr int C_TSTART_INV = 14, C_TEND = 15;
+// Kernel kinds with their own device clock stamps (s_memrealtime, 100 MHz) per
+// counter slot: first block start (stored complemented, so a max over
+// zero-initialised slots gives the min) and last block end. Every block of
+// every launch stamps, no-op exits included, so a kind's time per round is
+// comparable with rocprofv3's dispatch durations.
+enum Kind : int { K_PREP = 0, K_EXPAND = 1, K_STREAM = 2, K_NKIND = 3 };
+constexpr int kStamp0 = 20;  // stamps at kStamp0 + 2*kind (+0 start~, +1 end)
+constexpr int kBytes0 = 26;  // C_BYTES of each kind lands at kBytes0 + kind
+static_assert(C_NUM <= kStamp0 && kStamp0 + 2 * K_NKIND <= kBytes0 && kBytes0 + K_NKIND <= kCounters, "slot layout");
 
 __device__ __forceinline__ unsigned long long clock100() { return __builtin_amdgcn_s_memrealtime(); }
 
@@ -109,9 +122,11 @@ struct RoundArgs {
     uint8_t* flg_cur;
     uint8_t* cand;              // [rows] candidate bytes of this round (cleared by expand)
     uint8_t* zmark;             // [rows] F row of this parity is stale (node active 2 rounds ago)
-    uint8_t* tile_cand;         // [n_tiles rounded to 8] tile has a candidate
-    struct TileWork* work;      // live tiles of the round (compact_tiles)
-    uint32_t* n_work;           // number of live tiles
+    uint8_t* tile_cand;         // [n_tiles rounded to 8] tile has a candidate (sparse rounds)
+    struct TileWork* work;      // live tiles of a sparse round (compact_round; expand_round)
+    uint32_t* n_work;           // [2]: live tiles, candidate nodes
+    uint32_t* nodes;            // candidate nodes of a sparse lean round (compact_round; expand_stream)
+    uint32_t* act;              // [4] ring: nodes that became active in round r (slot r&3)
     const uint64_t* fired_m1;   // sync-fired bitmaps of rounds r-1, r-2, r-3
     const uint64_t* fired_m2;
     const uint64_t* fired_m3;
@@ -129,6 +144,8 @@ struct RoundArgs {
     uint64_t n_edges;           // in_col entries of this engine
     uint64_t rows;              // replica rows
     int32_t mark_all;           // sharded engines: every owned node is a candidate
+    int32_t stream_ok;          // lean round (no sync events in expand, no masks) with nwp >= 2:
+                                // expand_stream takes it when it is dense (dense_round)
     uint32_t ablate;            // DIAGNOSTIC timing builds only (GG_ABLATE): 1 no row stores,
                                 // 2 no sender-row gathers, 4 no own-row loads, 8 no hash; results invalid
     int64_t round;
@@ -178,6 +195,19 @@ __device__ __forceinline__ void store_row(uint64_t* p, const Row<WPL>& r) {
 __device__ __forceinline__ bool bit_at(const uint64_t* bm, uint64_t row) {
     return (bm[row >> 6] >> (row & 63)) & 1ull;
 }
+
+// Most nodes are candidates this round: the nodes that became active in r-1
+// times the mean out-degree cover at least half of the owned nodes (sharded
+// engines: always, since remote senders cannot mark). Read from the act ring,
+// which no kernel of round r writes, so every launch of the round agrees.
+__device__ __forceinline__ bool busy_round(const RoundArgs& a) {
+    if (a.mark_all) return true;
+    const double act = (double)a.act[(a.round - 1) & 3];
+    return 2.0 * act * (double)a.n_edges >= (double)a.n_own * (double)a.n_own;
+}
+// Dense lean round: expand_stream visits every node, round_prep marks nothing
+// and expand_round exits.
+__device__ __forceinline__ bool dense_round(const RoundArgs& a) { return a.stream_ok && busy_round(a); }
 
 // message from replica row ra to replica row rb in round (r-3+k) dropped?
 template <bool MASKW>
@@ -250,8 +280,20 @@ __device__ __forceinline__ void dma16(const void* src, const void* lds_wave_base
                  : "memory");
 }
 
+__device__ __forceinline__ void stamp(const RoundArgs& a, int kind, unsigned long long t_start) {
+    unsigned long long* slot = a.counters + (blockIdx.x % kSlots) * kCounters + kStamp0 + 2 * kind;
+    atomicMax(slot, ~t_start);
+    atomicMax(slot + 1, clock100());
+}
+
+// A launch with nothing to do this round (the other kernel kind takes it).
+__device__ __forceinline__ void noop_exit(const RoundArgs& a, int kind, unsigned long long t_start) {
+    if (threadIdx.x == 0) stamp(a, kind, t_start);
+}
+
 __device__ __forceinline__ void flush_counters(const RoundArgs& a, unsigned long long (&acc)[C_NUM],
-                                               unsigned long long (*s_red)[C_NUM], unsigned long long t_start) {
+                                               unsigned long long (*s_red)[C_NUM], unsigned long long t_start,
+                                               int kind) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
     for (int k = 0; k < C_NUM; ++k) {
@@ -263,61 +305,86 @@ __device__ __forceinline__ void flush_counters(const RoundArgs& a, unsigned long
         unsigned long long s = 0;
 #pragma unroll
         for (int w = 0; w < kBlock / 64; ++w) s += s_red[w][threadIdx.x];
-        if (s) atomicAdd(&a.counters[(blockIdx.x % kSlots) * kCounters + threadIdx.x], s);
+        const int idx = threadIdx.x == C_BYTES ? kBytes0 + kind : (int)threadIdx.x;
+        if (s) atomicAdd(&a.counters[(blockIdx.x % kSlots) * kCounters + idx], s);
+        if (threadIdx.x == C_NACT && s) atomicAdd(&a.act[a.round & 3], (uint32_t)s);
     }
-    if (threadIdx.x == 0) {
-        unsigned long long* slot = a.counters + (blockIdx.x % kSlots) * kCounters;
-        atomicMax(slot + C_TSTART_INV, ~t_start);
-        atomicMax(slot + C_TEND, clock100());
-    }
+    if (threadIdx.x == 0) stamp(a, kind, t_start);
 }
 
 // ---------------------------------------------------------------------------
 // round_prep: one thread per owned node (64 consecutive nodes per wave, so a
-// wave owns whole words of the fired bitmap).
+// wave owns whole words of the fired bitmap). In dense rounds the per-node
+// flag/stale-row work moves into expand_stream and no candidates are marked,
+// so without sync timers the launch is a no-op.
 template <bool SYNCW, bool MASKW>
 __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
     __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
     const unsigned long long t_start = clock100();
-    unsigned long long c_reads = 0, c_read_oks = 0, c_dropped = 0, c_fired = 0;
+    const bool dense = dense_round(a);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.act[(a.round + 1) & 3] = 0;  // next round's act slot
+        a.n_work[0] = a.n_work[1] = 0;  // compact_round runs after this kernel
+    }
+    if (!SYNCW && dense) {
+        noop_exit(a, K_PREP, t_start);
+        return;
+    }
+    unsigned long long c_reads = 0, c_read_oks = 0, c_dropped = 0, c_fired = 0, c_bytes = 0;
     const uint64_t nwords = (a.n_own + 63) / 64;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *a.n_work = 0;  // compact_tiles runs after this kernel
     for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < nwords * 64; t += stride) {
         const uint64_t i = t;
         const bool valid = i < a.n_own;
         const uint64_t rep = a.own0 + i;
         bool fire = false;
         if (valid) {
-            const uint8_t f = a.flg_prev[rep];
-            // flg_cur still holds round r-2's flags: an F row written then is
-            // stale in this round's F buffer; expand zeroes it unless the node
-            // writes a new one, so F rows stay zero for inactive nodes.
-            if (a.flg_cur[rep] & FL_ACT) {
-                a.zmark[rep] = 1;
-                a.tile_cand[i / a.tile_nodes] = 1;
-            }
-            a.flg_cur[rep] = 0;  // expand_round sets the flags of changed nodes
-            const int64_t o0 = a.out_ptr[i], o1 = a.out_ptr[i + 1];
+            int64_t o0 = 0, o1 = 0;
             bool fm1 = false, fm2 = false, fm3 = false;
             if constexpr (SYNCW) {
                 fm1 = bit_at(a.fired_m1, rep);
                 fm2 = bit_at(a.fired_m2, rep);
                 fm3 = bit_at(a.fired_m3, rep);
             }
-            // candidates of this round
-            if (a.mark_all || (f & FL_LAG) || fm2) {
-                a.cand[rep] = CA_NODE;
-                a.tile_cand[i / a.tile_nodes] = 1;
-            }
-            if (!a.mark_all && ((f & FL_ACT) || fm3)) {  // senders mark their receivers
-                for (int64_t e = o0; e < o1; ++e) {
-                    const uint64_t w = a.out_col[e] & kColMask;  // single engine: w == local row
-                    a.cand[w] = CA_NODE;
-                    a.tile_cand[(w - a.own0) / a.tile_nodes] = 1;
+            if (!dense) {
+                const uint8_t f = a.flg_prev[rep];
+                // flg_cur still holds round r-2's flags: an F row written then is
+                // stale in this round's F buffer; the expand kernel zeroes it unless
+                // the node writes a new one, so F rows stay zero for inactive nodes.
+                if (a.stream_ok) {
+                    // sparse lean round: expand_stream takes the node (it reads and
+                    // rewrites the old flag byte itself); no tile flags (node list)
+                    if (a.flg_cur[rep] & FL_ACT) a.cand[rep] = CA_NODE;
+                    c_bytes += 2;
+                } else {
+                    if (a.flg_cur[rep] & FL_ACT) {
+                        a.zmark[rep] = 1;
+                        a.tile_cand[i / a.tile_nodes] = 1;
+                    }
+                    a.flg_cur[rep] = 0;  // expand_round sets the flags of changed nodes
+                    c_bytes += 3;
+                }
+                // candidates of this round
+                if (a.mark_all || (f & FL_LAG) || fm2) {
+                    a.cand[rep] = CA_NODE;
+                    if (!a.stream_ok) a.tile_cand[i / a.tile_nodes] = 1;
+                }
+                if (!a.mark_all && ((f & FL_ACT) || fm3)) {  // senders mark their receivers
+                    o0 = a.out_ptr[i];
+                    o1 = a.out_ptr[i + 1];
+                    c_bytes += 16 + 5 * (unsigned long long)(o1 - o0);
+                    for (int64_t e = o0; e < o1; ++e) {
+                        const uint64_t w = a.out_col[e] & kColMask;  // single engine: w == local row
+                        a.cand[w] = CA_NODE;
+                        if (!a.stream_ok) a.tile_cand[(w - a.own0) / a.tile_nodes] = 1;
+                    }
                 }
             }
             if constexpr (SYNCW) {
+                if (fm1 || (int64_t)a.sync_next[i] == a.round) {
+                    o0 = a.out_ptr[i];
+                    o1 = a.out_ptr[i + 1];
+                }
                 // reads v sent in r-1 arrive now; each answered by a read_ok (:131)
                 if (fm1) {
                     for (int64_t e = o0; e < o1; ++e) {
@@ -328,6 +395,7 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                     }
                 }
                 // (5) the sync timer (main.go:42-51): read RPC to every neighbour (:119-121)
+                c_bytes += 4;
                 if ((int64_t)a.sync_next[i] == a.round) {
                     fire = true;
                     c_fired++;
@@ -343,8 +411,10 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                 }
             }
         }
-        const unsigned long long word = __ballot(fire);
-        if ((threadIdx.x & 63) == 0) a.fired_cur[(a.own0 + (i & ~63ull)) >> 6] = word;
+        if constexpr (SYNCW) {  // before the first timer every fired word is still zero
+            const unsigned long long word = __ballot(fire);
+            if ((threadIdx.x & 63) == 0) a.fired_cur[(a.own0 + (i & ~63ull)) >> 6] = word;
+        }
     }
     unsigned long long acc[C_NUM];
 #pragma unroll
@@ -353,7 +423,8 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
     acc[C_READ_OKS] = c_read_oks;
     acc[C_DROPPED] = c_dropped;
     acc[C_FIRED] = c_fired;
-    flush_counters(a, acc, s_red, t_start);
+    acc[C_BYTES] = c_bytes;
+    flush_counters(a, acc, s_red, t_start, K_PREP);
 }
 
 // Client broadcasts of this round mark their nodes (after round_prep).
@@ -361,24 +432,44 @@ __global__ void mark_injections(RoundArgs a) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= a.n_inj) return;
     const uint64_t i = a.inj[2 * k];
-    a.cand[a.own0 + i] = CA_NODE | CA_INJ;
-    a.tile_cand[i / a.tile_nodes] = 1;
+    a.cand[a.own0 + i] |= CA_NODE | CA_INJ;  // same value from every thread of a node
+    if (!a.stream_ok) a.tile_cand[i / a.tile_nodes] = 1;  // lean rounds use the node list
 }
 
-// Live tiles -> worklist (order irrelevant: tiles are independent and counters
-// are sums). 8 tile flags per thread; clears the flags for the next round.
-__global__ __launch_bounds__(kBlock) void compact_tiles(RoundArgs a) {
+// Sparse rounds: the candidate nodes -> node list (lean rounds, expand_stream;
+// node-granular, so every node group gets the same share; one thread per 8
+// candidate bytes, a coalesced pass over them), or the live tiles -> work list
+// (expand_round; 8 tile flags per thread, cleared for the next round). Order is
+// irrelevant: nodes/tiles are independent within a round and the counters are sums.
+__global__ __launch_bounds__(kBlock) void compact_round(RoundArgs a) {
     __shared__ uint32_t s_cnt[kBlock / 64];
     __shared__ uint32_t s_base;
-    const uint64_t ntiles = (a.n_own + a.tile_nodes - 1) / a.tile_nodes;
-    const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;  // 8-tile group
-    unsigned long long tb = 0;
-    if (q * 8 < ntiles) {
-        tb = *reinterpret_cast<const unsigned long long*>(a.tile_cand + q * 8);
-        if (tb) *reinterpret_cast<unsigned long long*>(a.tile_cand + q * 8) = 0ull;
+    const unsigned long long t_start = clock100();
+    if (dense_round(a)) {
+        noop_exit(a, K_PREP, t_start);
+        return;
     }
+    const bool nodes = a.stream_ok != 0;
+    const uint64_t NG = a.tile_nodes;
+    const uint64_t ntiles = (a.n_own + NG - 1) / NG;
+    const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;  // 8-byte group
+    unsigned long long x = 0;  // 8 candidate bytes (nodes) or 8 tile flags (tiles)
     uint32_t c = 0;
-    for (int t = 0; t < 8; ++t) c += ((tb >> (8 * t)) & 0xff) ? 1u : 0u;
+    if (nodes) {
+        const uint64_t n = q * 8;
+        if (n + 8 <= a.n_own) {  // own0 is a multiple of 64: aligned
+            x = *reinterpret_cast<const unsigned long long*>(a.cand + a.own0 + n);
+        } else {
+            for (uint64_t k = n; k < a.n_own; ++k) x |= (unsigned long long)a.cand[a.own0 + k] << (8 * (k - n));
+        }
+    } else if (q * 8 < ntiles) {
+        x = *reinterpret_cast<const unsigned long long*>(a.tile_cand + q * 8);
+        if (x) *reinterpret_cast<unsigned long long*>(a.tile_cand + q * 8) = 0ull;
+    }
+    {
+        const unsigned long long lo7 = 0x7f7f7f7f7f7f7f7full;
+        c = (uint32_t)__popcll((((x & lo7) + lo7) | x) & ~lo7);  // non-zero bytes
+    }
     // block exclusive scan of c
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t incl = c;
@@ -392,25 +483,30 @@ __global__ __launch_bounds__(kBlock) void compact_tiles(RoundArgs a) {
     if (threadIdx.x == 0) {
         uint32_t tot = 0;
         for (int w = 0; w < kBlock / 64; ++w) {
-            const uint32_t x = s_cnt[w];
+            const uint32_t v = s_cnt[w];
             s_cnt[w] = tot;
-            tot += x;
+            tot += v;
         }
-        s_base = tot ? atomicAdd(a.n_work, tot) : 0u;
+        s_base = tot ? atomicAdd(&a.n_work[nodes ? 1 : 0], tot) : 0u;
     }
     __syncthreads();
     uint32_t pos = s_base + s_cnt[wave] + incl - c;
     for (int t = 0; t < 8; ++t) {
-        if (!((tb >> (8 * t)) & 0xff)) continue;
-        const uint64_t tile = q * 8 + t;
-        const uint64_t n0 = tile * a.tile_nodes;
-        const uint64_t n1 = n0 + a.tile_nodes < a.n_own ? n0 + a.tile_nodes : a.n_own;
-        TileWork w;
-        w.tile = (uint32_t)tile;
-        w.eb = a.in_ptr[n0];
-        w.ne = (uint32_t)(a.in_ptr[n1] - w.eb);
-        a.work[pos++] = w;
+        if (!((x >> (8 * t)) & 0xff)) continue;
+        if (nodes) {
+            a.nodes[pos++] = (uint32_t)(q * 8 + t);
+        } else {
+            const uint64_t tile = q * 8 + t;
+            const uint64_t n0 = tile * NG;
+            const uint64_t n1 = n0 + NG < a.n_own ? n0 + NG : a.n_own;
+            TileWork w;
+            w.tile = (uint32_t)tile;
+            w.eb = a.in_ptr[n0];
+            w.ne = (uint32_t)(a.in_ptr[n1] - w.eb);
+            a.work[pos++] = w;
+        }
     }
+    if (threadIdx.x == 0) stamp(a, K_PREP, t_start);
 }
 
 // ---------------------------------------------------------------------------
@@ -421,13 +517,10 @@ template <int G, int WPL, bool SYNCW, bool MASKW>
 __device__ __forceinline__ void expand_body(const RoundArgs& a) {
     constexpr int NG = kBlock / G;  // nodes per tile
     constexpr int kBatch = 4;       // flags-first: contributing rows in flight per lane
-    constexpr int kSpec = GG_SPEC_BATCH;  // dense lean rounds: (flag, row) pairs in flight per lane
+    constexpr int kSpec = GG_SPEC_BATCH;  // busy lean rounds (W = 64): (flag, row) pairs in flight per lane
     constexpr int kPre = 64;        // worklist entries preloaded per chunk
     constexpr bool LEAN = !SYNCW && !MASKW;
-    constexpr int kDmaRows = 6;     // dense lean rounds: sender rows in flight per lane (via LDS)
     constexpr uint8_t L_PUSH = 1, L_LAG = 2;  // compacted-list flags
-    // per-wave LDS landing slots of the dense lean path (kDmaRows x 1 KiB per wave)
-    __shared__ __attribute__((aligned(16))) uint8_t s_rows[(LEAN && WPL == 2) ? 4 * kDmaRows * 1024 : 16];
     __shared__ int64_t s_ptr[NG + 1];
     __shared__ uint32_t s_col[kEdgeStage];
     __shared__ uint8_t s_ef[kEdgeStage];
@@ -441,27 +534,21 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
     const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
     const unsigned long long t_start = clock100();
     // always-live counters
-    unsigned long long c_new = 0, c_fwd = 0, c_hash = 0, c_active = 0, c_gathers = 0;
+    unsigned long long c_new = 0, c_fwd = 0, c_hash = 0, c_active = 0, c_gathers = 0, c_nact = 0, c_bytes = 0;
     // MASKW-only
     unsigned long long c_fwd_deliv = 0, c_push_deliv = 0, c_dropped = 0, c_next_ackdrop = 0;
     // SYNCW-only
     unsigned long long c_push = 0;
 
-    const uint64_t n_work = *a.n_work;
-    const uint64_t ntiles = (a.n_own + NG - 1) / NG;
-    // most tiles live: load sender flags together with their rows (speculative
-    // gathers; a row of an inactive sender is ignored) instead of flags first
-    const bool dense = LEAN && n_work * 2 > ntiles;
-    if constexpr (LEAN && WPL == 2) {
-        if (dense) {  // expand_stream runs this round
-            unsigned long long acc[C_NUM];
-#pragma unroll
-            for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
-            flush_counters(a, acc, s_red, t_start);
-            return;
-        }
+    if (LEAN && a.stream_ok) {  // expand_stream takes every lean round with nwp >= 2
+        noop_exit(a, K_EXPAND, t_start);
+        return;
     }
+    // busy lean round (W = 64): load sender flags together with their rows
+    // (speculative gathers; a row of an inactive sender is zero) instead of flags first
+    const bool dense = LEAN && busy_round(a);
 
+    const uint64_t n_work = *a.n_work;
     for (uint64_t base = blockIdx.x; base < n_work; base += (uint64_t)kPre * gridDim.x) {
         if (threadIdx.x < kPre) {
             const uint64_t idx = base + (uint64_t)threadIdx.x * gridDim.x;
@@ -490,6 +577,8 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                 s_col[k] = c;
                 if (!dense) s_ef[k] = sender_flags<SYNCW>(a, c & kColMask);
             }
+            // row_ptr + col (+ one sender flag byte per edge) + per-node cand/zmark/flag bytes
+            if (threadIdx.x == 0) c_bytes += 8ull * (NG + 1) + (dense ? 4ull : 5ull) * tw.ne + 3ull * NG;
             lds_barrier();
 
             if (zm && !ca) {  // only the stale F row to clear
@@ -499,9 +588,13 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                     for (int w = 0; w < WPL; ++w) z.w[w] = 0;
                     store_row<WPL>(a.F_cur + rep * a.nwp + off, z);
                 }
-                if (lg == 0) a.zmark[rep] = 0;
+                if (lg == 0) {
+                    a.zmark[rep] = 0;
+                    c_bytes += 8ull * a.nwp;
+                }
             }
             if (ca) {
+                unsigned long long nrows = 0, nextra = 0;  // rows moved / other bytes for this node
                 if (lg == 0) a.cand[rep] = 0;
                 const int64_t k0 = s_ptr[j] - eb, k1 = s_ptr[j + 1] - eb;
                 const bool staged = k1 <= ns;  // else: hub slow path straight from global
@@ -529,6 +622,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                         for (int w = 0; w < WPL; ++w) sp.w[w] |= f.w[w];
                     }
                     S = sp;
+                    nrows += lag ? 2 : 1;
                     // (1) client broadcasts of this round
                     if (has_inj) {
                         uint32_t lo = 0, hi = a.n_inj;
@@ -581,39 +675,9 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                 if (dense) {
                     // ---- lean dense path: own row + (flag, row) of every sender.
                     load_own();
-                    if constexpr (WPL == 2) {
-                        // Each lane DMAs its own 16-byte chunk of kDmaRows sender rows
-                        // into its wave's LDS slots (global_load_lds_dwordx4: LDS
-                        // address = wave-uniform base + lane*16), waits vmcnt, and
-                        // reads back exactly what it loaded: in-flight rows cost
-                        // LDS, not VGPRs, and no other wave touches the slots.
-                        uint8_t* const my = &s_rows[(threadIdx.x >> 6) * kDmaRows * 1024];
-                        const uint32_t lane16 = (threadIdx.x & 63) * 16;
-                        for (int64_t k = k0; k < k1; k += kDmaRows) {
-                            uint32_t cb[kDmaRows];
-#pragma unroll
-                            for (int b = 0; b < kDmaRows; ++b) {
-                                const bool v = k + b < k1;
-                                cb[b] = v ? (k + b < ns ? s_col[k + b] : a.in_col[eb + k + b]) : 0u;
-                                const uint64_t u = cb[b] & kColMask;
-                                if (v && !(a.ablate & 2))
-                                    dma16((const void*)(a.F_prev + u * a.nwp + off), my + b * 1024);
-                            }
-                            vm_drain();
-                            // F rows of inactive senders are zero: claim every row
-#pragma unroll
-                            for (int b = 0; b < kDmaRows; ++b) {
-                                if (k + b < k1) {
-                                    const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(my + b * 1024 + lane16);
-                                    Row<WPL> src;
-                                    src.w[0] = x.x;
-                                    src.w[1 % WPL] = x.y;
-                                    claim(src, cb[b]);
-                                    c_gathers += (lg == 0) ? 1ull : 0ull;
-                                }
-                            }
-                        }
-                    } else {
+                    nrows += (unsigned long long)(k1 - k0);  // every sender row and flag byte
+                    nextra += (unsigned long long)(k1 - k0);
+                    {
                         for (int64_t k = k0; k < k1; k += kSpec) {
                             uint32_t cb[kSpec];
                             uint8_t fb[kSpec];
@@ -674,6 +738,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                         load_own();
                         if (staged) {
                             c_gathers += (lg == 0) ? (unsigned long long)m : 0ull;
+                            nrows += (unsigned long long)m;
                             for (int b0 = 0; b0 < m; b0 += kBatch) {
                                 uint32_t cb[kBatch];
                                 Row<WPL> src[kBatch];
@@ -701,6 +766,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                                 const bool p = is_push<SYNCW, MASKW>(a, ef, u, rep);
                                 if (!(ef & SE_ACT) && !p) continue;
                                 c_gathers += (lg == 0) ? 1ull : 0ull;
+                                nrows++;
                                 claim(sender_row(c, p, (ef & SE_LAG) != 0), c);
                             }
                         }
@@ -713,6 +779,8 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                                     if (masked<MASKW>(a, 1, rep, w) || masked<MASKW>(a, 2, w, rep)) continue;
                                     const Row<WPL> R =
                                         sender_row((uint32_t)w, true, (a.flg_prev[w] & FL_LAG) != 0);
+                                    nrows++;
+                                    nextra += 13;  // out_col + flag
                                     unsigned long long pn = 0, pp = 0;
 #pragma unroll
                                     for (int q2 = 0; q2 < WPL; ++q2) {
@@ -753,13 +821,17 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                     const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
                     if ((any || zm) && !(a.ablate & 1)) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
                     if (zm && lg == 0) a.zmark[rep] = 0;
+                    nrows += (any || zm) ? 1 : 0;
                     if (a.ablate & 1) {
                     } else if (keep) {
                         if (lag) store_row<WPL>(a.base + rep * a.nwp + off, sp);
+                        nrows += lag ? 1 : 0;
                     } else if (any || lag) {
                         store_row<WPL>(a.base + rep * a.nwp + off, S);
+                        nrows++;
                     }
                     if (lg == 0 && any) a.flg_cur[rep] = (uint8_t)(FL_ACT | (keep ? FL_LAG : 0));
+                    c_nact += (lg == 0 && any) ? 1ull : 0ull;
 
                     // messages v sends in round r (rebroadcastAllExcept :50-57, pushes :106)
                     const unsigned long long fs = deg * T - cl_recip - cb_new;
@@ -786,6 +858,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                         c_next_ackdrop += AD * T - cl_ackdrop - cb_new_ackdrop + push_ackdrop;
                     }
                 }
+                if (lg == 0) c_bytes += nrows * 8ull * a.nwp + nextra + 16;  // + out_ptr
             }
             lds_barrier();  // LDS reuse by the next tile
         }
@@ -811,7 +884,9 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
     acc[C_NEXT_ACKDROP] = c_next_ackdrop;
     acc[C_ACTIVE] = c_active;
     acc[C_GATHERS] = c_gathers;
-    flush_counters(a, acc, s_red, t_start);
+    acc[C_NACT] = c_nact;
+    acc[C_BYTES] = c_bytes;
+    flush_counters(a, acc, s_red, t_start, K_EXPAND);
 }
 
 template <int G, int WPL, bool SYNCW, bool MASKW>
@@ -827,13 +902,17 @@ void expand_round_lean(RoundArgs a) {
 
 
 // ---------------------------------------------------------------------------
-// expand_stream: the dense propagation round (no sync events, no masks, most
-// tiles live). No tiles, no barriers: node group q (G lanes) walks nodes
-// q, q + n_groups, ... with a software pipeline — while node i's own row and
-// sender rows land in its wave's LDS slots by DMA, node i+1's column list and
-// node i+2's row pointers and bytes are already in flight — so each node
-// costs about one memory round trip. F rows of inactive senders are zero, so
-// every sender row is claimed without looking at sender flags.
+// expand_stream: every lean round (no sync events in expand, no masks) with
+// nwp >= 2. Dense rounds (dense_round) visit EVERY node; sparse ones the
+// candidate-node list of compact_round. No tiles, no barriers: node group q (G
+// lanes) walks items q, q + n_groups, ... with a software pipeline — while
+// item k's own row and sender rows land in its wave's LDS slots by DMA, item
+// k+1's column list, item k+2's row pointers and bytes and item k+3's list
+// entry are already in flight — so each node costs about one memory round
+// trip. F rows of inactive senders are zero, so every sender row is claimed
+// without looking at sender flags, and a node nobody reached finds no new
+// bits. The node-local part of round_prep (stale F row of round r-2, flag
+// reset) is done here from the node's old flag byte.
 template <int G, int WPL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GG_STREAM_WAVES_PER_EU)))
 void expand_stream(RoundArgs a) {
@@ -843,166 +922,178 @@ void expand_stream(RoundArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t s_slots[(kBlock / 64) * (D + 1) * 1024];
     __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
     const unsigned long long t_start = clock100();
-    unsigned long long c_new = 0, c_fwd = 0, c_hash = 0, c_active = 0, c_gathers = 0;
+    if (!a.stream_ok) {
+        noop_exit(a, K_STREAM, t_start);
+        return;
+    }
+    const bool dense = dense_round(a);
+    const uint32_t n_items = dense ? (uint32_t)a.n_own : a.n_work[1];
+    // per-lane counts that fit 32 bits stay 32-bit (register budget)
+    uint32_t c_new = 0, c_active = 0, c_gathers = 0, c_nact = 0;
+    unsigned long long c_fwd = 0, c_hash = 0, c_bytes = 0;
+    const int lg = threadIdx.x % G;
+    const uint32_t off = (uint32_t)lg * WPL;
+    const int gshift = (threadIdx.x & 63) / G * G;
+    const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+    uint8_t* const my = &s_slots[(threadIdx.x >> 6) * (D + 1) * 1024];
+    const uint32_t lane16 = (threadIdx.x & 63) * 16;
+    const uint32_t stride = gridDim.x * NGB;
+    const unsigned long long rowb = 8ull * a.nwp;
 
-    const uint64_t n_work = *a.n_work;
-    const uint64_t ntiles = (a.n_own + a.tile_nodes - 1) / a.tile_nodes;
-    if (n_work * 2 > ntiles) {
-        const int lg = threadIdx.x % G;
-        const uint64_t off = (uint64_t)lg * WPL;
-        const int gshift = (threadIdx.x & 63) / G * G;
-        const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
-        uint8_t* const my = &s_slots[(threadIdx.x >> 6) * (D + 1) * 1024];
-        const uint32_t lane16 = (threadIdx.x & 63) * 16;
-        const uint64_t stride = (uint64_t)gridDim.x * NGB;
-
-        struct Meta {
-            int64_t p0, p1;
-            uint8_t ca, zm;
-        };
-        auto fetch_meta = [&](uint64_t n, Meta& m) {
-            if (n < a.n_own && (a.ablate & 64)) {  // diagnostic: synthetic metadata
-                m.p0 = 2 * n;
-                m.p1 = 2 * n + 2;
-                m.ca = CA_NODE;
-                m.zm = 0;
-            } else if (n < a.n_own) {
-                m.p0 = a.in_ptr[n];
-                m.p1 = a.in_ptr[n + 1];
-                m.ca = a.cand[a.own0 + n];
-                m.zm = a.zmark[a.own0 + n];
-            } else {
-                m.p0 = m.p1 = 0;
-                m.ca = m.zm = 0;
-            }
-        };
-        auto fetch_cols = [&](const Meta& m, uint32_t (&c)[D]) {
-#pragma unroll
-            for (int b = 0; b < D; ++b)
-                c[b] = (m.ca && m.p0 + b < m.p1) ? ((a.ablate & 32) ? (uint32_t)((m.p0 + b) / 2) : a.in_col[m.p0 + b])
-                                                 : 0u;
-        };
-
-        uint64_t i = (uint64_t)blockIdx.x * NGB + threadIdx.x / G;
-        Meta m0, m1;
-        uint32_t c0[D], c1[D];
-        fetch_meta(i, m0);
-        fetch_cols(m0, c0);
-        fetch_meta(i + stride, m1);
-        vm_drain();  // nothing pending at the loop head: no compiler drains inside
-        for (; i < a.n_own; i += stride) {
-            const uint64_t rep = a.own0 + i;
-            const bool work = m0.ca != 0;
-            // (a) DMA node i's own row and its first D sender rows
-            if (work) {
-                if (!(a.ablate & 4))
-                    dma16((const void*)(a.base + rep * a.nwp + off), my + D * 1024);
-#pragma unroll
-                for (int b = 0; b < D; ++b) {
-                    if (m0.p0 + b < m0.p1 && !(a.ablate & 2))
-                        dma16((const void*)(a.F_prev + (uint64_t)(c0[b] & kColMask) * a.nwp + off), my + b * 1024);
-                }
-            }
-            // (b) prefetch: columns of node i+stride, row pointers of node i+2*stride
-            Meta m2;
-            fetch_cols(m1, c1);
-            fetch_meta(i + 2 * stride, m2);
-            vm_drain();
-            if (work) {
-                const bool lag = false;  // lean rounds precede every sync timer: no LAG
-                (void)lag;
-                const ulonglong2 o = *reinterpret_cast<const ulonglong2*>(my + D * 1024 + lane16);
-                Row<WPL> sp, S;
-                sp.w[0] = o.x;
-                sp.w[1] = o.y;
-                S = sp;
-                if (m0.ca & CA_INJ) {  // (1) client broadcasts of this round
-                    uint32_t lo = 0, hi = a.n_inj;
-                    while (lo < hi) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (a.inj[2 * mid] < (uint32_t)i) lo = mid + 1;
-                        else hi = mid;
-                    }
-                    for (uint32_t k = lo; k < a.n_inj && a.inj[2 * k] == (uint32_t)i; ++k) {
-                        const uint32_t lane = a.inj[2 * k + 1];
-                        const uint32_t word = lane >> 6;
-                        if (word / WPL == (uint32_t)lg) set_lane_bit<WPL>(S, word % WPL, lane & 63);
-                    }
-                }
-                // (2) node broadcasts, ascending sender: first deliverer claims
-                unsigned long long cl_recip = 0;
-                auto claim = [&](uint64_t x0, uint64_t x1, uint32_t c) {
-                    const uint64_t w0 = x0 & ~S.w[0], w1 = x1 & ~S.w[1];
-                    S.w[0] |= w0;
-                    S.w[1] |= w1;
-                    if (c & kRecipBit) cl_recip += __popcll(w0) + __popcll(w1);
-                };
-#pragma unroll
-                for (int b = 0; b < D; ++b) {
-                    if (m0.p0 + b < m0.p1) {
-                        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(my + b * 1024 + lane16);
-                        claim(x.x, x.y, c0[b]);
-                    }
-                }
-                for (int64_t k = m0.p0 + D; k < m0.p1; k += D) {  // more than D senders
-                    uint32_t cb[D];
-#pragma unroll
-                    for (int b = 0; b < D; ++b) {
-                        cb[b] = k + b < m0.p1 ? a.in_col[k + b] : 0u;
-                        if (k + b < m0.p1)
-                            dma16((const void*)(a.F_prev + (uint64_t)(cb[b] & kColMask) * a.nwp + off), my + b * 1024);
-                    }
-                    vm_drain();
-#pragma unroll
-                    for (int b = 0; b < D; ++b) {
-                        if (k + b < m0.p1) {
-                            const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(my + b * 1024 + lane16);
-                            claim(x.x, x.y, cb[b]);
-                        }
-                    }
-                }
-                c_gathers += (lg == 0) ? (unsigned long long)(m0.p1 - m0.p0) : 0ull;
-                // new state
-                Row<WPL> F;
-                unsigned long long T = 0;
-                const uint64_t g = a.lo + i;
-#pragma unroll
-                for (int w = 0; w < WPL; ++w) {
-                    F.w[w] = S.w[w] & ~sp.w[w];
-                    T += __popcll(F.w[w]);
-                    if (F.w[w] && !(a.ablate & 8)) {
-                        const uint64_t idx = g * a.nw + off + w;
-                        c_hash += gg_word_hash(idx, S.w[w]) - (sp.w[w] ? gg_word_hash(idx, sp.w[w]) : 0ull);
-                    }
-                }
-                const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
-                if (!(a.ablate & 1)) {
-                    if (any || m0.zm) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
-                    if (any) store_row<WPL>(a.base + rep * a.nwp + off, S);
-                }
-                if (lg == 0 && !(a.ablate & 16)) {
-                    if (any) a.flg_cur[rep] = FL_ACT;
-                    a.cand[rep] = 0;
-                    if (m0.zm) a.zmark[rep] = 0;
-                }
-                const unsigned long long deg = a.symmetric ? (unsigned long long)(m0.p1 - m0.p0)
-                                                           : (unsigned long long)(a.out_ptr[i + 1] - a.out_ptr[i]);
-                c_new += T;
-                c_fwd += deg * T - cl_recip;
-                c_active += (lg == 0) ? 1ull : 0ull;
-            } else if (m0.zm) {  // only a stale F row to clear
-                if (!(a.ablate & 1)) {
-                    Row<WPL> z;
-                    z.w[0] = z.w[1] = 0;
-                    store_row<WPL>(a.F_cur + rep * a.nwp + off, z);
-                }
-                if (lg == 0) a.zmark[rep] = 0;
-            }
-            m0 = m1;
-            m1 = m2;
-#pragma unroll
-            for (int b = 0; b < D; ++b) c0[b] = c1[b];
+    // node ids are < 2^31 (gg_create), so 32-bit ids and in-degrees keep the
+    // three in-flight items within the 5-waves/SIMD register budget
+    struct Meta {
+        int64_t p0;
+        uint32_t deg, node;
+        uint8_t ca, fl;
+    };
+    constexpr uint32_t kNone = ~0u;
+    auto node_of = [&](uint32_t k) -> uint32_t {
+        return k < n_items ? (dense ? (uint32_t)k : a.nodes[k]) : kNone;
+    };
+    auto fetch_meta = [&](uint32_t n, Meta& m) {
+        m.node = n;
+        if (n < a.n_own && (a.ablate & 64)) {  // diagnostic: synthetic metadata
+            m.p0 = 2 * (int64_t)n;
+            m.deg = 2;
+            m.ca = 0;
+            m.fl = 0;
+        } else if (n < a.n_own) {
+            m.p0 = a.in_ptr[n];
+            m.deg = (uint32_t)(a.in_ptr[n + 1] - m.p0);
+            m.ca = a.cand[a.own0 + n];      // CA_INJ: client broadcasts this round
+            m.fl = a.flg_cur[a.own0 + n];   // flags of round r-2 (ACT: stale F row)
+        } else {
+            m.p0 = 0;
+            m.deg = 0;
+            m.ca = m.fl = 0;
         }
+    };
+    auto fetch_cols = [&](const Meta& m, uint32_t (&c)[D]) {
+#pragma unroll
+        for (int b = 0; b < D; ++b)
+            c[b] = ((uint32_t)b < m.deg) ? ((a.ablate & 32) ? (uint32_t)((m.p0 + b) / 2) : a.in_col[m.p0 + b]) : 0u;
+    };
+
+    uint32_t k = blockIdx.x * NGB + threadIdx.x / G;
+    Meta m0, m1;
+    uint32_t c0[D], c1[D];
+    const uint32_t n0 = node_of(k), n1 = node_of(k + stride);
+    uint32_t n2 = node_of(k + 2 * stride);
+    vm_drain();
+    fetch_meta(n0, m0);
+    fetch_meta(n1, m1);
+    vm_drain();
+    fetch_cols(m0, c0);
+    vm_drain();  // nothing pending at the loop head: no compiler drains inside
+    for (; k < n_items; k += stride) {
+        const uint64_t i = m0.node;
+        const uint64_t rep = a.own0 + i;
+        // (a) DMA node i's own row and its first D sender rows
+        if (!(a.ablate & 4)) dma16((const void*)(a.base + rep * a.nwp + off), my + D * 1024);
+#pragma unroll
+        for (int b = 0; b < D; ++b) {
+            if ((uint32_t)b < m0.deg && !(a.ablate & 2))
+                dma16((const void*)(a.F_prev + (uint64_t)(c0[b] & kColMask) * a.nwp + off), my + b * 1024);
+        }
+        // (b) prefetch: columns of item k+stride, row pointers of item k+2*stride,
+        // list entry of item k+3*stride
+        Meta m2;
+        fetch_cols(m1, c1);
+        fetch_meta(n2, m2);
+        const uint32_t n3 = node_of(k + 3 * stride);
+        vm_drain();
+        const ulonglong2 o = *reinterpret_cast<const ulonglong2*>(my + D * 1024 + lane16);
+        Row<WPL> sp, S;
+        sp.w[0] = o.x;  // lean rounds precede every sync timer: no LAG
+        sp.w[1] = o.y;
+        S = sp;
+        if (m0.ca & CA_INJ) {  // (1) client broadcasts of this round
+            uint32_t lo = 0, hi = a.n_inj;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (a.inj[2 * mid] < (uint32_t)i) lo = mid + 1;
+                else hi = mid;
+            }
+            for (uint32_t q = lo; q < a.n_inj && a.inj[2 * q] == (uint32_t)i; ++q) {
+                const uint32_t lane = a.inj[2 * q + 1];
+                const uint32_t word = lane >> 6;
+                if (word / WPL == (uint32_t)lg) set_lane_bit<WPL>(S, word % WPL, lane & 63);
+            }
+        }
+        // (2) node broadcasts, ascending sender: first deliverer claims
+        unsigned long long cl_recip = 0;
+        auto claim = [&](uint64_t x0, uint64_t x1, uint32_t c) {
+            const uint64_t w0 = x0 & ~S.w[0], w1 = x1 & ~S.w[1];
+            S.w[0] |= w0;
+            S.w[1] |= w1;
+            if (c & kRecipBit) cl_recip += __popcll(w0) + __popcll(w1);
+        };
+#pragma unroll
+        for (int b = 0; b < D; ++b) {
+            if ((uint32_t)b < m0.deg) {
+                const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(my + b * 1024 + lane16);
+                claim(x.x, x.y, c0[b]);
+            }
+        }
+        const int64_t p1 = m0.p0 + m0.deg;
+        for (int64_t e = m0.p0 + D; e < p1; e += D) {  // more than D senders
+            uint32_t cb[D];
+#pragma unroll
+            for (int b = 0; b < D; ++b) {
+                cb[b] = e + b < p1 ? a.in_col[e + b] : 0u;
+                if (e + b < p1)
+                    dma16((const void*)(a.F_prev + (uint64_t)(cb[b] & kColMask) * a.nwp + off), my + b * 1024);
+            }
+            vm_drain();
+#pragma unroll
+            for (int b = 0; b < D; ++b) {
+                if (e + b < p1) {
+                    const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(my + b * 1024 + lane16);
+                    claim(x.x, x.y, cb[b]);
+                }
+            }
+        }
+        const unsigned long long nin = m0.deg;
+        c_gathers += (lg == 0) ? m0.deg : 0u;
+        // new state
+        Row<WPL> F;
+        uint32_t T = 0;
+        const uint64_t g = a.lo + i;
+#pragma unroll
+        for (int w = 0; w < WPL; ++w) {
+            F.w[w] = S.w[w] & ~sp.w[w];
+            T += __popcll(F.w[w]);
+            if (F.w[w] && !(a.ablate & 8)) {
+                const uint64_t idx = g * a.nw + off + w;
+                c_hash += gg_word_hash(idx, S.w[w]) - (sp.w[w] ? gg_word_hash(idx, sp.w[w]) : 0ull);
+            }
+        }
+        const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
+        const bool zm = (m0.fl & FL_ACT) != 0;  // F row of round r-2 in this buffer
+        if (!(a.ablate & 1)) {
+            if (any || zm) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
+            if (any) store_row<WPL>(a.base + rep * a.nwp + off, S);
+        }
+        if (lg == 0 && !(a.ablate & 16)) {
+            if (any || m0.fl) a.flg_cur[rep] = any ? FL_ACT : 0;
+            if (m0.ca) a.cand[rep] = 0;
+        }
+        const unsigned long long deg = a.symmetric ? nin : (unsigned long long)(a.out_ptr[i + 1] - a.out_ptr[i]);
+        c_new += T;
+        c_fwd += deg * (unsigned long long)T - cl_recip;
+        if (lg == 0) {
+            c_active += 1;
+            c_nact += any ? 1 : 0;
+            // row_ptr + cand + flag bytes + col, own row + sender rows, F / base / flag writes
+            c_bytes += (dense ? 0 : 4) + 8 + 2 + 4 * nin + (1 + nin) * rowb + ((any || zm) ? rowb : 0) +
+                       (any ? rowb + 1 : 0);
+        }
+        m0 = m1;
+        m1 = m2;
+        n2 = n3;
+#pragma unroll
+        for (int b = 0; b < D; ++b) c0[b] = c1[b];
     }
     unsigned long long acc[C_NUM];
 #pragma unroll
@@ -1014,7 +1105,9 @@ void expand_stream(RoundArgs a) {
     acc[C_NEXT_ACKS] = c_fwd;
     acc[C_ACTIVE] = c_active;
     acc[C_GATHERS] = c_gathers;
-    flush_counters(a, acc, s_red, t_start);
+    acc[C_NACT] = c_nact;
+    acc[C_BYTES] = c_bytes;
+    flush_counters(a, acc, s_red, t_start, K_STREAM);
 }
 
 // First-seen round of every new bit (GG_TRACK_DELIVERY only; observation).

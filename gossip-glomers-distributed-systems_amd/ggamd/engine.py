@@ -59,6 +59,12 @@ class GGRoundStats(C.Structure):
         ("kernel_ms", C.c_double),
         ("work_rows", C.c_uint64),
         ("work_gathers", C.c_uint64),
+        ("prep_ms", C.c_double),
+        ("expand_ms", C.c_double),
+        ("stream_ms", C.c_double),
+        ("prep_bytes", C.c_uint64),
+        ("expand_bytes", C.c_uint64),
+        ("stream_bytes", C.c_uint64),
     ]
 
 
@@ -80,7 +86,8 @@ class GGExchange(C.Structure):
 
 
 STAT_FIELDS = [f for f, _ in GGRoundStats._fields_]
-DIAG_FIELDS = ("round", "kernel_ms", "work_rows", "work_gathers")
+DIAG_FIELDS = ("round", "kernel_ms", "work_rows", "work_gathers", "prep_ms", "expand_ms", "stream_ms",
+               "prep_bytes", "expand_bytes", "stream_bytes")
 COUNT_FIELDS = [f for f in STAT_FIELDS if f not in DIAG_FIELDS]
 
 GG_SYMBOLS = [

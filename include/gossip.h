@@ -93,6 +93,12 @@ typedef struct {
     double kernel_ms;        /* device time of the round (0 for the CPU oracle) */
     uint64_t work_rows;      /* diagnostics, engine-specific (not part of parity): */
     uint64_t work_gathers;   /*   nodes that moved rows, sender rows gathered */
+    double prep_ms;          /*   device time of the round's kernels by kind: timers/marking, */
+    double expand_ms;        /*   sparse/sync expand, dense streaming expand (first block */
+    double stream_ms;        /*   start to last block end; 0 for the CPU oracle) */
+    uint64_t prep_bytes;     /*   algorithmic bytes each kind had to move this round */
+    uint64_t expand_bytes;   /*   (DESIGN.md §4), counted by the kernels */
+    uint64_t stream_bytes;
 } gg_round_stats;
 
 /* Inter-node messages of a round = fwd_sent + pushes + acks + reads + read_oks. */

@@ -502,6 +502,8 @@ static void fill_stats(gg_engine* e, const Acc& a, gg_round_stats* s) {
     s->kernel_ms = 0.0;
     s->work_rows = 0;
     s->work_gathers = 0;
+    s->prep_ms = s->expand_ms = s->stream_ms = 0.0;
+    s->prep_bytes = s->expand_bytes = s->stream_bytes = 0;
 }
 
 int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {

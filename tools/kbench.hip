@@ -45,18 +45,10 @@ int main(int argc, char** argv) {
     auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
     for (auto& w : hb) w = rnd() & rnd();
     for (auto& w : hf) w = rnd() & rnd() & rnd();
-    std::vector<gg::TileWork> work(ntiles);
-    for (uint64_t t = 0; t < ntiles; ++t) {
-        const uint64_t n0 = t * NG, n1 = std::min<uint64_t>(n0 + NG, V);
-        work[t].tile = (uint32_t)t;
-        work[t].eb = ptr[n0];
-        work[t].ne = (uint32_t)(ptr[n1] - ptr[n0]);
-    }
     int64_t* d_ptr;
-    uint32_t *d_col, *d_nwork;
+    uint32_t *d_col, *d_act;
     uint64_t *d_base, *d_base0, *d_Fp, *d_Fc, *d_fired;
     uint8_t *d_flgp, *d_flgc, *d_cand, *d_tc, *d_zm;
-    gg::TileWork* d_work;
     unsigned long long* d_ctr;
     CK(hipMalloc(&d_ptr, (V + 1) * 8));
     CK(hipMalloc(&d_col, E * 4));
@@ -71,16 +63,14 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&d_zm, rows));
     CK(hipMemset(d_zm, 0, rows));
     CK(hipMalloc(&d_tc, ntiles + 8));
-    CK(hipMalloc(&d_work, ntiles * sizeof(gg::TileWork)));
-    CK(hipMalloc(&d_nwork, 4));
+    CK(hipMalloc(&d_act, 16));
     CK(hipMalloc(&d_ctr, gg::kSlots * gg::kCounters * 8));
     CK(hipMemcpy(d_ptr, ptr.data(), (V + 1) * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_col, col.data(), E * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_base0, hb.data(), rows * nwp * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_Fp, hf.data(), rows * nwp * 8, hipMemcpyHostToDevice));
-    CK(hipMemcpy(d_work, work.data(), ntiles * sizeof(gg::TileWork), hipMemcpyHostToDevice));
-    const uint32_t nw = (uint32_t)ntiles;
-    CK(hipMemcpy(d_nwork, &nw, 4, hipMemcpyHostToDevice));
+    const uint32_t act[4] = {(uint32_t)V, (uint32_t)V, (uint32_t)V, (uint32_t)V};  // every round dense
+    CK(hipMemcpy(d_act, act, 16, hipMemcpyHostToDevice));
     CK(hipMemset(d_flgp, gg::FL_ACT, rows));
     CK(hipMemset(d_fired, 0, rows / 8 * 4));
 
@@ -97,8 +87,7 @@ int main(int argc, char** argv) {
     a.cand = d_cand;
     a.zmark = d_zm;
     a.tile_cand = d_tc;
-    a.work = d_work;
-    a.n_work = d_nwork;
+    a.act = d_act;
     a.fired_m1 = a.fired_m2 = a.fired_m3 = d_fired;
     a.fired_cur = d_fired + rows / 64;
     a.counters = d_ctr;
@@ -121,9 +110,11 @@ int main(int argc, char** argv) {
            (unsigned long long)E, (unsigned long long)w, bytes / 1e6);
     for (uint32_t abl : {0u}) {
         a.ablate = abl;
+        a.stream_ok = 0;  // sparse path over every tile
         float best = 1e30f, sum = 0;
         for (int r = 0; r < reps; ++r) {
             CK(hipMemcpyAsync(d_base, d_base0, rows * nwp * 8, hipMemcpyDeviceToDevice, 0));
+            CK(hipMemsetAsync(d_tc, 1, ntiles, 0));
             CK(hipMemsetAsync(d_cand, gg::CA_NODE, rows, 0));
             CK(hipMemsetAsync(d_ctr, 0, gg::kSlots * gg::kCounters * 8, 0));
             CK(hipEventRecord(e0, 0));
@@ -141,6 +132,7 @@ int main(int argc, char** argv) {
     // streaming kernel (the dense-round path of the library for WPL == 2)
     for (uint32_t abl : {0u, 15u, 31u, 47u, 79u, 63u, 127u, 111u, 95u}) {
         a.ablate = abl;
+        a.stream_ok = 1;
         for (int blocks : {1024}) {
             float best = 1e30f, sum = 0;
             for (int r = 0; r < reps; ++r) {

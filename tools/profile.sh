@@ -13,5 +13,6 @@ echo "== kernel trace" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --o
 && echo "== WRITE_SIZE" && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py $ARGS > $OUT/write.log 2>&1
 rc=$?
 echo "rc=$rc"
+[ $rc -eq 0 ] && python3 tools/traffic.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv "rocprofv3 --pmc passes over: bench.py $ARGS ($TAG)" $OUT/traffic.json
 find $OUT -name "*.csv" | head -20
 exit $rc
