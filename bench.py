@@ -163,8 +163,12 @@ def main():
     # roofline of the dominant kernel: per-kind device times (first block start
     # to last block end of each launch, stamped by the kernels) and the bytes
     # each launch had to move (counted by the kernels)
-    lo, hi = eng.dist_range() if world > 1 else (0, V)
-    E_own = int(topo.row_ptr[hi] - topo.row_ptr[lo])
+    if world > 1:
+        owned = eng.dist_owned().astype(np.int64)
+        n_own = int(owned.size)
+        E_own = int((topo.row_ptr[owned + 1] - topo.row_ptr[owned]).sum())
+    else:
+        n_own, E_own = V, int(topo.nnz)
     nwp = next_pow2(K // 64)
     rounds_local = [s for ep in local_stats for s in ep]
     kinds = {}
@@ -218,7 +222,7 @@ def main():
                 "algorithmic_bytes_per_launch": D["bytes"] / D["launches"],
                 "avg_launch_ms": D["avg_launch_ms"],
                 "launches": D["launches"],
-                "dense_bytes_per_round": dense_bytes_per_round(hi - lo, E_own, nwp),
+                "dense_bytes_per_round": dense_bytes_per_round(n_own, E_own, nwp),
                 "timing": "per launch: device clock (s_memrealtime) from the first block start to the last "
                           "block end of that kernel, stamped by every block (no-op launches included, as in "
                           "rocprofv3's average); cross-check: HIP events around each step's launch sequence "

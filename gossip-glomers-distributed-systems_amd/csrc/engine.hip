@@ -10,11 +10,11 @@
 // W/64 rounded up to a power of two), node-major: `base` (sets, updated in
 // place), F[2] (new bits of a round = what the node forwards next round) and
 // flags[2] (ACT: F row valid; LAG: set = base | F); fired[4] is a ring of
-// per-round sync-timer bitmaps; CSR in-lists carry the
-// sender's row with bit 31 set when the sender is also in the receiver's
-// out-list (forward exclusion, `:52`). In sharded mode every buffer is a
-// replica laid out [world][slice_rows], columns index replica rows, and the
-// caller all-gathers each rank's slices between gg_dist_round_begin/end.
+// per-round sync-timer bitmaps; CSR in-lists carry the sender's local row with
+// bit 31 set when the sender is also in the receiver's out-list (forward
+// exclusion, `:52`). Local rows: the owned nodes first, then (sharded mode,
+// from ghost0 on) read-only ghost copies of the remote nodes adjacent to them,
+// refreshed every round by the exchange (pack_ghosts / unpack_ghosts).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -78,9 +78,24 @@ struct gg_engine {
     hipStream_t stream = nullptr;
     uint64_t V = 0, nw = 0, nwp = 0;
     uint32_t rank = 0, world = 1;
-    uint64_t lo = 0, hi = 0, slice = 0, rows = 0;
-    std::vector<uint64_t> rank_lo;
+    uint64_t n_own = 0, ghost0 = 0, n_ghost = 0, rows = 0;  // local rows: own, then ghosts
+    std::vector<uint32_t> gid;     // [rows] original id of each local row (~0u: padding)
+    std::vector<uint32_t> loc_of;  // [V] local row of an owned node, ~0u otherwise (sharded)
     bool have_topo = false, symmetric = true;
+    uint32_t* d_gid = nullptr;     // sharded only (single engine: row == id)
+    // exchange: owned rows each rank needs (concatenated per destination) and
+    // ghost counts per source rank; outgoing ghost edges (ghost -> owned receivers)
+    std::vector<uint64_t> send_off, recv_off;  // [world+1] node counts
+    uint32_t* d_send_idx = nullptr;
+    int64_t* d_gout_ptr = nullptr;
+    uint32_t* d_gout_col = nullptr;
+    uint8_t* d_xsend = nullptr;
+    uint8_t* d_xrecv = nullptr;
+    std::vector<uint64_t> xsend_bytes, xrecv_bytes;
+    uint32_t dist_k = 0;                       // pending rounds (counter slots in use)
+    std::vector<int64_t> dist_round_of;        // round of each pending slot
+    std::vector<gg_round_stats> dist_done;     // folded, not yet flushed
+    size_t inj_off = 0;                        // pinned injection ring offset (async rounds)
 
     int64_t* d_in_ptr = nullptr;
     uint32_t* d_in_col = nullptr;
@@ -102,7 +117,6 @@ struct gg_engine {
     int32_t* d_sync_next = nullptr;
     uint32_t* d_sync_k = nullptr;
     int32_t* d_dr = nullptr;
-    uint64_t* d_rank_lo = nullptr;
     unsigned long long* d_counters = nullptr;
     unsigned long long* h_counters = nullptr;  // pinned
     uint32_t* d_inj = nullptr;
@@ -167,7 +181,12 @@ void gg_engine::free_topology() {
     dfree(d_sync_next);
     dfree(d_sync_k);
     dfree(d_dr);
-    dfree(d_rank_lo);
+    dfree(d_gid);
+    dfree(d_send_idx);
+    dfree(d_gout_ptr);
+    dfree(d_gout_col);
+    dfree(d_xsend);
+    dfree(d_xrecv);
     for (auto& w : windows) dfree(w.d_grp);
     have_topo = false;
 }
@@ -200,10 +219,10 @@ int reset_device_state(gg_engine* e) {
     HIPCHK(hipMemsetAsync(e->d_zmark, 0, e->rows, e->stream));
     HIPCHK(hipMemsetAsync(e->d_tile_cand, 0, e->tile_bytes, e->stream));
     HIPCHK(hipMemsetAsync(e->d_act, 0, 4 * sizeof(uint32_t), e->stream));
-    const uint64_t n_own = e->hi - e->lo;
+    const uint64_t n_own = e->n_own;
     if (n_own) {
         hipLaunchKernelGGL(gg::sync_init, dim3((unsigned)((n_own + 255) / 256)), dim3(256), 0, e->stream,
-                           e->d_sync_next, e->d_sync_k, n_own, e->lo, e->cfg.seed,
+                           e->d_sync_next, e->d_sync_k, n_own, e->d_gid, e->cfg.seed,
                            e->cfg.sync_base_ticks, e->cfg.sync_jitter_ticks);
         HIPCHK(hipGetLastError());
     }
@@ -213,23 +232,26 @@ int reset_device_state(gg_engine* e) {
 }
 
 int materialize_windows(gg_engine* e) {
+    bool any = false;
     for (auto& w : e->windows) {
         if (w.d_grp) continue;
+        any = true;
         HIPCHK(hipMalloc(&w.d_grp, e->rows));
         if (w.seeded) {
+            const uint64_t valid = e->d_gid ? e->rows : e->n_own;
             hipLaunchKernelGGL(gg::fill_seeded_groups, dim3((unsigned)((e->rows + 255) / 256)), dim3(256), 0,
-                               e->stream, w.d_grp, e->rows, e->slice, e->d_rank_lo, e->world,
-                               e->cfg.seed, w.epoch_seed);
+                               e->stream, w.d_grp, e->rows, valid, e->d_gid, e->cfg.seed, w.epoch_seed);
             HIPCHK(hipGetLastError());
         } else {
             std::vector<uint8_t> h(e->rows, 0);
-            for (uint32_t p = 0; p < e->world; ++p)
-                for (uint64_t g = e->rank_lo[p]; g < e->rank_lo[p + 1]; ++g)
-                    h[(uint64_t)p * e->slice + (g - e->rank_lo[p])] = w.group[g];
+            for (uint64_t r = 0; r < e->rows; ++r) {
+                const uint64_t g = e->gid.empty() ? r : e->gid[r];
+                if (g < e->V) h[r] = w.group[g];
+            }
             HIPCHK(hipMemcpy(w.d_grp, h.data(), e->rows, hipMemcpyHostToDevice));
         }
     }
-    HIPCHK(hipStreamSynchronize(e->stream));
+    if (any) HIPCHK(hipStreamSynchronize(e->stream));
     return GG_OK;
 }
 
@@ -323,7 +345,11 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.symmetric = e->symmetric ? 1 : 0;
     a.n_edges = e->n_in_edges;
     a.rows = e->rows;
-    a.mark_all = e->world > 1;
+    a.gid = e->d_gid;
+    a.ghost0 = e->ghost0;
+    a.n_ghost = e->n_ghost;
+    a.gout_ptr = e->d_gout_ptr;
+    a.gout_col = e->d_gout_col;
     {
         static const uint32_t ablate = getenv("GG_ABLATE") ? (uint32_t)atoi(getenv("GG_ABLATE")) : 0u;
         a.ablate = ablate;  // diagnostic timing only
@@ -342,9 +368,9 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.inj = d_inj;
     a.n_inj = n_inj;
     a.counters = d_ctr;
-    a.n_own = e->hi - e->lo;
-    a.own0 = (uint64_t)e->rank * e->slice;
-    a.lo = e->lo;
+    a.n_own = e->n_own;
+    a.own0 = 0;
+    a.lo = 0;
     a.nwp = (uint32_t)e->nwp;
     a.nw = (uint32_t)e->nw;
     a.round = r;
@@ -401,7 +427,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
 
 // Host-side stats of one round from its 64 counter slots; per-kind times from
 // the device clock stamps (first block start .. last block end, 100 MHz).
-void fold_stats(gg_engine* e, const unsigned long long* slots, gg_round_stats* s) {
+void fold_stats(gg_engine* e, const unsigned long long* slots, int64_t round, gg_round_stats* s) {
     unsigned long long c[gg::kCounters] = {0};
     unsigned long long t0[gg::K_NKIND], t1[gg::K_NKIND];
     for (int q = 0; q < gg::K_NKIND; ++q) t0[q] = ~0ull, t1[q] = 0;
@@ -425,7 +451,7 @@ void fold_stats(gg_engine* e, const unsigned long long* slots, gg_round_stats* s
     s->prep_bytes = c[gg::kBytes0 + gg::K_PREP];
     s->expand_bytes = c[gg::kBytes0 + gg::K_EXPAND];
     s->stream_bytes = c[gg::kBytes0 + gg::K_STREAM];
-    s->round = e->round;
+    s->round = round;
     s->new_bits = c[gg::C_NEW];
     s->fwd_sent = c[gg::C_FWD_SENT];
     s->fwd_delivered = c[gg::C_FWD_DELIV];
@@ -467,8 +493,15 @@ int ensure_inj(gg_engine* e, size_t pairs) {
     return GG_OK;
 }
 
+// Local row of an owned node, ~0u if another engine owns it.
+uint32_t local_row(const gg_engine* e, uint64_t node) {
+    if (node >= e->V) return ~0u;
+    if (e->loc_of.empty()) return (uint32_t)node;
+    return e->loc_of[node];
+}
+
 // Pack the owned injections of rounds [r0, r0+n) into h_inj; off[k] = first pair of round r0+k.
-size_t pack_injections(gg_engine* e, int64_t r0, uint32_t n, std::vector<size_t>& off) {
+size_t pack_injections(gg_engine* e, int64_t r0, uint32_t n, std::vector<size_t>& off, size_t base = 0) {
     off.assign(n + 1, 0);
     std::vector<std::pair<uint32_t, uint32_t>> tmp;
     for (uint32_t k = 0; k < n; ++k) {
@@ -476,16 +509,18 @@ size_t pack_injections(gg_engine* e, int64_t r0, uint32_t n, std::vector<size_t>
         auto it = e->inj.find(r0 + k);
         if (it == e->inj.end()) continue;
         const size_t b = tmp.size();
-        for (const auto& x : it->second)
-            if (x.node >= e->lo && x.node < e->hi) tmp.emplace_back((uint32_t)(x.node - e->lo), x.lane);
+        for (const auto& x : it->second) {
+            const uint32_t l = local_row(e, x.node);
+            if (l != ~0u) tmp.emplace_back(l, x.lane);
+        }
         std::stable_sort(tmp.begin() + b, tmp.end(),
                          [](const auto& p, const auto& q) { return p.first < q.first; });
     }
     off[n] = tmp.size();
-    if (ensure_inj(e, tmp.size()) != GG_OK) return (size_t)-1;
+    if (ensure_inj(e, base + tmp.size()) != GG_OK) return (size_t)-1;
     for (size_t t = 0; t < tmp.size(); ++t) {
-        e->h_inj[2 * t] = tmp[t].first;
-        e->h_inj[2 * t + 1] = tmp[t].second;
+        e->h_inj[2 * (base + t)] = tmp[t].first;
+        e->h_inj[2 * (base + t) + 1] = tmp[t].second;
     }
     return tmp.size();
 }
@@ -549,6 +584,99 @@ int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& o
     HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
     e->step_event_ms += ms;
     return GG_OK;
+}
+
+
+// Payload bytes of one node in the exchange (pack_ghosts layout): F row, set
+// row when `with_set`, 16-byte tail; rows padded to 16 bytes.
+uint64_t exchange_stride(uint64_t nwp, bool with_set) {
+    const uint64_t rowc = nwp / 2 + (nwp & 1);
+    return (rowc * (with_set ? 2 : 1) + 1) * 16;
+}
+
+// Edge-balanced cut of a node order into `parts` contiguous ranges (weight of a
+// node: in-degree + 1, the pull work of its row).
+void balanced_ranges(uint64_t V, const int64_t* tin, const std::vector<uint32_t>& order, uint32_t parts,
+                     std::vector<uint64_t>& plo) {
+    plo.assign(parts + 1, V);
+    plo[0] = 0;
+    const uint64_t total = (uint64_t)tin[V] + V;
+    uint64_t cum = 0;
+    uint32_t p = 1;
+    for (uint64_t pos = 0; pos < V && p < parts; ++pos) {
+        const uint64_t v = order.empty() ? pos : order[pos];
+        cum += (uint64_t)(tin[v + 1] - tin[v]) + 1;
+        while (p < parts && cum >= total * p / parts) plo[p++] = pos + 1;
+    }
+    while (p < parts) plo[p++] = V;
+}
+
+void owners_of(uint64_t V, const std::vector<uint32_t>& order, const std::vector<uint64_t>& plo,
+               std::vector<uint32_t>& owner) {
+    owner.assign(V, 0);
+    for (uint32_t p = 0; p + 1 < plo.size(); ++p)
+        for (uint64_t pos = plo[p]; pos < plo[p + 1]; ++pos) owner[order.empty() ? pos : order[pos]] = p;
+}
+
+uint64_t cut_edges(uint64_t V, const int64_t* row_ptr, const int32_t* col, const std::vector<uint32_t>& owner) {
+    uint64_t cut = 0;
+    for (uint64_t v = 0; v < V; ++v)
+        for (int64_t k = row_ptr[v]; k < row_ptr[v + 1]; ++k) cut += owner[v] != owner[(uint32_t)col[k]];
+    return cut;
+}
+
+// The sharded engine's node order: the native id order or a DFS preorder over
+// the out-lists (roots in ascending id, neighbours ascending), whichever cuts
+// fewer edges when split into edge-balanced ranges (trees: subtrees stay whole;
+// grids: native rows). Deterministic, so every rank computes the same one.
+void choose_partition(uint64_t V, const int64_t* row_ptr, const int32_t* col, const int64_t* tin, uint32_t parts,
+                      std::vector<uint32_t>& order, std::vector<uint64_t>& plo, std::vector<uint32_t>& owner) {
+    std::vector<uint64_t> plo_n;
+    std::vector<uint32_t> own_n;
+    balanced_ranges(V, tin, {}, parts, plo_n);
+    owners_of(V, {}, plo_n, own_n);
+    const uint64_t cut_n = cut_edges(V, row_ptr, col, own_n);
+    std::vector<uint32_t> dfs;
+    dfs.reserve(V);
+    {
+        std::vector<uint8_t> seen(V, 0);
+        std::vector<uint32_t> stack;
+        std::vector<int64_t> next(V);
+        for (uint64_t root = 0; root < V; ++root) {
+            if (seen[root]) continue;
+            seen[root] = 1;
+            dfs.push_back((uint32_t)root);
+            next[root] = row_ptr[root];
+            stack.push_back((uint32_t)root);
+            while (!stack.empty()) {
+                const uint32_t v = stack.back();
+                if (next[v] == row_ptr[v + 1]) {
+                    stack.pop_back();
+                    continue;
+                }
+                const uint32_t u = (uint32_t)col[next[v]++];
+                if (seen[u]) continue;
+                seen[u] = 1;
+                dfs.push_back(u);
+                next[u] = row_ptr[u];
+                stack.push_back(u);
+            }
+        }
+    }
+    std::vector<uint64_t> plo_d;
+    std::vector<uint32_t> own_d;
+    balanced_ranges(V, tin, dfs, parts, plo_d);
+    owners_of(V, dfs, plo_d, own_d);
+    const uint64_t cut_d = cut_edges(V, row_ptr, col, own_d);
+    if (cut_d < cut_n) {
+        order.swap(dfs);
+        plo.swap(plo_d);
+        owner.swap(own_d);
+    } else {
+        order.clear();
+        plo.swap(plo_n);
+        owner.swap(own_n);
+    }
 }
 
 }  // namespace
@@ -632,47 +760,113 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
             if ((int64_t)tcol[tin[v] + k] != col[row_ptr[v] + k]) { sym = false; break; }
     }
     e->symmetric = sym;
-    // edge-balanced vertex ranges over the in-lists
+    // ---- partition (sharded): a locality order of the nodes cut into
+    // edge-balanced contiguous ranges; rank p owns order[plo[p] .. plo[p+1])
     const uint32_t Wd = e->world;
-    e->rank_lo.assign(Wd + 1, V);
-    e->rank_lo[0] = 0;
-    {
-        const uint64_t total = nnz + V;
-        uint32_t p = 1;
-        for (uint64_t v = 0; v < V && p < Wd; ++v) {
-            uint64_t cum = (uint64_t)tin[v + 1] + v + 1;
-            while (p < Wd && cum >= total * p / Wd) e->rank_lo[p++] = v + 1;
-        }
-        while (p < Wd) e->rank_lo[p++] = V;
+    std::vector<uint32_t> order;    // position -> node (empty: identity)
+    std::vector<uint64_t> plo;      // [Wd+1] position ranges
+    std::vector<uint32_t> owner;    // node -> rank (sharded)
+    if (Wd > 1) {
+        choose_partition(V, row_ptr, col, tin.data(), Wd, order, plo, owner);
+    } else {
+        plo = {0, V};
     }
-    uint64_t maxrows = 0;
-    for (uint32_t p = 0; p < Wd; ++p) maxrows = std::max<uint64_t>(maxrows, e->rank_lo[p + 1] - e->rank_lo[p]);
-    e->slice = std::max<uint64_t>(64, (maxrows + 63) / 64 * 64);
-    e->rows = (uint64_t)Wd * e->slice;
-    e->lo = e->rank_lo[e->rank];
-    e->hi = e->rank_lo[e->rank + 1];
-    const uint64_t n_own = e->hi - e->lo;
-    auto rep_of = [&](uint64_t g) -> uint32_t {
-        uint32_t p = (uint32_t)(std::upper_bound(e->rank_lo.begin(), e->rank_lo.end(), g) - e->rank_lo.begin()) - 1;
-        return (uint32_t)((uint64_t)p * e->slice + (g - e->rank_lo[p]));
+    auto node_at = [&](uint64_t pos) -> uint32_t { return order.empty() ? (uint32_t)pos : order[pos]; };
+    const uint64_t n_own = plo[e->rank + 1] - plo[e->rank];
+    e->n_own = n_own;
+    e->loc_of.clear();
+    e->gid.clear();
+    std::vector<uint32_t> ghosts;                     // ghost nodes in local ghost order
+    std::vector<std::vector<uint32_t>> sendl(Wd);     // owned local rows per destination
+    if (Wd > 1) {
+        e->loc_of.assign(V, ~0u);
+        for (uint64_t i = 0; i < n_own; ++i) e->loc_of[node_at(plo[e->rank] + i)] = (uint32_t)i;
+        // ghosts: remote nodes adjacent (in or out) to owned ones; send lists:
+        // owned nodes adjacent to each remote rank. Both sorted by node id, so
+        // rank q's receive order from p equals p's send order to q.
+        std::vector<std::vector<uint32_t>> gfrom(Wd);
+        std::vector<uint32_t> peers;
+        for (uint64_t i = 0; i < n_own; ++i) {
+            const uint32_t v = node_at(plo[e->rank] + i);
+            peers.clear();
+            auto visit = [&](uint32_t u) {
+                const uint32_t q = owner[u];
+                if (q == e->rank) return;
+                gfrom[q].push_back(u);
+                peers.push_back(q);
+            };
+            for (int64_t k = row_ptr[v]; k < row_ptr[v + 1]; ++k) visit((uint32_t)col[k]);
+            for (int64_t k = tin[v]; k < tin[v + 1]; ++k) visit(tcol[k]);
+            std::sort(peers.begin(), peers.end());
+            peers.erase(std::unique(peers.begin(), peers.end()), peers.end());
+            for (uint32_t q : peers) sendl[q].push_back(v);
+        }
+        e->send_off.assign(Wd + 1, 0);
+        e->recv_off.assign(Wd + 1, 0);
+        for (uint32_t q = 0; q < Wd; ++q) {
+            auto& g = gfrom[q];
+            std::sort(g.begin(), g.end());
+            g.erase(std::unique(g.begin(), g.end()), g.end());
+            std::sort(sendl[q].begin(), sendl[q].end());
+            for (auto& v : sendl[q]) v = e->loc_of[v];  // node -> owned local row
+            ghosts.insert(ghosts.end(), g.begin(), g.end());
+            e->recv_off[q + 1] = e->recv_off[q] + g.size();
+            e->send_off[q + 1] = e->send_off[q] + sendl[q].size();
+        }
+    }
+    e->n_ghost = ghosts.size();
+    e->ghost0 = Wd > 1 ? (n_own + 63) / 64 * 64 : n_own;
+    e->rows = std::max<uint64_t>(64, (e->ghost0 + e->n_ghost + 63) / 64 * 64);
+    if (e->rows > 0x7fffffffull) return e->fail(GG_EINVAL, "local rows exceed 2^31");
+    std::unordered_map<uint32_t, uint32_t> ghost_row;  // ghost node -> local row
+    if (Wd > 1) {
+        e->gid.assign(e->rows, ~0u);
+        for (uint64_t i = 0; i < n_own; ++i) e->gid[i] = node_at(plo[e->rank] + i);
+        ghost_row.reserve(ghosts.size() * 2);
+        for (uint64_t k = 0; k < ghosts.size(); ++k) {
+            e->gid[e->ghost0 + k] = ghosts[k];
+            ghost_row.emplace(ghosts[k], (uint32_t)(e->ghost0 + k));
+        }
+    }
+    auto row_of = [&](uint32_t u) -> uint32_t {
+        if (Wd == 1) return u;
+        const uint32_t l = e->loc_of[u];
+        return l != ~0u ? l : ghost_row.at(u);
     };
-    if (e->rows > 0x7fffffffull) return e->fail(GG_EINVAL, "replica rows exceed 2^31");
+    // ---- owned rows: in-lists (ascending sender id: claim order) and out-lists
+    // (ascending receiver id: callback order) with local-row columns
     std::vector<int64_t> iptr(n_own + 1, 0), optr(n_own + 1, 0);
     for (uint64_t i = 0; i < n_own; ++i) {
-        iptr[i + 1] = iptr[i] + (tin[e->lo + i + 1] - tin[e->lo + i]);
-        optr[i + 1] = optr[i] + (row_ptr[e->lo + i + 1] - row_ptr[e->lo + i]);
+        const uint32_t v = node_at(plo[e->rank] + i);
+        iptr[i + 1] = iptr[i] + (tin[v + 1] - tin[v]);
+        optr[i + 1] = optr[i] + (row_ptr[v + 1] - row_ptr[v]);
     }
     std::vector<uint32_t> icol(iptr[n_own]), ocol(optr[n_own]);
+    std::vector<int64_t> gcnt(e->n_ghost + 1, 0);
     for (uint64_t i = 0; i < n_own; ++i) {
-        const uint64_t v = e->lo + i;
+        const uint32_t v = node_at(plo[e->rank] + i);
         const int32_t* ob = col + row_ptr[v];
         const int32_t* oe = col + row_ptr[v + 1];
         for (int64_t k = 0; k < tin[v + 1] - tin[v]; ++k) {
             const uint32_t u = tcol[tin[v] + k];
             const bool recip = sym || std::binary_search(ob, oe, (int32_t)u);
-            icol[iptr[i] + k] = rep_of(u) | (recip ? gg::kRecipBit : 0u);
+            const uint32_t ru = row_of(u);
+            icol[iptr[i] + k] = ru | (recip ? gg::kRecipBit : 0u);
+            if (ru >= e->ghost0) gcnt[ru - e->ghost0 + 1]++;
         }
-        for (int64_t k = 0; k < row_ptr[v + 1] - row_ptr[v]; ++k) ocol[optr[i] + k] = rep_of((uint64_t)ob[k]);
+        for (int64_t k = 0; k < row_ptr[v + 1] - row_ptr[v]; ++k) ocol[optr[i] + k] = row_of((uint32_t)ob[k]);
+    }
+    // ghost -> owned receivers (candidate marking from remote senders)
+    std::vector<uint32_t> gocol;
+    if (e->n_ghost) {
+        for (uint64_t g = 0; g < e->n_ghost; ++g) gcnt[g + 1] += gcnt[g];
+        gocol.resize(gcnt[e->n_ghost]);
+        std::vector<int64_t> fill(gcnt.begin(), gcnt.end() - 1);
+        for (uint64_t i = 0; i < n_own; ++i)
+            for (int64_t k = iptr[i]; k < iptr[i + 1]; ++k) {
+                const uint32_t ru = icol[k] & gg::kColMask;
+                if (ru >= e->ghost0) gocol[fill[ru - e->ghost0]++] = (uint32_t)i;
+            }
     }
     // device buffers
     e->n_in_edges = icol.size();
@@ -689,6 +883,22 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
         HIPCHK(hipMalloc(&e->d_out_col, std::max<size_t>(1, ocol.size()) * 4));
         HIPCHK(hipMemcpy(e->d_out_ptr, optr.data(), (n_own + 1) * 8, hipMemcpyHostToDevice));
         if (!ocol.empty()) HIPCHK(hipMemcpy(e->d_out_col, ocol.data(), ocol.size() * 4, hipMemcpyHostToDevice));
+    }
+    if (Wd > 1) {
+        HIPCHK(hipMalloc(&e->d_gid, e->rows * 4));
+        HIPCHK(hipMemcpy(e->d_gid, e->gid.data(), e->rows * 4, hipMemcpyHostToDevice));
+        std::vector<uint32_t> sidx;
+        for (uint32_t q = 0; q < Wd; ++q) sidx.insert(sidx.end(), sendl[q].begin(), sendl[q].end());
+        HIPCHK(hipMalloc(&e->d_send_idx, std::max<size_t>(1, sidx.size()) * 4));
+        if (!sidx.empty()) HIPCHK(hipMemcpy(e->d_send_idx, sidx.data(), sidx.size() * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMalloc(&e->d_gout_ptr, (e->n_ghost + 1) * 8));
+        HIPCHK(hipMemcpy(e->d_gout_ptr, gcnt.data(), (e->n_ghost + 1) * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMalloc(&e->d_gout_col, std::max<size_t>(1, gocol.size()) * 4));
+        if (!gocol.empty())
+            HIPCHK(hipMemcpy(e->d_gout_col, gocol.data(), gocol.size() * 4, hipMemcpyHostToDevice));
+        const uint64_t pb = exchange_stride(e->nwp, true);
+        HIPCHK(hipMalloc(&e->d_xsend, std::max<uint64_t>(16, e->send_off[Wd] * pb)));
+        HIPCHK(hipMalloc(&e->d_xrecv, std::max<uint64_t>(16, e->recv_off[Wd] * pb)));
     }
     const size_t rowbytes = e->rows * e->nwp * 8;
     e->tile_nodes = gg::kBlock / lanes_per_node((uint32_t)e->nwp);
@@ -709,10 +919,11 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     for (int b = 0; b < 4; ++b) HIPCHK(hipMalloc(&e->d_fired[b], e->rows / 8));
     HIPCHK(hipMalloc(&e->d_sync_next, std::max<uint64_t>(1, n_own) * 4));
     HIPCHK(hipMalloc(&e->d_sync_k, std::max<uint64_t>(1, n_own) * 4));
-    HIPCHK(hipMalloc(&e->d_rank_lo, (Wd + 1) * 8));
-    HIPCHK(hipMemcpy(e->d_rank_lo, e->rank_lo.data(), (Wd + 1) * 8, hipMemcpyHostToDevice));
     if (e->cfg.flags & GG_TRACK_DELIVERY) HIPCHK(hipMalloc(&e->d_dr, std::max<uint64_t>(1, n_own) * e->cfg.n_lanes * 4));
     e->have_topo = true;
+    e->dist_k = 0;
+    e->dist_done.clear();
+    e->inj_off = 0;
     e->lanes.clear();
     e->lane_value.clear();
     e->inj.clear();
@@ -824,10 +1035,7 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
         HIPCHK(hipStreamSynchronize(e->stream));
         for (uint32_t k = 0; k < m; ++k) {
             gg_round_stats s;
-            const int64_t save = e->round;
-            e->round = r0 + k;
-            fold_stats(e, e->h_counters + (size_t)k * gg::kSlots * gg::kCounters, &s);
-            e->round = save;
+            fold_stats(e, e->h_counters + (size_t)k * gg::kSlots * gg::kCounters, r0 + k, &s);
             if (out) out[done + k] = s;
             e->inj.erase(r0 + k);
         }
@@ -842,89 +1050,205 @@ int gg_step_device_ms(const gg_engine* e, double* ms) {
     return GG_OK;
 }
 
-int gg_dist_range(const gg_engine* e, uint64_t* lo, uint64_t* hi) {
+int gg_dist_owned(const gg_engine* e, uint32_t* nodes, uint64_t cap, uint64_t* n_out) {
     if (!e || !e->have_topo) return GG_EINVAL;
-    if (lo) *lo = e->lo;
-    if (hi) *hi = e->hi;
+    if (n_out) *n_out = e->n_own;
+    if (nodes)
+        for (uint64_t i = 0; i < e->n_own && i < cap; ++i) nodes[i] = e->gid.empty() ? (uint32_t)i : e->gid[i];
+    return GG_OK;
+}
+
+// Counters of the pending sharded rounds -> dist_done (waits for the stream).
+static int fold_pending(gg_engine* e) {
+    if (e->dist_k) {
+        const size_t slot = (size_t)gg::kSlots * gg::kCounters;
+        HIPCHK(hipMemcpyAsync(e->h_counters, e->d_counters, e->dist_k * slot * 8, hipMemcpyDeviceToHost, e->stream));
+    }
+    HIPCHK(hipStreamSynchronize(e->stream));
+    for (uint32_t k = 0; k < e->dist_k; ++k) {
+        gg_round_stats s;
+        fold_stats(e, e->h_counters + (size_t)k * gg::kSlots * gg::kCounters, e->dist_round_of[k], &s);
+        e->dist_done.push_back(s);
+    }
+    e->dist_k = 0;
+    e->inj_off = 0;
     return GG_OK;
 }
 
 int gg_dist_round_begin(gg_engine* e, gg_exchange* x) {
     if (!e || !x) return GG_EINVAL;
     if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
+    if (e->world < 2) return e->fail(GG_EINVAL, "not a sharded engine (world == 1): use gg_step");
     if (e->dist_open) return e->fail(GG_EINVAL, "round already open");
     HIPCHK(hipSetDevice(e->device));
     int rc = materialize_windows(e);
     if (rc) return rc;
-    if ((rc = ensure_events(e, 2))) return rc;
-    std::vector<size_t> off;
-    const size_t total = pack_injections(e, e->round, 1, off);
-    if (total == (size_t)-1) return GG_EIO;
-    if (total) HIPCHK(hipMemcpyAsync(e->d_inj, e->h_inj, total * 8, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(hipMemsetAsync(e->d_counters, 0, (size_t)gg::kSlots * gg::kCounters * 8, e->stream));
-    rc = enqueue_round(e, total ? e->d_inj : nullptr, (uint32_t)total, e->d_counters);
-    if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(e->h_counters, e->d_counters, (size_t)gg::kSlots * gg::kCounters * 8,
-                          hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
+    if (e->dist_k == kMaxBatch && (rc = fold_pending(e))) return rc;
     const int64_t r = e->round;
-    x->node_lo = e->lo;
-    x->node_hi = e->hi;
-    x->slice_rows = e->slice;
-    x->frontier = e->d_F[r & 1];
-    x->seen = e->d_base;
-    x->fired = e->d_fired[r & 3];
-    x->flags = e->d_flg[r & 1];
-    x->frontier_bytes = e->slice * e->nwp * 8;
-    x->seen_bytes = e->slice * e->nwp * 8;
-    x->fired_bytes = e->slice / 8;
-    x->flags_bytes = e->slice;
-    x->need_seen = (e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks) ? 1 : 0;
+    std::vector<size_t> off;
+    const size_t total = pack_injections(e, r, 1, off, e->inj_off);
+    if (total == (size_t)-1) return GG_EIO;
+    const uint32_t* d_inj = nullptr;
+    if (total) {
+        HIPCHK(hipMemcpyAsync(e->d_inj + 2 * e->inj_off, e->h_inj + 2 * e->inj_off, total * 8,
+                              hipMemcpyHostToDevice, e->stream));
+        d_inj = e->d_inj + 2 * e->inj_off;
+        e->inj_off += total;
+    }
+    const size_t slot = (size_t)gg::kSlots * gg::kCounters;
+    unsigned long long* ctr = e->d_counters + e->dist_k * slot;
+    HIPCHK(hipMemsetAsync(ctr, 0, slot * 8, e->stream));
+    if ((rc = enqueue_round(e, d_inj, (uint32_t)total, ctr))) return rc;
+    // ghost payloads of this round: F rows, flags, fired bits (+ sets while the
+    // next round may read remote sets: sync callbacks and push edges)
+    const bool with_set = e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks;
+    const uint64_t pb = exchange_stride(e->nwp, with_set);
+    const uint64_t n_send = e->send_off[e->world];
+    if (n_send) {
+        const uint64_t chunks = n_send * (pb / 16);
+        const unsigned blocks = (unsigned)std::min<uint64_t>((chunks + gg::kBlock - 1) / gg::kBlock, 4096);
+        hipLaunchKernelGGL(gg::pack_ghosts, dim3(blocks), dim3(gg::kBlock), 0, e->stream, e->d_F[r & 1], e->d_base,
+                           e->d_flg[r & 1], e->d_fired[r & 3], e->d_send_idx, n_send, (uint32_t)e->nwp,
+                           with_set ? 1 : 0, e->d_xsend);
+        HIPCHK(hipGetLastError());
+    }
+    e->xsend_bytes.assign(e->world, 0);
+    e->xrecv_bytes.assign(e->world, 0);
+    for (uint32_t q = 0; q < e->world; ++q) {
+        e->xsend_bytes[q] = (e->send_off[q + 1] - e->send_off[q]) * pb;
+        e->xrecv_bytes[q] = (e->recv_off[q + 1] - e->recv_off[q]) * pb;
+    }
+    if (e->dist_round_of.size() < kMaxBatch) e->dist_round_of.resize(kMaxBatch);
+    e->dist_round_of[e->dist_k] = r;
+    x->send = e->d_xsend;
+    x->recv = e->d_xrecv;
+    x->send_bytes = e->xsend_bytes.data();
+    x->recv_bytes = e->xrecv_bytes.data();
+    x->send_total = n_send * pb;
+    x->recv_total = e->recv_off[e->world] * pb;
+    x->on_device = 1;
+    x->stream = (void*)e->stream;
     e->dist_open = true;
     return GG_OK;
 }
 
 int gg_dist_round_end(gg_engine* e, gg_round_stats* out) {
     if (!e || !e->dist_open) return GG_EINVAL;
-    gg_round_stats s;
-    fold_stats(e, e->h_counters, &s);
-    if (out) *out = s;
-    e->inj.erase(e->round);
+    HIPCHK(hipSetDevice(e->device));
+    const int64_t r = e->round;
+    if (e->n_ghost) {
+        const bool with_set = e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks;
+        const uint64_t chunks = e->n_ghost * (exchange_stride(e->nwp, with_set) / 16);
+        const unsigned blocks = (unsigned)std::max<uint64_t>(
+            1, std::min<uint64_t>((chunks + gg::kBlock - 1) / gg::kBlock, 4096));
+        hipLaunchKernelGGL(gg::unpack_ghosts, dim3(blocks), dim3(gg::kBlock), 0, e->stream, e->d_F[r & 1], e->d_base,
+                           e->d_flg[r & 1], e->d_fired[r & 3], e->d_act + (r & 3), e->d_xrecv, e->n_ghost,
+                           e->ghost0, (uint32_t)e->nwp, with_set ? 1 : 0);
+        HIPCHK(hipGetLastError());
+    }
+    e->dist_k++;
+    e->inj.erase(r);
     e->round++;
     e->dist_open = false;
+    if (out) {
+        int rc = fold_pending(e);
+        if (rc) return rc;
+        *out = e->dist_done.back();
+        e->dist_done.pop_back();
+    }
     return GG_OK;
 }
 
-static bool owned(const gg_engine* e, uint64_t a, uint64_t b) { return a <= b && a >= e->lo && b <= e->hi; }
+int gg_dist_flush(gg_engine* e, gg_round_stats* out, uint64_t cap, uint64_t* n_out) {
+    if (!e) return GG_EINVAL;
+    if (e->dist_open) return e->fail(GG_EINVAL, "round still open");
+    HIPCHK(hipSetDevice(e->device));
+    int rc = fold_pending(e);
+    if (rc) return rc;
+    const uint64_t n = e->dist_done.size();
+    if (n_out) *n_out = n;
+    if (!out) return GG_OK;
+    if (cap < n) return e->fail(GG_EINVAL, "stats buffer too small");
+    for (uint64_t i = 0; i < n; ++i) out[i] = e->dist_done[i];
+    e->dist_done.clear();
+    return GG_OK;
+}
 
-// Node sets of owned nodes [a, b) after the last completed round:
-// base | F_last where the node's flag says LAG.
+// Sets of owned local rows [a, b) after the last completed round: base | F_last
+// where the row's flag says LAG.
 static int copy_rows(gg_engine* e, uint64_t a, uint64_t b, std::vector<uint64_t>& h) {
-    const uint64_t rep = (uint64_t)e->rank * e->slice + (a - e->lo);
     const uint64_t n = b - a;
     h.resize(n * e->nwp);
     if (!n) return GG_OK;
     HIPCHK(hipStreamSynchronize(e->stream));
-    HIPCHK(hipMemcpy(h.data(), e->d_base + rep * e->nwp, h.size() * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h.data(), e->d_base + a * e->nwp, h.size() * 8, hipMemcpyDeviceToHost));
     if (e->round == 0) return GG_OK;
     const int last = (int)((e->round - 1) & 1);
     std::vector<uint8_t> fl(n);
-    HIPCHK(hipMemcpy(fl.data(), e->d_flg[last] + rep, n, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(fl.data(), e->d_flg[last] + a, n, hipMemcpyDeviceToHost));
     std::vector<uint64_t> f(e->nwp);
     for (uint64_t i = 0; i < n; ++i) {
         if (!(fl[i] & gg::FL_LAG)) continue;
-        HIPCHK(hipMemcpy(f.data(), e->d_F[last] + (rep + i) * e->nwp, e->nwp * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(f.data(), e->d_F[last] + (a + i) * e->nwp, e->nwp * 8, hipMemcpyDeviceToHost));
         for (uint64_t j = 0; j < e->nwp; ++j) h[i * e->nwp + j] |= f[j];
     }
     return GG_OK;
 }
 
-int gg_read(gg_engine* e, uint32_t node, int64_t* out, uint64_t cap, uint64_t* n_out) {
-    if (!e || !e->have_topo) return GG_EINVAL;
-    if (!owned(e, node, (uint64_t)node + 1)) return e->fail(GG_EINVAL, "node not owned by this engine");
+// Local rows of owned nodes (GG_EINVAL if one is not owned).
+static int rows_of(gg_engine* e, const uint32_t* nodes, uint64_t n, std::vector<uint32_t>& rows, uint64_t& lo,
+                   uint64_t& hi) {
+    rows.resize(n);
+    lo = ~0ull;
+    hi = 0;
+    for (uint64_t k = 0; k < n; ++k) {
+        const uint32_t l = local_row(e, nodes[k]);
+        if (l == ~0u || l >= e->n_own) return e->fail(GG_EINVAL, "node not owned by this engine");
+        rows[k] = l;
+        lo = std::min<uint64_t>(lo, l);
+        hi = std::max<uint64_t>(hi, (uint64_t)l + 1);
+    }
+    if (!n) lo = hi = 0;
+    return GG_OK;
+}
+
+static int read_bits_rows(gg_engine* e, const uint32_t* nodes, uint64_t n, uint64_t* out) {
+    std::vector<uint32_t> rows;
+    uint64_t lo, hi;
+    int rc = rows_of(e, nodes, n, rows, lo, hi);
+    if (rc) return rc;
     HIPCHK(hipSetDevice(e->device));
     std::vector<uint64_t> h;
-    int rc = copy_rows(e, node, (uint64_t)node + 1, h);
+    if ((rc = copy_rows(e, lo, hi, h))) return rc;
+    for (uint64_t k = 0; k < n; ++k) std::memcpy(out + k * e->nw, h.data() + (rows[k] - lo) * e->nwp, e->nw * 8);
+    return GG_OK;
+}
+
+static int delivery_rows(gg_engine* e, const uint32_t* nodes, uint64_t n, int32_t* out) {
+    if (!e->d_dr) return e->fail(GG_EINVAL, "GG_TRACK_DELIVERY not enabled");
+    std::vector<uint32_t> rows;
+    uint64_t lo, hi;
+    int rc = rows_of(e, nodes, n, rows, lo, hi);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    const uint64_t W = e->cfg.n_lanes;
+    std::vector<int32_t> h((hi - lo) * W);
+    if (!h.empty()) HIPCHK(hipMemcpy(h.data(), e->d_dr + lo * W, h.size() * 4, hipMemcpyDeviceToHost));
+    for (uint64_t k = 0; k < n; ++k) std::memcpy(out + k * W, h.data() + (rows[k] - lo) * W, W * 4);
+    return GG_OK;
+}
+
+static std::vector<uint32_t> node_range(uint32_t a, uint32_t b) {
+    std::vector<uint32_t> v;
+    for (uint32_t x = a; x < b; ++x) v.push_back(x);
+    return v;
+}
+
+int gg_read(gg_engine* e, uint32_t node, int64_t* out, uint64_t cap, uint64_t* n_out) {
+    if (!e || !e->have_topo) return GG_EINVAL;
+    std::vector<uint64_t> h(e->nw);
+    int rc = read_bits_rows(e, &node, 1, h.data());
     if (rc) return rc;
     std::vector<int64_t> vals;
     for (uint64_t j = 0; j < e->nw; ++j) {
@@ -944,31 +1268,34 @@ int gg_read(gg_engine* e, uint32_t node, int64_t* out, uint64_t cap, uint64_t* n
 }
 
 int gg_read_bits(gg_engine* e, uint32_t a, uint32_t b, uint64_t* out) {
-    if (!e || !e->have_topo || !out) return GG_EINVAL;
-    if (!owned(e, a, b)) return e->fail(GG_EINVAL, "range not owned by this engine");
-    HIPCHK(hipSetDevice(e->device));
-    std::vector<uint64_t> h;
-    int rc = copy_rows(e, a, b, h);
-    if (rc) return rc;
-    for (uint64_t i = 0; i < (uint64_t)(b - a); ++i)
-        std::memcpy(out + i * e->nw, h.data() + i * e->nwp, e->nw * 8);
-    return GG_OK;
+    if (!e || !e->have_topo || !out || a > b) return GG_EINVAL;
+    const auto v = node_range(a, b);
+    return read_bits_rows(e, v.data(), v.size(), out);
+}
+
+int gg_read_bits_nodes(gg_engine* e, const uint32_t* nodes, uint64_t n, uint64_t* out) {
+    if (!e || !e->have_topo || (n && (!nodes || !out))) return GG_EINVAL;
+    return read_bits_rows(e, nodes, n, out);
 }
 
 int gg_delivery_rounds(gg_engine* e, uint32_t a, uint32_t b, int32_t* out, uint64_t cap) {
-    if (!e || !e->have_topo || !out) return GG_EINVAL;
-    if (!e->d_dr) return e->fail(GG_EINVAL, "GG_TRACK_DELIVERY not enabled");
-    if (!owned(e, a, b)) return e->fail(GG_EINVAL, "range not owned by this engine");
-    const uint64_t n = (uint64_t)(b - a) * e->cfg.n_lanes;
-    if (cap < n) return e->fail(GG_EINVAL, "output buffer too small");
-    HIPCHK(hipSetDevice(e->device));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    if (n) HIPCHK(hipMemcpy(out, e->d_dr + (a - e->lo) * e->cfg.n_lanes, n * 4, hipMemcpyDeviceToHost));
-    return GG_OK;
+    if (!e || !e->have_topo || !out || a > b) return GG_EINVAL;
+    if (cap < (uint64_t)(b - a) * e->cfg.n_lanes) return e->fail(GG_EINVAL, "output buffer too small");
+    const auto v = node_range(a, b);
+    return delivery_rows(e, v.data(), v.size(), out);
+}
+
+int gg_delivery_rounds_nodes(gg_engine* e, const uint32_t* nodes, uint64_t n, int32_t* out) {
+    if (!e || !e->have_topo || (n && (!nodes || !out))) return GG_EINVAL;
+    return delivery_rows(e, nodes, n, out);
 }
 
 int gg_reset(gg_engine* e) {
     if (!e) return GG_EINVAL;
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    e->dist_k = 0;
+    e->dist_done.clear();
+    e->inj_off = 0;
     e->lanes.clear();
     e->lane_value.clear();
     e->inj.clear();

@@ -137,13 +137,17 @@ struct RoundArgs {
     const uint32_t* inj;        // (local node, lane) pairs sorted by node
     uint32_t n_inj;
     unsigned long long* counters;  // [kSlots][kCounters]
-    uint64_t n_own, own0, lo;
+    uint64_t n_own, own0, lo;   // own rows are local rows own0 .. own0+n_own-1 (own0 = 0)
+    const uint32_t* gid;        // [rows] original node id of each local row (sharded), or
+                                // nullptr: original id = lo + row (single engine)
+    uint64_t ghost0, n_ghost;   // sharded: ghost rows ghost0 .. ghost0+n_ghost-1
+    const int64_t* gout_ptr;    // [n_ghost+1] per ghost: the owned nodes it sends to
+    const uint32_t* gout_col;
     uint32_t nwp, nw;
     uint32_t tile_nodes;        // NG of the expand kernel
     int32_t symmetric;          // out-lists == in-lists
     uint64_t n_edges;           // in_col entries of this engine
     uint64_t rows;              // replica rows
-    int32_t mark_all;           // sharded engines: every owned node is a candidate
     int32_t stream_ok;          // lean round (no sync events in expand, no masks) with nwp >= 2:
                                 // expand_stream takes it when it is dense (dense_round)
     uint32_t ablate;            // DIAGNOSTIC timing builds only (GG_ABLATE): 1 no row stores,
@@ -197,17 +201,21 @@ __device__ __forceinline__ bool bit_at(const uint64_t* bm, uint64_t row) {
 }
 
 // Most nodes are candidates this round: the nodes that became active in r-1
-// times the mean out-degree cover at least half of the owned nodes (sharded
-// engines: always, since remote senders cannot mark). Read from the act ring,
+// (owned ones and, in sharded engines, ghosts) times the mean out-degree cover
+// at least half of the owned nodes. Read from the act ring,
 // which no kernel of round r writes, so every launch of the round agrees.
 __device__ __forceinline__ bool busy_round(const RoundArgs& a) {
-    if (a.mark_all) return true;
     const double act = (double)a.act[(a.round - 1) & 3];
     return 2.0 * act * (double)a.n_edges >= (double)a.n_own * (double)a.n_own;
 }
 // Dense lean round: expand_stream visits every node, round_prep marks nothing
 // and expand_round exits.
 __device__ __forceinline__ bool dense_round(const RoundArgs& a) { return a.stream_ok && busy_round(a); }
+
+// Original node id of local row i (hashes, sync timers, partition groups).
+__device__ __forceinline__ uint64_t gid_of(const RoundArgs& a, uint64_t i) {
+    return a.gid ? (uint64_t)a.gid[i] : a.lo + i;
+}
 
 // message from replica row ra to replica row rb in round (r-3+k) dropped?
 template <bool MASKW>
@@ -365,18 +373,19 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                     c_bytes += 3;
                 }
                 // candidates of this round
-                if (a.mark_all || (f & FL_LAG) || fm2) {
+                if ((f & FL_LAG) || fm2) {
                     a.cand[rep] = CA_NODE;
                     if (!a.stream_ok) a.tile_cand[i / a.tile_nodes] = 1;
                 }
-                if (!a.mark_all && ((f & FL_ACT) || fm3)) {  // senders mark their receivers
+                if ((f & FL_ACT) || fm3) {  // senders mark their (owned) receivers
                     o0 = a.out_ptr[i];
                     o1 = a.out_ptr[i + 1];
                     c_bytes += 16 + 5 * (unsigned long long)(o1 - o0);
                     for (int64_t e = o0; e < o1; ++e) {
-                        const uint64_t w = a.out_col[e] & kColMask;  // single engine: w == local row
+                        const uint64_t w = a.out_col[e] & kColMask;
+                        if (w >= a.n_own) continue;  // a ghost: its owner marks it
                         a.cand[w] = CA_NODE;
-                        if (!a.stream_ok) a.tile_cand[(w - a.own0) / a.tile_nodes] = 1;
+                        if (!a.stream_ok) a.tile_cand[w / a.tile_nodes] = 1;
                     }
                 }
             }
@@ -406,7 +415,7 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                     }
                     const uint32_t kk = a.sync_k[i] + 1;
                     a.sync_k[i] = kk;
-                    a.sync_next[i] = (int32_t)(a.round + gg_sync_interval(a.seed, a.lo + i, kk,
+                    a.sync_next[i] = (int32_t)(a.round + gg_sync_interval(a.seed, gid_of(a, i), kk,
                                                                           a.sync_base, a.sync_jitter));
                 }
             }
@@ -414,6 +423,21 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
         if constexpr (SYNCW) {  // before the first timer every fired word is still zero
             const unsigned long long word = __ballot(fire);
             if ((threadIdx.x & 63) == 0) a.fired_cur[(a.own0 + (i & ~63ull)) >> 6] = word;
+        }
+    }
+    // sharded: ghost senders (remote nodes, state from last round's exchange)
+    // that were active or pushed mark their owned receivers
+    if (!dense) {
+        for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < a.n_ghost; g += stride) {
+            const uint64_t row = a.ghost0 + g;
+            bool fm3 = false;
+            if constexpr (SYNCW) fm3 = bit_at(a.fired_m3, row);
+            if (!((a.flg_prev[row] & FL_ACT) || fm3)) continue;
+            for (int64_t e = a.gout_ptr[g]; e < a.gout_ptr[g + 1]; ++e) {
+                const uint32_t w = a.gout_col[e];
+                a.cand[w] = CA_NODE;
+                if (!a.stream_ok) a.tile_cand[w / a.tile_nodes] = 1;
+            }
         }
     }
     unsigned long long acc[C_NUM];
@@ -808,7 +832,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                     // ---- new state
                     Row<WPL> F;
                     unsigned long long T = 0;
-                    const uint64_t g = a.lo + i;
+                    const uint64_t g = gid_of(a, i);
 #pragma unroll
                     for (int w = 0; w < WPL; ++w) {
                         F.w[w] = S.w[w] & ~sp.w[w];
@@ -1059,7 +1083,7 @@ void expand_stream(RoundArgs a) {
         // new state
         Row<WPL> F;
         uint32_t T = 0;
-        const uint64_t g = a.lo + i;
+        const uint64_t g = gid_of(a, i);
 #pragma unroll
         for (int w = 0; w < WPL; ++w) {
             F.w[w] = S.w[w] & ~sp.w[w];
@@ -1125,23 +1149,98 @@ __global__ void track_delivery(const uint64_t* F_cur, const uint8_t* flg_cur, in
     }
 }
 
-__global__ void sync_init(int32_t* sync_next, uint32_t* sync_k, uint64_t n_own, uint64_t lo,
+__global__ void sync_init(int32_t* sync_next, uint32_t* sync_k, uint64_t n_own, const uint32_t* gid,
                           uint64_t seed, uint32_t base, uint32_t jitter) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_own) return;
     sync_k[i] = 0;
-    sync_next[i] = (int32_t)gg_sync_interval(seed, lo + i, 0, base, jitter);
+    sync_next[i] = (int32_t)gg_sync_interval(seed, gid ? (uint64_t)gid[i] : i, 0, base, jitter);
 }
 
-// Seeded bisection groups in replica-row order (padding rows: group 0, unused).
-__global__ void fill_seeded_groups(uint8_t* grp, uint64_t rows, uint64_t slice,
-                                   const uint64_t* rank_lo, uint32_t world, uint64_t seed,
-                                   uint64_t epoch_seed) {
+// Seeded bisection groups of the local rows (padding rows: group 0, unused).
+__global__ void fill_seeded_groups(uint8_t* grp, uint64_t rows, uint64_t n_valid, const uint32_t* gid,
+                                   uint64_t seed, uint64_t epoch_seed) {
     const uint64_t rr = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (rr >= rows) return;
-    const uint64_t p = rr / slice;
-    const uint64_t g = rank_lo[p] + (rr - p * slice);
-    grp[rr] = (p < world && g < rank_lo[p + 1]) ? (uint8_t)gg_part_group(seed, epoch_seed, g) : 0;
+    const uint32_t g = gid ? gid[rr] : (uint32_t)rr;
+    grp[rr] = (rr < n_valid && g != ~0u) ? (uint8_t)gg_part_group(seed, epoch_seed, g) : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Sharded exchange. Payload slot of one node (stride bytes, 16-byte aligned):
+// its F row, its set row (base, when the round ships sets), then a 16-byte tail
+// {flag byte, sync-fired byte}. pack_ghosts writes the slots of the owned rows
+// listed in idx (concatenated per destination rank); unpack_ghosts writes slot
+// k into ghost row ghost0 + k (ghosts are numbered in receive order), rebuilds
+// the ghost words of the fired bitmap and counts the active ghosts into the
+// act ring (next round's dense/sparse choice).
+__global__ __launch_bounds__(kBlock) void pack_ghosts(const uint64_t* F_cur, const uint64_t* base,
+                                                      const uint8_t* flg_cur, const uint64_t* fired_cur,
+                                                      const uint32_t* idx, uint64_t n, uint32_t nwp,
+                                                      int32_t with_set, uint8_t* out) {
+    const uint64_t rowc = nwp / 2 + (nwp & 1);           // 16-byte chunks of a row (nwp=1: 1)
+    const uint64_t chunks = rowc * (with_set ? 2 : 1) + 1;
+    const uint64_t stride = chunks * 16;
+    const uint64_t total = n * chunks;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = t / chunks, c = t % chunks;
+        const uint64_t row = idx[k];
+        uint8_t* dst = out + k * stride + c * 16;
+        if (c < rowc * (with_set ? 2 : 1)) {
+            const uint64_t* src = (c < rowc ? F_cur : base) + row * nwp + (c % rowc) * 2;
+            ulonglong2 v;
+            v.x = src[0];
+            v.y = nwp > 1 ? src[1] : 0ull;
+            *reinterpret_cast<ulonglong2*>(dst) = v;
+        } else {
+            ulonglong2 v;
+            v.x = (uint64_t)flg_cur[row] | ((uint64_t)((fired_cur[row >> 6] >> (row & 63)) & 1ull) << 8);
+            v.y = 0;
+            *reinterpret_cast<ulonglong2*>(dst) = v;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void unpack_ghosts(uint64_t* F_cur, uint64_t* base, uint8_t* flg_cur,
+                                                        uint64_t* fired_cur, uint32_t* act_cur,
+                                                        const uint8_t* in, uint64_t n, uint64_t ghost0,
+                                                        uint32_t nwp, int32_t with_set) {
+    const uint64_t rowc = nwp / 2 + (nwp & 1);
+    const uint64_t chunks = rowc * (with_set ? 2 : 1) + 1;
+    const uint64_t stride = chunks * 16;
+    const uint64_t total = n * chunks;
+    uint32_t nact = 0;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = t / chunks, c = t % chunks;
+        const uint64_t row = ghost0 + k;
+        const uint8_t* src = in + k * stride + c * 16;
+        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(src);
+        if (c < rowc * (with_set ? 2 : 1)) {
+            uint64_t* dst = (c < rowc ? F_cur : base) + row * nwp + (c % rowc) * 2;
+            dst[0] = v.x;
+            if (nwp > 1) dst[1] = v.y;
+        } else {
+            const uint8_t f = (uint8_t)(v.x & 0xff);
+            flg_cur[row] = f;
+            nact += (f & FL_ACT) ? 1u : 0u;
+        }
+    }
+    // fired words of the ghost rows (ghost0 is a multiple of 64)
+    const uint64_t nwords = (n + 63) / 64;
+    for (uint64_t wi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; wi < nwords;
+         wi += (uint64_t)gridDim.x * blockDim.x) {
+        unsigned long long word = 0;
+        for (uint64_t b = 0; b < 64 && wi * 64 + b < n; ++b) {
+            const uint64_t k = wi * 64 + b;
+            const uint8_t fb = in[k * stride + (chunks - 1) * 16 + 1];
+            word |= (unsigned long long)(fb & 1) << b;
+        }
+        fired_cur[(ghost0 >> 6) + wi] = word;
+    }
+    const unsigned long long s = wave_sum(nact);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(act_cur, (uint32_t)s);
 }
 
 }  // namespace gg

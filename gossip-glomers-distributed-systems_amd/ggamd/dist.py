@@ -1,19 +1,24 @@
-"""Sharded rounds: one engine per GPU (rank), vertex-range shards, one
-all-gather of boundary state per round through torch.distributed.
+"""Sharded rounds: one engine per GPU (rank), locality-ordered vertex ranges,
+one all-to-all-v of packed ghost payloads per round through torch.distributed.
 
 The reference has no equivalent (each Maelstrom node is its own process and
 every gossip hop crosses a pipe); here the per-round exchange replaces the
-network delivery of every forward/push/read crossing a shard boundary
+network delivery of every forward/push/read/read_ok crossing a shard boundary
 (SURVEY.md §8e). A round on every rank is
 
-    gg_dist_round_begin   -> the rank's kernels for its own nodes
-    all_gather            -> frontier (always), fired bitmap (always) and seen
-                             (rounds whose successor may read remote sets) slices
-    gg_dist_round_end     -> this rank's counters; all_reduce sums them
+    gg_dist_round_begin   -> the rank's kernels for its owned nodes, then a pack
+                             kernel: for each other rank q, the owned nodes q
+                             holds as ghosts (F row, flags, sync-fired bit, and
+                             the set row in sync rounds)
+    all_to_all_single     -> per-peer byte counts from the engine
+    gg_dist_round_end     -> unpack kernel into this rank's ghost rows
 
-On GPUs the backend is "nccl" (= RCCL over xGMI on ROCm) and the gather is
-in place on the engine's own device buffers; on CPU (tests) it is gloo over
-host buffers of the CPU oracle engine.
+On GPUs the backend is "nccl" (= RCCL over xGMI on ROCm): the collective is
+enqueued on the engine's own HIP stream (torch.cuda.ExternalStream), so a
+multi-round step runs without host synchronisation and the per-round counters
+are collected once at the end (gg_dist_flush) and summed over ranks with one
+all_reduce. With "gloo" (CPU tests, or several ranks sharing one GPU in the GPU
+tests) the payloads are staged through host memory.
 """
 from __future__ import annotations
 
@@ -34,8 +39,10 @@ class _CudaBuf:
                                          "data": (ptr, False), "version": 3, "strides": None}
 
 
-def _view(ptr: int, nbytes: int, device: torch.device) -> torch.Tensor:
-    if device.type == "cuda":
+def _view(ptr: int, nbytes: int, on_device: bool, device: torch.device) -> torch.Tensor:
+    if nbytes == 0 or not ptr:
+        return torch.empty(0, dtype=torch.uint8, device=device if on_device else "cpu")
+    if on_device:
         return torch.as_tensor(_CudaBuf(ptr, nbytes), device=device)
     arr = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(ptr))
     return torch.from_numpy(arr)
@@ -49,31 +56,44 @@ class ShardedRunner:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         assert self.world == eng.world and self.rank == eng.rank
-        self.inplace = dist.get_backend(group) == "nccl"
+        self.nccl = dist.get_backend(group) == "nccl"
 
-    def _gather(self, ptr: int, slice_bytes: int):
-        full = _view(ptr, slice_bytes * self.world, self.device)
-        own = full[self.rank * slice_bytes:(self.rank + 1) * slice_bytes]
-        if self.inplace:
-            dist.all_gather_into_tensor(full, own, group=self.group)
-        else:
-            parts = [full[p * slice_bytes:(p + 1) * slice_bytes] for p in range(self.world)]
-            dist.all_gather(parts, own.clone(), group=self.group)
-
-    def round(self) -> dict:
+    def round(self, wait: bool = False) -> dict | None:
         x = self.eng.dist_round_begin()
-        self._gather(x.frontier, x.frontier_bytes)
-        self._gather(x.fired, x.fired_bytes)
-        if x.flags_bytes:
-            self._gather(x.flags, x.flags_bytes)
-        if x.need_seen:
-            self._gather(x.seen, x.seen_bytes)
-        if self.device.type == "cuda":
-            torch.cuda.current_stream(self.device).synchronize()
-        return self.eng.dist_round_end()
+        on_dev = bool(x.on_device)
+        ss = [int(x.send_bytes[q]) for q in range(self.world)]
+        rs = [int(x.recv_bytes[q]) for q in range(self.world)]
+        send = _view(x.send, int(x.send_total), on_dev, self.device)
+        recv = _view(x.recv, int(x.recv_total), on_dev, self.device)
+        if self.nccl:
+            assert on_dev, "nccl backend needs device buffers"
+            ext = torch.cuda.ExternalStream(x.stream, device=self.device) if x.stream else None
+            if ext is not None:
+                with torch.cuda.stream(ext):
+                    dist.all_to_all_single(recv, send, rs, ss, group=self.group)
+            else:
+                dist.all_to_all_single(recv, send, rs, ss, group=self.group)
+        elif on_dev:
+            # gloo with device buffers (several ranks on one GPU): stage via host
+            ext = torch.cuda.ExternalStream(x.stream, device=self.device) if x.stream else None
+            if ext is not None:
+                ext.synchronize()
+            send_h = send.cpu()
+            recv_h = torch.empty(recv.numel(), dtype=torch.uint8)
+            dist.all_to_all_single(recv_h, send_h, rs, ss, group=self.group)
+            if ext is not None:
+                with torch.cuda.stream(ext):
+                    recv.copy_(recv_h, non_blocking=False)
+            else:
+                recv.copy_(recv_h)
+        else:
+            dist.all_to_all_single(recv, send, rs, ss, group=self.group)
+        return self.eng.dist_round_end(wait=wait)
 
     def step(self, n_rounds: int, reduce: bool = True) -> list[dict]:
-        local = [self.round() for _ in range(n_rounds)]
+        for _ in range(n_rounds):
+            self.round(wait=False)
+        local = self.eng.dist_flush()
         return self.reduce(local) if reduce else local
 
     def reduce(self, local: list[dict]) -> list[dict]:
@@ -83,16 +103,17 @@ class ShardedRunner:
         vals = np.array([[s[f] for f in COUNT_FIELDS] for s in local], dtype=np.uint64)
         t = torch.from_numpy(vals.view(np.int64).copy())
         ms = torch.tensor([s["kernel_ms"] for s in local], dtype=torch.float64)
-        if self.inplace:
+        if self.nccl:
             t = t.to(self.device)
             ms = ms.to(self.device)
         dist.all_reduce(t, group=self.group)
         dist.all_reduce(ms, op=dist.ReduceOp.MAX, group=self.group)
         tot = t.cpu().numpy().view(np.uint64)
+        ms = ms.cpu()
         out = []
         for k, s in enumerate(local):
-            d = {"round": s["round"], "kernel_ms": float(ms[k]),
-                 "work_rows": s["work_rows"], "work_gathers": s["work_gathers"]}
+            d = dict(s)
+            d["kernel_ms"] = float(ms[k])
             for j, f in enumerate(COUNT_FIELDS):
                 d[f] = int(tot[k, j]) & M64
             out.append(d)

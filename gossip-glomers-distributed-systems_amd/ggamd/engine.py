@@ -70,18 +70,14 @@ class GGRoundStats(C.Structure):
 
 class GGExchange(C.Structure):
     _fields_ = [
-        ("node_lo", C.c_uint64),
-        ("node_hi", C.c_uint64),
-        ("slice_rows", C.c_uint64),
-        ("frontier", C.c_void_p),
-        ("seen", C.c_void_p),
-        ("fired", C.c_void_p),
-        ("flags", C.c_void_p),
-        ("frontier_bytes", C.c_uint64),
-        ("seen_bytes", C.c_uint64),
-        ("fired_bytes", C.c_uint64),
-        ("flags_bytes", C.c_uint64),
-        ("need_seen", C.c_int32),
+        ("send", C.c_void_p),
+        ("recv", C.c_void_p),
+        ("send_bytes", C.POINTER(C.c_uint64)),
+        ("recv_bytes", C.POINTER(C.c_uint64)),
+        ("send_total", C.c_uint64),
+        ("recv_total", C.c_uint64),
+        ("on_device", C.c_int32),
+        ("stream", C.c_void_p),
     ]
 
 
@@ -95,7 +91,8 @@ GG_SYMBOLS = [
     "gg_partition_seeded", "gg_partition_groups", "gg_broadcast", "gg_broadcast_many",
     "gg_lane_of", "gg_step",
     "gg_current_round", "gg_step_device_ms", "gg_read", "gg_read_bits", "gg_delivery_rounds", "gg_reset",
-    "gg_dist_round_begin", "gg_dist_round_end", "gg_dist_range",
+    "gg_read_bits_nodes", "gg_delivery_rounds_nodes",
+    "gg_dist_round_begin", "gg_dist_round_end", "gg_dist_flush", "gg_dist_owned",
 ]
 
 _LIBS: dict[str, C.CDLL] = {}
@@ -131,7 +128,10 @@ def load_library(path: str) -> C.CDLL:
     lib.gg_reset.argtypes = [C.c_void_p]
     lib.gg_dist_round_begin.argtypes = [C.c_void_p, P(GGExchange)]
     lib.gg_dist_round_end.argtypes = [C.c_void_p, P(GGRoundStats)]
-    lib.gg_dist_range.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint64)]
+    lib.gg_dist_flush.argtypes = [C.c_void_p, P(GGRoundStats), C.c_uint64, P(C.c_uint64)]
+    lib.gg_dist_owned.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]
+    lib.gg_read_bits_nodes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+    lib.gg_delivery_rounds_nodes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
     _LIBS[path] = lib
     return lib
 
@@ -264,25 +264,50 @@ class Engine:
         self._ok(self.lib.gg_delivery_rounds(self.h, lo, hi, out.ctypes.data, out.size))
         return out
 
+    def read_bits_nodes(self, nodes) -> np.ndarray:
+        nodes = np.ascontiguousarray(nodes, np.uint32)
+        out = np.zeros((nodes.size, self.nw), np.uint64)
+        self._ok(self.lib.gg_read_bits_nodes(self.h, nodes.ctypes.data, nodes.size, out.ctypes.data))
+        return out
+
+    def delivery_rounds_nodes(self, nodes) -> np.ndarray:
+        nodes = np.ascontiguousarray(nodes, np.uint32)
+        out = np.zeros((nodes.size, self.W), np.int32)
+        self._ok(self.lib.gg_delivery_rounds_nodes(self.h, nodes.ctypes.data, nodes.size, out.ctypes.data))
+        return out
+
     def reset(self):
         self._ok(self.lib.gg_reset(self.h))
 
     # ---- sharded rounds ------------------------------------------------------
 
-    def dist_range(self) -> tuple[int, int]:
-        lo, hi = C.c_uint64(0), C.c_uint64(0)
-        self._ok(self.lib.gg_dist_range(self.h, C.byref(lo), C.byref(hi)))
-        return lo.value, hi.value
+    def dist_owned(self) -> np.ndarray:
+        """Original ids of the nodes this engine owns (sharded mode), in its row order."""
+        n = C.c_uint64(0)
+        self._ok(self.lib.gg_dist_owned(self.h, None, 0, C.byref(n)))
+        out = np.zeros(max(1, n.value), np.uint32)
+        self._ok(self.lib.gg_dist_owned(self.h, out.ctypes.data, out.size, C.byref(n)))
+        return out[: n.value]
 
     def dist_round_begin(self) -> GGExchange:
         x = GGExchange()
         self._ok(self.lib.gg_dist_round_begin(self.h, C.byref(x)))
         return x
 
-    def dist_round_end(self) -> dict:
+    def dist_round_end(self, wait: bool = True) -> dict | None:
+        if not wait:
+            self._ok(self.lib.gg_dist_round_end(self.h, None))
+            return None
         s = GGRoundStats()
         self._ok(self.lib.gg_dist_round_end(self.h, C.byref(s)))
         return stats_dict(s)
+
+    def dist_flush(self) -> list[dict]:
+        n = C.c_uint64(0)
+        self._ok(self.lib.gg_dist_flush(self.h, None, 0, C.byref(n)))
+        arr = (GGRoundStats * max(1, n.value))()
+        self._ok(self.lib.gg_dist_flush(self.h, arr, n.value, C.byref(n)))
+        return [stats_dict(arr[i]) for i in range(n.value)]
 
 
 def missing_symbols(path: str) -> list[str]:

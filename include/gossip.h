@@ -22,7 +22,8 @@
  *                             (`main.go:38-40`) event of those rounds
  * gg_read / gg_read_bits      client `read` -> HandleRead `broadcast.go:124-132`
  * gg_delivery_rounds          observation only (first round each value was seen)
- * gg_dist_*                   one-engine-per-GPU vertex-range sharding (new)
+ * gg_dist_*                   one engine per GPU: locality-ordered vertex ranges with
+ *                             ghost copies of adjacent remote nodes (new)
  *
  * Determinization contract (restated in DESIGN.md §2):
  * one round per 100 ms tick; every message sent in round r is delivered in
@@ -50,7 +51,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 1
+#define GG_ABI_VERSION 2
 
 #define GG_OK 0
 #define GG_EIO (-5)
@@ -145,30 +146,45 @@ int gg_delivery_rounds(gg_engine* e, uint32_t node_lo, uint32_t node_hi, int32_t
  * topology and partition windows are kept. */
 int gg_reset(gg_engine* e);
 
-/* ---- sharded mode (cfg.world > 1): one engine per GPU, vertex-range shards ----
- * Every rank gives gg_topology the whole graph and keeps the rows of its own
- * range (edge-balanced cut points, identical on every rank). A round is
- *   gg_dist_round_begin -> caller all-gathers the exchange slices ->
- *   gg_dist_round_end   -> caller sums the per-rank stats.
- * The exchange buffers are laid out [world][slice_rows][...]; each rank writes
- * its own slice and the all-gather fills the rest (equal-size slices). */
+/* ---- sharded mode (cfg.world > 1): one engine per GPU -------------------------
+ * Every rank gives gg_topology the whole graph. The engine orders the nodes for
+ * locality (its choice, identical on every rank: the native order or a DFS
+ * preorder, whichever cuts fewer edges), splits that order into edge-balanced
+ * contiguous ranges, and keeps its range's nodes ("owned") plus read-only copies
+ * of the remote nodes adjacent to them ("ghosts"). Results do not depend on the
+ * order: claims still go by ascending original sender id. A round is
+ *   gg_dist_round_begin -> caller moves the packed ghost payloads between ranks
+ *                          (an all-to-all-v of bytes: send_bytes[q] from `send`
+ *                          to rank q, recv_bytes[p] from rank p into `recv`, both
+ *                          concatenated in rank order)
+ *   gg_dist_round_end   -> the engine unpacks the ghosts; per-rank counters are
+ *                          summed over ranks by the caller.
+ * When `stream` is non-NULL the round's kernels are only enqueued on that HIP
+ * stream; the caller enqueues its collective on the same stream and passes
+ * out = NULL to gg_dist_round_end, then collects the counters of all pending
+ * rounds with gg_dist_flush (no host synchronisation per round). */
 typedef struct {
-    uint64_t node_lo, node_hi; /* owned node range */
-    uint64_t slice_rows;       /* rows per rank slice (>= node_hi - node_lo) */
-    void* frontier;            /* [world][slice_rows][W/64] u64 new-bit buffer */
-    void* seen;                /* [world][slice_rows][W/64] u64 set buffer */
-    void* fired;               /* [world][slice_rows/64] u64 sync-fired bitmap */
-    void* flags;               /* [world][slice_rows] u8 per-node row flags (may be NULL) */
-    uint64_t frontier_bytes;   /* bytes per rank slice of each buffer */
-    uint64_t seen_bytes;
-    uint64_t fired_bytes;
-    uint64_t flags_bytes;      /* 0 when the engine has no flags buffer */
-    int32_t need_seen;         /* 1 if this round's seen slices must be exchanged */
+    void* send;                 /* packed payloads, [world] segments */
+    void* recv;
+    const uint64_t* send_bytes; /* [world] bytes to each rank this round */
+    const uint64_t* recv_bytes; /* [world] bytes from each rank this round */
+    uint64_t send_total, recv_total;
+    int32_t on_device;          /* 1: send/recv are device memory of the engine's GPU */
+    void* stream;               /* hipStream_t the round was enqueued on (NULL: done on return) */
 } gg_exchange;
 
 int gg_dist_round_begin(gg_engine* e, gg_exchange* xch);
+/* out != NULL: wait for the round and return its counters; NULL: leave them pending. */
 int gg_dist_round_end(gg_engine* e, gg_round_stats* out);
-int gg_dist_range(const gg_engine* e, uint64_t* node_lo, uint64_t* node_hi);
+/* Wait for every pending round and return their counters in round order (n_out =
+ * count); out = NULL only reports the count (after waiting) and keeps them pending. */
+int gg_dist_flush(gg_engine* e, gg_round_stats* out, uint64_t cap, uint64_t* n_out);
+/* Original ids of the owned nodes (n_out = count, even if > cap). */
+int gg_dist_owned(const gg_engine* e, uint32_t* nodes, uint64_t cap, uint64_t* n_out);
+
+/* gg_read_bits / gg_delivery_rounds for a list of owned nodes (any engine). */
+int gg_read_bits_nodes(gg_engine* e, const uint32_t* nodes, uint64_t n, uint64_t* out);
+int gg_delivery_rounds_nodes(gg_engine* e, const uint32_t* nodes, uint64_t n, int32_t* out);
 
 #ifdef __cplusplus
 }

@@ -94,6 +94,11 @@ struct gg_engine {
     int threads = 1;
     bool dist_open = false;
     Acc dist_acc;
+    // sharded exchange (dense: every owned node's seen row, F row and fired
+    // bit to every other rank; the HIP engine sends ghosts only)
+    std::vector<uint8_t> xsend, xrecv;
+    std::vector<uint64_t> xsend_bytes, xrecv_bytes;
+    std::vector<gg_round_stats> dist_pending;
 
     int fail(int code, const std::string& m) { err = m; return code; }
 
@@ -529,12 +534,17 @@ int gg_step_device_ms(const gg_engine* e, double* ms) {
     return GG_OK;
 }
 
-int gg_dist_range(const gg_engine* e, uint64_t* lo, uint64_t* hi) {
+int gg_dist_owned(const gg_engine* e, uint32_t* nodes, uint64_t cap, uint64_t* n_out) {
     if (!e || !e->have_topo) return GG_EINVAL;
-    if (lo) *lo = e->lo;
-    if (hi) *hi = e->hi;
+    const uint64_t n = e->hi - e->lo;
+    if (n_out) *n_out = n;
+    if (nodes)
+        for (uint64_t i = 0; i < n && i < cap; ++i) nodes[i] = (uint32_t)(e->lo + i);
     return GG_OK;
 }
+
+// payload of one node: seen row, F row (nw words each), fired byte (8-byte slot)
+static uint64_t node_payload(const gg_engine* e) { return (2 * e->nw + 1) * 8; }
 
 int gg_dist_round_begin(gg_engine* e, gg_exchange* x) {
     if (!e || !x) return GG_EINVAL;
@@ -543,33 +553,76 @@ int gg_dist_round_begin(gg_engine* e, gg_exchange* x) {
     e->dist_acc = Acc();
     e->compute_round(e->dist_acc);
     const int64_t r = e->round;
-    x->node_lo = e->lo;
-    x->node_hi = e->hi;
-    x->slice_rows = e->slice;
-    x->frontier = e->F[r & 1].data();
-    x->seen = e->seen[r & 1].data();
-    x->fired = e->fired[r & 3].data();
-    x->frontier_bytes = e->slice * e->nw * 8;
-    x->seen_bytes = e->slice * e->nw * 8;
-    x->fired_bytes = e->slice / 8;
-    x->flags = nullptr;
-    x->flags_bytes = 0;
-    // remote seen_prev is read in round r+1 by callbacks (fired r-1) and push
-    // edges (fired r-2); fires start at round >= sync_base.
-    x->need_seen = (e->cfg.enable_sync && r + 1 >= (int64_t)e->cfg.sync_base_ticks + 1) ? 1 : 0;
+    const uint64_t pb = node_payload(e), n_own = e->hi - e->lo, own0 = (uint64_t)e->rank * e->slice;
+    e->xsend_bytes.assign(e->world, 0);
+    e->xrecv_bytes.assign(e->world, 0);
+    uint64_t st = 0, rt = 0;
+    for (uint32_t q = 0; q < e->world; ++q) {
+        if (q == e->rank) continue;
+        e->xsend_bytes[q] = n_own * pb;
+        e->xrecv_bytes[q] = (e->rank_lo[q + 1] - e->rank_lo[q]) * pb;
+        st += e->xsend_bytes[q];
+        rt += e->xrecv_bytes[q];
+    }
+    e->xsend.assign(std::max<uint64_t>(1, st), 0);
+    e->xrecv.assign(std::max<uint64_t>(1, rt), 0);
+    uint8_t* p = e->xsend.data();
+    for (uint32_t q = 0; q < e->world; ++q) {
+        if (q == e->rank) continue;
+        for (uint64_t i = 0; i < n_own; ++i, p += pb) {
+            const uint64_t rep = own0 + i;
+            std::memcpy(p, &e->seen[r & 1][rep * e->nw], e->nw * 8);
+            std::memcpy(p + e->nw * 8, &e->F[r & 1][rep * e->nw], e->nw * 8);
+            p[2 * e->nw * 8] = e->fired_at(r, rep) ? 1 : 0;
+        }
+    }
+    x->send = e->xsend.data();
+    x->recv = e->xrecv.data();
+    x->send_bytes = e->xsend_bytes.data();
+    x->recv_bytes = e->xrecv_bytes.data();
+    x->send_total = st;
+    x->recv_total = rt;
+    x->on_device = 0;
+    x->stream = nullptr;
     e->dist_open = true;
     return GG_OK;
 }
 
 int gg_dist_round_end(gg_engine* e, gg_round_stats* out) {
     if (!e || !e->dist_open) return GG_EINVAL;
+    const int64_t r = e->round;
+    const uint64_t pb = node_payload(e);
+    const uint8_t* p = e->xrecv.data();
+    for (uint32_t q = 0; q < e->world; ++q) {
+        if (q == e->rank) continue;
+        for (uint64_t g = e->rank_lo[q]; g < e->rank_lo[q + 1]; ++g, p += pb) {
+            const uint64_t rep = (uint64_t)q * e->slice + (g - e->rank_lo[q]);
+            std::memcpy(&e->seen[r & 1][rep * e->nw], p, e->nw * 8);
+            std::memcpy(&e->F[r & 1][rep * e->nw], p + e->nw * 8, e->nw * 8);
+            uint64_t& w = e->fired[r & 3][rep >> 6];
+            if (p[2 * e->nw * 8]) w |= 1ull << (rep & 63);
+            else w &= ~(1ull << (rep & 63));
+        }
+    }
     gg_round_stats s;
     fill_stats(e, e->dist_acc, &s);
     if (out) *out = s;
+    else e->dist_pending.push_back(s);
     e->pend_acks = e->dist_acc.next_acks;
     e->pend_ackdrop = e->dist_acc.next_ackdrop;
     e->round++;
     e->dist_open = false;
+    return GG_OK;
+}
+
+int gg_dist_flush(gg_engine* e, gg_round_stats* out, uint64_t cap, uint64_t* n_out) {
+    if (!e) return GG_EINVAL;
+    const uint64_t n = e->dist_pending.size();
+    if (n_out) *n_out = n;
+    if (!out) return GG_OK;  // count only
+    if (cap < n) return e->fail(GG_EINVAL, "stats buffer too small");
+    for (uint64_t i = 0; i < n; ++i) out[i] = e->dist_pending[i];
+    e->dist_pending.clear();
     return GG_OK;
 }
 
@@ -616,9 +669,28 @@ int gg_delivery_rounds(gg_engine* e, uint32_t a, uint32_t b, int32_t* out, uint6
     return GG_OK;
 }
 
+int gg_read_bits_nodes(gg_engine* e, const uint32_t* nodes, uint64_t n, uint64_t* out) {
+    if (!e || !e->have_topo || (n && (!nodes || !out))) return GG_EINVAL;
+    for (uint64_t k = 0; k < n; ++k) {
+        int rc = gg_read_bits(e, nodes[k], nodes[k] + 1, out + k * e->nw);
+        if (rc) return rc;
+    }
+    return GG_OK;
+}
+
+int gg_delivery_rounds_nodes(gg_engine* e, const uint32_t* nodes, uint64_t n, int32_t* out) {
+    if (!e || !e->have_topo || (n && (!nodes || !out))) return GG_EINVAL;
+    for (uint64_t k = 0; k < n; ++k) {
+        int rc = gg_delivery_rounds(e, nodes[k], nodes[k] + 1, out + k * e->cfg.n_lanes, e->cfg.n_lanes);
+        if (rc) return rc;
+    }
+    return GG_OK;
+}
+
 int gg_reset(gg_engine* e) {
     if (!e) return GG_EINVAL;
     if (e->have_topo) e->reset_state();
+    e->dist_pending.clear();
     return GG_OK;
 }
 

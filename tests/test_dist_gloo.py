@@ -36,10 +36,10 @@ def _worker(rank, world, port, lib, sc, q):
         e = make_engine(lib, sc, rank=rank, world=world)
         r = ShardedRunner(e, torch.device("cpu"))
         stats = r.step(sc.rounds)
-        lo, hi = e.dist_range()
-        bits = e.read_bits(lo, hi)
-        dr = e.delivery_rounds(lo, hi)
-        q.put((rank, stats, lo, hi, bits, dr))
+        owned = e.dist_owned()
+        bits = e.read_bits_nodes(owned)
+        dr = e.delivery_rounds_nodes(owned)
+        q.put((rank, stats, owned, bits, dr))
     finally:
         dist.destroy_process_group()
 
@@ -62,13 +62,13 @@ def _check(lib, sc, world=2):
     single = make_engine(lib, sc)
     s1 = single.step(sc.rounds)
     res = _run_dist(lib, sc, world)
-    for rank, stats, lo, hi, bits, dr in res:
+    for rank, stats, owned, bits, dr in res:
         d = diff_stats(s1, stats)
         assert not d, (rank, d[:10])
-        assert np.array_equal(bits, single.read_bits(lo, hi))
-        assert np.array_equal(dr, single.delivery_rounds(lo, hi))
-    assert res[0][2] == 0 and res[-1][3] == sc.topo.n_nodes
-    assert all(res[k][3] == res[k + 1][2] for k in range(world - 1))
+        assert np.array_equal(bits, single.read_bits_nodes(owned))
+        assert np.array_equal(dr, single.delivery_rounds_nodes(owned))
+    allown = np.sort(np.concatenate([x[2] for x in res]))
+    assert np.array_equal(allown, np.arange(sc.topo.n_nodes))  # a partition of the nodes
 
 
 def test_c1_two_ranks(cpu_lib):

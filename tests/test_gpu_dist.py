@@ -1,0 +1,105 @@
+"""Sharded HIP engine on the GPU: world_size 2 and 3, every rank an engine on
+the same MI355X (cuda:0), ghost payloads moved by ggamd.dist.ShardedRunner over
+gloo (staged through host memory; the multi-GPU runs use RCCL on the same
+buffers and stream). Counters summed over ranks, and the node sets and delivery
+rounds of every rank's owned nodes, must equal one unsharded HIP engine — which
+the other GPU tests pin to the CPU oracle.
+
+Scenarios cover both partition orders (a tree: DFS preorder wins; a grid and
+random graphs: native order), directed edges, sync timers, seeded and explicit
+partition windows, and the dense (stream) and sparse paths.
+"""
+import os
+import random
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from helpers import Scenario, c1_scenario, diff_stats, make_engine, random_scenario
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, lib, scenarios, q):
+    import torch
+    import torch.distributed as dist
+
+    from ggamd.dist import ShardedRunner
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        out = []
+        dev = torch.device("cuda", 0)
+        for sc in scenarios:
+            e = make_engine(lib, sc, rank=rank, world=world, device=0)
+            r = ShardedRunner(e, dev)
+            half = sc.rounds // 2
+            stats = r.step(half) + r.step(sc.rounds - half)  # two flushes
+            owned = e.dist_owned()
+            out.append((stats, owned, e.read_bits_nodes(owned), e.delivery_rounds_nodes(owned)))
+            e.close()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(lib, scenarios, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, lib, scenarios, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return [res[r] for r in range(world)]
+
+
+def _scenarios():
+    from ggamd import topology as T
+    from ggamd.workload import uniform_injections
+    rnd = random.Random(7)
+    out = [random_scenario(random.Random(s), max_v=300, W=128, rounds=50) for s in (3, 4)]
+    tree = T.tree(3000, 4)
+    out.append(Scenario(tree, 256, 40, uniform_injections(3000, 200, 5), seed=9, sync_base=6,
+                        sync_jitter=3, windows=[("seeded", 3, 9, 77)]))
+    grid = T.grid_links(48, seed=11)
+    out.append(Scenario(grid, 64, 45, uniform_injections(48 * 48, 64, 6), seed=10, sync_base=8,
+                        sync_jitter=4))
+    rr = T.random_regular(4000, 8, seed=12)
+    out.append(Scenario(rr, 1024, 30, uniform_injections(4000, 1000, 7), seed=12, sync_base=10,
+                        sync_jitter=5, windows=[("seeded", 2, 7, 5)]))
+    out.append(c1_scenario(partition=True, rounds=120))
+    del rnd
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_equals_single(hip_lib, world):
+    scs = _scenarios()
+    res = _run(hip_lib, scs, world)
+    for k, sc in enumerate(scs):
+        single = make_engine(hip_lib, sc, device=0)
+        s1 = single.step(sc.rounds)
+        owned_all = []
+        for rank in range(world):
+            stats, owned, bits, dr = res[rank][k]
+            d = diff_stats(s1, stats)
+            assert not d, (k, rank, d[:10])
+            assert np.array_equal(bits, single.read_bits_nodes(owned)), (k, rank)
+            assert np.array_equal(dr, single.delivery_rounds_nodes(owned)), (k, rank)
+            owned_all.append(owned)
+        allown = np.sort(np.concatenate(owned_all))
+        assert np.array_equal(allown, np.arange(sc.topo.n_nodes)), k
+        single.close()
