@@ -74,6 +74,8 @@ def main():
     ap.add_argument("--lanes", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-episodes", type=int, default=2)
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 "
+                    "(nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -89,10 +91,15 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+    if args.backend == "gloo":  # rehearsal: every rank on the one visible GPU
+        local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.backend)
 
     V = args.nodes_per_gpu * world
     K = args.lanes
@@ -108,7 +115,10 @@ def main():
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local])
+            if args.backend == "nccl":
+                dist.barrier(device_ids=[local])
+            else:
+                dist.barrier()
         torch.cuda.synchronize()
 
     def run_rounds(n):
@@ -151,7 +161,8 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=device if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         per_ep = [runner.reduce(s) for s in local_stats]
@@ -163,6 +174,7 @@ def main():
     # roofline of the dominant kernel: per-kind device times (first block start
     # to last block end of each launch, stamped by the kernels) and the bytes
     # each launch had to move (counted by the kernels)
+    dinfo = eng.dist_info() if world > 1 else None
     if world > 1:
         owned = eng.dist_owned().astype(np.int64)
         n_own = int(owned.size)
@@ -209,6 +221,7 @@ def main():
                 "inter_node_msgs_per_step": msgs,
                 "msgs_per_op": msgs / K,
                 "parallelism": f"vertex-range x{world}" if world > 1 else "single GPU",
+                "shard": dinfo,
             },
             "roofline": {
                 "bound": "hbm",
@@ -238,7 +251,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(topo, inj, V, K, seed, R, args.cpu_episodes)
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.barrier(device_ids=[local])
+        barrier()
         dist.destroy_process_group()
 
 

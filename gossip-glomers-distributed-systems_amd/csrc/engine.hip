@@ -1050,6 +1050,14 @@ int gg_step_device_ms(const gg_engine* e, double* ms) {
     return GG_OK;
 }
 
+int gg_dist_info(const gg_engine* e, uint64_t* n_own, uint64_t* n_ghost, uint64_t* n_send) {
+    if (!e || !e->have_topo) return GG_EINVAL;
+    if (n_own) *n_own = e->n_own;
+    if (n_ghost) *n_ghost = e->n_ghost;
+    if (n_send) *n_send = e->send_off.empty() ? 0 : e->send_off[e->world];
+    return GG_OK;
+}
+
 int gg_dist_owned(const gg_engine* e, uint32_t* nodes, uint64_t cap, uint64_t* n_out) {
     if (!e || !e->have_topo) return GG_EINVAL;
     if (n_out) *n_out = e->n_own;

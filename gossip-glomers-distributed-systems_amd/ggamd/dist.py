@@ -57,17 +57,34 @@ class ShardedRunner:
         self.rank = dist.get_rank(group)
         assert self.world == eng.world and self.rank == eng.rank
         self.nccl = dist.get_backend(group) == "nccl"
+        self._views = {}   # (ptr, bytes, on_device) -> tensor view of engine memory
+        self._streams = {}  # stream ptr -> torch.cuda.ExternalStream
+
+    def _view(self, ptr, nbytes, on_dev):
+        key = (ptr, nbytes, on_dev)
+        v = self._views.get(key)
+        if v is None:
+            v = self._views[key] = _view(ptr, nbytes, on_dev, self.device)
+        return v
+
+    def _stream(self, ptr):
+        if not ptr:
+            return None
+        s = self._streams.get(ptr)
+        if s is None:
+            s = self._streams[ptr] = torch.cuda.ExternalStream(ptr, device=self.device)
+        return s
 
     def round(self, wait: bool = False) -> dict | None:
         x = self.eng.dist_round_begin()
         on_dev = bool(x.on_device)
-        ss = [int(x.send_bytes[q]) for q in range(self.world)]
-        rs = [int(x.recv_bytes[q]) for q in range(self.world)]
-        send = _view(x.send, int(x.send_total), on_dev, self.device)
-        recv = _view(x.recv, int(x.recv_total), on_dev, self.device)
+        ss = x.send_bytes[:self.world]
+        rs = x.recv_bytes[:self.world]
+        send = self._view(x.send, x.send_total, on_dev)
+        recv = self._view(x.recv, x.recv_total, on_dev)
+        ext = self._stream(x.stream)
         if self.nccl:
             assert on_dev, "nccl backend needs device buffers"
-            ext = torch.cuda.ExternalStream(x.stream, device=self.device) if x.stream else None
             if ext is not None:
                 with torch.cuda.stream(ext):
                     dist.all_to_all_single(recv, send, rs, ss, group=self.group)
@@ -75,7 +92,6 @@ class ShardedRunner:
                 dist.all_to_all_single(recv, send, rs, ss, group=self.group)
         elif on_dev:
             # gloo with device buffers (several ranks on one GPU): stage via host
-            ext = torch.cuda.ExternalStream(x.stream, device=self.device) if x.stream else None
             if ext is not None:
                 ext.synchronize()
             send_h = send.cpu()
@@ -83,7 +99,7 @@ class ShardedRunner:
             dist.all_to_all_single(recv_h, send_h, rs, ss, group=self.group)
             if ext is not None:
                 with torch.cuda.stream(ext):
-                    recv.copy_(recv_h, non_blocking=False)
+                    recv.copy_(recv_h)
             else:
                 recv.copy_(recv_h)
         else:

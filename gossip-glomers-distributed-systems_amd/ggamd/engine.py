@@ -92,7 +92,7 @@ GG_SYMBOLS = [
     "gg_lane_of", "gg_step",
     "gg_current_round", "gg_step_device_ms", "gg_read", "gg_read_bits", "gg_delivery_rounds", "gg_reset",
     "gg_read_bits_nodes", "gg_delivery_rounds_nodes",
-    "gg_dist_round_begin", "gg_dist_round_end", "gg_dist_flush", "gg_dist_owned",
+    "gg_dist_round_begin", "gg_dist_round_end", "gg_dist_flush", "gg_dist_owned", "gg_dist_info",
 ]
 
 _LIBS: dict[str, C.CDLL] = {}
@@ -130,6 +130,7 @@ def load_library(path: str) -> C.CDLL:
     lib.gg_dist_round_end.argtypes = [C.c_void_p, P(GGRoundStats)]
     lib.gg_dist_flush.argtypes = [C.c_void_p, P(GGRoundStats), C.c_uint64, P(C.c_uint64)]
     lib.gg_dist_owned.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]
+    lib.gg_dist_info.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_uint64)]
     lib.gg_read_bits_nodes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
     lib.gg_delivery_rounds_nodes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
     _LIBS[path] = lib
@@ -288,6 +289,11 @@ class Engine:
         out = np.zeros(max(1, n.value), np.uint32)
         self._ok(self.lib.gg_dist_owned(self.h, out.ctypes.data, out.size, C.byref(n)))
         return out[: n.value]
+
+    def dist_info(self) -> dict:
+        a, b, c = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+        self._ok(self.lib.gg_dist_info(self.h, C.byref(a), C.byref(b), C.byref(c)))
+        return {"owned": a.value, "ghosts": b.value, "sent_per_round": c.value}
 
     def dist_round_begin(self) -> GGExchange:
         x = GGExchange()

@@ -179,6 +179,8 @@ int gg_dist_round_end(gg_engine* e, gg_round_stats* out);
 /* Wait for every pending round and return their counters in round order (n_out =
  * count); out = NULL only reports the count (after waiting) and keeps them pending. */
 int gg_dist_flush(gg_engine* e, gg_round_stats* out, uint64_t cap, uint64_t* n_out);
+/* Owned rows, ghost rows, and owned rows shipped per round (summed over peers). */
+int gg_dist_info(const gg_engine* e, uint64_t* n_own, uint64_t* n_ghost, uint64_t* n_send);
 /* Original ids of the owned nodes (n_out = count, even if > cap). */
 int gg_dist_owned(const gg_engine* e, uint32_t* nodes, uint64_t cap, uint64_t* n_out);
 

@@ -534,6 +534,15 @@ int gg_step_device_ms(const gg_engine* e, double* ms) {
     return GG_OK;
 }
 
+int gg_dist_info(const gg_engine* e, uint64_t* n_own, uint64_t* n_ghost, uint64_t* n_send) {
+    if (!e || !e->have_topo) return GG_EINVAL;
+    const uint64_t n = e->hi - e->lo;
+    if (n_own) *n_own = n;
+    if (n_ghost) *n_ghost = e->world > 1 ? e->V - n : 0;  // full replicas
+    if (n_send) *n_send = e->world > 1 ? n * (e->world - 1) : 0;
+    return GG_OK;
+}
+
 int gg_dist_owned(const gg_engine* e, uint32_t* nodes, uint64_t cap, uint64_t* n_out) {
     if (!e || !e->have_topo) return GG_EINVAL;
     const uint64_t n = e->hi - e->lo;
