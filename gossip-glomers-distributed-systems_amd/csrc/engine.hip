@@ -111,6 +111,15 @@ struct gg_engine {
     uint32_t* d_n_work = nullptr;    // [2] live tiles, candidate nodes
     uint32_t* d_nodes = nullptr;     // [n_own] candidate-node list (sparse lean rounds)
     uint32_t* d_act = nullptr;       // [4] ring: nodes that became active per round
+    // hubs (see expand_kernels.hpp): in-edge chunks of high in-degree nodes,
+    // out-edge chunks of high out-degree senders, per-chunk partial rows
+    uint32_t hub_deg = 0;
+    uint64_t n_hubs = 0, n_hchunks = 0, n_mchunks = 0;
+    uint32_t* d_hubs = nullptr;
+    uint32_t* d_hub_c0 = nullptr;
+    gg::HubChunk* d_hchunks = nullptr;
+    gg::HubChunk* d_mchunks = nullptr;
+    uint64_t* d_hscratch = nullptr;
     uint64_t tile_nodes = 0, tile_bytes = 0;
     uint64_t n_in_edges = 0;
     uint64_t* d_fired[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -173,6 +182,12 @@ void gg_engine::free_topology() {
     dfree(d_cand);
     dfree(d_zmark);
     dfree(d_tile_cand);
+    dfree(d_hubs);
+    dfree(d_hub_c0);
+    dfree(d_hchunks);
+    dfree(d_mchunks);
+    dfree(d_hscratch);
+    n_hubs = n_hchunks = n_mchunks = 0;
     dfree(d_work);
     dfree(d_n_work);
     dfree(d_nodes);
@@ -308,6 +323,27 @@ void launch_stream_t(const gg::RoundArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((gg::expand_stream<G, 2>), dim3((unsigned)blocks), dim3(gg::kBlock), 0, s, a);
 }
 
+template <int G>
+void launch_hubs_t(const gg::RoundArgs& a, hipStream_t s) {
+    const unsigned bc = (unsigned)std::min<uint64_t>(a.n_hchunks, 8192);
+    const unsigned bh = (unsigned)std::min<uint64_t>(a.n_hubs, 8192);
+    hipLaunchKernelGGL((gg::hub_chunks<G, 2>), dim3(bc), dim3(gg::kBlock), 0, s, a);
+    hipLaunchKernelGGL((gg::hub_finish<G, 2>), dim3(bh), dim3(gg::kBlock), 0, s, a);
+}
+
+void launch_hubs(const gg::RoundArgs& a, hipStream_t s) {
+    switch (a.nwp) {
+        case 2: launch_hubs_t<1>(a, s); break;
+        case 4: launch_hubs_t<2>(a, s); break;
+        case 8: launch_hubs_t<4>(a, s); break;
+        case 16: launch_hubs_t<8>(a, s); break;
+        case 32: launch_hubs_t<16>(a, s); break;
+        case 64: launch_hubs_t<32>(a, s); break;
+        case 128: launch_hubs_t<64>(a, s); break;
+        default: break;
+    }
+}
+
 void launch_stream(const gg::RoundArgs& a, hipStream_t s) {
     switch (a.nwp) {
         case 2: launch_stream_t<1>(a, s); break;
@@ -350,6 +386,15 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.n_ghost = e->n_ghost;
     a.gout_ptr = e->d_gout_ptr;
     a.gout_col = e->d_gout_col;
+    a.hub_deg = e->hub_deg;
+    a.hchunks = e->d_hchunks;
+    a.n_hchunks = e->n_hchunks;
+    a.hubs = e->d_hubs;
+    a.hub_c0 = e->d_hub_c0;
+    a.n_hubs = e->n_hubs;
+    a.hscratch = e->d_hscratch;
+    a.mchunks = e->d_mchunks;
+    a.n_mchunks = e->n_mchunks;
     {
         static const uint32_t ablate = getenv("GG_ABLATE") ? (uint32_t)atoi(getenv("GG_ABLATE")) : 0u;
         a.ablate = ablate;  // diagnostic timing only
@@ -398,6 +443,12 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             }
             HIPCHK(hipGetLastError());
         }
+        if (e->n_mchunks) {  // high out-degree senders mark their receivers (sparse rounds);
+        // before mark_injections, whose CA_INJ bit these plain stores would clear
+            const unsigned blocks = (unsigned)std::min<uint64_t>(e->n_mchunks, 4096);
+            hipLaunchKernelGGL(gg::hub_mark, dim3(blocks), dim3(gg::kBlock), 0, e->stream, a);
+            HIPCHK(hipGetLastError());
+        }
         if (n_inj) {
             hipLaunchKernelGGL(gg::mark_injections, dim3((n_inj + 255) / 256), dim3(256), 0, e->stream, a);
             HIPCHK(hipGetLastError());
@@ -410,6 +461,10 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         }
         if (a.stream_ok) {  // lean rounds: all nodes (dense) or the candidate list (sparse)
             launch_stream(a, e->stream);
+            if (e->n_hubs) {
+                HIPCHK(hipGetLastError());
+                launch_hubs(a, e->stream);
+            }
         } else {
             launch_expand(a, syncw, maskw, e->stream);
         }
@@ -899,6 +954,47 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
         const uint64_t pb = exchange_stride(e->nwp, true);
         HIPCHK(hipMalloc(&e->d_xsend, std::max<uint64_t>(16, e->send_off[Wd] * pb)));
         HIPCHK(hipMalloc(&e->d_xrecv, std::max<uint64_t>(16, e->recv_off[Wd] * pb)));
+    }
+    // hubs: in-degree > hub_deg (hub_chunks/hub_finish in lean rounds), senders
+    // with out-degree > hub_deg (hub_mark); W = 64 rows have no streaming path
+    e->hub_deg = 0;
+    if (e->nwp >= 2) {
+        e->hub_deg = 512;
+        if (const char* h = getenv("GG_HUB_DEG")) e->hub_deg = (uint32_t)std::max(1, atoi(h));
+        uint64_t per = 128ull * (gg::kBlock / lanes_per_node((uint32_t)e->nwp));  // senders per chunk
+        if (const char* h = getenv("GG_HUB_CHUNK")) per = (uint64_t)std::max(1, atoi(h));
+        std::vector<uint32_t> hubs, hub_c0;
+        std::vector<gg::HubChunk> hch, mch;
+        for (uint64_t i = 0; i < n_own; ++i) {
+            const int64_t din = iptr[i + 1] - iptr[i];
+            if (din > (int64_t)e->hub_deg) {
+                hubs.push_back((uint32_t)i);
+                hub_c0.push_back((uint32_t)hch.size());
+                for (int64_t x = iptr[i]; x < iptr[i + 1]; x += (int64_t)per)
+                    hch.push_back({(uint32_t)i, (uint32_t)std::min<int64_t>((int64_t)per, iptr[i + 1] - x), x});
+            }
+            const int64_t o0 = sym ? iptr[i] : optr[i], o1 = sym ? iptr[i + 1] : optr[i + 1];
+            if (o1 - o0 > (int64_t)e->hub_deg)
+                for (int64_t x = o0; x < o1; x += 1024)
+                    mch.push_back({(uint32_t)i, (uint32_t)std::min<int64_t>(1024, o1 - x), x});
+        }
+        hub_c0.push_back((uint32_t)hch.size());
+        e->n_hubs = hubs.size();
+        e->n_hchunks = hch.size();
+        e->n_mchunks = mch.size();
+        if (e->n_hubs) {
+            HIPCHK(hipMalloc(&e->d_hubs, hubs.size() * 4));
+            HIPCHK(hipMemcpy(e->d_hubs, hubs.data(), hubs.size() * 4, hipMemcpyHostToDevice));
+            HIPCHK(hipMalloc(&e->d_hub_c0, hub_c0.size() * 4));
+            HIPCHK(hipMemcpy(e->d_hub_c0, hub_c0.data(), hub_c0.size() * 4, hipMemcpyHostToDevice));
+            HIPCHK(hipMalloc(&e->d_hchunks, hch.size() * sizeof(gg::HubChunk)));
+            HIPCHK(hipMemcpy(e->d_hchunks, hch.data(), hch.size() * sizeof(gg::HubChunk), hipMemcpyHostToDevice));
+            HIPCHK(hipMalloc(&e->d_hscratch, hch.size() * 2 * e->nwp * 8));
+        }
+        if (e->n_mchunks) {
+            HIPCHK(hipMalloc(&e->d_mchunks, mch.size() * sizeof(gg::HubChunk)));
+            HIPCHK(hipMemcpy(e->d_mchunks, mch.data(), mch.size() * sizeof(gg::HubChunk), hipMemcpyHostToDevice));
+        }
     }
     const size_t rowbytes = e->rows * e->nwp * 8;
     e->tile_nodes = gg::kBlock / lanes_per_node((uint32_t)e->nwp);

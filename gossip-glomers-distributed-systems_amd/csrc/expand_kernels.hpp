@@ -110,6 +110,14 @@ struct TileWork {
     int64_t eb;      // in_ptr of the tile's first node
 };
 
+// A contiguous piece of a hub node's in-list (or, for marking, of a high
+// out-degree sender's out-list).
+struct HubChunk {
+    uint32_t node;   // local row
+    uint32_t n;      // edges in the piece
+    int64_t e0;      // first edge
+};
+
 struct RoundArgs {
     const int64_t* in_ptr;      // [n_own+1]
     const uint32_t* in_col;     // replica row of the sender | kRecipBit if sender in out(v)
@@ -127,6 +135,18 @@ struct RoundArgs {
     uint32_t* n_work;           // [2]: live tiles, candidate nodes
     uint32_t* nodes;            // candidate nodes of a sparse lean round (compact_round; expand_stream)
     uint32_t* act;              // [4] ring: nodes that became active in round r (slot r&3)
+    // hubs (lean rounds): owned nodes with in-degree > hub_deg skip expand_stream
+    // and take hub_chunks + hub_finish; senders with out-degree > hub_deg are
+    // marked by hub_mark instead of round_prep (0: no hubs)
+    uint32_t hub_deg;
+    const struct HubChunk* hchunks;  // in-edge chunks of the hubs, hub by hub
+    uint64_t n_hchunks;
+    const uint32_t* hubs;            // [n_hubs] hub local rows
+    const uint32_t* hub_c0;          // [n_hubs+1] first chunk of each hub
+    uint64_t n_hubs;
+    uint64_t* hscratch;              // [n_hchunks][2][nwp] (union, first-claimer-recip) per chunk
+    const struct HubChunk* mchunks;  // out-edge chunks of high out-degree senders
+    uint64_t n_mchunks;
     const uint64_t* fired_m1;   // sync-fired bitmaps of rounds r-1, r-2, r-3
     const uint64_t* fired_m2;
     const uint64_t* fired_m3;
@@ -380,6 +400,7 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                 if ((f & FL_ACT) || fm3) {  // senders mark their (owned) receivers
                     o0 = a.out_ptr[i];
                     o1 = a.out_ptr[i + 1];
+                    if (a.hub_deg && o1 - o0 > (int64_t)a.hub_deg) o1 = o0;  // hub_mark does it
                     c_bytes += 16 + 5 * (unsigned long long)(o1 - o0);
                     for (int64_t e = o0; e < o1; ++e) {
                         const uint64_t w = a.out_col[e] & kColMask;
@@ -882,6 +903,14 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                         c_next_ackdrop += AD * T - cl_ackdrop - cb_new_ackdrop + push_ackdrop;
                     }
                 }
+                if (!work && zm) {  // a candidate whose senders were all dropped: still
+                    Row<WPL> z;     // clear its stale F row (rows of inactive nodes are zero)
+#pragma unroll
+                    for (int w = 0; w < WPL; ++w) z.w[w] = 0;
+                    if (!(a.ablate & 1)) store_row<WPL>(a.F_cur + rep * a.nwp + off, z);
+                    if (lg == 0) a.zmark[rep] = 0;
+                    nrows++;
+                }
                 if (lg == 0) c_bytes += nrows * 8ull * a.nwp + nextra + 16;  // + out_ptr
             }
             lds_barrier();  // LDS reuse by the next tile
@@ -972,6 +1001,7 @@ void expand_stream(RoundArgs a) {
         uint8_t ca, fl;
     };
     constexpr uint32_t kNone = ~0u;
+    constexpr uint32_t kHubBit = 0x80000000u;  // node ids < 2^31
     auto node_of = [&](uint32_t k) -> uint32_t {
         return k < n_items ? (dense ? (uint32_t)k : a.nodes[k]) : kNone;
     };
@@ -987,6 +1017,10 @@ void expand_stream(RoundArgs a) {
             m.deg = (uint32_t)(a.in_ptr[n + 1] - m.p0);
             m.ca = a.cand[a.own0 + n];      // CA_INJ: client broadcasts this round
             m.fl = a.flg_cur[a.own0 + n];   // flags of round r-2 (ACT: stale F row)
+            if (a.hub_deg && m.deg > a.hub_deg) {  // a hub: hub_chunks/hub_finish take it
+                m.node |= kHubBit;
+                m.deg = 0;
+            }
         } else {
             m.p0 = 0;
             m.deg = 0;
@@ -1011,10 +1045,11 @@ void expand_stream(RoundArgs a) {
     fetch_cols(m0, c0);
     vm_drain();  // nothing pending at the loop head: no compiler drains inside
     for (; k < n_items; k += stride) {
-        const uint64_t i = m0.node;
+        const bool hub = (m0.node & kHubBit) != 0;
+        const uint64_t i = m0.node & ~kHubBit;
         const uint64_t rep = a.own0 + i;
         // (a) DMA node i's own row and its first D sender rows
-        if (!(a.ablate & 4)) dma16((const void*)(a.base + rep * a.nwp + off), my + D * 1024);
+        if (!hub && !(a.ablate & 4)) dma16((const void*)(a.base + rep * a.nwp + off), my + D * 1024);
 #pragma unroll
         for (int b = 0; b < D; ++b) {
             if ((uint32_t)b < m0.deg && !(a.ablate & 2))
@@ -1027,6 +1062,7 @@ void expand_stream(RoundArgs a) {
         fetch_meta(n2, m2);
         const uint32_t n3 = node_of(k + 3 * stride);
         vm_drain();
+        if (!hub) {
         const ulonglong2 o = *reinterpret_cast<const ulonglong2*>(my + D * 1024 + lane16);
         Row<WPL> sp, S;
         sp.w[0] = o.x;  // lean rounds precede every sync timer: no LAG
@@ -1113,6 +1149,7 @@ void expand_stream(RoundArgs a) {
             c_bytes += (dense ? 0 : 4) + 8 + 2 + 4 * nin + (1 + nin) * rowb + ((any || zm) ? rowb : 0) +
                        (any ? rowb + 1 : 0);
         }
+        }  // !hub
         m0 = m1;
         m1 = m2;
         n2 = n3;
@@ -1132,6 +1169,243 @@ void expand_stream(RoundArgs a) {
     acc[C_NACT] = c_nact;
     acc[C_BYTES] = c_bytes;
     flush_counters(a, acc, s_red, t_start, K_STREAM);
+}
+
+// ---------------------------------------------------------------------------
+// Hubs (power-law graphs, lean rounds). The claim chain of a node is an ordered
+// scan, and its result is all the counters need: the union O of the sender rows
+// and, per bit, whether the first sender holding it (ascending id) is
+// reciprocal (mask R). Pieces combine associatively in sender order:
+//     (O1, R1) . (O2, R2) = (O1 | O2, R1 | (R2 & ~O1))
+// and with the node's own row (+ client broadcasts) S0: new bits = O & ~S0,
+// reciprocal claims = popcount(O & ~S0 & R). hub_chunks reduces each in-edge
+// chunk of a hub with one block (its node groups take consecutive slices and
+// combine in order in LDS) into hscratch; hub_finish combines a hub's chunks
+// the same way and writes the node like expand_stream does.
+template <int WPL>
+__device__ __forceinline__ void hub_combine(Row<WPL>& O, Row<WPL>& R, const Row<WPL>& O2, const Row<WPL>& R2) {
+#pragma unroll
+    for (int w = 0; w < WPL; ++w) {
+        R.w[w] |= R2.w[w] & ~O.w[w];
+        O.w[w] |= O2.w[w];
+    }
+}
+
+// Ordered tree reduction of the NGB node-group partials of a block in LDS;
+// node group 0 ends with the combined (O, R). s_or/s_rc: [NGB][G*WPL] words.
+template <int G, int WPL>
+__device__ __forceinline__ void hub_block_reduce(Row<WPL>& O, Row<WPL>& R, uint64_t* s_or, uint64_t* s_rc) {
+    constexpr int NGB = kBlock / G;
+    const int j = threadIdx.x / G, lg = threadIdx.x % G;
+#pragma unroll
+    for (int w = 0; w < WPL; ++w) {
+        s_or[j * G * WPL + lg * WPL + w] = O.w[w];
+        s_rc[j * G * WPL + lg * WPL + w] = R.w[w];
+    }
+    __syncthreads();
+    for (int st = 1; st < NGB; st <<= 1) {
+        if (j % (2 * st) == 0 && j + st < NGB) {
+            Row<WPL> O2, R2;
+#pragma unroll
+            for (int w = 0; w < WPL; ++w) {
+                O2.w[w] = s_or[(j + st) * G * WPL + lg * WPL + w];
+                R2.w[w] = s_rc[(j + st) * G * WPL + lg * WPL + w];
+            }
+            hub_combine<WPL>(O, R, O2, R2);
+#pragma unroll
+            for (int w = 0; w < WPL; ++w) {
+                s_or[j * G * WPL + lg * WPL + w] = O.w[w];
+                s_rc[j * G * WPL + lg * WPL + w] = R.w[w];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <int G, int WPL>
+__global__ __launch_bounds__(kBlock) void hub_chunks(RoundArgs a) {
+    constexpr int NGB = kBlock / G;
+    constexpr int D = 4;  // sender rows in flight per lane
+    __shared__ uint64_t s_or[NGB * G * WPL], s_rc[NGB * G * WPL];
+    __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
+    const unsigned long long t_start = clock100();
+    if (!a.stream_ok || !a.n_hchunks) {
+        noop_exit(a, K_STREAM, t_start);
+        return;
+    }
+    const bool dense = dense_round(a);
+    const int j = threadIdx.x / G, lg = threadIdx.x % G;
+    const uint64_t off = (uint64_t)lg * WPL;
+    unsigned long long c_bytes = 0;
+    for (uint64_t c = blockIdx.x; c < a.n_hchunks; c += gridDim.x) {
+        const HubChunk hc = a.hchunks[c];
+        if (!dense && !a.cand[hc.node]) continue;  // block-uniform
+        const uint32_t per = (hc.n + NGB - 1) / NGB;
+        const int64_t e0 = hc.e0 + (int64_t)j * per;
+        const int64_t e1 = min(hc.e0 + (int64_t)hc.n, e0 + (int64_t)per);
+        Row<WPL> O, R;
+#pragma unroll
+        for (int w = 0; w < WPL; ++w) O.w[w] = R.w[w] = 0;
+        for (int64_t e = e0; e < e1; e += D) {
+            uint32_t cb[D];
+            Row<WPL> src[D];
+#pragma unroll
+            for (int b = 0; b < D; ++b) {
+                cb[b] = e + b < e1 ? a.in_col[e + b] : 0u;
+                if (e + b < e1) {
+                    src[b] = load_row<WPL>(a.F_prev + (uint64_t)(cb[b] & kColMask) * a.nwp + off);
+                } else {
+#pragma unroll
+                    for (int w = 0; w < WPL; ++w) src[b].w[w] = 0;
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < D; ++b) {
+#pragma unroll
+                for (int w = 0; w < WPL; ++w) {
+                    const uint64_t cw = src[b].w[w] & ~O.w[w];
+                    O.w[w] |= cw;
+                    if (cb[b] & kRecipBit) R.w[w] |= cw;
+                }
+            }
+        }
+        if (lg == 0 && e1 > e0) c_bytes += (unsigned long long)(e1 - e0) * (4 + 8ull * a.nwp);
+        hub_block_reduce<G, WPL>(O, R, s_or, s_rc);
+        if (j == 0) {
+            uint64_t* dst = a.hscratch + c * 2 * a.nwp;
+            store_row<WPL>(dst + off, O);
+            store_row<WPL>(dst + a.nwp + off, R);
+            if (lg == 0) c_bytes += 16ull * a.nwp;
+        }
+        __syncthreads();  // LDS reuse
+    }
+    unsigned long long acc[C_NUM];
+#pragma unroll
+    for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
+    acc[C_BYTES] = c_bytes;
+    flush_counters(a, acc, s_red, t_start, K_STREAM);
+}
+
+template <int G, int WPL>
+__global__ __launch_bounds__(kBlock) void hub_finish(RoundArgs a) {
+    constexpr int NGB = kBlock / G;
+    __shared__ uint64_t s_or[NGB * G * WPL], s_rc[NGB * G * WPL];
+    __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
+    const unsigned long long t_start = clock100();
+    if (!a.stream_ok || !a.n_hubs) {
+        noop_exit(a, K_STREAM, t_start);
+        return;
+    }
+    const bool dense = dense_round(a);
+    const int j = threadIdx.x / G, lg = threadIdx.x % G;
+    const uint64_t off = (uint64_t)lg * WPL;
+    const int gshift = (threadIdx.x & 63) / G * G;
+    const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+    unsigned long long c_new = 0, c_fwd = 0, c_hash = 0, c_active = 0, c_gathers = 0, c_nact = 0, c_bytes = 0;
+    for (uint64_t h = blockIdx.x; h < a.n_hubs; h += gridDim.x) {
+        const uint32_t i = a.hubs[h];
+        const uint8_t ca = a.cand[i];
+        if (!dense && !ca) continue;  // block-uniform
+        const uint32_t c0 = a.hub_c0[h], c1 = a.hub_c0[h + 1];
+        const uint32_t per = (c1 - c0 + NGB - 1) / NGB;
+        const uint32_t q0 = c0 + j * per, q1 = min(c1, q0 + per);
+        Row<WPL> O, R;
+#pragma unroll
+        for (int w = 0; w < WPL; ++w) O.w[w] = R.w[w] = 0;
+        for (uint32_t q = q0; q < q1; ++q) {
+            const uint64_t* src = a.hscratch + (uint64_t)q * 2 * a.nwp;
+            hub_combine<WPL>(O, R, load_row<WPL>(src + off), load_row<WPL>(src + a.nwp + off));
+        }
+        hub_block_reduce<G, WPL>(O, R, s_or, s_rc);
+        if (j == 0) {
+            const uint64_t rep = a.own0 + i;
+            Row<WPL> sp = load_row<WPL>(a.base + rep * a.nwp + off), S = sp;  // lean: no LAG
+            if (ca & CA_INJ) {  // (1) client broadcasts of this round
+                uint32_t lo = 0, hi = a.n_inj;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (a.inj[2 * mid] < i) lo = mid + 1;
+                    else hi = mid;
+                }
+                for (uint32_t k = lo; k < a.n_inj && a.inj[2 * k] == i; ++k) {
+                    const uint32_t lane = a.inj[2 * k + 1];
+                    const uint32_t word = lane >> 6;
+                    if (word / WPL == (uint32_t)lg) set_lane_bit<WPL>(S, word % WPL, lane & 63);
+                }
+            }
+            // (2) node broadcasts: every new bit's first deliverer claims it
+            unsigned long long cl_recip = 0;
+            Row<WPL> F;
+            unsigned long long T = 0;
+            const uint64_t g = gid_of(a, i);
+#pragma unroll
+            for (int w = 0; w < WPL; ++w) {
+                const uint64_t claim = O.w[w] & ~S.w[w];
+                cl_recip += __popcll(claim & R.w[w]);
+                S.w[w] |= claim;
+                F.w[w] = S.w[w] & ~sp.w[w];
+                T += __popcll(F.w[w]);
+                if (F.w[w]) {
+                    const uint64_t idx = g * a.nw + off + w;
+                    c_hash += gg_word_hash(idx, S.w[w]) - (sp.w[w] ? gg_word_hash(idx, sp.w[w]) : 0ull);
+                }
+            }
+            const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
+            const uint8_t fl = a.flg_cur[rep];
+            const bool zm = (fl & FL_ACT) != 0;
+            if (any || zm) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
+            if (any) store_row<WPL>(a.base + rep * a.nwp + off, S);
+            const uint64_t nin = (uint64_t)(a.in_ptr[i + 1] - a.in_ptr[i]);
+            const unsigned long long deg = a.symmetric ? nin : (unsigned long long)(a.out_ptr[i + 1] - a.out_ptr[i]);
+            c_new += T;
+            c_fwd += deg * T - cl_recip;
+            if (lg == 0) {
+                if (any || fl) a.flg_cur[rep] = any ? FL_ACT : 0;
+                if (ca) a.cand[rep] = 0;
+                c_active += 1;
+                c_gathers += nin;
+                c_nact += any ? 1 : 0;
+                c_bytes += 16 + 2 + (uint64_t)(c1 - c0) * 16 * a.nwp + 8 * a.nwp +
+                           ((any || zm) ? 8 * a.nwp : 0) + (any ? 8 * a.nwp + 1 : 0);
+            }
+        }
+        __syncthreads();  // LDS reuse
+    }
+    unsigned long long acc[C_NUM];
+#pragma unroll
+    for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
+    acc[C_NEW] = c_new;
+    acc[C_FWD_SENT] = c_fwd;
+    acc[C_FWD_DELIV] = c_fwd;
+    acc[C_HASH] = c_hash;
+    acc[C_NEXT_ACKS] = c_fwd;
+    acc[C_ACTIVE] = c_active;
+    acc[C_GATHERS] = c_gathers;
+    acc[C_NACT] = c_nact;
+    acc[C_BYTES] = c_bytes;
+    flush_counters(a, acc, s_red, t_start, K_STREAM);
+}
+
+// Senders with out-degree > hub_deg that were active (or pushed) last round
+// mark their owned receivers; one block per out-edge chunk (sparse rounds).
+__global__ __launch_bounds__(kBlock) void hub_mark(RoundArgs a) {
+    const unsigned long long t_start = clock100();
+    if (dense_round(a)) {
+        noop_exit(a, K_PREP, t_start);
+        return;
+    }
+    for (uint64_t c = blockIdx.x; c < a.n_mchunks; c += gridDim.x) {
+        const HubChunk hc = a.mchunks[c];
+        const uint64_t u = a.own0 + hc.node;
+        if (!((a.flg_prev[u] & FL_ACT) || bit_at(a.fired_m3, u))) continue;
+        for (uint32_t t = threadIdx.x; t < hc.n; t += kBlock) {
+            const uint64_t w = a.out_col[hc.e0 + t] & kColMask;
+            if (w >= a.n_own) continue;
+            a.cand[w] = CA_NODE;
+            if (!a.stream_ok) a.tile_cand[w / a.tile_nodes] = 1;
+        }
+    }
+    if (threadIdx.x == 0) stamp(a, K_PREP, t_start);
 }
 
 // First-seen round of every new bit (GG_TRACK_DELIVERY only; observation).

@@ -1,0 +1,70 @@
+"""GPU parity of the hub path (power-law graphs): nodes with in-degree above the
+hub threshold skip the streaming kernel and take hub_chunks + hub_finish (the
+ordered (union, first-claimer-reciprocal) scan over in-edge chunks); senders
+with out-degree above it are marked by hub_mark. GG_HUB_DEG / GG_HUB_CHUNK
+lower the threshold and the chunk size so small graphs exercise many hubs,
+multi-chunk scans and chunk boundaries; results must equal the CPU oracle O2
+bit for bit (counters of every round, node sets, delivery rounds).
+"""
+import random
+
+import numpy as np
+import pytest
+
+from ggamd import topology as T
+from ggamd.workload import uniform_injections
+from helpers import Scenario, diff_stats, make_engine, random_scenario
+
+pytestmark = pytest.mark.gpu
+
+
+def _compare(sc, hip_lib, cpu_lib):
+    g = make_engine(hip_lib, sc, device=0)
+    c = make_engine(cpu_lib, sc)
+    d = diff_stats(g.step(sc.rounds), c.step(sc.rounds))
+    assert not d, d[:10]
+    assert np.array_equal(g.read_bits(), c.read_bits())
+    assert np.array_equal(g.delivery_rounds(), c.delivery_rounds())
+
+
+@pytest.mark.parametrize("deg,chunk", [(16, 7), (40, 1), (8, 1000)])
+def test_rmat_hubs(hip_lib, cpu_lib, monkeypatch, deg, chunk):
+    monkeypatch.setenv("GG_HUB_DEG", str(deg))
+    monkeypatch.setenv("GG_HUB_CHUNK", str(chunk))
+    topo = T.rmat(4096, 16, seed=41)
+    assert int(np.diff(topo.row_ptr).max()) > 4 * deg  # real hubs
+    sc = Scenario(topo, 256, 14, uniform_injections(4096, 256, 42), seed=43, sync_base=9, sync_jitter=2)
+    _compare(sc, hip_lib, cpu_lib)
+
+
+def test_rmat_hubs_wide_rows(hip_lib, cpu_lib, monkeypatch):
+    """W = 4096 (C4's lane count): 32 lanes per row in every hub kernel."""
+    monkeypatch.setenv("GG_HUB_DEG", "24")
+    monkeypatch.setenv("GG_HUB_CHUNK", "13")
+    topo = T.rmat(2048, 16, seed=44)
+    sc = Scenario(topo, 4096, 10, uniform_injections(2048, 4000, 45), seed=46, enable_sync=False)
+    _compare(sc, hip_lib, cpu_lib)
+
+
+def test_random_with_hub_threshold(hip_lib, cpu_lib, monkeypatch):
+    """Directed graphs, partitions, sync: hubs only in lean rounds, the tile
+    path everywhere else."""
+    monkeypatch.setenv("GG_HUB_DEG", "3")
+    monkeypatch.setenv("GG_HUB_CHUNK", "2")
+    rnd = random.Random(4242)
+    for _ in range(8):
+        _compare(random_scenario(rnd, max_v=200, W=128, rounds=45), hip_lib, cpu_lib)
+
+
+@pytest.mark.parametrize("deg", ["3", "1000000000"])
+def test_partition_then_lean_rounds(hip_lib, cpu_lib, monkeypatch, deg):
+    """Partition windows without sync: masked (tile-path) rounds hand over to
+    streaming rounds, which gather every sender row — so a candidate whose
+    senders were all dropped must still clear its stale F row (regression)."""
+    monkeypatch.setenv("GG_HUB_DEG", deg)
+    monkeypatch.setenv("GG_HUB_CHUNK", "2")
+    rnd = random.Random(4242)
+    for _ in range(8):
+        sc = random_scenario(rnd, max_v=200, W=128, rounds=45)
+        sc.enable_sync = False
+        _compare(sc, hip_lib, cpu_lib)
