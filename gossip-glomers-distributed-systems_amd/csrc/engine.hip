@@ -18,10 +18,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <map>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -45,6 +47,20 @@ struct Injection {
     uint32_t node;
     uint32_t lane;
 };
+
+// Host loops over nodes on up to 16 threads (topology ingest of 10^8-node graphs).
+template <class F>
+void host_parallel(uint64_t n, F f) {
+    unsigned hc = std::thread::hardware_concurrency();
+    uint64_t T = std::min<uint64_t>(std::max(1u, std::min(hc, 16u)), std::max<uint64_t>(1, n / 65536));
+    if (T <= 1) {
+        f(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (uint64_t t = 0; t < T; ++t) th.emplace_back(f, n * t / T, n * (t + 1) / T);
+    for (auto& x : th) x.join();
+}
 
 uint32_t next_pow2(uint32_t x) {
     uint32_t p = 1;
@@ -784,37 +800,56 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     HIPCHK(hipSetDevice(e->device));
     const uint64_t V = e->V;
     if (row_ptr[0] != 0 || (uint64_t)row_ptr[V] != nnz) return e->fail(GG_EINVAL, "row_ptr[0]/row_ptr[V] mismatch");
-    for (uint64_t v = 0; v < V; ++v) {
-        if (row_ptr[v + 1] < row_ptr[v]) return e->fail(GG_EINVAL, "row_ptr not monotone");
-        for (int64_t k = row_ptr[v]; k < row_ptr[v + 1]; ++k) {
-            if (col[k] < 0 || (uint64_t)col[k] >= V) return e->fail(GG_EINVAL, "neighbour id out of range");
-            if (k > row_ptr[v] && col[k] <= col[k - 1])
-                return e->fail(GG_EINVAL, "neighbour list not ascending/unique");
-        }
+    {
+        std::atomic<int> bad{0};  // 1 monotone, 2 range, 3 order
+        host_parallel(V, [&](uint64_t lo, uint64_t hi) {
+            for (uint64_t v = lo; v < hi && !bad.load(std::memory_order_relaxed); ++v) {
+                if (row_ptr[v + 1] < row_ptr[v]) { bad = 1; return; }
+                for (int64_t k = row_ptr[v]; k < row_ptr[v + 1]; ++k) {
+                    if (col[k] < 0 || (uint64_t)col[k] >= V) { bad = 2; return; }
+                    if (k > row_ptr[v] && col[k] <= col[k - 1]) { bad = 3; return; }
+                }
+            }
+        });
+        if (bad == 1) return e->fail(GG_EINVAL, "row_ptr not monotone");
+        if (bad == 2) return e->fail(GG_EINVAL, "neighbour id out of range");
+        if (bad == 3) return e->fail(GG_EINVAL, "neighbour list not ascending/unique");
     }
-    if (nnz >= (1ull << 32)) return e->fail(GG_EINVAL, "more than 2^32 edges per engine not supported yet");
     HIPCHK(hipStreamSynchronize(e->stream));
     e->free_topology();
-    // transpose: in-lists ascending by sender
-    std::vector<int64_t> tin(V + 1, 0);
-    for (uint64_t k = 0; k < nnz; ++k) tin[col[k] + 1]++;
-    for (uint64_t v = 0; v < V; ++v) tin[v + 1] += tin[v];
-    std::vector<uint32_t> tcol(nnz);
-    {
-        std::vector<int64_t> pos(tin.begin(), tin.end() - 1);
-        for (uint64_t u = 0; u < V; ++u)
-            for (int64_t k = row_ptr[u]; k < row_ptr[u + 1]; ++k) tcol[pos[col[k]]++] = (uint32_t)u;
-    }
+    // symmetric (u lists v iff v lists u)? then the in-lists are the rows themselves
     bool sym = true;
-    for (uint64_t v = 0; v < V && sym; ++v) {
-        if (tin[v + 1] - tin[v] != row_ptr[v + 1] - row_ptr[v]) {
-            sym = false;
-            break;
-        }
-        for (int64_t k = 0; k < tin[v + 1] - tin[v]; ++k)
-            if ((int64_t)tcol[tin[v] + k] != col[row_ptr[v] + k]) { sym = false; break; }
+    {
+        std::atomic<bool> asym{false};
+        host_parallel(V, [&](uint64_t lo, uint64_t hi) {
+            for (uint64_t u = lo; u < hi && !asym.load(std::memory_order_relaxed); ++u)
+                for (int64_t k = row_ptr[u]; k < row_ptr[u + 1]; ++k) {
+                    const uint32_t v = (uint32_t)col[k];
+                    if (!std::binary_search(col + row_ptr[v], col + row_ptr[v + 1], (int32_t)u)) {
+                        asym = true;
+                        return;
+                    }
+                }
+        });
+        sym = !asym.load();
     }
     e->symmetric = sym;
+    // transpose (directed lists only): in-lists ascending by sender
+    std::vector<int64_t> tin_v;
+    std::vector<uint32_t> tcol_v;
+    const int64_t* tin = row_ptr;
+    const uint32_t* tcol = reinterpret_cast<const uint32_t*>(col);
+    if (!sym) {
+        tin_v.assign(V + 1, 0);
+        for (uint64_t k = 0; k < nnz; ++k) tin_v[col[k] + 1]++;
+        for (uint64_t v = 0; v < V; ++v) tin_v[v + 1] += tin_v[v];
+        tcol_v.resize(nnz);
+        std::vector<int64_t> pos(tin_v.begin(), tin_v.end() - 1);
+        for (uint64_t u = 0; u < V; ++u)
+            for (int64_t k = row_ptr[u]; k < row_ptr[u + 1]; ++k) tcol_v[pos[col[k]]++] = (uint32_t)u;
+        tin = tin_v.data();
+        tcol = tcol_v.data();
+    }
     // ---- partition (sharded): a locality order of the nodes cut into
     // edge-balanced contiguous ranges; rank p owns order[plo[p] .. plo[p+1])
     const uint32_t Wd = e->world;
@@ -822,7 +857,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     std::vector<uint64_t> plo;      // [Wd+1] position ranges
     std::vector<uint32_t> owner;    // node -> rank (sharded)
     if (Wd > 1) {
-        choose_partition(V, row_ptr, col, tin.data(), Wd, order, plo, owner);
+        choose_partition(V, row_ptr, col, tin, Wd, order, plo, owner);
     } else {
         plo = {0, V};
     }
@@ -896,20 +931,27 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
         iptr[i + 1] = iptr[i] + (tin[v + 1] - tin[v]);
         optr[i + 1] = optr[i] + (row_ptr[v + 1] - row_ptr[v]);
     }
-    std::vector<uint32_t> icol(iptr[n_own]), ocol(optr[n_own]);
+    std::vector<uint32_t> icol(iptr[n_own]), ocol(sym ? 0 : optr[n_own]);
     std::vector<int64_t> gcnt(e->n_ghost + 1, 0);
-    for (uint64_t i = 0; i < n_own; ++i) {
-        const uint32_t v = node_at(plo[e->rank] + i);
-        const int32_t* ob = col + row_ptr[v];
-        const int32_t* oe = col + row_ptr[v + 1];
-        for (int64_t k = 0; k < tin[v + 1] - tin[v]; ++k) {
-            const uint32_t u = tcol[tin[v] + k];
-            const bool recip = sym || std::binary_search(ob, oe, (int32_t)u);
-            const uint32_t ru = row_of(u);
-            icol[iptr[i] + k] = ru | (recip ? gg::kRecipBit : 0u);
-            if (ru >= e->ghost0) gcnt[ru - e->ghost0 + 1]++;
+    auto build_rows = [&](uint64_t lo, uint64_t hi) {
+        for (uint64_t i = lo; i < hi; ++i) {
+            const uint32_t v = node_at(plo[e->rank] + i);
+            const int32_t* ob = col + row_ptr[v];
+            const int32_t* oe = col + row_ptr[v + 1];
+            for (int64_t k = 0; k < tin[v + 1] - tin[v]; ++k) {
+                const uint32_t u = tcol[tin[v] + k];
+                const bool recip = sym || std::binary_search(ob, oe, (int32_t)u);
+                icol[iptr[i] + k] = row_of(u) | (recip ? gg::kRecipBit : 0u);
+            }
+            if (!sym)
+                for (int64_t k = 0; k < row_ptr[v + 1] - row_ptr[v]; ++k) ocol[optr[i] + k] = row_of((uint32_t)ob[k]);
         }
-        for (int64_t k = 0; k < row_ptr[v + 1] - row_ptr[v]; ++k) ocol[optr[i] + k] = row_of((uint32_t)ob[k]);
+    };
+    if (Wd == 1) host_parallel(n_own, build_rows);  // row_of is pure here
+    else build_rows(0, n_own);
+    for (uint64_t k = 0; k < icol.size() && e->n_ghost; ++k) {
+        const uint32_t ru = icol[k] & gg::kColMask;
+        if (ru >= e->ghost0) gcnt[ru - e->ghost0 + 1]++;
     }
     // ghost -> owned receivers (candidate marking from remote senders)
     std::vector<uint32_t> gocol;

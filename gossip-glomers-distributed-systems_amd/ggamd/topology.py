@@ -37,6 +37,8 @@ def host_lib():
         _lib.ggh_grid_links.argtypes = [C.c_uint64, C.c_uint64, P]
         _lib.ggh_csr_free.argtypes = [P]
         _lib.ggh_is_symmetric.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        _lib.ggh_components.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+        _lib.ggh_bfs.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]
     return _lib
 
 
@@ -74,3 +76,17 @@ def grid_links(side: int, seed: int = BASE_SEED + 5) -> Topology:
 
 def is_symmetric(t: Topology) -> bool:
     return bool(host_lib().ggh_is_symmetric(t.row_ptr.ctypes.data, t.col.ctypes.data, t.n_nodes))
+
+
+def components(t: Topology) -> np.ndarray:
+    """Weak component label (smallest member id) of every node."""
+    lab = np.empty(t.n_nodes, np.uint32)
+    host_lib().ggh_components(t.row_ptr.ctypes.data, t.col.ctypes.data, t.n_nodes, lab.ctypes.data)
+    return lab
+
+
+def bfs(t: Topology, src: int) -> np.ndarray:
+    """Hop distance from src along the rows (-1: unreachable)."""
+    d = np.empty(t.n_nodes, np.int32)
+    host_lib().ggh_bfs(t.row_ptr.ctypes.data, t.col.ctypes.data, t.n_nodes, src, d.ctypes.data)
+    return d

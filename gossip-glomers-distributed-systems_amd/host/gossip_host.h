@@ -23,6 +23,8 @@ int ggh_rmat(uint64_t V, uint32_t edge_factor, double a, double b, double c, uin
              gg_csr* out);
 int ggh_grid_links(uint64_t side, uint64_t seed, gg_csr* out);
 int ggh_is_symmetric(const int64_t* row_ptr, const int32_t* col, uint64_t V);
+int ggh_components(const int64_t* row_ptr, const int32_t* col, uint64_t V, uint32_t* label);
+int ggh_bfs(const int64_t* row_ptr, const int32_t* col, uint64_t V, uint32_t src, int32_t* dist);
 
 #ifdef __cplusplus
 }

@@ -229,6 +229,51 @@ int ggh_grid_links(uint64_t side, uint64_t seed, gg_csr* out) {
     return build_sym_csr(V, a, b, out);
 }
 
+// Weakly connected components (union-find with path halving): label[v] = the
+// smallest node id of v's component. Test/measurement helper (size-independent
+// properties of full-size runs: a message reaches exactly its source's component).
+int ggh_components(const int64_t* rp, const int32_t* col, uint64_t V, uint32_t* label) {
+    std::vector<uint32_t> p(V);
+    for (uint64_t v = 0; v < V; ++v) p[v] = (uint32_t)v;
+    auto find = [&](uint32_t x) {
+        while (p[x] != x) {
+            p[x] = p[p[x]];
+            x = p[x];
+        }
+        return x;
+    };
+    for (uint64_t u = 0; u < V; ++u)
+        for (int64_t k = rp[u]; k < rp[u + 1]; ++k) {
+            uint32_t a = find((uint32_t)u), b = find((uint32_t)col[k]);
+            if (a == b) continue;
+            if (a < b) p[b] = a;
+            else p[a] = b;
+        }
+    for (uint64_t v = 0; v < V; ++v) label[v] = find((uint32_t)v);
+    return 0;
+}
+
+// Directed hop distance from src along the rows (dist -1 = unreachable).
+int ggh_bfs(const int64_t* rp, const int32_t* col, uint64_t V, uint32_t src, int32_t* dist) {
+    if (src >= V) return -22;
+    for (uint64_t v = 0; v < V; ++v) dist[v] = -1;
+    std::vector<uint32_t> cur{src}, nxt;
+    dist[src] = 0;
+    for (int32_t d = 1; !cur.empty(); ++d) {
+        nxt.clear();
+        for (uint32_t u : cur)
+            for (int64_t k = rp[u]; k < rp[u + 1]; ++k) {
+                const uint32_t w = (uint32_t)col[k];
+                if (dist[w] < 0) {
+                    dist[w] = d;
+                    nxt.push_back(w);
+                }
+            }
+        cur.swap(nxt);
+    }
+    return 0;
+}
+
 // Symmetric iff every edge u->v has v->u (rows ascending).
 int ggh_is_symmetric(const int64_t* rp, const int32_t* col, uint64_t V) {
     for (uint64_t u = 0; u < V; ++u)
