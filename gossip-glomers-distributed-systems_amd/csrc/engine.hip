@@ -112,6 +112,7 @@ struct gg_engine {
     std::vector<int64_t> dist_round_of;        // round of each pending slot
     std::vector<gg_round_stats> dist_done;     // folded, not yet flushed
     size_t inj_off = 0;                        // pinned injection ring offset (async rounds)
+    uint32_t quiet = 0;                        // trailing rounds without new bits (gg_step)
 
     int64_t* d_in_ptr = nullptr;
     uint32_t* d_in_col = nullptr;
@@ -238,13 +239,20 @@ gg_engine::~gg_engine() {
 
 namespace {
 
+// Back to round 0, asynchronously: every call that reads results waits on the stream.
 int reset_device_state(gg_engine* e) {
     const size_t rowbytes = e->rows * e->nwp * 8;
     HIPCHK(hipMemsetAsync(e->d_base, 0, rowbytes, e->stream));
-    for (int b = 0; b < 2; ++b) {
-        HIPCHK(hipMemsetAsync(e->d_F[b], 0, rowbytes, e->stream));  // F rows are zero unless ACT
-        HIPCHK(hipMemsetAsync(e->d_flg[b], 0, e->rows, e->stream));
+    // F rows and flags are already all zero after two rounds without new bits
+    // (a stale row is cleared in the round it expires), e.g. after an episode
+    // run to quiescence. Single engine only: ghost rows follow remote rounds.
+    if (!(e->world == 1 && e->quiet >= 2)) {
+        for (int b = 0; b < 2; ++b) {
+            HIPCHK(hipMemsetAsync(e->d_F[b], 0, rowbytes, e->stream));  // F rows are zero unless ACT
+            HIPCHK(hipMemsetAsync(e->d_flg[b], 0, e->rows, e->stream));
+        }
     }
+    e->quiet = 2;
     for (int b = 0; b < 4; ++b) HIPCHK(hipMemsetAsync(e->d_fired[b], 0, e->rows / 8, e->stream));
     HIPCHK(hipMemsetAsync(e->d_cand, 0, e->rows, e->stream));
     HIPCHK(hipMemsetAsync(e->d_zmark, 0, e->rows, e->stream));
@@ -258,7 +266,6 @@ int reset_device_state(gg_engine* e) {
         HIPCHK(hipGetLastError());
     }
     if (e->d_dr) HIPCHK(hipMemsetAsync(e->d_dr, 0xff, n_own * e->cfg.n_lanes * 4, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
     return GG_OK;
 }
 
@@ -339,16 +346,17 @@ void launch_stream_t(const gg::RoundArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((gg::expand_stream<G, 2>), dim3((unsigned)blocks), dim3(gg::kBlock), 0, s, a);
 }
 
-template <int G>
+template <int G, int WPL = 2>
 void launch_hubs_t(const gg::RoundArgs& a, hipStream_t s) {
     const unsigned bc = (unsigned)std::min<uint64_t>(a.n_hchunks, 8192);
     const unsigned bh = (unsigned)std::min<uint64_t>(a.n_hubs, 8192);
-    hipLaunchKernelGGL((gg::hub_chunks<G, 2>), dim3(bc), dim3(gg::kBlock), 0, s, a);
-    hipLaunchKernelGGL((gg::hub_finish<G, 2>), dim3(bh), dim3(gg::kBlock), 0, s, a);
+    hipLaunchKernelGGL((gg::hub_chunks<G, WPL>), dim3(bc), dim3(gg::kBlock), 0, s, a);
+    hipLaunchKernelGGL((gg::hub_finish<G, WPL>), dim3(bh), dim3(gg::kBlock), 0, s, a);
 }
 
 void launch_hubs(const gg::RoundArgs& a, hipStream_t s) {
     switch (a.nwp) {
+        case 1: launch_hubs_t<1, 1>(a, s); break;
         case 2: launch_hubs_t<1>(a, s); break;
         case 4: launch_hubs_t<2>(a, s); break;
         case 8: launch_hubs_t<4>(a, s); break;
@@ -360,8 +368,23 @@ void launch_hubs(const gg::RoundArgs& a, hipStream_t s) {
     }
 }
 
+void launch_stream1(const gg::RoundArgs& a, hipStream_t s) {
+    static int resident = 0;
+    if (!resident) {
+        int dev = 0, cus = 0, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gg::expand_stream1, gg::kBlock, 0);
+        resident = std::max(1, cus) * std::max(1, per_cu);
+    }
+    uint64_t blocks = (a.n_own + gg::kBlock - 1) / gg::kBlock;
+    blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)resident));
+    hipLaunchKernelGGL(gg::expand_stream1, dim3((unsigned)blocks), dim3(gg::kBlock), 0, s, a);
+}
+
 void launch_stream(const gg::RoundArgs& a, hipStream_t s) {
     switch (a.nwp) {
+        case 1: launch_stream1(a, s); break;
         case 2: launch_stream_t<1>(a, s); break;
         case 4: launch_stream_t<2>(a, s); break;
         case 8: launch_stream_t<4>(a, s); break;
@@ -444,7 +467,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     const int64_t base = (int64_t)e->cfg.sync_base_ticks;
     const bool syncw_prep = e->cfg.enable_sync && r >= base;
     const bool syncw = e->cfg.enable_sync && r >= base + 2;
-    a.stream_ok = (!syncw && !maskw && e->nwp >= 2) ? 1 : 0;
+    a.stream_ok = (!syncw && !maskw) ? 1 : 0;
 
     if (a.n_own) {
         {
@@ -998,9 +1021,9 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
         HIPCHK(hipMalloc(&e->d_xrecv, std::max<uint64_t>(16, e->recv_off[Wd] * pb)));
     }
     // hubs: in-degree > hub_deg (hub_chunks/hub_finish in lean rounds), senders
-    // with out-degree > hub_deg (hub_mark); W = 64 rows have no streaming path
+    // with out-degree > hub_deg (hub_mark)
     e->hub_deg = 0;
-    if (e->nwp >= 2) {
+    {
         e->hub_deg = 512;
         if (const char* h = getenv("GG_HUB_DEG")) e->hub_deg = (uint32_t)std::max(1, atoi(h));
         uint64_t per = 128ull * (gg::kBlock / lanes_per_node((uint32_t)e->nwp));  // senders per chunk
@@ -1059,6 +1082,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     HIPCHK(hipMalloc(&e->d_sync_k, std::max<uint64_t>(1, n_own) * 4));
     if (e->cfg.flags & GG_TRACK_DELIVERY) HIPCHK(hipMalloc(&e->d_dr, std::max<uint64_t>(1, n_own) * e->cfg.n_lanes * 4));
     e->have_topo = true;
+    e->quiet = 0;  // fresh buffers: clear everything
     e->dist_k = 0;
     e->dist_done.clear();
     e->inj_off = 0;
@@ -1174,6 +1198,7 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
         for (uint32_t k = 0; k < m; ++k) {
             gg_round_stats s;
             fold_stats(e, e->h_counters + (size_t)k * gg::kSlots * gg::kCounters, r0 + k, &s);
+            e->quiet = s.new_bits ? 0 : e->quiet + 1;
             if (out) out[done + k] = s;
             e->inj.erase(r0 + k);
         }

@@ -956,7 +956,7 @@ void expand_round_lean(RoundArgs a) {
 
 // ---------------------------------------------------------------------------
 // expand_stream: every lean round (no sync events in expand, no masks) with
-// nwp >= 2. Dense rounds (dense_round) visit EVERY node; sparse ones the
+// nwp >= 2 (expand_stream1 below: nwp = 1). Dense rounds (dense_round) visit EVERY node; sparse ones the
 // candidate-node list of compact_round. No tiles, no barriers: node group q (G
 // lanes) walks items q, q + n_groups, ... with a software pipeline — while
 // item k's own row and sender rows land in its wave's LDS slots by DMA, item
@@ -1159,6 +1159,158 @@ void expand_stream(RoundArgs a) {
     unsigned long long acc[C_NUM];
 #pragma unroll
     for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
+    acc[C_NEW] = c_new;
+    acc[C_FWD_SENT] = c_fwd;
+    acc[C_FWD_DELIV] = c_fwd;
+    acc[C_HASH] = c_hash;
+    acc[C_NEXT_ACKS] = c_fwd;
+    acc[C_ACTIVE] = c_active;
+    acc[C_GATHERS] = c_gathers;
+    acc[C_NACT] = c_nact;
+    acc[C_BYTES] = c_bytes;
+    flush_counters(a, acc, s_red, t_start, K_STREAM);
+}
+
+// ---------------------------------------------------------------------------
+// expand_stream1: expand_stream for W = 64 (one u64 per node). One lane per
+// node, plain 8-byte loads (LDS-DMA has no 8-byte width) into registers; the
+// same three-stage pipeline (list entry k+3, row pointers k+2, columns k+1)
+// keeps each node to about one memory round trip. Same semantics and counters
+// as expand_stream.
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GG_STREAM_WAVES_PER_EU)))
+void expand_stream1(RoundArgs a) {
+    constexpr int D = 8;  // sender rows in flight per lane
+    __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
+    const unsigned long long t_start = clock100();
+    if (!a.stream_ok) {
+        noop_exit(a, K_STREAM, t_start);
+        return;
+    }
+    const bool dense = dense_round(a);
+    const uint32_t n_items = dense ? (uint32_t)a.n_own : a.n_work[1];
+    uint32_t c_new = 0, c_active = 0, c_gathers = 0, c_nact = 0;
+    unsigned long long c_fwd = 0, c_hash = 0, c_bytes = 0;
+    const uint32_t stride = gridDim.x * kBlock;
+
+    struct Meta {
+        int64_t p0;
+        uint32_t deg, node;
+        uint8_t ca, fl;
+    };
+    constexpr uint32_t kNone = ~0u;
+    constexpr uint32_t kHubBit = 0x80000000u;
+    auto node_of = [&](uint32_t k) -> uint32_t {
+        return k < n_items ? (dense ? (uint32_t)k : a.nodes[k]) : kNone;
+    };
+    auto fetch_meta = [&](uint32_t n, Meta& m) {
+        m.node = n;
+        if (n < a.n_own) {
+            m.p0 = a.in_ptr[n];
+            m.deg = (uint32_t)(a.in_ptr[n + 1] - m.p0);
+            m.ca = a.cand[a.own0 + n];
+            m.fl = a.flg_cur[a.own0 + n];
+            if (a.hub_deg && m.deg > a.hub_deg) {
+                m.node |= kHubBit;
+                m.deg = 0;
+            }
+        } else {
+            m.p0 = 0;
+            m.deg = 0;
+            m.ca = m.fl = 0;
+        }
+    };
+    auto fetch_cols = [&](const Meta& m, uint32_t (&c)[D]) {
+#pragma unroll
+        for (int b = 0; b < D; ++b) c[b] = ((uint32_t)b < m.deg) ? a.in_col[m.p0 + b] : 0u;
+    };
+
+    uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    Meta m0, m1;
+    uint32_t c0[D], c1[D];
+    const uint32_t n0 = node_of(k), n1 = node_of(k + stride);
+    uint32_t n2 = node_of(k + 2 * stride);
+    fetch_meta(n0, m0);
+    fetch_meta(n1, m1);
+    fetch_cols(m0, c0);
+    for (; k < n_items; k += stride) {
+        const bool hub = (m0.node & kHubBit) != 0;
+        const uint64_t i = m0.node & ~kHubBit;
+        const uint64_t rep = a.own0 + i;
+        // (a) own row and the first D sender rows
+        uint64_t sp = 0, src[D];
+        if (!hub) sp = a.base[rep];
+#pragma unroll
+        for (int b = 0; b < D; ++b) src[b] = ((uint32_t)b < m0.deg) ? a.F_prev[c0[b] & kColMask] : 0ull;
+        // (b) prefetch the next items' columns, row pointers and list entry
+        Meta m2;
+        fetch_cols(m1, c1);
+        fetch_meta(n2, m2);
+        const uint32_t n3 = node_of(k + 3 * stride);
+        if (!hub) {
+            uint64_t S = sp;
+            if (m0.ca & CA_INJ) {  // (1) client broadcasts of this round
+                uint32_t lo = 0, hi = a.n_inj;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (a.inj[2 * mid] < (uint32_t)i) lo = mid + 1;
+                    else hi = mid;
+                }
+                for (uint32_t q = lo; q < a.n_inj && a.inj[2 * q] == (uint32_t)i; ++q)
+                    S |= 1ull << (a.inj[2 * q + 1] & 63);
+            }
+            // (2) node broadcasts, ascending sender: first deliverer claims
+            unsigned long long cl_recip = 0;
+#pragma unroll
+            for (int b = 0; b < D; ++b) {
+                const uint64_t cw = src[b] & ~S;
+                S |= cw;
+                if (c0[b] & kRecipBit) cl_recip += __popcll(cw);
+            }
+            const int64_t p1 = m0.p0 + m0.deg;
+            for (int64_t e = m0.p0 + D; e < p1; e += D) {  // more than D senders
+                uint32_t cb[D];
+                uint64_t xb[D];
+#pragma unroll
+                for (int b = 0; b < D; ++b) cb[b] = e + b < p1 ? a.in_col[e + b] : 0u;
+#pragma unroll
+                for (int b = 0; b < D; ++b) xb[b] = e + b < p1 ? a.F_prev[cb[b] & kColMask] : 0ull;
+#pragma unroll
+                for (int b = 0; b < D; ++b) {
+                    const uint64_t cw = xb[b] & ~S;
+                    S |= cw;
+                    if (cb[b] & kRecipBit) cl_recip += __popcll(cw);
+                }
+            }
+            const uint32_t nin = m0.deg;
+            c_gathers += nin;
+            const uint64_t F = S & ~sp;
+            const uint32_t T = (uint32_t)__popcll(F);
+            if (F) {
+                const uint64_t idx = gid_of(a, i) * a.nw;
+                c_hash += gg_word_hash(idx, S) - (sp ? gg_word_hash(idx, sp) : 0ull);
+            }
+            const bool any = F != 0;
+            const bool zm = (m0.fl & FL_ACT) != 0;
+            if (any || zm) a.F_cur[rep] = F;
+            if (any) a.base[rep] = S;
+            if (any || m0.fl) a.flg_cur[rep] = any ? FL_ACT : 0;
+            if (m0.ca) a.cand[rep] = 0;
+            const unsigned long long deg = a.symmetric ? nin : (unsigned long long)(a.out_ptr[i + 1] - a.out_ptr[i]);
+            c_new += T;
+            c_fwd += deg * (unsigned long long)T - cl_recip;
+            c_active += 1;
+            c_nact += any ? 1 : 0;
+            c_bytes += (dense ? 0 : 4) + 8 + 2 + 4ull * nin + 8ull * (1 + nin) + ((any || zm) ? 8 : 0) + (any ? 9 : 0);
+        }
+        m0 = m1;
+        m1 = m2;
+        n2 = n3;
+#pragma unroll
+        for (int b = 0; b < D; ++b) c0[b] = c1[b];
+    }
+    unsigned long long acc[C_NUM];
+#pragma unroll
+    for (int q = 0; q < C_NUM; ++q) acc[q] = 0;
     acc[C_NEW] = c_new;
     acc[C_FWD_SENT] = c_fwd;
     acc[C_FWD_DELIV] = c_fwd;
