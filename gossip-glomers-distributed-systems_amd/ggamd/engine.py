@@ -231,9 +231,13 @@ class Engine:
     def lane_of(self, value: int) -> int:
         return self.lib.gg_lane_of(self.h, value)
 
-    def step(self, n_rounds: int = 1) -> list[dict]:
+    def step(self, n_rounds: int = 1, raw: bool = False):
+        """Run n lockstep rounds; per-round stats as dicts (raw=True: the ctypes
+        array, to convert later with stats_dict — keeps timed loops lean)."""
         arr = (GGRoundStats * max(1, n_rounds))()
         self._ok(self.lib.gg_step(self.h, n_rounds, arr))
+        if raw:
+            return arr
         return [stats_dict(arr[i]) for i in range(n_rounds)]
 
     def step_device_ms(self) -> float:

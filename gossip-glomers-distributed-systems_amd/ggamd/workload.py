@@ -43,11 +43,23 @@ class Workload:
         inject(eng, self.injections)
 
 
+def injection_arrays(injections):
+    """(nodes u32, values i64, rounds i64) contiguous arrays of a list of
+    (node, value, round) client broadcasts, for repeated inject() calls."""
+    a = np.asarray(injections, dtype=np.int64).reshape(-1, 3)
+    return (np.ascontiguousarray(a[:, 0], np.uint32), np.ascontiguousarray(a[:, 1]),
+            np.ascontiguousarray(a[:, 2]))
+
+
 def inject(eng, injections):
+    """Client broadcasts in call order: a list of (node, value, round) or the
+    tuple of arrays from injection_arrays()."""
+    if isinstance(injections, tuple) and len(injections) == 3 and isinstance(injections[0], np.ndarray):
+        eng.broadcast_many(*injections)
+        return
     if not injections:
         return
-    a = np.asarray(injections, dtype=np.int64)
-    eng.broadcast_many(a[:, 0], a[:, 1], a[:, 2])
+    eng.broadcast_many(*injection_arrays(injections))
 
 
 def uniform_injections(V: int, K: int, seed: int, rnd: int = 0) -> list:
