@@ -40,7 +40,8 @@ struct Window {
     bool seeded;
     uint64_t epoch_seed;
     std::vector<uint8_t> group;  // explicit: global node -> group
-    uint8_t* d_grp = nullptr;    // replica-row groups on device
+    uint8_t* d_grp = nullptr;    // local-row groups on device
+    uint64_t* d_ebits = nullptr; // in-edge bitmap: ends in different groups (build_edge_mask)
 };
 
 struct Injection {
@@ -219,7 +220,10 @@ void gg_engine::free_topology() {
     dfree(d_gout_col);
     dfree(d_xsend);
     dfree(d_xrecv);
-    for (auto& w : windows) dfree(w.d_grp);
+    for (auto& w : windows) {
+        dfree(w.d_grp);
+        dfree(w.d_ebits);
+    }
     have_topo = false;
 }
 
@@ -288,14 +292,21 @@ int materialize_windows(gg_engine* e) {
             }
             HIPCHK(hipMemcpy(w.d_grp, h.data(), e->rows, hipMemcpyHostToDevice));
         }
+        const uint64_t words = std::max<uint64_t>(1, (e->n_in_edges + 63) / 64);
+        HIPCHK(hipMalloc(&w.d_ebits, words * 8));
+        if (e->n_in_edges) {
+            hipLaunchKernelGGL(gg::build_edge_mask, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, e->stream,
+                               e->d_in_ptr, e->d_in_col, e->n_own, e->n_in_edges, w.d_grp, w.d_ebits);
+            HIPCHK(hipGetLastError());
+        }
     }
     if (any) HIPCHK(hipStreamSynchronize(e->stream));
     return GG_OK;
 }
 
-const uint8_t* group_at(const gg_engine* e, int64_t r) {
+const Window* window_at(const gg_engine* e, int64_t r) {
     for (const auto& w : e->windows)
-        if (w.from <= r && r < w.to) return w.d_grp;
+        if (w.from <= r && r < w.to) return &w;
     return nullptr;
 }
 
@@ -330,20 +341,30 @@ void launch_expand(const gg::RoundArgs& a, bool syncw, bool maskw, hipStream_t s
 
 // expand_stream grid: one resident wave of blocks (node groups walk their
 // items grid-stride), so no partial second wave of blocks trails the round.
-template <int G>
+template <int G, bool MASKW>
 void launch_stream_t(const gg::RoundArgs& a, hipStream_t s) {
     static int resident = 0;
     if (!resident) {
         int dev = 0, cus = 0, per_cu = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gg::expand_stream<G, 2>, gg::kBlock, 0);
+        if (MASKW)
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gg::expand_stream_masked<G, 2>, gg::kBlock, 0);
+        else
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gg::expand_stream<G, 2>, gg::kBlock, 0);
         resident = std::max(1, cus) * std::max(1, per_cu);
     }
     const uint64_t ngb = gg::kBlock / G;
     uint64_t blocks = (a.n_own + ngb - 1) / ngb;
     blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)resident));
-    hipLaunchKernelGGL((gg::expand_stream<G, 2>), dim3((unsigned)blocks), dim3(gg::kBlock), 0, s, a);
+    if (MASKW) hipLaunchKernelGGL((gg::expand_stream_masked<G, 2>), dim3((unsigned)blocks), dim3(gg::kBlock), 0, s, a);
+    else hipLaunchKernelGGL((gg::expand_stream<G, 2>), dim3((unsigned)blocks), dim3(gg::kBlock), 0, s, a);
+}
+
+template <int G>
+void launch_stream_m(const gg::RoundArgs& a, bool maskw, hipStream_t s) {
+    if (maskw) launch_stream_t<G, true>(a, s);
+    else launch_stream_t<G, false>(a, s);
 }
 
 template <int G, int WPL = 2>
@@ -382,16 +403,16 @@ void launch_stream1(const gg::RoundArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(gg::expand_stream1, dim3((unsigned)blocks), dim3(gg::kBlock), 0, s, a);
 }
 
-void launch_stream(const gg::RoundArgs& a, hipStream_t s) {
+void launch_stream(const gg::RoundArgs& a, bool maskw, hipStream_t s) {
     switch (a.nwp) {
-        case 1: launch_stream1(a, s); break;
-        case 2: launch_stream_t<1>(a, s); break;
-        case 4: launch_stream_t<2>(a, s); break;
-        case 8: launch_stream_t<4>(a, s); break;
-        case 16: launch_stream_t<8>(a, s); break;
-        case 32: launch_stream_t<16>(a, s); break;
-        case 64: launch_stream_t<32>(a, s); break;
-        case 128: launch_stream_t<64>(a, s); break;
+        case 1: launch_stream1(a, s); break;  // never with masks (stream_ok)
+        case 2: launch_stream_m<1>(a, maskw, s); break;
+        case 4: launch_stream_m<2>(a, maskw, s); break;
+        case 8: launch_stream_m<4>(a, maskw, s); break;
+        case 16: launch_stream_m<8>(a, maskw, s); break;
+        case 32: launch_stream_m<16>(a, maskw, s); break;
+        case 64: launch_stream_m<32>(a, maskw, s); break;
+        case 128: launch_stream_m<64>(a, maskw, s); break;
         default: break;
     }
 }
@@ -446,7 +467,9 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.sync_k = e->d_sync_k;
     bool maskw = false;
     for (int k = 0; k < 5; ++k) {
-        a.grp[k] = group_at(e, r - 3 + k);
+        const Window* w = window_at(e, r - 3 + k);
+        a.grp[k] = w ? w->d_grp : nullptr;
+        a.ebits[k] = w ? w->d_ebits : nullptr;
         maskw |= a.grp[k] != nullptr;
     }
     a.inj = d_inj;
@@ -467,7 +490,9 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     const int64_t base = (int64_t)e->cfg.sync_base_ticks;
     const bool syncw_prep = e->cfg.enable_sync && r >= base;
     const bool syncw = e->cfg.enable_sync && r >= base + 2;
-    a.stream_ok = (!syncw && !maskw) ? 1 : 0;
+    // streaming rounds: no sync event reaches the expand; partition windows only
+    // on symmetric graphs without hubs at W >= 128 (expand_stream<.., MASKW>)
+    a.stream_ok = (!syncw && (!maskw || (e->symmetric && e->n_hubs == 0 && e->nwp >= 2))) ? 1 : 0;
 
     if (a.n_own) {
         {
@@ -499,7 +524,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             HIPCHK(hipGetLastError());
         }
         if (a.stream_ok) {  // lean rounds: all nodes (dense) or the candidate list (sparse)
-            launch_stream(a, e->stream);
+            launch_stream(a, maskw, e->stream);
             if (e->n_hubs) {
                 HIPCHK(hipGetLastError());
                 launch_hubs(a, e->stream);

@@ -154,6 +154,8 @@ struct RoundArgs {
     int32_t* sync_next;         // [n_own]
     uint32_t* sync_k;
     const uint8_t* grp[5];      // partition groups of rounds r-3..r+1 (nullptr: no window)
+    const uint64_t* ebits[5];   // the same windows as in-edge bitmaps: bit e = the two ends of
+                                // in-edge e are in different groups (masked streaming rounds)
     const uint32_t* inj;        // (local node, lane) pairs sorted by node
     uint32_t n_inj;
     unsigned long long* counters;  // [kSlots][kCounters]
@@ -966,9 +968,8 @@ void expand_round_lean(RoundArgs a) {
 // without looking at sender flags, and a node nobody reached finds no new
 // bits. The node-local part of round_prep (stale F row of round r-2, flag
 // reset) is done here from the node's old flag byte.
-template <int G, int WPL>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GG_STREAM_WAVES_PER_EU)))
-void expand_stream(RoundArgs a) {
+template <int G, int WPL, bool MASKW>
+__device__ __forceinline__ void stream_body(RoundArgs a) {
     static_assert(WPL == 2, "DMA slots hold 16 bytes per lane");
     constexpr int NGB = kBlock / G;  // node groups per block
     constexpr int D = kStreamRows;   // sender rows per DMA batch
@@ -984,6 +985,7 @@ void expand_stream(RoundArgs a) {
     // per-lane counts that fit 32 bits stay 32-bit (register budget)
     uint32_t c_new = 0, c_active = 0, c_gathers = 0, c_nact = 0;
     unsigned long long c_fwd = 0, c_hash = 0, c_bytes = 0;
+    unsigned long long c_fwd_deliv = 0, c_dropped = 0, c_next_ackdrop = 0;  // MASKW
     const int lg = threadIdx.x % G;
     const uint32_t off = (uint32_t)lg * WPL;
     const int gshift = (threadIdx.x & 63) / G * G;
@@ -1048,8 +1050,18 @@ void expand_stream(RoundArgs a) {
         const bool hub = (m0.node & kHubBit) != 0;
         const uint64_t i = m0.node & ~kHubBit;
         const uint64_t rep = a.own0 + i;
-        // (a) DMA node i's own row and its first D sender rows
+        // (a) DMA node i's own row and its first D sender rows (masked rounds:
+        // and the words of the window bitmaps covering its first D in-edges)
         if (!hub && !(a.ablate & 4)) dma16((const void*)(a.base + rep * a.nwp + off), my + D * 1024);
+        uint64_t mw[3][2];
+        if constexpr (MASKW) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const uint64_t* eb = a.ebits[2 + q];
+                mw[q][0] = (eb && m0.deg) ? eb[m0.p0 >> 6] : 0ull;
+                mw[q][1] = (eb && m0.deg) ? eb[(m0.p0 + D - 1) >> 6] : 0ull;
+            }
+        }
 #pragma unroll
         for (int b = 0; b < D; ++b) {
             if ((uint32_t)b < m0.deg && !(a.ablate & 2))
@@ -1081,19 +1093,58 @@ void expand_stream(RoundArgs a) {
                 if (word / WPL == (uint32_t)lg) set_lane_bit<WPL>(S, word % WPL, lane & 63);
             }
         }
-        // (2) node broadcasts, ascending sender: first deliverer claims
-        unsigned long long cl_recip = 0;
-        auto claim = [&](uint64_t x0, uint64_t x1, uint32_t c) {
-            const uint64_t w0 = x0 & ~S.w[0], w1 = x1 & ~S.w[1];
-            S.w[0] |= w0;
-            S.w[1] |= w1;
-            if (c & kRecipBit) cl_recip += __popcll(w0) + __popcll(w1);
+        // (2) node broadcasts, ascending sender: first deliverer claims.
+        // Masked rounds: a sender whose message of r-1 was dropped is skipped;
+        // claims of reciprocal senders count as delivered forwards unless v's
+        // own forwards to them in r are dropped (bit in window r), and their
+        // acks in r+1 as dropped when window r+1 separates them.
+        unsigned long long cl_recip = 0, cl_deliv = 0, cl_ackdrop = 0;
+        uint32_t n_m3 = 0, n_ad = 0;  // out-neighbours (= in, symmetric) cut in r; of the rest, cut in r+1
+        auto claim = [&](uint64_t x0, uint64_t x1, uint32_t c, uint32_t mb) {
+            if constexpr (MASKW) {
+                if (mb & 1) return;  // dropped in flight
+                const uint64_t w0 = x0 & ~S.w[0], w1 = x1 & ~S.w[1];
+                S.w[0] |= w0;
+                S.w[1] |= w1;
+                if (c & kRecipBit) {
+                    const unsigned long long pc = __popcll(w0) + __popcll(w1);
+                    cl_recip += pc;
+                    if (!(mb & 2)) {
+                        cl_deliv += pc;
+                        if (mb & 4) cl_ackdrop += pc;
+                    }
+                }
+            } else {
+                const uint64_t w0 = x0 & ~S.w[0], w1 = x1 & ~S.w[1];
+                S.w[0] |= w0;
+                S.w[1] |= w1;
+                if (c & kRecipBit) cl_recip += __popcll(w0) + __popcll(w1);
+            }
+        };
+        // bit b of the three window masks (r-1, r, r+1) for sender slot b of a batch at edge e0
+        auto mask_bits = [&](uint64_t (&w)[3][2], int64_t e0, int b) -> uint32_t {
+            uint32_t mb = 0;
+            if constexpr (MASKW) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const uint64_t e = (uint64_t)(e0 + b);
+                    const uint64_t word = ((e >> 6) == ((uint64_t)e0 >> 6)) ? w[q][0] : w[q][1];
+                    mb |= (uint32_t)((word >> (e & 63)) & 1ull) << q;
+                }
+            }
+            return mb;
         };
 #pragma unroll
         for (int b = 0; b < D; ++b) {
             if ((uint32_t)b < m0.deg) {
                 const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(my + b * 1024 + lane16);
-                claim(x.x, x.y, c0[b]);
+                uint32_t mb = 0;
+                if constexpr (MASKW) {
+                    mb = mask_bits(mw, m0.p0, b);
+                    n_m3 += (mb >> 1) & 1;
+                    n_ad += ((mb >> 1) & 1) ? 0u : ((mb >> 2) & 1);
+                }
+                claim(x.x, x.y, c0[b], mb);
             }
         }
         const int64_t p1 = m0.p0 + m0.deg;
@@ -1105,12 +1156,27 @@ void expand_stream(RoundArgs a) {
                 if (e + b < p1)
                     dma16((const void*)(a.F_prev + (uint64_t)(cb[b] & kColMask) * a.nwp + off), my + b * 1024);
             }
+            uint64_t ew[3][2];
+            if constexpr (MASKW) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const uint64_t* eb = a.ebits[2 + q];
+                    ew[q][0] = eb ? eb[e >> 6] : 0ull;
+                    ew[q][1] = eb ? eb[(e + D - 1) >> 6] : 0ull;
+                }
+            }
             vm_drain();
 #pragma unroll
             for (int b = 0; b < D; ++b) {
                 if (e + b < p1) {
                     const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(my + b * 1024 + lane16);
-                    claim(x.x, x.y, cb[b]);
+                    uint32_t mb = 0;
+                    if constexpr (MASKW) {
+                        mb = mask_bits(ew, e, b);
+                        n_m3 += (mb >> 1) & 1;
+                        n_ad += ((mb >> 1) & 1) ? 0u : ((mb >> 2) & 1);
+                    }
+                    claim(x.x, x.y, cb[b], mb);
                 }
             }
         }
@@ -1141,7 +1207,14 @@ void expand_stream(RoundArgs a) {
         }
         const unsigned long long deg = a.symmetric ? nin : (unsigned long long)(a.out_ptr[i + 1] - a.out_ptr[i]);
         c_new += T;
-        c_fwd += deg * (unsigned long long)T - cl_recip;
+        const unsigned long long fs = deg * (unsigned long long)T - cl_recip;
+        c_fwd += fs;
+        if constexpr (MASKW) {  // symmetric only (host): out-neighbours = in-neighbours
+            const unsigned long long fd = (deg - n_m3) * (unsigned long long)T - cl_deliv;
+            c_fwd_deliv += fd;
+            c_dropped += fs - fd;
+            c_next_ackdrop += (unsigned long long)n_ad * T - cl_ackdrop;
+        }
         if (lg == 0) {
             c_active += 1;
             c_nact += any ? 1 : 0;
@@ -1159,16 +1232,32 @@ void expand_stream(RoundArgs a) {
     unsigned long long acc[C_NUM];
 #pragma unroll
     for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
+    if constexpr (!MASKW) c_fwd_deliv = c_fwd;
     acc[C_NEW] = c_new;
     acc[C_FWD_SENT] = c_fwd;
-    acc[C_FWD_DELIV] = c_fwd;
+    acc[C_FWD_DELIV] = c_fwd_deliv;
+    acc[C_DROPPED] = c_dropped;
     acc[C_HASH] = c_hash;
-    acc[C_NEXT_ACKS] = c_fwd;
+    acc[C_NEXT_ACKS] = c_fwd_deliv;
+    acc[C_NEXT_ACKDROP] = c_next_ackdrop;
     acc[C_ACTIVE] = c_active;
     acc[C_GATHERS] = c_gathers;
     acc[C_NACT] = c_nact;
     acc[C_BYTES] = c_bytes;
     flush_counters(a, acc, s_red, t_start, K_STREAM);
+}
+
+template <int G, int WPL>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GG_STREAM_WAVES_PER_EU)))
+void expand_stream(RoundArgs a) {
+    stream_body<G, WPL, false>(a);
+}
+
+// Partition-window rounds: the mask bookkeeping needs more registers (4 waves/SIMD).
+template <int G, int WPL>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+void expand_stream_masked(RoundArgs a) {
+    stream_body<G, WPL, true>(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -1590,6 +1679,28 @@ __global__ void fill_seeded_groups(uint8_t* grp, uint64_t rows, uint64_t n_valid
     if (rr >= rows) return;
     const uint32_t g = gid ? gid[rr] : (uint32_t)rr;
     grp[rr] = (rr < n_valid && g != ~0u) ? (uint8_t)gg_part_group(seed, epoch_seed, g) : 0;
+}
+
+// In-edge bitmap of a partition window: bit e = the sender and the receiver of
+// in-edge e are in different groups (messages between them are dropped while
+// the window is active). One thread per 64-edge word.
+__global__ void build_edge_mask(const int64_t* in_ptr, const uint32_t* in_col, uint64_t n_own, uint64_t n_edges,
+                                const uint8_t* grp, uint64_t* out) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t e0 = w * 64;
+    if (e0 >= n_edges) return;
+    uint64_t lo = 0, hi = n_own;  // the node whose in-list holds e0: in_ptr[v] <= e0 < in_ptr[v+1]
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi + 1) >> 1;
+        if ((uint64_t)in_ptr[mid] <= e0) lo = mid;
+        else hi = mid - 1;
+    }
+    uint64_t v = lo, bits = 0;
+    for (uint64_t e = e0; e < e0 + 64 && e < n_edges; ++e) {
+        while ((uint64_t)in_ptr[v + 1] <= e) ++v;
+        if (grp[in_col[e] & kColMask] != grp[v]) bits |= 1ull << (e - e0);
+    }
+    out[w] = bits;
 }
 
 // ---------------------------------------------------------------------------

@@ -68,3 +68,18 @@ def test_partition_then_lean_rounds(hip_lib, cpu_lib, monkeypatch, deg):
         sc = random_scenario(rnd, max_v=200, W=128, rounds=45)
         sc.enable_sync = False
         _compare(sc, hip_lib, cpu_lib)
+
+
+@pytest.mark.parametrize("W", [128, 1024, 4096])
+def test_masked_streaming_rounds(hip_lib, cpu_lib, monkeypatch, W):
+    """Symmetric graphs without hubs stream through partition windows too
+    (expand_stream_masked: per-window in-edge bitmaps for drops, delivered
+    forwards and dropped acks) — seeded and explicit windows, back to back."""
+    monkeypatch.setenv("GG_HUB_DEG", "1000000000")
+    rnd = random.Random(W)
+    for _ in range(6):
+        sc = random_scenario(rnd, max_v=300, W=W, rounds=40, directed_p=0.0)
+        sc.enable_sync = False
+        sc.windows = [("seeded", 2, 6, rnd.randrange(1 << 30)), ("seeded", 6, 9, rnd.randrange(1 << 30)),
+                      ("groups", 12, 20, np.array([rnd.randrange(3) for _ in range(sc.topo.n_nodes)], np.uint8))]
+        _compare(sc, hip_lib, cpu_lib)
