@@ -37,6 +37,7 @@ def host_lib():
         _lib.ggh_grid_links.argtypes = [C.c_uint64, C.c_uint64, P]
         _lib.ggh_csr_free.argtypes = [P]
         _lib.ggh_is_symmetric.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        _lib.ggh_topology_json.argtypes = [C.c_char_p, C.c_uint64, P]
         _lib.ggh_components.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
         _lib.ggh_bfs.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]
     return _lib
@@ -72,6 +73,23 @@ def rmat(V: int, edge_factor: int = 16, a=0.57, b=0.19, c=0.19, seed: int = BASE
 
 def grid_links(side: int, seed: int = BASE_SEED + 5) -> Topology:
     return _take("ggh_grid_links", side, seed)
+
+
+def from_maelstrom(msg) -> Topology:
+    """A Maelstrom `topology` message (JSON text/bytes, or the decoded dict) -> CSR.
+    HandleTopology (`broadcast/broadcast.go:36-48`) keeps topology["n<id>"] per node;
+    here every row at once, sorted and de-duplicated, missing rows empty."""
+    if isinstance(msg, dict):
+        import json
+        msg = json.dumps(msg)
+    if isinstance(msg, str):
+        msg = msg.encode()
+    return _take("ggh_topology_json", msg, len(msg))
+
+
+def to_maelstrom(t: Topology) -> dict:
+    """CSR -> the `topology` map Maelstrom sends (node "n<i>")."""
+    return {f"n{v}": [f"n{int(u)}" for u in t.col[t.row_ptr[v]:t.row_ptr[v + 1]]] for v in range(t.n_nodes)}
 
 
 def is_symmetric(t: Topology) -> bool:

@@ -69,6 +69,29 @@ def uniform_injections(V: int, K: int, seed: int, rnd: int = 0) -> list:
     return [(int(nodes[k]), k, rnd) for k in range(K)]
 
 
+def c1(partition: bool = False, rounds: int = 260, seed: int = BASE_SEED + 1):
+    """Config C1, the reference's own test setting (Maelstrom `--node-count 25
+    --topology tree4 --rate 100 --latency 100 --time-limit 20`): 10 client ops
+    per 100 ms round for 200 rounds, each a broadcast of a fresh value to a
+    uniform node with probability 1/2, else a read; sync on; then drain.
+    partition: a seeded bisection for rounds [50, 100) (`--nemesis partition`).
+    Returns (Workload, number of read ops)."""
+    import random
+    rnd = random.Random(seed)
+    inj, val, reads = [], 0, 0
+    for r in range(200):
+        for _ in range(10):
+            if rnd.random() < 0.5:
+                inj.append((rnd.randrange(25), val, r))
+                val += 1
+            else:
+                reads += 1
+    W = ((val + 63) // 64) * 64
+    windows = [("seeded", 50, 100, seed ^ 0xB15EC7)] if partition else []
+    wl = Workload("C1", T.tree(25, 4), W, inj, seed, windows=windows, max_rounds=rounds)
+    return wl, reads
+
+
 def c2(V: int = 1 << 20, K: int = 1024) -> Workload:
     """1M-node tree4, 1024 concurrent messages (1 Kbit sets), sync on, no partitions."""
     seed = BASE_SEED + 2

@@ -22,6 +22,7 @@ int ggh_random_regular(uint64_t V, uint32_t d, uint64_t seed, gg_csr* out);
 int ggh_rmat(uint64_t V, uint32_t edge_factor, double a, double b, double c, uint64_t seed,
              gg_csr* out);
 int ggh_grid_links(uint64_t side, uint64_t seed, gg_csr* out);
+int ggh_topology_json(const char* text, uint64_t len, gg_csr* out);
 int ggh_is_symmetric(const int64_t* row_ptr, const int32_t* col, uint64_t V);
 int ggh_components(const int64_t* row_ptr, const int32_t* col, uint64_t V, uint32_t* label);
 int ggh_bfs(const int64_t* row_ptr, const int32_t* col, uint64_t V, uint32_t src, int32_t* dist);

@@ -15,6 +15,8 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -271,6 +273,138 @@ int ggh_bfs(const int64_t* rp, const int32_t* col, uint64_t V, uint32_t src, int
             }
         cur.swap(nxt);
     }
+    return 0;
+}
+
+// Maelstrom `topology` message -> CSR (HandleTopology, broadcast/broadcast.go:36-48;
+// TopologyMsgBody :18-20): accepts the whole body {"type":"topology",
+// "topology":{"n0":["n1",...],...}} or just the map. Node "n<i>" is id i; V =
+// 1 + the largest id named; a node without a row gets an empty list (:41-42);
+// rows are sorted and de-duplicated (the engine's claim order is by id, not by
+// list position). Returns -22 on malformed input.
+int ggh_topology_json(const char* text, uint64_t len, gg_csr* out) {
+    if (!text || !out) return -22;
+    const char* p = text;
+    const char* end = text + len;
+    auto ws = [&]() { while (p < end && (*p == ' ' || *p == '\n' || *p == '\t' || *p == '\r')) ++p; };
+    auto lit = [&](char c) { ws(); if (p < end && *p == c) { ++p; return true; } return false; };
+    auto str = [&](std::string& s) -> bool {
+        ws();
+        if (p >= end || *p != '"') return false;
+        ++p;
+        s.clear();
+        while (p < end && *p != '"') {
+            if (*p == '\\' && p + 1 < end) ++p;
+            s.push_back(*p++);
+        }
+        if (p >= end) return false;
+        ++p;
+        return true;
+    };
+    auto node_id = [](const std::string& s, int64_t& id) -> bool {
+        if (s.size() < 2 || s[0] != 'n') return false;
+        id = 0;
+        for (size_t k = 1; k < s.size(); ++k) {
+            if (s[k] < '0' || s[k] > '9' || id > 0x7fffffff) return false;
+            id = id * 10 + (s[k] - '0');
+        }
+        return id <= 0x7ffffffe;
+    };
+    // skip any JSON value (for the body's other keys)
+    std::function<bool()> skip = [&]() -> bool {
+        ws();
+        if (p >= end) return false;
+        if (*p == '"') { std::string t; return str(t); }
+        if (*p == '{' || *p == '[') {
+            const char close = *p == '{' ? '}' : ']';
+            ++p;
+            if (lit(close)) return true;
+            do {
+                if (close == '}') { std::string k; if (!str(k) || !lit(':')) return false; }
+                if (!skip()) return false;
+            } while (lit(','));
+            return lit(close);
+        }
+        while (p < end && *p != ',' && *p != '}' && *p != ']') ++p;
+        return true;
+    };
+    std::vector<std::pair<int64_t, std::vector<int64_t>>> rows;
+    int64_t maxid = -1;
+    auto parse_map = [&]() -> bool {  // {"n0": ["n1", ...], ...}
+        if (!lit('{')) return false;
+        if (lit('}')) return true;
+        do {
+            std::string k;
+            int64_t u;
+            if (!str(k) || !node_id(k, u) || !lit(':') || !lit('[')) return false;
+            std::vector<int64_t> nb;
+            if (!lit(']')) {
+                do {
+                    std::string t;
+                    int64_t v;
+                    if (!str(t) || !node_id(t, v)) return false;
+                    nb.push_back(v);
+                    maxid = std::max(maxid, v);
+                } while (lit(','));
+                if (!lit(']')) return false;
+            }
+            maxid = std::max(maxid, u);
+            rows.emplace_back(u, std::move(nb));
+        } while (lit(','));
+        return lit('}');
+    };
+    // body or bare map: look for a "topology" key at the top level
+    const char* save = p;
+    bool ok = false;
+    if (lit('{')) {
+        std::string k;
+        const char* key_at = p;
+        if (str(k) && k.rfind("n", 0) == 0 && k.size() > 1 && k[1] >= '0' && k[1] <= '9') {
+            p = save;
+            ok = parse_map();
+        } else {
+            p = key_at;
+            bool found = false;
+            if (!lit('}')) {
+                do {
+                    if (!str(k) || !lit(':')) return -22;
+                    if (k == "topology") {
+                        if (!parse_map()) return -22;
+                        found = true;
+                    } else if (!skip()) {
+                        return -22;
+                    }
+                } while (lit(','));
+                if (!lit('}')) return -22;
+            }
+            ok = found;
+        }
+    }
+    if (!ok) return -22;
+    const uint64_t V = (uint64_t)(maxid + 1);
+    std::vector<std::vector<int64_t>> adj(V);
+    for (auto& r : rows) {
+        auto& a = adj[r.first];
+        a.insert(a.end(), r.second.begin(), r.second.end());
+    }
+    int64_t* rp = (int64_t*)malloc((V + 1) * sizeof(int64_t));
+    uint64_t nnz = 0;
+    for (auto& a : adj) {
+        std::sort(a.begin(), a.end());
+        a.erase(std::unique(a.begin(), a.end()), a.end());
+        nnz += a.size();
+    }
+    int32_t* col = (int32_t*)malloc(std::max<uint64_t>(1, nnz) * sizeof(int32_t));
+    if (!rp || !col) { free(rp); free(col); return -12; }
+    rp[0] = 0;
+    for (uint64_t v = 0; v < V; ++v) {
+        for (uint64_t k = 0; k < adj[v].size(); ++k) col[rp[v] + k] = (int32_t)adj[v][k];
+        rp[v + 1] = rp[v] + (int64_t)adj[v].size();
+    }
+    out->n_nodes = V;
+    out->nnz = nnz;
+    out->row_ptr = rp;
+    out->col = col;
     return 0;
 }
 
