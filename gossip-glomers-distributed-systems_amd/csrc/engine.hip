@@ -137,6 +137,10 @@ struct gg_engine {
     uint32_t* d_hub_c0 = nullptr;
     gg::HubChunk* d_hchunks = nullptr;
     gg::HubChunk* d_mchunks = nullptr;
+    uint4* d_srec = nullptr;         // [2 n_own] sync records (streamed sync rounds), or none
+    uint8_t* d_sstate = nullptr;     // [rows] sender states (streamed sync rounds)
+    uint64_t* d_ibits = nullptr;     // [rows/64] non-zero sender states
+    bool sync_tiles = false;         // GG_SYNC_TILES=1: sync rounds on the tile path (A/B)
     uint64_t* d_hscratch = nullptr;
     uint64_t tile_nodes = 0, tile_bytes = 0;
     uint64_t n_in_edges = 0;
@@ -204,6 +208,9 @@ void gg_engine::free_topology() {
     dfree(d_hub_c0);
     dfree(d_hchunks);
     dfree(d_mchunks);
+    dfree(d_srec);
+    dfree(d_sstate);
+    dfree(d_ibits);
     dfree(d_hscratch);
     n_hubs = n_hchunks = n_mchunks = 0;
     dfree(d_work);
@@ -417,6 +424,37 @@ void launch_stream(const gg::RoundArgs& a, bool maskw, hipStream_t s) {
     }
 }
 
+template <int G>
+void launch_stream_sync_t(const gg::RoundArgs& a, hipStream_t s) {
+    static int resident = 0;
+    if (!resident) {
+        int dev = 0, cus = 0, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gg::expand_stream_sync<G>, gg::kBlock, 0);
+        resident = std::max(1, cus) * std::max(1, per_cu);
+    }
+    const uint64_t rb = std::min<uint64_t>((a.n_own + gg::kBlock - 1) / gg::kBlock, 16384);
+    hipLaunchKernelGGL(gg::sync_records, dim3((unsigned)std::max<uint64_t>(1, rb)), dim3(gg::kBlock), 0, s, a);
+    const uint64_t ngb = gg::kBlock / G;
+    uint64_t blocks = (a.n_own + ngb - 1) / ngb;
+    blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)resident));
+    hipLaunchKernelGGL((gg::expand_stream_sync<G>), dim3((unsigned)blocks), dim3(gg::kBlock), 0, s, a);
+}
+
+void launch_stream_sync(const gg::RoundArgs& a, hipStream_t s) {
+    switch (a.nwp) {
+        case 2: launch_stream_sync_t<1>(a, s); break;
+        case 4: launch_stream_sync_t<2>(a, s); break;
+        case 8: launch_stream_sync_t<4>(a, s); break;
+        case 16: launch_stream_sync_t<8>(a, s); break;
+        case 32: launch_stream_sync_t<16>(a, s); break;
+        case 64: launch_stream_sync_t<32>(a, s); break;
+        case 128: launch_stream_sync_t<64>(a, s); break;
+        default: break;
+    }
+}
+
 // Enqueue round e->round (kernels only). inj: device pairs for this round.
 int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned long long* d_ctr) {
     const int64_t r = e->round;
@@ -454,6 +492,9 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.n_hubs = e->n_hubs;
     a.hscratch = e->d_hscratch;
     a.mchunks = e->d_mchunks;
+    a.srec = e->d_srec;
+    a.sstate = e->d_sstate;
+    a.ibits = e->d_ibits;
     a.n_mchunks = e->n_mchunks;
     {
         static const uint32_t ablate = getenv("GG_ABLATE") ? (uint32_t)atoi(getenv("GG_ABLATE")) : 0u;
@@ -492,7 +533,9 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     const bool syncw = e->cfg.enable_sync && r >= base + 2;
     // streaming rounds: no sync event reaches the expand; partition windows only
     // on symmetric graphs without hubs at W >= 128 (expand_stream<.., MASKW>)
-    a.stream_ok = (!syncw && (!maskw || (e->symmetric && e->n_hubs == 0 && e->nwp >= 2))) ? 1 : 0;
+    // streamed sync rounds (sync_records + expand_stream_sync): no masks, no in-hubs, nwp >= 2
+    const bool sync_stream = syncw && !maskw && e->d_srec != nullptr;
+    a.stream_ok = ((!syncw && (!maskw || (e->symmetric && e->n_hubs == 0 && e->nwp >= 2))) || sync_stream) ? 1 : 0;
 
     if (a.n_own) {
         {
@@ -523,7 +566,9 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
                                dim3(gg::kBlock), 0, e->stream, a);
             HIPCHK(hipGetLastError());
         }
-        if (a.stream_ok) {  // lean rounds: all nodes (dense) or the candidate list (sparse)
+        if (sync_stream) {
+            launch_stream_sync(a, e->stream);
+        } else if (a.stream_ok) {  // lean rounds: all nodes (dense) or the candidate list (sparse)
             launch_stream(a, maskw, e->stream);
             if (e->n_hubs) {
                 HIPCHK(hipGetLastError());
@@ -1085,6 +1130,16 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
             HIPCHK(hipMalloc(&e->d_mchunks, mch.size() * sizeof(gg::HubChunk)));
             HIPCHK(hipMemcpy(e->d_mchunks, mch.data(), mch.size() * sizeof(gg::HubChunk), hipMemcpyHostToDevice));
         }
+    }
+    // streamed sync rounds need no in-hubs and two words per lane
+    e->sync_tiles = getenv("GG_SYNC_TILES") && atoi(getenv("GG_SYNC_TILES")) != 0;
+    dfree(e->d_srec);
+    dfree(e->d_sstate);
+    dfree(e->d_ibits);
+    if (e->cfg.enable_sync && e->n_hubs == 0 && e->nwp >= 2 && !e->sync_tiles && n_own) {
+        HIPCHK(hipMalloc(&e->d_srec, 2 * n_own * sizeof(uint4)));
+        HIPCHK(hipMalloc(&e->d_sstate, e->rows));
+        HIPCHK(hipMalloc(&e->d_ibits, e->rows / 8));
     }
     const size_t rowbytes = e->rows * e->nwp * 8;
     e->tile_nodes = gg::kBlock / lanes_per_node((uint32_t)e->nwp);

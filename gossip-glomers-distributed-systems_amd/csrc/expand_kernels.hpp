@@ -147,6 +147,9 @@ struct RoundArgs {
     uint64_t* hscratch;              // [n_hchunks][2][nwp] (union, first-claimer-recip) per chunk
     const struct HubChunk* mchunks;  // out-edge chunks of high out-degree senders
     uint64_t n_mchunks;
+    uint4* srec;                // [2 n_own] sync records (streamed sync rounds), or nullptr
+    uint8_t* sstate;            // [rows] sender state of round r (round_prep; streamed sync rounds)
+    uint64_t* ibits;            // [rows/64] bit: sstate non-zero (a cache-resident filter for it)
     const uint64_t* fired_m1;   // sync-fired bitmaps of rounds r-1, r-2, r-3
     const uint64_t* fired_m2;
     const uint64_t* fired_m3;
@@ -368,6 +371,7 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
         const bool valid = i < a.n_own;
         const uint64_t rep = a.own0 + i;
         bool fire = false;
+        uint8_t st = 0;  // sender state (SYNCW, streamed sync rounds)
         if (valid) {
             int64_t o0 = 0, o1 = 0;
             bool fm1 = false, fm2 = false, fm3 = false;
@@ -375,6 +379,10 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                 fm1 = bit_at(a.fired_m1, rep);
                 fm2 = bit_at(a.fired_m2, rep);
                 fm3 = bit_at(a.fired_m3, rep);
+                if (a.sstate) {  // sender state for sync_records / expand_stream_sync
+                    st = (uint8_t)((a.flg_prev[rep] & (FL_ACT | FL_LAG)) | (fm2 ? SE_FM2 : 0) | (fm3 ? SE_FM3 : 0));
+                    a.sstate[rep] = st;
+                }
             }
             if (!dense) {
                 const uint8_t f = a.flg_prev[rep];
@@ -446,6 +454,26 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
         if constexpr (SYNCW) {  // before the first timer every fired word is still zero
             const unsigned long long word = __ballot(fire);
             if ((threadIdx.x & 63) == 0) a.fired_cur[(a.own0 + (i & ~63ull)) >> 6] = word;
+            if (a.ibits) {
+                const unsigned long long iw = __ballot(st != 0);
+                if ((threadIdx.x & 63) == 0) a.ibits[(a.own0 + (i & ~63ull)) >> 6] = iw;
+            }
+        }
+    }
+    if constexpr (SYNCW) {  // sender states of the ghost rows
+        if (a.sstate) {  // whole waves over 64 consecutive ghost rows (ghost0 % 64 == 0)
+            const uint64_t gw = (a.n_ghost + 63) / 64 * 64;
+            for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < gw; g += stride) {
+                const uint64_t row = a.ghost0 + g;
+                uint8_t st = 0;
+                if (g < a.n_ghost) {
+                    st = (uint8_t)((a.flg_prev[row] & (FL_ACT | FL_LAG)) | (bit_at(a.fired_m2, row) ? SE_FM2 : 0) |
+                                   (bit_at(a.fired_m3, row) ? SE_FM3 : 0));
+                    a.sstate[row] = st;
+                }
+                const unsigned long long iw = __ballot(st != 0);
+                if ((threadIdx.x & 63) == 0) a.ibits[row >> 6] = iw;
+            }
         }
     }
     // sharded: ghost senders (remote nodes, state from last round's exchange)
@@ -1405,6 +1433,343 @@ void expand_stream1(RoundArgs a) {
     acc[C_FWD_DELIV] = c_fwd;
     acc[C_HASH] = c_hash;
     acc[C_NEXT_ACKS] = c_fwd;
+    acc[C_ACTIVE] = c_active;
+    acc[C_GATHERS] = c_gathers;
+    acc[C_NACT] = c_nact;
+    acc[C_BYTES] = c_bytes;
+    flush_counters(a, acc, s_red, t_start, K_STREAM);
+}
+
+// ---------------------------------------------------------------------------
+// Sync rounds, streamed (no partition masks, no in-hubs, nwp >= 2). After the
+// timers start most senders are idle and a few push their whole set
+// (SyncBroadcast callback, `broadcast.go:98-110`), so gathering every sender's
+// F row the way expand_stream does would move mostly zero rows. Instead:
+//   round_prep         writes each node's sender-state byte sstate (FL_ACT,
+//                      FL_LAG of r-1, SE_FM2, SE_FM3): one lookup per edge below
+//                      instead of a flag byte and two bitmap words.
+//   sync_records       one thread per item (dense: every node; sparse: the node
+//                      list): walks the in-list once (sender states), and for a
+//                      callback node its out-list, and writes a 32-byte record:
+//                      the node's own bits, up to three contributing senders
+//                      (active last round, or pushing) with push/LAG bits, the
+//                      out-list offset and its peers' LAG mask. Clears the
+//                      candidate byte.
+//   expand_stream_sync G lanes per node, records one item ahead: the own row,
+//                      the recorded senders' rows and the first callback peers'
+//                      columns are in flight together; nodes with more
+//                      contributing senders walk their in-list, callback nodes
+//                      their out-list, in batches.
+// A node's whole set is base | F_prev, and base alone unless it is LAG (F rows
+// are zero for idle nodes, and folded into base unless LAG); nodes whose sets
+// are pushed or read keep base this round.
+constexpr uint32_t SR_DEG = 0x000fffffu;       // forward recipients (out-degree)
+constexpr int SR_NC = 20;                      // bits 20-21: recorded contributing senders
+constexpr uint32_t SR_SLOW = 1u << 22;         // more than 3 of them (or a huge degree): walk the in-list
+constexpr uint32_t SR_KEEP = 1u << 26;         // the node's set is read this round: base stays
+constexpr uint32_t SR_CB = 1u << 27;           // sync callback (fired in r-2)
+constexpr uint32_t SR_LAG = 1u << 28;          // base lacks F_prev
+constexpr uint32_t SR_STALE = 1u << 29;        // F row of round r-2 in this round's F buffer
+constexpr uint32_t SR_INJ = 1u << 30;          // client broadcasts this round
+// second word: .x/.y out_ptr[i] (callback), .z peers' LAG mask (first 32 peers),
+// .w bits 0-2: recorded sender j pushes, bits 3-5: recorded sender j is LAG
+
+__global__ __launch_bounds__(kBlock) void sync_records(RoundArgs a) {
+    __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
+    const unsigned long long t_start = clock100();
+    const bool dense = dense_round(a);
+    const uint32_t n_items = dense ? (uint32_t)a.n_own : a.n_work[1];
+    unsigned long long c_bytes = 0;
+    constexpr int B = 8;
+    for (uint32_t k = blockIdx.x * kBlock + threadIdx.x; k < n_items; k += gridDim.x * kBlock) {
+        const uint32_t i = dense ? k : a.nodes[k];
+        const uint64_t rep = a.own0 + i;
+        const uint8_t ca = a.cand[rep];
+        const uint8_t fo = a.flg_cur[rep];
+        const uint8_t st = a.sstate[rep];
+        const int64_t p0 = a.in_ptr[i], p1 = a.in_ptr[i + 1];
+        const int64_t o0 = a.out_ptr[i], o1 = a.out_ptr[i + 1];
+        const uint64_t dout = (uint64_t)(o1 - o0);
+        if (ca) a.cand[rep] = 0;
+        bool keep = (st & SE_FM3) != 0;
+        uint32_t nc = 0, sbits = 0, col0 = 0, col1 = 0, col2 = 0;
+        for (int64_t e0 = p0; e0 < p1; e0 += B) {
+            uint32_t cb[B];
+            uint8_t f[B];
+#pragma unroll
+            for (int b = 0; b < B; ++b) cb[b] = e0 + b < p1 ? a.in_col[e0 + b] : 0u;
+#pragma unroll
+            for (int b = 0; b < B; ++b) f[b] = e0 + b < p1 ? (uint8_t)bit_at(a.ibits, cb[b] & kColMask) : (uint8_t)0;
+#pragma unroll
+            for (int b = 0; b < B; ++b) f[b] = f[b] ? a.sstate[cb[b] & kColMask] : (uint8_t)0;
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                keep |= (f[b] & SE_FM2) != 0;
+                if (f[b] & (FL_ACT | SE_FM3)) {
+                    if (nc == 0) col0 = cb[b];
+                    else if (nc == 1) col1 = cb[b];
+                    else if (nc == 2) col2 = cb[b];
+                    if (nc < 3)
+                        sbits |= ((f[b] & SE_FM3) ? 1u << nc : 0u) | ((f[b] & FL_LAG) ? 8u << nc : 0u);
+                    ++nc;
+                }
+            }
+        }
+        uint32_t lagm = 0;
+        if (st & SE_FM2) {  // callback: which peers' base rows lag their F rows
+            const int64_t oe = o1 < o0 + 32 ? o1 : o0 + 32;
+            for (int64_t e0 = o0; e0 < oe; e0 += B) {
+                uint8_t f[B];
+#pragma unroll
+                for (int b = 0; b < B; ++b) {
+                    const uint64_t w = e0 + b < oe ? (uint64_t)(a.out_col[e0 + b] & kColMask) : 0ull;
+                    f[b] = (e0 + b < oe && bit_at(a.ibits, w)) ? a.sstate[w] : (uint8_t)0;
+                }
+#pragma unroll
+                for (int b = 0; b < B; ++b) lagm |= (f[b] & FL_LAG) ? 1u << (e0 - o0 + b) : 0u;
+            }
+            c_bytes += 5ull * (uint64_t)(oe - o0);
+        }
+        uint32_t x = (uint32_t)(dout < SR_DEG ? dout : SR_DEG);
+        if (nc > 3 || dout >= SR_DEG) x |= SR_SLOW;
+        else x |= nc << SR_NC;
+        if (keep) x |= SR_KEEP;
+        if (st & SE_FM2) x |= SR_CB;
+        if (st & FL_LAG) x |= SR_LAG;
+        if (fo & FL_ACT) x |= SR_STALE;
+        if (ca & CA_INJ) x |= SR_INJ;
+        a.srec[2 * (uint64_t)i] = make_uint4(x, col0, col1, col2);
+        a.srec[2 * (uint64_t)i + 1] = make_uint4((uint32_t)o0, (uint32_t)((uint64_t)o0 >> 32), lagm, sbits);
+        // row_ptr, out_ptr, own bytes, per in-edge: column + sender state; the record
+        c_bytes += 32 + 3 + (ca ? 1 : 0) + 5ull * (uint64_t)(p1 - p0) + 32;
+    }
+    unsigned long long acc[C_NUM];
+#pragma unroll
+    for (int q = 0; q < C_NUM; ++q) acc[q] = 0;
+    acc[C_BYTES] = c_bytes;
+    flush_counters(a, acc, s_red, t_start, K_PREP);
+}
+
+template <int G>
+__global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
+    constexpr int WPL = 2;
+    constexpr int kCb = 4;  // callback peers / in-list senders per batch
+    __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
+    const unsigned long long t_start = clock100();
+    const bool dense = dense_round(a);
+    const uint32_t n_items = dense ? (uint32_t)a.n_own : a.n_work[1];
+    uint32_t c_new = 0, c_active = 0, c_gathers = 0, c_nact = 0;
+    unsigned long long c_fwd = 0, c_push = 0, c_hash = 0, c_bytes = 0;
+    const int lg = threadIdx.x % G;
+    const uint32_t off = (uint32_t)lg * WPL;
+    const int gshift = (threadIdx.x & 63) / G * G;
+    const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+    const uint32_t stride = gridDim.x * (kBlock / G);
+    const unsigned long long rowb = 8ull * a.nwp;
+    constexpr uint32_t kNone = ~0u;
+    auto node_of = [&](uint32_t k) -> uint32_t {
+        return k < n_items ? (dense ? k : a.nodes[k]) : kNone;
+    };
+    auto zero = []() {
+        Row<WPL> z;
+        z.w[0] = z.w[1] = 0;
+        return z;
+    };
+    auto row_at = [&](const uint64_t* arr, uint64_t u) { return load_row<WPL>(arr + u * a.nwp + off); };
+
+    uint32_t k = blockIdx.x * (kBlock / G) + threadIdx.x / G;
+    uint32_t n0 = node_of(k), n1 = node_of(k + stride);
+    uint4 r0 = make_uint4(0, 0, 0, 0), q0 = r0;
+    if (n0 < a.n_own) {
+        r0 = a.srec[2 * (uint64_t)n0];
+        q0 = a.srec[2 * (uint64_t)n0 + 1];
+    }
+    for (; k < n_items; k += stride) {
+        const uint64_t i = n0;
+        const uint64_t rep = a.own0 + i;
+        const uint32_t x = r0.x;
+        const bool lag = (x & SR_LAG) != 0, slow = (x & SR_SLOW) != 0, cbk = (x & SR_CB) != 0;
+        const uint32_t nc = slow ? 0u : (x >> SR_NC) & 3u;
+        const uint32_t sb = q0.w;
+        const int64_t o0 = (int64_t)(((uint64_t)q0.y << 32) | q0.x);
+        uint64_t dout = x & SR_DEG;
+        if (dout == SR_DEG) dout = (uint64_t)(a.out_ptr[i + 1] - a.out_ptr[i]);
+        // own row (+ its F row when base lags), the recorded senders' rows (F,
+        // or base for pushes, + F when that base lags), the first callback
+        // peers' columns: one round trip
+        Row<WPL> sp = row_at(a.base, rep);
+        const Row<WPL> of = lag ? row_at(a.F_prev, rep) : zero();
+        const uint32_t cs[3] = {r0.y, r0.z, r0.w};
+        Row<WPL> fr[3], br[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint64_t u = cs[j] & kColMask;
+            const bool v = (uint32_t)j < nc, push = (sb >> j) & 1u, slag = (sb >> (3 + j)) & 1u;
+            fr[j] = (v && (!push || slag)) ? row_at(a.F_prev, u) : zero();
+            br[j] = (v && push) ? row_at(a.base, u) : zero();
+        }
+        uint64_t pw[kCb];
+#pragma unroll
+        for (int b = 0; b < kCb; ++b)
+            pw[b] = (cbk && (uint64_t)b < dout) ? (uint64_t)(a.out_col[o0 + b] & kColMask) : 0ull;
+        // next item's record, the item after's list entry
+        const uint32_t n2 = node_of(k + 2 * stride);
+        uint4 r1 = make_uint4(0, 0, 0, 0), q1 = r1;
+        if (n1 < a.n_own) {
+            r1 = a.srec[2 * (uint64_t)n1];
+            q1 = a.srec[2 * (uint64_t)n1 + 1];
+        }
+
+        sp.w[0] |= of.w[0];
+        sp.w[1] |= of.w[1];
+        Row<WPL> S = sp;
+        if (x & SR_INJ) {  // (1) client broadcasts of this round
+            uint32_t lo = 0, hi = a.n_inj;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (a.inj[2 * mid] < (uint32_t)i) lo = mid + 1;
+                else hi = mid;
+            }
+            for (uint32_t q = lo; q < a.n_inj && a.inj[2 * q] == (uint32_t)i; ++q) {
+                const uint32_t lane = a.inj[2 * q + 1];
+                const uint32_t word = lane >> 6;
+                if (word / WPL == (uint32_t)lg) set_lane_bit<WPL>(S, word % WPL, lane & 63);
+            }
+        }
+        // (2) node broadcasts and pushes, ascending sender: first deliverer claims
+        unsigned long long cl_recip = 0;
+        auto claim = [&](const Row<WPL>& src, uint32_t c) {
+            const uint64_t w0 = src.w[0] & ~S.w[0], w1 = src.w[1] & ~S.w[1];
+            S.w[0] |= w0;
+            S.w[1] |= w1;
+            if (c & kRecipBit) cl_recip += __popcll(w0) + __popcll(w1);
+        };
+        unsigned long long nrows = 1 + (lag ? 1 : 0), nextra = 32;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            if ((uint32_t)j < nc) {
+                Row<WPL> r = fr[j];
+                r.w[0] |= br[j].w[0];
+                r.w[1] |= br[j].w[1];
+                claim(r, cs[j]);
+                const bool push = (sb >> j) & 1u, slag = (sb >> (3 + j)) & 1u;
+                nrows += (push ? 1 : 0) + ((!push || slag) ? 1 : 0);
+            }
+        }
+        if (slow) {  // walk the in-list: sender states, then the contributing rows
+            const int64_t p0 = a.in_ptr[i], p1 = a.in_ptr[i + 1];
+            nextra += 16 + 5ull * (uint64_t)(p1 - p0);
+            for (int64_t e0 = p0; e0 < p1; e0 += kCb) {
+                uint32_t cb[kCb];
+                uint8_t f[kCb];
+                Row<WPL> r[kCb];
+#pragma unroll
+                for (int b = 0; b < kCb; ++b) cb[b] = e0 + b < p1 ? a.in_col[e0 + b] : 0u;
+#pragma unroll
+                for (int b = 0; b < kCb; ++b) f[b] = e0 + b < p1 ? a.sstate[cb[b] & kColMask] : (uint8_t)0;
+#pragma unroll
+                for (int b = 0; b < kCb; ++b) {
+                    const uint64_t u = cb[b] & kColMask;
+                    const bool push = f[b] & SE_FM3, con = f[b] & (FL_ACT | SE_FM3), slag = f[b] & FL_LAG;
+                    const Row<WPL> fb = (con && (!push || slag)) ? row_at(a.F_prev, u) : zero();
+                    r[b] = push ? row_at(a.base, u) : zero();
+                    r[b].w[0] |= fb.w[0];
+                    r[b].w[1] |= fb.w[1];
+                    nrows += (push ? 1 : 0) + ((con && (!push || slag)) ? 1 : 0);
+                    c_gathers += (lg == 0 && con) ? 1u : 0u;
+                }
+#pragma unroll
+                for (int b = 0; b < kCb; ++b)
+                    if (f[b] & (FL_ACT | SE_FM3)) claim(r[b], cb[b]);
+            }
+        }
+        // (3) sync callback: v fired in r-2; read_oks of its peers, ascending peer
+        unsigned long long cb_new = 0, push_sent = 0;
+        if (cbk) {
+            const uint32_t lagm = q0.z;
+            nextra += 16 + 4 * dout;
+            for (uint64_t e0 = 0; e0 < dout; e0 += kCb) {
+                Row<WPL> R[kCb];
+#pragma unroll
+                for (int b = 0; b < kCb; ++b) {
+                    const uint64_t e = e0 + b;
+                    const bool slag = e >= 32 || ((lagm >> e) & 1u);
+                    R[b] = e < dout ? row_at(a.base, pw[b]) : zero();
+                    const Row<WPL> f = (e < dout && slag) ? row_at(a.F_prev, pw[b]) : zero();
+                    R[b].w[0] |= f.w[0];
+                    R[b].w[1] |= f.w[1];
+                    nrows += e < dout ? (slag ? 2 : 1) : 0;
+                }
+                // columns of the next batch, in flight with these rows
+#pragma unroll
+                for (int b = 0; b < kCb; ++b) {
+                    const uint64_t e = e0 + kCb + b;
+                    pw[b] = e < dout ? (uint64_t)(a.out_col[o0 + e] & kColMask) : 0ull;
+                }
+#pragma unroll
+                for (int b = 0; b < kCb; ++b) {
+                    if (e0 + b >= dout) continue;
+                    unsigned long long pn = 0, pp = 0;
+#pragma unroll
+                    for (int q = 0; q < WPL; ++q) {
+                        pn += __popcll(R[b].w[q] & ~S.w[q]);
+                        pp += __popcll(S.w[q] & ~R[b].w[q]);
+                        S.w[q] |= R[b].w[q];
+                    }
+                    cb_new += pn;
+                    push_sent += pp;
+                }
+            }
+        }
+        // new state (as expand_round)
+        Row<WPL> F;
+        uint32_t T = 0;
+        const uint64_t g = gid_of(a, i);
+#pragma unroll
+        for (int w = 0; w < WPL; ++w) {
+            F.w[w] = S.w[w] & ~sp.w[w];
+            T += __popcll(F.w[w]);
+            if (F.w[w]) {
+                const uint64_t idx = g * a.nw + off + w;
+                c_hash += gg_word_hash(idx, S.w[w]) - (sp.w[w] ? gg_word_hash(idx, sp.w[w]) : 0ull);
+            }
+        }
+        const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
+        const bool zm = (x & SR_STALE) != 0, keep = (x & SR_KEEP) != 0;
+        if (any || zm) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
+        nrows += (any || zm) ? 1 : 0;
+        if (keep) {
+            if (lag) store_row<WPL>(a.base + rep * a.nwp + off, sp);
+            nrows += lag ? 1 : 0;
+        } else if (any || lag) {
+            store_row<WPL>(a.base + rep * a.nwp + off, S);
+            nrows++;
+        }
+        if (lg == 0 && (any || zm)) a.flg_cur[rep] = any ? (uint8_t)(FL_ACT | (keep ? FL_LAG : 0)) : (uint8_t)0;
+        c_new += T;
+        c_fwd += dout * (unsigned long long)T - cl_recip - cb_new;
+        c_push += push_sent;
+        if (lg == 0) {
+            c_active += 1;
+            c_gathers += nc;
+            c_nact += any ? 1u : 0u;
+            c_bytes += nrows * rowb + nextra + ((any || zm) ? 1 : 0);
+        }
+        n0 = n1;
+        n1 = n2;
+        r0 = r1;
+        q0 = q1;
+    }
+    unsigned long long acc[C_NUM];
+#pragma unroll
+    for (int q = 0; q < C_NUM; ++q) acc[q] = 0;
+    acc[C_NEW] = c_new;
+    acc[C_FWD_SENT] = c_fwd;
+    acc[C_FWD_DELIV] = c_fwd;
+    acc[C_PUSH] = c_push;
+    acc[C_PUSH_DELIV] = c_push;
+    acc[C_HASH] = c_hash;
+    acc[C_NEXT_ACKS] = c_fwd + c_push;
     acc[C_ACTIVE] = c_active;
     acc[C_GATHERS] = c_gathers;
     acc[C_NACT] = c_nact;

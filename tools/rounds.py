@@ -18,7 +18,7 @@ wl.apply(e)
 rounds = int(os.environ.get("ROUNDS", "40"))
 for rep in range(2):
     e.reset()
-    wl.apply_events(e)
+    inject(e, wl.injections)  # reset keeps topology and partition windows
     st = e.step(rounds)
 tot = 0.0
 print(f"{name}: V={wl.topo.n_nodes} E={wl.topo.nnz} W={wl.n_lanes}")
@@ -26,5 +26,5 @@ for s in st:
     tot += s["kernel_ms"]
     print(f'r{s["round"]:3d} ms={s["kernel_ms"]:.4f} p/e/s={s["prep_ms"]:.4f}/{s["expand_ms"]:.4f}/{s["stream_ms"]:.4f} '
           f'new={s["new_bits"]:>11d} active={s["work_rows"]:>9d} '
-          f'gathers={s["work_gathers"]:>9d} fired={s["syncs_fired"]:>7d} sbytes={s["stream_bytes"]/1e6:.1f}MB')
+          f'gathers={s["work_gathers"]:>9d} fired={s["syncs_fired"]:>7d} sbytes={s["stream_bytes"]/1e6:.1f}MB ebytes={s["expand_bytes"]/1e6:.1f}MB')
 print(f"total kernel ms {tot:.3f}")
