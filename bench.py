@@ -8,7 +8,7 @@ timers on, no partitions; the episode is reset -> inject -> lockstep rounds
 until the round after the last delivery (quiescence, fixed during warmup).
 `value` = all (node,msg) deliveries of the timed episodes on all ranks / the
 max-over-ranks wall time. On N GPUs the tree has N * 2^20 nodes, vertex-range
-sharded, with one RCCL all-gather of frontier slices per round ("scaling":
+sharded (locality order), with one RCCL all-to-all of ghost payloads per round ("scaling":
 "weak").
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]

@@ -88,6 +88,47 @@ struct BatchKey {
 
 }  // namespace
 
+// message value -> lane: open addressing over 2x the lane count; clear() is
+// O(1) (an epoch bump), so reset + re-inject of a benchmark episode costs no
+// allocation.
+struct LaneTable {
+    std::vector<int64_t> key;
+    std::vector<uint32_t> val, epoch_of;
+    uint32_t epoch = 1;
+    uint64_t mask = 0;
+    void init(uint64_t lanes) {
+        uint64_t cap = 16;
+        while (cap < 2 * lanes) cap <<= 1;
+        key.assign(cap, 0);
+        val.assign(cap, 0);
+        epoch_of.assign(cap, 0);
+        mask = cap - 1;
+        epoch = 1;
+    }
+    uint64_t slot(int64_t k) const {
+        uint64_t h = gg_mix64((uint64_t)k) & mask;
+        while (epoch_of[h] == epoch && key[h] != k) h = (h + 1) & mask;
+        return h;
+    }
+    uint32_t find(int64_t k) const {  // ~0u: absent
+        if (!mask) return ~0u;
+        const uint64_t h = slot(k);
+        return epoch_of[h] == epoch ? val[h] : ~0u;
+    }
+    void insert(int64_t k, uint32_t v) {  // k absent; at most `lanes` keys live
+        const uint64_t h = slot(k);
+        key[h] = k;
+        val[h] = v;
+        epoch_of[h] = epoch;
+    }
+    void clear() {
+        if (++epoch == 0) {
+            std::fill(epoch_of.begin(), epoch_of.end(), 0u);
+            epoch = 1;
+        }
+    }
+};
+
 struct gg_engine {
     gg_config cfg{};
     std::string err;
@@ -154,9 +195,11 @@ struct gg_engine {
     uint32_t* h_inj = nullptr;  // pinned
     size_t inj_cap = 0;         // pairs
     std::vector<hipEvent_t> ev;  // 2 per batched round
+    hipEvent_t inj_ev = nullptr;   // after the last copy out of h_inj (gg_step reuses h_inj)
+    bool inj_ev_live = false;
 
     std::vector<Window> windows;
-    std::unordered_map<int64_t, uint32_t> lanes;
+    LaneTable lanes;                 // message value -> lane
     std::vector<int64_t> lane_value;
     std::map<int64_t, std::vector<Injection>> inj;
     int64_t round = 0;
@@ -243,6 +286,7 @@ gg_engine::~gg_engine() {
     if (h_counters) (void)hipHostFree(h_counters);
     if (h_inj) (void)hipHostFree(h_inj);
     for (auto& x : ev) (void)hipEventDestroy(x);
+    if (inj_ev) (void)hipEventDestroy(inj_ev);
     if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -253,30 +297,40 @@ namespace {
 // Back to round 0, asynchronously: every call that reads results waits on the stream.
 int reset_device_state(gg_engine* e) {
     const size_t rowbytes = e->rows * e->nwp * 8;
-    HIPCHK(hipMemsetAsync(e->d_base, 0, rowbytes, e->stream));
+    // one launch clears every per-episode array (sizes are multiples of 8
+    // bytes: rows is a multiple of 64) and starts the sync timers
+    gg::ResetArgs ra{};
+    auto seg = [&](void* p, uint64_t bytes, uint64_t val) {
+        ra.seg[ra.n_seg++] = {reinterpret_cast<uint64_t*>(p), bytes / 8, val};
+    };
+    seg(e->d_base, rowbytes, 0);
     // F rows and flags are already all zero after two rounds without new bits
     // (a stale row is cleared in the round it expires), e.g. after an episode
     // run to quiescence. Single engine only: ghost rows follow remote rounds.
     if (!(e->world == 1 && e->quiet >= 2)) {
         for (int b = 0; b < 2; ++b) {
-            HIPCHK(hipMemsetAsync(e->d_F[b], 0, rowbytes, e->stream));  // F rows are zero unless ACT
-            HIPCHK(hipMemsetAsync(e->d_flg[b], 0, e->rows, e->stream));
+            seg(e->d_F[b], rowbytes, 0);  // F rows are zero unless ACT
+            seg(e->d_flg[b], e->rows, 0);
         }
     }
     e->quiet = 2;
-    for (int b = 0; b < 4; ++b) HIPCHK(hipMemsetAsync(e->d_fired[b], 0, e->rows / 8, e->stream));
-    HIPCHK(hipMemsetAsync(e->d_cand, 0, e->rows, e->stream));
-    HIPCHK(hipMemsetAsync(e->d_zmark, 0, e->rows, e->stream));
-    HIPCHK(hipMemsetAsync(e->d_tile_cand, 0, e->tile_bytes, e->stream));
-    HIPCHK(hipMemsetAsync(e->d_act, 0, 4 * sizeof(uint32_t), e->stream));
+    for (int b = 0; b < 4; ++b) seg(e->d_fired[b], e->rows / 8, 0);
+    seg(e->d_cand, e->rows, 0);
+    seg(e->d_zmark, e->rows, 0);
+    seg(e->d_tile_cand, e->tile_bytes, 0);
+    seg(e->d_act, 16, 0);
     const uint64_t n_own = e->n_own;
-    if (n_own) {
-        hipLaunchKernelGGL(gg::sync_init, dim3((unsigned)((n_own + 255) / 256)), dim3(256), 0, e->stream,
-                           e->d_sync_next, e->d_sync_k, n_own, e->d_gid, e->cfg.seed,
-                           e->cfg.sync_base_ticks, e->cfg.sync_jitter_ticks);
-        HIPCHK(hipGetLastError());
-    }
-    if (e->d_dr) HIPCHK(hipMemsetAsync(e->d_dr, 0xff, n_own * e->cfg.n_lanes * 4, e->stream));
+    if (e->d_dr) seg(e->d_dr, n_own * e->cfg.n_lanes * 4, ~0ull);
+    ra.sync_next = e->d_sync_next;
+    ra.sync_k = e->d_sync_k;
+    ra.n_own = n_own;
+    ra.gid = e->d_gid;
+    ra.seed = e->cfg.seed;
+    ra.sync_base = e->cfg.sync_base_ticks;
+    ra.sync_jitter = e->cfg.sync_jitter_ticks;
+    const uint64_t blocks = std::min<uint64_t>(std::max<uint64_t>(1, rowbytes / 16384), 4096);
+    hipLaunchKernelGGL(gg::reset_state, dim3((unsigned)blocks), dim3(gg::kBlock), 0, e->stream, ra);
+    HIPCHK(hipGetLastError());
     return GG_OK;
 }
 
@@ -591,11 +645,12 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
 
 // Host-side stats of one round from its 64 counter slots; per-kind times from
 // the device clock stamps (first block start .. last block end, 100 MHz).
-void fold_stats(gg_engine* e, const unsigned long long* slots, int64_t round, gg_round_stats* s) {
+// slots: nslots x kCounters (kSlots raw slots, or 1 slot folded by gg::fold_slots)
+void fold_stats(gg_engine* e, const unsigned long long* slots, int64_t round, gg_round_stats* s, int nslots = gg::kSlots) {
     unsigned long long c[gg::kCounters] = {0};
     unsigned long long t0[gg::K_NKIND], t1[gg::K_NKIND];
     for (int q = 0; q < gg::K_NKIND; ++q) t0[q] = ~0ull, t1[q] = 0;
-    for (int k = 0; k < gg::kSlots; ++k) {
+    for (int k = 0; k < nslots; ++k) {
         for (int j = 0; j < gg::kCounters; ++j) c[j] += slots[k * gg::kCounters + j];
         for (int q = 0; q < gg::K_NKIND; ++q) {
             const unsigned long long si = slots[k * gg::kCounters + gg::kStamp0 + 2 * q];
@@ -698,7 +753,12 @@ size_t pack_injections(gg_engine* e, int64_t r0, uint32_t n, std::vector<size_t>
 template <class F>
 int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& off, size_t total, F&& enqueue) {
     static const bool no_graph = getenv("GG_NO_GRAPH") != nullptr;
-    if (total) HIPCHK(hipMemcpyAsync(e->d_inj, e->h_inj, total * 8, hipMemcpyHostToDevice, e->stream));
+    if (total) {
+        HIPCHK(hipMemcpyAsync(e->d_inj, e->h_inj, total * 8, hipMemcpyHostToDevice, e->stream));
+        if (!e->inj_ev) HIPCHK(hipEventCreateWithFlags(&e->inj_ev, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(e->inj_ev, e->stream));
+        e->inj_ev_live = true;
+    }
     if (no_graph || m < 4 || e->graph_broken) {
         HIPCHK(hipEventRecord(e->ev[0], e->stream));
         int rc = enqueue();
@@ -862,6 +922,7 @@ int gg_create(const gg_config* cfg, gg_engine** out) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GG_EIO;
     auto* e = new gg_engine();
     e->cfg = *cfg;
+    e->lanes.init(cfg->n_lanes);
     e->V = cfg->n_nodes;
     e->nw = cfg->n_lanes / 64;
     e->nwp = next_pow2((uint32_t)e->nw);
@@ -875,7 +936,7 @@ int gg_create(const gg_config* cfg, gg_engine** out) {
         return GG_EIO;
     }
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&e->d_counters, (size_t)kMaxBatch * gg::kSlots * gg::kCounters * 8) != hipSuccess ||
+        hipMalloc(&e->d_counters, (size_t)kMaxBatch * (gg::kSlots + 1) * gg::kCounters * 8) != hipSuccess ||
         hipHostMalloc(&e->h_counters, (size_t)kMaxBatch * gg::kSlots * gg::kCounters * 8) != hipSuccess) {
         delete e;
         return GG_EIO;
@@ -1203,29 +1264,41 @@ int gg_partition_groups(gg_engine* e, int64_t a, int64_t b, const uint8_t* group
     return add_window(e, a, b, std::move(w));
 }
 
-int gg_broadcast(gg_engine* e, uint32_t node, int64_t message, int64_t round) {
-    if (!e) return GG_EINVAL;
+// One client broadcast into the round's list `dst` (e->inj[round]).
+static int add_broadcast(gg_engine* e, uint32_t node, int64_t message, int64_t round,
+                         std::vector<Injection>& dst) {
     if (node >= e->V) return e->fail(GG_EINVAL, "node out of range");
     if (round < e->round) return e->fail(GG_EINVAL, "broadcast scheduled in the past");
-    auto it = e->lanes.find(message);
-    uint32_t lane;
-    if (it == e->lanes.end()) {
+    uint32_t lane = e->lanes.find(message);
+    if (lane == ~0u) {
         if (e->lane_value.size() >= e->cfg.n_lanes) return e->fail(GG_ENOSPC, "all message lanes in use");
         lane = (uint32_t)e->lane_value.size();
-        e->lanes.emplace(message, lane);
+        e->lanes.insert(message, lane);
         e->lane_value.push_back(message);
-    } else {
-        lane = it->second;
     }
-    e->inj[round].push_back({node, lane});
+    dst.push_back({node, lane});
     return GG_OK;
+}
+
+int gg_broadcast(gg_engine* e, uint32_t node, int64_t message, int64_t round) {
+    if (!e) return GG_EINVAL;
+    if (round < e->round) return e->fail(GG_EINVAL, "broadcast scheduled in the past");
+    return add_broadcast(e, node, message, round, e->inj[round]);
 }
 
 int gg_broadcast_many(gg_engine* e, const uint32_t* nodes, const int64_t* messages,
                       const int64_t* rounds, uint64_t n) {
     if (!e || (n && (!nodes || !messages || !rounds))) return GG_EINVAL;
+    std::vector<Injection>* dst = nullptr;
+    int64_t dst_round = 0;
     for (uint64_t k = 0; k < n; ++k) {
-        int rc = gg_broadcast(e, nodes[k], messages[k], rounds[k]);
+        if (rounds[k] < e->round) return e->fail(GG_EINVAL, "broadcast scheduled in the past");
+        if (!dst || rounds[k] != dst_round) {  // runs of one round: one map lookup
+            dst = &e->inj[rounds[k]];
+            dst_round = rounds[k];
+            if (dst->empty()) dst->reserve(n - k);
+        }
+        int rc = add_broadcast(e, nodes[k], messages[k], rounds[k], *dst);
         if (rc) return rc;
     }
     return GG_OK;
@@ -1233,8 +1306,8 @@ int gg_broadcast_many(gg_engine* e, const uint32_t* nodes, const int64_t* messag
 
 int gg_lane_of(const gg_engine* e, int64_t message) {
     if (!e) return GG_EINVAL;
-    auto it = e->lanes.find(message);
-    return it == e->lanes.end() ? GG_EINVAL : (int)it->second;
+    const uint32_t lane = e->lanes.find(message);
+    return lane == ~0u ? GG_EINVAL : (int)lane;
 }
 
 int64_t gg_current_round(const gg_engine* e) { return e ? e->round : -1; }
@@ -1253,10 +1326,12 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
         const uint32_t m = std::min<uint32_t>(kMaxBatch, n - done);
         const int64_t r0 = e->round;
         if ((rc = ensure_events(e, 2))) return rc;
-        HIPCHK(hipStreamSynchronize(e->stream));  // h_inj reuse
+        if (e->inj_ev_live) {  // h_inj reuse: only the copy out of it must be done (not e.g. a reset)
+            HIPCHK(hipEventSynchronize(e->inj_ev));
+            e->inj_ev_live = false;
+        }
         const size_t total = pack_injections(e, r0, m, off);
         if (total == (size_t)-1) return GG_EIO;
-        if (total) HIPCHK(hipMemcpyAsync(e->d_inj, e->h_inj, total * 8, hipMemcpyHostToDevice, e->stream));
         const int64_t save_round = e->round;
         auto enqueue_batch = [&]() -> int {
             HIPCHK(hipMemsetAsync(e->d_counters, 0, (size_t)m * gg::kSlots * gg::kCounters * 8, e->stream));
@@ -1267,8 +1342,12 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
                                         e->d_counters + (size_t)k * gg::kSlots * gg::kCounters);
                 if (rc2) return rc2;
             }
-            HIPCHK(hipMemcpyAsync(e->h_counters, e->d_counters, (size_t)m * gg::kSlots * gg::kCounters * 8,
-                                  hipMemcpyDeviceToHost, e->stream));
+            // fold the 64 slots of each round on the device: one 256-byte row per round to the host
+            unsigned long long* folded = e->d_counters + (size_t)kMaxBatch * gg::kSlots * gg::kCounters;
+            hipLaunchKernelGGL(gg::fold_slots, dim3(m), dim3(gg::kCounters), 0, e->stream, e->d_counters, folded);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipMemcpyAsync(e->h_counters, folded, (size_t)m * gg::kCounters * 8, hipMemcpyDeviceToHost,
+                                  e->stream));
             return GG_OK;
         };
         rc = run_batch(e, r0, m, off, total, enqueue_batch);
@@ -1277,7 +1356,7 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
         HIPCHK(hipStreamSynchronize(e->stream));
         for (uint32_t k = 0; k < m; ++k) {
             gg_round_stats s;
-            fold_stats(e, e->h_counters + (size_t)k * gg::kSlots * gg::kCounters, r0 + k, &s);
+            fold_stats(e, e->h_counters + (size_t)k * gg::kCounters, r0 + k, &s, 1);
             e->quiet = s.new_bits ? 0 : e->quiet + 1;
             if (out) out[done + k] = s;
             e->inj.erase(r0 + k);

@@ -2029,12 +2029,62 @@ __global__ void track_delivery(const uint64_t* F_cur, const uint8_t* flg_cur, in
     }
 }
 
-__global__ void sync_init(int32_t* sync_next, uint32_t* sync_k, uint64_t n_own, const uint32_t* gid,
-                          uint64_t seed, uint32_t base, uint32_t jitter) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_own) return;
-    sync_k[i] = 0;
-    sync_next[i] = (int32_t)gg_sync_interval(seed, gid ? (uint64_t)gid[i] : i, 0, base, jitter);
+// Sum a round's 64 counter slots into one (stamps: max, see kStamp0). One block
+// per round, one thread per counter.
+__global__ void fold_slots(const unsigned long long* ctr, unsigned long long* out) {
+    const int j = threadIdx.x;
+    const unsigned long long* c = ctr + (size_t)blockIdx.x * kSlots * kCounters;
+    const bool stampj = j >= kStamp0 && j < kStamp0 + 2 * K_NKIND;
+    unsigned long long v = 0;
+    for (int k = 0; k < kSlots; ++k) {
+        const unsigned long long x = c[k * kCounters + j];
+        v = stampj ? (x > v ? x : v) : v + x;
+    }
+    out[(size_t)blockIdx.x * kCounters + j] = v;
+}
+
+// Episode reset: fill up to kResetSegs arrays (8-byte words) and start the
+// sync timers, in one launch.
+constexpr int kResetSegs = 16;
+struct ResetSeg {
+    uint64_t* p;
+    uint64_t n;    // 8-byte words
+    uint64_t val;
+};
+struct ResetArgs {
+    ResetSeg seg[kResetSegs];
+    int n_seg;
+    int32_t* sync_next;
+    uint32_t* sync_k;
+    uint64_t n_own;
+    const uint32_t* gid;
+    uint64_t seed;
+    uint32_t sync_base, sync_jitter;
+};
+
+__global__ __launch_bounds__(kBlock) void reset_state(ResetArgs ra) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (int q = 0; q < ra.n_seg; ++q) {
+        const ResetSeg s = ra.seg[q];
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        const u64x2 v = {s.val, s.val};
+        // blocks own 16 KiB pieces (2048 words = 4 x kBlock 16-byte chunks): 4
+        // coalesced 16-byte stores per thread, streamed past the caches
+        constexpr uint64_t kPiece = 8 * kBlock;  // words
+        const uint64_t pieces = s.n / kPiece;
+        for (uint64_t b = blockIdx.x; b < pieces; b += gridDim.x) {
+            u64x2* p = reinterpret_cast<u64x2*>(s.p + b * kPiece) + threadIdx.x;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(v, p + k * kBlock);  // chunk < 4 * kBlock
+        }
+        for (uint64_t w = pieces * kPiece + t0; w < s.n; w += stride) s.p[w] = s.val;
+    }
+    for (uint64_t i = t0; i < ra.n_own; i += stride) {
+        ra.sync_k[i] = 0;
+        ra.sync_next[i] = (int32_t)gg_sync_interval(ra.seed, ra.gid ? (uint64_t)ra.gid[i] : i, 0, ra.sync_base,
+                                                    ra.sync_jitter);
+    }
 }
 
 // Seeded bisection groups of the local rows (padding rows: group 0, unused).
