@@ -155,6 +155,7 @@ struct gg_engine {
     std::vector<gg_round_stats> dist_done;     // folded, not yet flushed
     size_t inj_off = 0;                        // pinned injection ring offset (async rounds)
     uint32_t quiet = 0;                        // trailing rounds without new bits (gg_step)
+    int dirty_parity = 0;                      // gg_reset: parity of the round before the last one
 
     int64_t* d_in_ptr = nullptr;
     uint32_t* d_in_col = nullptr;
@@ -307,8 +308,11 @@ int reset_device_state(gg_engine* e) {
     // F rows and flags are already all zero after two rounds without new bits
     // (a stale row is cleared in the round it expires), e.g. after an episode
     // run to quiescence. Single engine only: ghost rows follow remote rounds.
+    // After exactly one quiet round r only the buffers of round r-1 (parity
+    // dirty_parity = (r+1) & 1, recorded by gg_reset) can hold non-zero rows.
     if (!(e->world == 1 && e->quiet >= 2)) {
         for (int b = 0; b < 2; ++b) {
+            if (e->world == 1 && e->quiet == 1 && b != e->dirty_parity) continue;
             seg(e->d_F[b], rowbytes, 0);  // F rows are zero unless ACT
             seg(e->d_flg[b], e->rows, 0);
         }
@@ -1629,6 +1633,7 @@ int gg_reset(gg_engine* e) {
     e->lanes.clear();
     e->lane_value.clear();
     e->inj.clear();
+    e->dirty_parity = (int)(e->round & 1);
     e->round = 0;
     e->pend_acks = e->pend_ackdrop = 0;
     e->hash_total = 0;

@@ -168,3 +168,33 @@ def test_launch_cache_replay_and_invalidation(hip_lib, cpu_lib):
         for n, v, r in inj2:
             eng.broadcast(n, v, r)
     assert not diff_stats(c.step(sc.rounds), g.step(sc.rounds))
+
+
+@pytest.mark.parametrize("shift", [0, 1])
+@pytest.mark.parametrize("extra_quiet", [-1, 0, 1, 2])
+def test_reset_after_quiet_rounds(hip_lib, cpu_lib, shift, extra_quiet):
+    """gg_reset clears only the F/flag buffers that can be dirty: none after two
+    quiet rounds, the round r-1 parity after exactly one (where bench episodes
+    end; `shift` moves that round's parity), both mid-propagation (-1). The
+    next episode must equal a fresh oracle run."""
+    topo = T.tree(4096, 4)
+    inj = [(n, v, shift) for n, v, _ in uniform_injections(4096, 256, 91)]
+    g = make_engine(hip_lib, Scenario(topo, 256, 40, inj, seed=92, enable_sync=False))
+    if extra_quiet < 0:
+        g.step(3)
+    else:
+        r = 0
+        while True:  # to the first quiet round after the injections
+            r += 1
+            if g.step(1)[0]["new_bits"] == 0 and r > shift + 1:
+                break
+        if extra_quiet:
+            g.step(extra_quiet)
+    g.reset()
+    c = make_engine(cpu_lib, Scenario(topo, 256, 30, [], seed=92, enable_sync=False))
+    for n, v, _ in uniform_injections(4096, 200, 93):
+        g.broadcast(n, v, 0)
+        c.broadcast(n, v, 0)
+    d = diff_stats(c.step(30), g.step(30))
+    assert not d, d[:5]
+    assert np.array_equal(c.read_bits(), g.read_bits())
