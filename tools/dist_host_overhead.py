@@ -34,7 +34,13 @@ def main():
     e.topology(topo)
     dev = torch.device("cuda", 0)
     R = 24
-    for mode in ("engine", "engine+views"):
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    a2a_send = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    a2a_recv = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    for mode in ("engine", "engine+views", "engine+views+a2a(world=1)"):
         host_us, dev_ms = [], []
         for ep in range(eps + 1):
             e.reset()
@@ -49,6 +55,8 @@ def main():
                     ext = torch.cuda.ExternalStream(x.stream, device=dev)
                     with torch.cuda.stream(ext):
                         recv.zero_()
+                        if mode.endswith("a2a(world=1)"):
+                            dist.all_to_all_single(a2a_recv, a2a_send, [4096], [4096])
                     del send
                 e.dist_round_end(wait=False)
             t1 = time.perf_counter()
@@ -62,6 +70,7 @@ def main():
               f"device {sum(dev_ms) / len(dev_ms):.3f} ms/episode ({R} rounds, "
               f"{sum(dev_ms) / len(dev_ms) / R * 1e3:.1f} us/round), wall {(t2 - t0) * 1e3:.2f} ms/episode",
               flush=True)
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

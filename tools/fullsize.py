@@ -77,7 +77,12 @@ def main():
 
     # host-side facts for the properties
     t2 = time.time()
-    lab = T.components(topo)
+    if wl.name == "C5":
+        # the side x side grid is a spanning connected subgraph: one component
+        # (skips a serial union-find over 6.4e9 entries at side 2^15)
+        lab = np.zeros(V, np.uint32)
+    else:
+        lab = T.components(topo)
     deg = np.diff(topo.row_ptr)
     comp_size = np.bincount(lab, minlength=V)
     comp_deg = np.bincount(lab, weights=deg.astype(np.float64), minlength=V)
