@@ -28,7 +28,9 @@
 #include <vector>
 
 #include "expand_kernels.hpp"
+#include "generate.h"
 #include "gossip.h"
+#include "gossip_gen.h"
 
 namespace {
 
@@ -953,6 +955,103 @@ void gg_destroy(gg_engine* e) { delete e; }
 
 const char* gg_last_error(const gg_engine* e) { return e ? e->err.c_str() : "null engine"; }
 
+// In-/out-degree above which a node takes the hub path (GG_HUB_DEG overrides).
+static uint32_t hub_threshold() {
+    if (const char* h = getenv("GG_HUB_DEG")) return (uint32_t)std::max(1, atoi(h));
+    return 512;
+}
+
+// Hubs, per-node state and the episode reset after the in-lists are on the
+// device. iptr/optr: host copies of the in-/out-list pointers (optr null:
+// symmetric, out-lists = in-lists); iptr null: the caller has checked that no
+// node's degree exceeds the hub threshold.
+static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* optr) {
+    const uint64_t n_own = e->n_own;
+    // hubs: in-degree > hub_deg (hub_chunks/hub_finish in lean rounds), senders
+    // with out-degree > hub_deg (hub_mark)
+    e->hub_deg = 0;
+    {
+        e->hub_deg = hub_threshold();
+        uint64_t per = 128ull * (gg::kBlock / lanes_per_node((uint32_t)e->nwp));  // senders per chunk
+        if (const char* h = getenv("GG_HUB_CHUNK")) per = (uint64_t)std::max(1, atoi(h));
+        std::vector<uint32_t> hubs, hub_c0;
+        std::vector<gg::HubChunk> hch, mch;
+        for (uint64_t i = 0; iptr && i < n_own; ++i) {
+            const int64_t din = iptr[i + 1] - iptr[i];
+            if (din > (int64_t)e->hub_deg) {
+                hubs.push_back((uint32_t)i);
+                hub_c0.push_back((uint32_t)hch.size());
+                for (int64_t x = iptr[i]; x < iptr[i + 1]; x += (int64_t)per)
+                    hch.push_back({(uint32_t)i, (uint32_t)std::min<int64_t>((int64_t)per, iptr[i + 1] - x), x});
+            }
+            const int64_t o0 = optr ? optr[i] : iptr[i], o1 = optr ? optr[i + 1] : iptr[i + 1];
+            if (o1 - o0 > (int64_t)e->hub_deg)
+                for (int64_t x = o0; x < o1; x += 1024)
+                    mch.push_back({(uint32_t)i, (uint32_t)std::min<int64_t>(1024, o1 - x), x});
+        }
+        hub_c0.push_back((uint32_t)hch.size());
+        e->n_hubs = hubs.size();
+        e->n_hchunks = hch.size();
+        e->n_mchunks = mch.size();
+        if (e->n_hubs) {
+            HIPCHK(hipMalloc(&e->d_hubs, hubs.size() * 4));
+            HIPCHK(hipMemcpy(e->d_hubs, hubs.data(), hubs.size() * 4, hipMemcpyHostToDevice));
+            HIPCHK(hipMalloc(&e->d_hub_c0, hub_c0.size() * 4));
+            HIPCHK(hipMemcpy(e->d_hub_c0, hub_c0.data(), hub_c0.size() * 4, hipMemcpyHostToDevice));
+            HIPCHK(hipMalloc(&e->d_hchunks, hch.size() * sizeof(gg::HubChunk)));
+            HIPCHK(hipMemcpy(e->d_hchunks, hch.data(), hch.size() * sizeof(gg::HubChunk), hipMemcpyHostToDevice));
+            HIPCHK(hipMalloc(&e->d_hscratch, hch.size() * 2 * e->nwp * 8));
+        }
+        if (e->n_mchunks) {
+            HIPCHK(hipMalloc(&e->d_mchunks, mch.size() * sizeof(gg::HubChunk)));
+            HIPCHK(hipMemcpy(e->d_mchunks, mch.data(), mch.size() * sizeof(gg::HubChunk), hipMemcpyHostToDevice));
+        }
+    }
+    // streamed sync rounds need no in-hubs and two words per lane
+    e->sync_tiles = getenv("GG_SYNC_TILES") && atoi(getenv("GG_SYNC_TILES")) != 0;
+    dfree(e->d_srec);
+    dfree(e->d_sstate);
+    dfree(e->d_ibits);
+    if (e->cfg.enable_sync && e->n_hubs == 0 && e->nwp >= 2 && !e->sync_tiles && n_own) {
+        HIPCHK(hipMalloc(&e->d_srec, 2 * n_own * sizeof(uint4)));
+        HIPCHK(hipMalloc(&e->d_sstate, e->rows));
+        HIPCHK(hipMalloc(&e->d_ibits, e->rows / 8));
+    }
+    const size_t rowbytes = e->rows * e->nwp * 8;
+    e->tile_nodes = gg::kBlock / lanes_per_node((uint32_t)e->nwp);
+    const uint64_t ntiles = (n_own + e->tile_nodes - 1) / e->tile_nodes;
+    e->tile_bytes = (ntiles + 8) / 8 * 8;
+    HIPCHK(hipMalloc(&e->d_cand, e->rows));
+    HIPCHK(hipMalloc(&e->d_zmark, e->rows));
+    HIPCHK(hipMalloc(&e->d_tile_cand, e->tile_bytes));
+    HIPCHK(hipMalloc(&e->d_work, std::max<uint64_t>(1, ntiles) * sizeof(gg::TileWork)));
+    HIPCHK(hipMalloc(&e->d_n_work, 2 * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&e->d_nodes, std::max<uint64_t>(1, n_own) * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&e->d_act, 4 * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&e->d_base, rowbytes));
+    for (int b = 0; b < 2; ++b) {
+        HIPCHK(hipMalloc(&e->d_F[b], rowbytes));
+        HIPCHK(hipMalloc(&e->d_flg[b], e->rows));
+    }
+    for (int b = 0; b < 4; ++b) HIPCHK(hipMalloc(&e->d_fired[b], e->rows / 8));
+    HIPCHK(hipMalloc(&e->d_sync_next, std::max<uint64_t>(1, n_own) * 4));
+    HIPCHK(hipMalloc(&e->d_sync_k, std::max<uint64_t>(1, n_own) * 4));
+    if (e->cfg.flags & GG_TRACK_DELIVERY) HIPCHK(hipMalloc(&e->d_dr, std::max<uint64_t>(1, n_own) * e->cfg.n_lanes * 4));
+    e->have_topo = true;
+    e->quiet = 0;  // fresh buffers: clear everything
+    e->dist_k = 0;
+    e->dist_done.clear();
+    e->inj_off = 0;
+    e->lanes.clear();
+    e->lane_value.clear();
+    e->inj.clear();
+    e->round = 0;
+    e->pend_acks = e->pend_ackdrop = 0;
+    e->hash_total = 0;
+    e->dist_open = false;
+    return reset_device_state(e);
+}
+
 int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64_t nnz) {
     if (!e || !row_ptr || (nnz && !col)) return GG_EINVAL;
     HIPCHK(hipSetDevice(e->device));
@@ -1155,90 +1254,62 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
         HIPCHK(hipMalloc(&e->d_xsend, std::max<uint64_t>(16, e->send_off[Wd] * pb)));
         HIPCHK(hipMalloc(&e->d_xrecv, std::max<uint64_t>(16, e->recv_off[Wd] * pb)));
     }
-    // hubs: in-degree > hub_deg (hub_chunks/hub_finish in lean rounds), senders
-    // with out-degree > hub_deg (hub_mark)
-    e->hub_deg = 0;
-    {
-        e->hub_deg = 512;
-        if (const char* h = getenv("GG_HUB_DEG")) e->hub_deg = (uint32_t)std::max(1, atoi(h));
-        uint64_t per = 128ull * (gg::kBlock / lanes_per_node((uint32_t)e->nwp));  // senders per chunk
-        if (const char* h = getenv("GG_HUB_CHUNK")) per = (uint64_t)std::max(1, atoi(h));
-        std::vector<uint32_t> hubs, hub_c0;
-        std::vector<gg::HubChunk> hch, mch;
-        for (uint64_t i = 0; i < n_own; ++i) {
-            const int64_t din = iptr[i + 1] - iptr[i];
-            if (din > (int64_t)e->hub_deg) {
-                hubs.push_back((uint32_t)i);
-                hub_c0.push_back((uint32_t)hch.size());
-                for (int64_t x = iptr[i]; x < iptr[i + 1]; x += (int64_t)per)
-                    hch.push_back({(uint32_t)i, (uint32_t)std::min<int64_t>((int64_t)per, iptr[i + 1] - x), x});
-            }
-            const int64_t o0 = sym ? iptr[i] : optr[i], o1 = sym ? iptr[i + 1] : optr[i + 1];
-            if (o1 - o0 > (int64_t)e->hub_deg)
-                for (int64_t x = o0; x < o1; x += 1024)
-                    mch.push_back({(uint32_t)i, (uint32_t)std::min<int64_t>(1024, o1 - x), x});
-        }
-        hub_c0.push_back((uint32_t)hch.size());
-        e->n_hubs = hubs.size();
-        e->n_hchunks = hch.size();
-        e->n_mchunks = mch.size();
-        if (e->n_hubs) {
-            HIPCHK(hipMalloc(&e->d_hubs, hubs.size() * 4));
-            HIPCHK(hipMemcpy(e->d_hubs, hubs.data(), hubs.size() * 4, hipMemcpyHostToDevice));
-            HIPCHK(hipMalloc(&e->d_hub_c0, hub_c0.size() * 4));
-            HIPCHK(hipMemcpy(e->d_hub_c0, hub_c0.data(), hub_c0.size() * 4, hipMemcpyHostToDevice));
-            HIPCHK(hipMalloc(&e->d_hchunks, hch.size() * sizeof(gg::HubChunk)));
-            HIPCHK(hipMemcpy(e->d_hchunks, hch.data(), hch.size() * sizeof(gg::HubChunk), hipMemcpyHostToDevice));
-            HIPCHK(hipMalloc(&e->d_hscratch, hch.size() * 2 * e->nwp * 8));
-        }
-        if (e->n_mchunks) {
-            HIPCHK(hipMalloc(&e->d_mchunks, mch.size() * sizeof(gg::HubChunk)));
-            HIPCHK(hipMemcpy(e->d_mchunks, mch.data(), mch.size() * sizeof(gg::HubChunk), hipMemcpyHostToDevice));
-        }
+    return finish_topology(e, iptr.data(), sym ? nullptr : optr.data());
+}
+
+// gossip_gen.h: the spec's graph built in HBM (csrc/generate.hip) and installed
+// as gg_topology would install the host builder's CSR: single engine, symmetric,
+// so the in-lists are the rows themselves with every entry reciprocal.
+int gg_topology_generate(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_out) {
+    if (!e || !spec) return GG_EINVAL;
+    if (e->world != 1) return e->fail(GG_EINVAL, "gg_topology_generate: sharded engines take gg_topology");
+    if (gg_gen::spec_nodes(*spec) != e->V) return e->fail(GG_EINVAL, "generator node count != engine n_nodes");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->free_topology();
+    e->have_topo = false;
+    gg_gen::Csr g{};
+    std::string err;
+    int rc = gg_gen::build_csr(*spec, e->stream, gg::kRecipBit, &g, &err);
+    if (rc) return e->fail(rc, err);
+    e->d_in_ptr = g.row_ptr;
+    e->d_in_col = g.col;
+    e->d_out_ptr = g.row_ptr;
+    e->d_out_col = g.col;
+    e->symmetric = true;
+    e->n_own = e->V;
+    e->n_ghost = 0;
+    e->ghost0 = e->V;
+    e->rows = std::max<uint64_t>(64, (e->V + 63) / 64 * 64);
+    e->loc_of.clear();
+    e->gid.clear();
+    e->n_in_edges = g.nnz;
+    if (nnz_out) *nnz_out = g.nnz;
+    uint64_t dmax = 0;
+    if ((rc = gg_gen::max_degree(g.row_ptr, e->V, e->stream, &dmax, &err))) return e->fail(rc, err);
+    std::vector<int64_t> iptr;
+    if (dmax > hub_threshold()) {  // hub chunks are planned on the host
+        iptr.resize(e->V + 1);
+        HIPCHK(hipMemcpy(iptr.data(), g.row_ptr, (e->V + 1) * 8, hipMemcpyDeviceToHost));
     }
-    // streamed sync rounds need no in-hubs and two words per lane
-    e->sync_tiles = getenv("GG_SYNC_TILES") && atoi(getenv("GG_SYNC_TILES")) != 0;
-    dfree(e->d_srec);
-    dfree(e->d_sstate);
-    dfree(e->d_ibits);
-    if (e->cfg.enable_sync && e->n_hubs == 0 && e->nwp >= 2 && !e->sync_tiles && n_own) {
-        HIPCHK(hipMalloc(&e->d_srec, 2 * n_own * sizeof(uint4)));
-        HIPCHK(hipMalloc(&e->d_sstate, e->rows));
-        HIPCHK(hipMalloc(&e->d_ibits, e->rows / 8));
-    }
-    const size_t rowbytes = e->rows * e->nwp * 8;
-    e->tile_nodes = gg::kBlock / lanes_per_node((uint32_t)e->nwp);
-    const uint64_t ntiles = (n_own + e->tile_nodes - 1) / e->tile_nodes;
-    e->tile_bytes = (ntiles + 8) / 8 * 8;
-    HIPCHK(hipMalloc(&e->d_cand, e->rows));
-    HIPCHK(hipMalloc(&e->d_zmark, e->rows));
-    HIPCHK(hipMalloc(&e->d_tile_cand, e->tile_bytes));
-    HIPCHK(hipMalloc(&e->d_work, std::max<uint64_t>(1, ntiles) * sizeof(gg::TileWork)));
-    HIPCHK(hipMalloc(&e->d_n_work, 2 * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&e->d_nodes, std::max<uint64_t>(1, n_own) * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&e->d_act, 4 * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&e->d_base, rowbytes));
-    for (int b = 0; b < 2; ++b) {
-        HIPCHK(hipMalloc(&e->d_F[b], rowbytes));
-        HIPCHK(hipMalloc(&e->d_flg[b], e->rows));
-    }
-    for (int b = 0; b < 4; ++b) HIPCHK(hipMalloc(&e->d_fired[b], e->rows / 8));
-    HIPCHK(hipMalloc(&e->d_sync_next, std::max<uint64_t>(1, n_own) * 4));
-    HIPCHK(hipMalloc(&e->d_sync_k, std::max<uint64_t>(1, n_own) * 4));
-    if (e->cfg.flags & GG_TRACK_DELIVERY) HIPCHK(hipMalloc(&e->d_dr, std::max<uint64_t>(1, n_own) * e->cfg.n_lanes * 4));
-    e->have_topo = true;
-    e->quiet = 0;  // fresh buffers: clear everything
-    e->dist_k = 0;
-    e->dist_done.clear();
-    e->inj_off = 0;
-    e->lanes.clear();
-    e->lane_value.clear();
-    e->inj.clear();
-    e->round = 0;
-    e->pend_acks = e->pend_ackdrop = 0;
-    e->hash_total = 0;
-    e->dist_open = false;
-    return reset_device_state(e);
+    return finish_topology(e, iptr.empty() ? nullptr : iptr.data(), nullptr);
+}
+
+int gg_topology_export(gg_engine* e, int64_t* row_ptr, int32_t* col, uint64_t cap, uint64_t* nnz_out) {
+    if (!e || !row_ptr) return GG_EINVAL;
+    if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
+    if (e->world != 1) return e->fail(GG_EINVAL, "gg_topology_export: single engine only");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (nnz_out) *nnz_out = e->n_in_edges;
+    HIPCHK(hipMemcpy(row_ptr, e->d_in_ptr, (e->V + 1) * 8, hipMemcpyDeviceToHost));
+    if (!col) return GG_OK;
+    if (cap < e->n_in_edges) return e->fail(GG_EINVAL, "col buffer too small");
+    if (e->n_in_edges) HIPCHK(hipMemcpy(col, e->d_in_col, e->n_in_edges * 4, hipMemcpyDeviceToHost));
+    host_parallel(e->n_in_edges, [&](uint64_t lo, uint64_t hi) {
+        for (uint64_t k = lo; k < hi; ++k) col[k] = (int32_t)((uint32_t)col[k] & gg::kColMask);
+    });
+    return GG_OK;
 }
 
 static int add_window(gg_engine* e, int64_t a, int64_t b, Window&& w) {

@@ -1,0 +1,368 @@
+// generate.hip — on-device builders of the synthetic topologies (gossip_gen.h).
+//
+// The graphs are the host builders' (host/topology.cpp), restated for the
+// device so that a 10^9-node CSR never exists in host memory:
+//   * ggh_tree              -> tree_csr: closed form, one thread per row;
+//   * ggh_grid_links        -> grid_pairs: right/down neighbour + the seeded
+//                              long link of every node (same splitmix stream);
+//   * ggh_random_regular    -> perm_pairs: (v, pi_j(v)) per seeded permutation;
+//   * ggh_rmat              -> rmat_pairs: the same per-sample stream, the same
+//                              rejection of ids >= V, the same relabelling.
+// Permutations are the host's sequential Fisher-Yates (host/topology.cpp:100),
+// drawn on the host (V x 4 bytes) and uploaded. Every undirected pair becomes
+// two packed keys (row << cb | col); self loops become the sentinel ~0. One
+// radix sort (rocPRIM, double buffer) orders them by (row, col); duplicates are
+// then adjacent, so a row's distinct columns come from one linear pass
+// (row_bounds -> row_count -> exclusive scan -> row_write) — the symmetrize +
+// dedup rule of build_sym_csr (host/topology.cpp:55-98).
+//
+// HBM at the 2^30-node grid (C5): keys 2 x 6.44e9 x 8 B = 103 GB (freed before
+// the engine allocates its state), bounds + counts + row_ptr 3 x 8.6 GB, columns
+// 25.8 GB.
+#include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include <algorithm>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "generate.h"
+#include "gossip_spec.h"
+
+namespace gg_gen {
+namespace {
+
+constexpr unsigned kBlk = 256;
+constexpr uint64_t kSentinel = ~0ull;
+
+struct DevRng {  // the host builders' splitmix64 stream (host/topology.cpp:28-35)
+    uint64_t s;
+    __device__ explicit DevRng(uint64_t seed) : s(seed) {}
+    __device__ uint64_t next() { return gg_mix64(s += 0x9E3779B97F4A7C15ull); }
+    __device__ uint64_t below(uint64_t n) { return __umul64hi(next(), n); }
+};
+
+__device__ __forceinline__ void put_pair(uint64_t* keys, uint64_t slot, uint64_t a, uint64_t b, uint32_t cb) {
+    const bool loop = a == b;
+    keys[2 * slot] = loop ? kSentinel : (a << cb) | b;
+    keys[2 * slot + 1] = loop ? kSentinel : (b << cb) | a;
+}
+
+__global__ void tree_csr(uint64_t V, uint32_t k, int64_t* rp, uint32_t* col, uint32_t col_or) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > V) return;
+    // row i starts after the i-1 parent links of rows 1..i-1 and the
+    // min(V-1, i*k) child links of rows 0..i-1 (ggh_tree, host/topology.cpp:121)
+    const int64_t start = (int64_t)(i ? i - 1 : 0) + (int64_t)std::min<uint64_t>(V - 1, i * k);
+    rp[i] = i == V ? (int64_t)(2 * (V - 1)) : start;
+    if (i == V) return;
+    int64_t p = start;
+    if (i > 0) col[p++] = (uint32_t)((i - 1) / k) | col_or;
+    for (uint64_t c = i * k + 1; c <= i * k + k && c < V; ++c) col[p++] = (uint32_t)c | col_or;
+}
+
+// slot 3v+0: right neighbour, 3v+1: down neighbour, 3v+2: the long link
+// (ggh_grid_links, host/topology.cpp:215-232)
+__global__ void grid_pairs(uint64_t side, uint64_t seed, uint64_t* keys, uint32_t cb) {
+    const uint64_t V = side * side;
+    const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= 3 * V) return;
+    const uint64_t v = slot / 3, t = slot % 3, x = v % side, y = v / side;
+    if (t == 0) {
+        if (x + 1 < side) put_pair(keys, slot, v, v + 1, cb);
+        else keys[2 * slot] = keys[2 * slot + 1] = kSentinel;
+    } else if (t == 1) {
+        if (y + 1 < side) put_pair(keys, slot, v, v + side, cb);
+        else keys[2 * slot] = keys[2 * slot + 1] = kSentinel;
+    } else {
+        DevRng r(gg_mix64(seed ^ 0x4c494e4bull) ^ gg_mix64(v));
+        put_pair(keys, slot, v, r.below(V), cb);
+    }
+}
+
+// block j of V pairs: (v, pi_j(v)) (ggh_random_regular, host/topology.cpp:150-163)
+__global__ void perm_pairs(uint64_t V, const uint32_t* perm, uint64_t slot0, uint64_t* keys, uint32_t cb) {
+    const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    put_pair(keys, slot0 + v, v, perm[v], cb);
+}
+
+// sample k of the R-MAT stream, relabelled (ggh_rmat, host/topology.cpp:168-211)
+__global__ void rmat_pairs(uint64_t V, uint32_t scale, uint64_t ta, uint64_t tb, uint64_t tc, uint64_t seed,
+                           const uint32_t* perm, uint64_t m, uint64_t* keys, uint32_t cb) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    DevRng r(gg_mix64(seed ^ 0x524d4154ull) ^ gg_mix64(k));
+    uint64_t u, v;
+    do {
+        u = v = 0;
+        for (uint32_t s = 0; s < scale; ++s) {
+            const uint64_t x = r.next();
+            uint64_t bu = 0, bv = 0;
+            if (x < ta) {
+            } else if (x < tb) {
+                bv = 1;
+            } else if (x < tc) {
+                bu = 1;
+            } else {
+                bu = bv = 1;
+            }
+            u = (u << 1) | bu;
+            v = (v << 1) | bv;
+        }
+    } while (u >= V || v >= V);
+    put_pair(keys, k, perm[u], perm[v], cb);
+}
+
+// first[r] = index of the first sorted key of row r (rows without keys take the
+// next row's index); first[V] = number of non-sentinel keys
+__global__ void row_bounds(const uint64_t* keys, uint64_t M, uint64_t V, uint32_t cb, int64_t* first) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > M) return;
+    auto row = [&](uint64_t i) -> uint64_t {
+        if (i >= M) return V;
+        const uint64_t key = keys[i];
+        return key == kSentinel ? V : key >> cb;
+    };
+    const uint64_t r = row(k);
+    const uint64_t prev = k ? row(k - 1) : 0;
+    const uint64_t lo = k ? prev + 1 : 0;
+    for (uint64_t q = lo; q <= r && q <= V; ++q) first[q] = (int64_t)k;
+}
+
+__global__ void row_count(const uint64_t* keys, const int64_t* first, uint64_t V, int64_t* cnt) {
+    const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v > V) return;
+    if (v == V) {
+        cnt[V] = 0;
+        return;
+    }
+    int64_t c = 0;
+    uint64_t last = kSentinel;
+    for (int64_t i = first[v]; i < first[v + 1]; ++i) {
+        const uint64_t key = keys[i];
+        c += key != last;
+        last = key;
+    }
+    cnt[v] = c;
+}
+
+__global__ void row_write(const uint64_t* keys, const int64_t* first, const int64_t* rp, uint64_t V, uint32_t cb,
+                          uint32_t col_or, uint32_t* col) {
+    const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    const uint64_t cmask = (1ull << cb) - 1;
+    int64_t p = rp[v];
+    uint64_t last = kSentinel;
+    for (int64_t i = first[v]; i < first[v + 1]; ++i) {
+        const uint64_t key = keys[i];
+        if (key != last) col[p++] = (uint32_t)(key & cmask) | col_or;
+        last = key;
+    }
+}
+
+__global__ void degree_max(const int64_t* rp, uint64_t V, unsigned long long* out) {
+    unsigned long long m = 0;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V; v += (uint64_t)gridDim.x * blockDim.x)
+        m = std::max<unsigned long long>(m, (unsigned long long)(rp[v + 1] - rp[v]));
+    __shared__ unsigned long long s[kBlk];
+    s[threadIdx.x] = m;
+    __syncthreads();
+    for (unsigned w = kBlk / 2; w; w >>= 1) {
+        if (threadIdx.x < w) s[threadIdx.x] = std::max(s[threadIdx.x], s[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicMax(out, s[0]);
+}
+
+unsigned grid_of(uint64_t n) { return (unsigned)((n + kBlk - 1) / kBlk); }
+
+// host/topology.cpp:100-106 (the permutation is part of the graph's definition)
+std::vector<uint32_t> permutation(uint64_t V, uint64_t seed) {
+    std::vector<uint32_t> p(V);
+    for (uint64_t i = 0; i < V; ++i) p[i] = (uint32_t)i;
+    uint64_t s = seed;
+    for (uint64_t i = V; i > 1; --i) {
+        const uint64_t x = gg_mix64(s += 0x9E3779B97F4A7C15ull);
+        std::swap(p[i - 1], p[(uint64_t)(((unsigned __int128)x * i) >> 64)]);
+    }
+    return p;
+}
+
+struct Scoped {  // device allocations released on every exit path
+    std::vector<void*> ptrs;
+    ~Scoped() {
+        for (void* p : ptrs) (void)hipFree(p);
+    }
+    template <class T>
+    hipError_t alloc(T** p, size_t bytes) {
+        hipError_t e = hipMalloc((void**)p, std::max<size_t>(bytes, 16));
+        if (e == hipSuccess) ptrs.push_back((void*)*p);
+        return e;
+    }
+    void release(void* p) {  // free now
+        auto it = std::find(ptrs.begin(), ptrs.end(), p);
+        if (it != ptrs.end()) {
+            (void)hipFree(p);
+            ptrs.erase(it);
+        }
+    }
+    void keep(void* p) {  // ownership to the caller
+        auto it = std::find(ptrs.begin(), ptrs.end(), p);
+        if (it != ptrs.end()) ptrs.erase(it);
+    }
+};
+
+}  // namespace
+
+#define GCHK(x)                                                              \
+    do {                                                                     \
+        hipError_t err_ = (x);                                               \
+        if (err_ != hipSuccess) {                                            \
+            *err = std::string(#x) + ": " + hipGetErrorString(err_);         \
+            return -5;                                                       \
+        }                                                                    \
+    } while (0)
+
+uint64_t spec_nodes(const gg_gen_spec& s) { return s.kind == GG_GEN_GRID_LINKS ? s.n * s.n : s.n; }
+
+int build_csr(const gg_gen_spec& s, hipStream_t st, uint32_t col_or, Csr* out, std::string* err) {
+    const uint64_t V = spec_nodes(s);
+    if (V == 0 || V > 0x7fffffffull) {
+        *err = "generator: node count must be in [1, 2^31)";
+        return -22;
+    }
+    Scoped mem;
+    int64_t* rp = nullptr;
+    uint32_t* col = nullptr;
+    GCHK(mem.alloc(&rp, (V + 1) * 8));
+    if (s.kind == GG_GEN_TREE) {
+        if (s.k == 0) {
+            *err = "generator: tree arity must be >= 1";
+            return -22;
+        }
+        const uint64_t nnz = 2 * (V - 1);
+        GCHK(mem.alloc(&col, nnz * 4));
+        hipLaunchKernelGGL(tree_csr, dim3(grid_of(V + 1)), dim3(kBlk), 0, st, V, s.k, rp, col, col_or);
+        GCHK(hipGetLastError());
+        GCHK(hipStreamSynchronize(st));
+        mem.keep(rp);
+        mem.keep(col);
+        *out = {rp, col, V, nnz};
+        return 0;
+    }
+    // undirected pairs -> packed keys (two per pair)
+    uint32_t cb = 1;
+    while ((1ull << cb) <= V) ++cb;  // V < 2^cb: sentinel rows (all ones) sort after every real row
+    uint64_t pairs = 0;
+    std::vector<uint32_t> perm;
+    uint32_t* d_perm = nullptr;
+    switch (s.kind) {
+    case GG_GEN_GRID_LINKS:
+        if (s.n < 2) { *err = "generator: grid side must be >= 2"; return -22; }
+        pairs = 3 * V;
+        break;
+    case GG_GEN_RANDOM_REGULAR:
+        if (s.k < 2 || s.k % 2) { *err = "generator: regular degree must be even and >= 2"; return -22; }
+        pairs = V * (s.k / 2);
+        break;
+    case GG_GEN_RMAT:
+        if (V < 2 || s.k == 0) { *err = "generator: R-MAT needs >= 2 nodes and edge factor >= 1"; return -22; }
+        pairs = V * s.k;
+        break;
+    default:
+        *err = "generator: unknown kind";
+        return -22;
+    }
+    const uint64_t M = 2 * pairs;
+    uint64_t* k0 = nullptr;
+    uint64_t* k1 = nullptr;
+    GCHK(mem.alloc(&k0, M * 8));
+    GCHK(mem.alloc(&k1, M * 8));
+    if (s.kind == GG_GEN_GRID_LINKS) {
+        hipLaunchKernelGGL(grid_pairs, dim3(grid_of(pairs)), dim3(kBlk), 0, st, s.n, s.seed, k0, cb);
+        GCHK(hipGetLastError());
+    } else if (s.kind == GG_GEN_RANDOM_REGULAR) {
+        GCHK(mem.alloc(&d_perm, V * 4));
+        for (uint32_t j = 0; j < s.k / 2; ++j) {
+            perm = permutation(V, gg_mix64(s.seed ^ (0x52454755ull + j)));
+            GCHK(hipStreamSynchronize(st));  // the previous block's kernel has read d_perm
+            GCHK(hipMemcpy(d_perm, perm.data(), V * 4, hipMemcpyHostToDevice));
+            hipLaunchKernelGGL(perm_pairs, dim3(grid_of(V)), dim3(kBlk), 0, st, V, d_perm, (uint64_t)j * V, k0, cb);
+            GCHK(hipGetLastError());
+        }
+    } else {
+        uint32_t scale = 0;
+        while ((1ull << scale) < V) ++scale;
+        const uint64_t ta = (uint64_t)(s.a * 18446744073709551616.0);
+        const uint64_t tb = (uint64_t)((s.a + s.b) * 18446744073709551616.0);
+        const uint64_t tc = (uint64_t)((s.a + s.b + s.c) * 18446744073709551616.0);
+        perm = permutation(V, gg_mix64(s.seed ^ 0x5045524dull));
+        GCHK(mem.alloc(&d_perm, V * 4));
+        GCHK(hipMemcpy(d_perm, perm.data(), V * 4, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(rmat_pairs, dim3(grid_of(pairs)), dim3(kBlk), 0, st, V, scale, ta, tb, tc, s.seed, d_perm,
+                           pairs, k0, cb);
+        GCHK(hipGetLastError());
+    }
+    // sort (row, col) keys; the sentinel's low 2*cb bits are all ones
+    rocprim::double_buffer<uint64_t> db(k0, k1);
+    size_t tmp_bytes = 0;
+    GCHK(rocprim::radix_sort_keys(nullptr, tmp_bytes, db, M, 0, 2 * cb, st));
+    void* tmp = nullptr;
+    GCHK(mem.alloc(&tmp, tmp_bytes));
+    GCHK(rocprim::radix_sort_keys(tmp, tmp_bytes, db, M, 0, 2 * cb, st));
+    GCHK(hipStreamSynchronize(st));
+    mem.release(tmp);
+    if (d_perm) mem.release(d_perm);
+    uint64_t* keys = db.current();
+    mem.release(keys == k0 ? (void*)k1 : (void*)k0);
+    // CSR of the distinct (row, col) keys
+    int64_t* first = nullptr;
+    int64_t* cnt = nullptr;
+    GCHK(mem.alloc(&first, (V + 1) * 8));
+    GCHK(mem.alloc(&cnt, (V + 1) * 8));
+    hipLaunchKernelGGL(row_bounds, dim3(grid_of(M + 1)), dim3(kBlk), 0, st, keys, M, V, cb, first);
+    GCHK(hipGetLastError());
+    hipLaunchKernelGGL(row_count, dim3(grid_of(V + 1)), dim3(kBlk), 0, st, keys, first, V, cnt);
+    GCHK(hipGetLastError());
+    tmp_bytes = 0;
+    GCHK(rocprim::exclusive_scan(nullptr, tmp_bytes, cnt, rp, (int64_t)0, V + 1, rocprim::plus<int64_t>(), st));
+    GCHK(mem.alloc(&tmp, tmp_bytes));
+    GCHK(rocprim::exclusive_scan(tmp, tmp_bytes, cnt, rp, (int64_t)0, V + 1, rocprim::plus<int64_t>(), st));
+    int64_t nnz = 0;
+    GCHK(hipMemcpyAsync(&nnz, rp + V, 8, hipMemcpyDeviceToHost, st));
+    GCHK(hipStreamSynchronize(st));
+    mem.release(tmp);
+    mem.release(cnt);
+    GCHK(mem.alloc(&col, (uint64_t)nnz * 4));
+    hipLaunchKernelGGL(row_write, dim3(grid_of(V)), dim3(kBlk), 0, st, keys, first, rp, V, cb, col_or, col);
+    GCHK(hipGetLastError());
+    GCHK(hipStreamSynchronize(st));
+    mem.keep(rp);
+    mem.keep(col);
+    *out = {rp, col, V, (uint64_t)nnz};
+    return 0;
+}
+
+int max_degree(const int64_t* d_rp, uint64_t V, hipStream_t st, uint64_t* out, std::string* err) {
+    unsigned long long* d = nullptr;
+    GCHK(hipMalloc(&d, 8));
+    hipError_t e1 = hipMemsetAsync(d, 0, 8, st);
+    if (e1 == hipSuccess) {
+        const unsigned blocks = (unsigned)std::min<uint64_t>(4096, std::max<uint64_t>(1, grid_of(V)));
+        hipLaunchKernelGGL(degree_max, dim3(blocks), dim3(kBlk), 0, st, d_rp, V, d);
+        e1 = hipGetLastError();
+    }
+    unsigned long long h = 0;
+    if (e1 == hipSuccess) e1 = hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, st);
+    if (e1 == hipSuccess) e1 = hipStreamSynchronize(st);
+    (void)hipFree(d);
+    GCHK(e1);
+    *out = h;
+    return 0;
+}
+
+}  // namespace gg_gen

@@ -81,6 +81,21 @@ class GGExchange(C.Structure):
     ]
 
 
+class GGGenSpec(C.Structure):  # include/gossip_gen.h
+    _fields_ = [
+        ("kind", C.c_uint32),
+        ("k", C.c_uint32),
+        ("n", C.c_uint64),
+        ("a", C.c_double),
+        ("b", C.c_double),
+        ("c", C.c_double),
+        ("seed", C.c_uint64),
+    ]
+
+
+GEN_KINDS = {"tree": 1, "random_regular": 2, "rmat": 3, "grid_links": 4}
+GEN_SYMBOLS = ["gg_topology_generate", "gg_topology_export"]  # HIP library only
+
 STAT_FIELDS = [f for f, _ in GGRoundStats._fields_]
 DIAG_FIELDS = ("round", "kernel_ms", "work_rows", "work_gathers", "prep_ms", "expand_ms", "stream_ms",
                "prep_bytes", "expand_bytes", "stream_bytes")
@@ -133,6 +148,9 @@ def load_library(path: str) -> C.CDLL:
     lib.gg_dist_info.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_uint64)]
     lib.gg_read_bits_nodes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
     lib.gg_delivery_rounds_nodes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+    if hasattr(lib, "gg_topology_generate"):
+        lib.gg_topology_generate.argtypes = [C.c_void_p, P(GGGenSpec), P(C.c_uint64)]
+        lib.gg_topology_export.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]
     _LIBS[path] = lib
     return lib
 
@@ -209,6 +227,28 @@ class Engine:
         rp = np.ascontiguousarray(topo.row_ptr, np.int64)
         col = np.ascontiguousarray(topo.col, np.int32)
         self._ok(self.lib.gg_topology(self.h, rp.ctypes.data, col.ctypes.data, col.size))
+
+    def generate(self, kind: str, n: int, k: int = 0, seed: int = 0, a: float = 0.0, b: float = 0.0,
+                 c: float = 0.0) -> int:
+        """Build a synthetic topology in HBM (gossip_gen.h; HIP library only) and
+        install it; the graph equals the host builder's (ggamd.topology.tree /
+        random_regular / rmat / grid_links with the same arguments). n = nodes,
+        or the grid side. Returns the number of adjacency entries."""
+        if not hasattr(self.lib, "gg_topology_generate"):
+            raise GGError(-38, f"{self.library} has no on-device generators")
+        spec = GGGenSpec(GEN_KINDS[kind], k, n, a, b, c, seed & ((1 << 64) - 1))
+        nnz = C.c_uint64(0)
+        self._ok(self.lib.gg_topology_generate(self.h, C.byref(spec), C.byref(nnz)))
+        return nnz.value
+
+    def export_topology(self) -> Topology:
+        """The installed topology as CSR (single engine; in-lists, = rows when symmetric)."""
+        n = C.c_uint64(0)
+        rp = np.zeros(self.V + 1, np.int64)
+        self._ok(self.lib.gg_topology_export(self.h, rp.ctypes.data, None, 0, C.byref(n)))
+        col = np.zeros(max(1, n.value), np.int32)
+        self._ok(self.lib.gg_topology_export(self.h, rp.ctypes.data, col.ctypes.data, col.size, C.byref(n)))
+        return Topology(self.V, rp, col[: n.value])
 
     def partition_seeded(self, r0: int, r1: int, epoch_seed: int):
         self._ok(self.lib.gg_partition_seeded(self.h, r0, r1, epoch_seed))
@@ -320,6 +360,6 @@ class Engine:
         return [stats_dict(arr[i]) for i in range(n.value)]
 
 
-def missing_symbols(path: str) -> list[str]:
+def missing_symbols(path: str, extra: tuple = ()) -> list[str]:
     lib = C.CDLL(os.path.abspath(path))
-    return [s for s in GG_SYMBOLS if not hasattr(lib, s)]
+    return [s for s in list(GG_SYMBOLS) + list(extra) if not hasattr(lib, s)]

@@ -48,3 +48,24 @@ def test_python_binding_symbol_list_matches_header():
     from ggamd.engine import GG_SYMBOLS
     declared = set(_declared(os.path.join(REPO, "include", "gossip.h")))
     assert set(GG_SYMBOLS) <= declared
+
+
+def test_hip_library_exports_generator_entry_points():
+    """include/gossip_gen.h (on-device generators) is exported by the HIP library only."""
+    names = [n for n in _declared(os.path.join(REPO, "include", "gossip_gen.h")) if n.startswith("gg_")]
+    assert set(names) == {"gg_topology_generate", "gg_topology_export"}
+    dll = C.CDLL(HIP_LIB)
+    assert all(hasattr(dll, n) for n in names)
+    from ggamd.engine import GEN_SYMBOLS, missing_symbols
+    assert set(GEN_SYMBOLS) == set(names)
+    assert missing_symbols(HIP_LIB, tuple(GEN_SYMBOLS)) == []
+
+
+def test_gen_spec_layout_matches_header():
+    """ctypes mirror of gg_gen_spec: field order and size of include/gossip_gen.h."""
+    from ggamd.engine import GEN_KINDS, GGGenSpec
+    src = open(os.path.join(REPO, "include", "gossip_gen.h")).read()
+    assert [f for f, _ in GGGenSpec._fields_] == ["kind", "k", "n", "a", "b", "c", "seed"]
+    assert C.sizeof(GGGenSpec) == 48
+    for name, val in GEN_KINDS.items():
+        assert re.search(rf"GG_GEN_{name.upper()}\s*=\s*{val}\b", src), name

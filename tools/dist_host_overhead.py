@@ -49,7 +49,7 @@ def main():
             t0 = time.perf_counter()
             for _ in range(R):
                 x = e.dist_round_begin()
-                if mode == "engine+views":
+                if mode != "engine":
                     send = _view(x.send, x.send_total, True, dev)
                     recv = _view(x.recv, x.recv_total, True, dev)
                     ext = torch.cuda.ExternalStream(x.stream, device=dev)
