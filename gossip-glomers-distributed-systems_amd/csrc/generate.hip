@@ -9,16 +9,19 @@
 //   * ggh_rmat              -> rmat_pairs: the same per-sample stream, the same
 //                              rejection of ids >= V, the same relabelling.
 // Permutations are the host's sequential Fisher-Yates (host/topology.cpp:100),
-// drawn on the host (V x 4 bytes) and uploaded. Every undirected pair becomes
-// two packed keys (row << cb | col); self loops become the sentinel ~0. One
-// radix sort (rocPRIM, double buffer) orders them by (row, col); duplicates are
-// then adjacent, so a row's distinct columns come from one linear pass
-// (row_bounds -> row_count -> exclusive scan -> row_write) — the symmetrize +
-// dedup rule of build_sym_csr (host/topology.cpp:55-98).
+// drawn on the host (V x 4 bytes each) and uploaded. Every undirected pair
+// becomes two packed keys (row << cb | col), self loops none. The keys are
+// emitted grouped into row-range parts of <= 2^31 keys (a bucket histogram of
+// the same deterministic pair stream plans the parts), and each part is radix
+// sorted on its own (rocPRIM, double buffer); the parts are in row order, so the
+// array is then sorted by (row, col) and duplicates are adjacent: a row's
+// distinct columns come from one linear pass (row_bounds -> row_count ->
+// exclusive scan -> row_write) — the symmetrize + dedup rule of build_sym_csr
+// (host/topology.cpp:55-98).
 //
-// HBM at the 2^30-node grid (C5): keys 2 x 6.44e9 x 8 B = 103 GB (freed before
-// the engine allocates its state), bounds + counts + row_ptr 3 x 8.6 GB, columns
-// 25.8 GB.
+// HBM at the 2^30-node grid (C5): keys 6.44e9 x 8 B = 51.5 GB + one part's
+// sort buffer 17.2 GB (both freed before the engine allocates its state),
+// bounds + counts + row_ptr 3 x 8.6 GB, columns 25.8 GB.
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -26,6 +29,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -45,10 +49,61 @@ struct DevRng {  // the host builders' splitmix64 stream (host/topology.cpp:28-3
     __device__ uint64_t below(uint64_t n) { return __umul64hi(next(), n); }
 };
 
-__device__ __forceinline__ void put_pair(uint64_t* keys, uint64_t slot, uint64_t a, uint64_t b, uint32_t cb) {
-    const bool loop = a == b;
-    keys[2 * slot] = loop ? kSentinel : (a << cb) | b;
-    keys[2 * slot + 1] = loop ? kSentinel : (b << cb) | a;
+// Pair generators, one undirected pair per slot (false: no pair — a missing
+// grid neighbour or a self loop, both dropped by build_sym_csr).
+struct GenParams {
+    uint32_t kind;
+    uint64_t V, side, seed;
+    uint32_t scale;           // R-MAT: log2 of the sampling square
+    uint64_t ta, tb, tc;      // R-MAT: quadrant thresholds (x < ta: a, < tb: b, < tc: c, else d)
+    const uint32_t* perm;     // R-MAT: relabelling; regular: the k/2 permutations, [j*V + v]
+};
+
+__device__ __forceinline__ bool pair_at(const GenParams& g, uint64_t slot, uint64_t& a, uint64_t& b) {
+    if (g.kind == GG_GEN_GRID_LINKS) {
+        // slot 3v+0: right neighbour, 3v+1: down neighbour, 3v+2: the long link
+        // (ggh_grid_links, host/topology.cpp:215-232)
+        const uint64_t v = slot / 3, t = slot % 3, x = v % g.side, y = v / g.side;
+        a = v;
+        if (t == 0) {
+            if (x + 1 >= g.side) return false;
+            b = v + 1;
+        } else if (t == 1) {
+            if (y + 1 >= g.side) return false;
+            b = v + g.side;
+        } else {
+            DevRng r(gg_mix64(g.seed ^ 0x4c494e4bull) ^ gg_mix64(v));
+            b = r.below(g.V);
+        }
+    } else if (g.kind == GG_GEN_RANDOM_REGULAR) {
+        // block j of V pairs: (v, pi_j(v)) (ggh_random_regular, host/topology.cpp:150-163)
+        a = slot % g.V;
+        b = g.perm[slot];
+    } else {
+        // sample `slot` of the R-MAT stream, relabelled (ggh_rmat, host/topology.cpp:168-211)
+        DevRng r(gg_mix64(g.seed ^ 0x524d4154ull) ^ gg_mix64(slot));
+        uint64_t u, v;
+        do {
+            u = v = 0;
+            for (uint32_t s = 0; s < g.scale; ++s) {
+                const uint64_t x = r.next();
+                uint64_t bu = 0, bv = 0;
+                if (x < g.ta) {
+                } else if (x < g.tb) {
+                    bv = 1;
+                } else if (x < g.tc) {
+                    bu = 1;
+                } else {
+                    bu = bv = 1;
+                }
+                u = (u << 1) | bu;
+                v = (v << 1) | bv;
+            }
+        } while (u >= g.V || v >= g.V);
+        a = g.perm[u];
+        b = g.perm[v];
+    }
+    return a != b;
 }
 
 __global__ void tree_csr(uint64_t V, uint32_t k, int64_t* rp, uint32_t* col, uint32_t col_or) {
@@ -64,61 +119,61 @@ __global__ void tree_csr(uint64_t V, uint32_t k, int64_t* rp, uint32_t* col, uin
     for (uint64_t c = i * k + 1; c <= i * k + k && c < V; ++c) col[p++] = (uint32_t)c | col_or;
 }
 
-// slot 3v+0: right neighbour, 3v+1: down neighbour, 3v+2: the long link
-// (ggh_grid_links, host/topology.cpp:215-232)
-__global__ void grid_pairs(uint64_t side, uint64_t seed, uint64_t* keys, uint32_t cb) {
-    const uint64_t V = side * side;
-    const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (slot >= 3 * V) return;
-    const uint64_t v = slot / 3, t = slot % 3, x = v % side, y = v / side;
-    if (t == 0) {
-        if (x + 1 < side) put_pair(keys, slot, v, v + 1, cb);
-        else keys[2 * slot] = keys[2 * slot + 1] = kSentinel;
-    } else if (t == 1) {
-        if (y + 1 < side) put_pair(keys, slot, v, v + side, cb);
-        else keys[2 * slot] = keys[2 * slot + 1] = kSentinel;
-    } else {
-        DevRng r(gg_mix64(seed ^ 0x4c494e4bull) ^ gg_mix64(v));
-        put_pair(keys, slot, v, r.below(V), cb);
+constexpr int kBuckets = 1024;  // row buckets of the part plan
+constexpr size_t kMaxParts = 64;
+constexpr uint64_t kPartKeys = 1ull << 31;  // keys per sort
+
+// Keys per row bucket (both directions of every pair); LDS histogram per
+// block, one global atomic per non-empty bucket per block.
+__global__ __launch_bounds__(kBlk) void bucket_hist(GenParams g, uint64_t pairs, uint32_t bshift,
+                                                    unsigned long long* hist) {
+    __shared__ unsigned int h[kBuckets];
+    for (int i = threadIdx.x; i < kBuckets; i += kBlk) h[i] = 0;
+    __syncthreads();
+    for (uint64_t s = (uint64_t)blockIdx.x * kBlk + threadIdx.x; s < pairs; s += (uint64_t)gridDim.x * kBlk) {
+        uint64_t a, b;
+        if (!pair_at(g, s, a, b)) continue;
+        atomicAdd(&h[a >> bshift], 1u);
+        atomicAdd(&h[b >> bshift], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kBuckets; i += kBlk)
+        if (h[i]) atomicAdd(&hist[i], (unsigned long long)h[i]);
+}
+
+// Both keys (row << cb | col) of every pair into the slice of their row's
+// part; cursor[p] starts at the part's offset. One atomic per part per wave.
+__global__ __launch_bounds__(kBlk) void emit_keys(GenParams g, uint64_t pairs, uint32_t cb, uint32_t n_parts,
+                                                  const uint64_t* part_row0, unsigned long long* cursor,
+                                                  uint64_t* keys) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (uint64_t base = (uint64_t)blockIdx.x * kBlk; base < pairs; base += (uint64_t)gridDim.x * kBlk) {
+        const uint64_t s = base + threadIdx.x;
+        uint64_t a = 0, b = 0;
+        const bool ok = s < pairs && pair_at(g, s, a, b);
+        for (int d = 0; d < 2; ++d) {
+            const uint64_t row = d ? b : a, colv = d ? a : b;
+            int p = -1;
+            if (ok) {
+                p = 0;
+                while (p + 1 < (int)n_parts && row >= part_row0[p + 1]) ++p;
+            }
+            for (uint32_t q = 0; q < n_parts; ++q) {
+                const unsigned long long m = __ballot(p == (int)q);
+                if (!m) continue;
+                const int leader = __ffsll((long long)m) - 1;
+                unsigned long long at = 0;
+                if (lane == leader) at = atomicAdd(&cursor[q], (unsigned long long)__popcll(m));
+                at = __shfl(at, leader, 64);
+                if (p == (int)q) keys[at + __popcll(m & lt)] = (row << cb) | colv;
+            }
+        }
     }
 }
 
-// block j of V pairs: (v, pi_j(v)) (ggh_random_regular, host/topology.cpp:150-163)
-__global__ void perm_pairs(uint64_t V, const uint32_t* perm, uint64_t slot0, uint64_t* keys, uint32_t cb) {
-    const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= V) return;
-    put_pair(keys, slot0 + v, v, perm[v], cb);
-}
-
-// sample k of the R-MAT stream, relabelled (ggh_rmat, host/topology.cpp:168-211)
-__global__ void rmat_pairs(uint64_t V, uint32_t scale, uint64_t ta, uint64_t tb, uint64_t tc, uint64_t seed,
-                           const uint32_t* perm, uint64_t m, uint64_t* keys, uint32_t cb) {
-    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= m) return;
-    DevRng r(gg_mix64(seed ^ 0x524d4154ull) ^ gg_mix64(k));
-    uint64_t u, v;
-    do {
-        u = v = 0;
-        for (uint32_t s = 0; s < scale; ++s) {
-            const uint64_t x = r.next();
-            uint64_t bu = 0, bv = 0;
-            if (x < ta) {
-            } else if (x < tb) {
-                bv = 1;
-            } else if (x < tc) {
-                bu = 1;
-            } else {
-                bu = bv = 1;
-            }
-            u = (u << 1) | bu;
-            v = (v << 1) | bv;
-        }
-    } while (u >= V || v >= V);
-    put_pair(keys, k, perm[u], perm[v], cb);
-}
-
 // first[r] = index of the first sorted key of row r (rows without keys take the
-// next row's index); first[V] = number of non-sentinel keys
+// next row's index); first[V] = M
 __global__ void row_bounds(const uint64_t* keys, uint64_t M, uint64_t V, uint32_t cb, int64_t* first) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k > M) return;
@@ -254,9 +309,14 @@ int build_csr(const gg_gen_spec& s, hipStream_t st, uint32_t col_or, Csr* out, s
         *out = {rp, col, V, nnz};
         return 0;
     }
-    // undirected pairs -> packed keys (two per pair)
+    // undirected pairs -> packed keys (row << cb | col), both directions
     uint32_t cb = 1;
-    while ((1ull << cb) <= V) ++cb;  // V < 2^cb: sentinel rows (all ones) sort after every real row
+    while ((1ull << cb) <= V) ++cb;
+    GenParams g{};
+    g.kind = s.kind;
+    g.V = V;
+    g.side = s.n;
+    g.seed = s.seed;
     uint64_t pairs = 0;
     std::vector<uint32_t> perm;
     uint32_t* d_perm = nullptr;
@@ -268,57 +328,98 @@ int build_csr(const gg_gen_spec& s, hipStream_t st, uint32_t col_or, Csr* out, s
     case GG_GEN_RANDOM_REGULAR:
         if (s.k < 2 || s.k % 2) { *err = "generator: regular degree must be even and >= 2"; return -22; }
         pairs = V * (s.k / 2);
+        GCHK(mem.alloc(&d_perm, pairs * 4));
+        for (uint32_t j = 0; j < s.k / 2; ++j) {
+            perm = permutation(V, gg_mix64(s.seed ^ (0x52454755ull + j)));
+            GCHK(hipMemcpy(d_perm + (uint64_t)j * V, perm.data(), V * 4, hipMemcpyHostToDevice));
+        }
         break;
     case GG_GEN_RMAT:
         if (V < 2 || s.k == 0) { *err = "generator: R-MAT needs >= 2 nodes and edge factor >= 1"; return -22; }
         pairs = V * s.k;
+        while ((1ull << g.scale) < V) ++g.scale;
+        g.ta = (uint64_t)(s.a * 18446744073709551616.0);
+        g.tb = (uint64_t)((s.a + s.b) * 18446744073709551616.0);
+        g.tc = (uint64_t)((s.a + s.b + s.c) * 18446744073709551616.0);
+        perm = permutation(V, gg_mix64(s.seed ^ 0x5045524dull));
+        GCHK(mem.alloc(&d_perm, V * 4));
+        GCHK(hipMemcpy(d_perm, perm.data(), V * 4, hipMemcpyHostToDevice));
         break;
     default:
         *err = "generator: unknown kind";
         return -22;
     }
-    const uint64_t M = 2 * pairs;
-    uint64_t* k0 = nullptr;
-    uint64_t* k1 = nullptr;
-    GCHK(mem.alloc(&k0, M * 8));
-    GCHK(mem.alloc(&k1, M * 8));
-    if (s.kind == GG_GEN_GRID_LINKS) {
-        hipLaunchKernelGGL(grid_pairs, dim3(grid_of(pairs)), dim3(kBlk), 0, st, s.n, s.seed, k0, cb);
-        GCHK(hipGetLastError());
-    } else if (s.kind == GG_GEN_RANDOM_REGULAR) {
-        GCHK(mem.alloc(&d_perm, V * 4));
-        for (uint32_t j = 0; j < s.k / 2; ++j) {
-            perm = permutation(V, gg_mix64(s.seed ^ (0x52454755ull + j)));
-            GCHK(hipStreamSynchronize(st));  // the previous block's kernel has read d_perm
-            GCHK(hipMemcpy(d_perm, perm.data(), V * 4, hipMemcpyHostToDevice));
-            hipLaunchKernelGGL(perm_pairs, dim3(grid_of(V)), dim3(kBlk), 0, st, V, d_perm, (uint64_t)j * V, k0, cb);
-            GCHK(hipGetLastError());
+    std::vector<uint32_t>().swap(perm);
+    g.perm = d_perm;
+    // part plan: row ranges of at most kPartKeys keys each, sorted one at a time
+    // (rocPRIM's radix sort keeps 32-bit digit counts: one sort stays < 2^32 keys)
+    uint64_t part_keys = kPartKeys;
+    if (const char* e = getenv("GG_GEN_PART_KEYS")) part_keys = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+    uint32_t bshift = 0;
+    while ((V - 1) >> bshift >= (uint64_t)kBuckets) ++bshift;
+    unsigned long long* d_hist = nullptr;
+    GCHK(mem.alloc(&d_hist, (kBuckets + kMaxParts) * 8));
+    GCHK(hipMemsetAsync(d_hist, 0, kBuckets * 8, st));
+    const unsigned gblocks = (unsigned)std::min<uint64_t>(grid_of(pairs), 4096);
+    hipLaunchKernelGGL(bucket_hist, dim3(gblocks), dim3(kBlk), 0, st, g, pairs, bshift, d_hist);
+    GCHK(hipGetLastError());
+    std::vector<unsigned long long> hist(kBuckets);
+    GCHK(hipMemcpyAsync(hist.data(), d_hist, kBuckets * 8, hipMemcpyDeviceToHost, st));
+    GCHK(hipStreamSynchronize(st));
+    std::vector<uint64_t> row0{0}, off{0};  // part p: rows [row0[p], row0[p+1]), keys [off[p], off[p+1])
+    uint64_t in_part = 0, M = 0;
+    for (int q = 0; q < kBuckets; ++q) {
+        if (in_part && in_part + hist[q] > part_keys && row0.size() < kMaxParts) {
+            row0.push_back((uint64_t)q << bshift);
+            off.push_back(M);
+            in_part = 0;
         }
-    } else {
-        uint32_t scale = 0;
-        while ((1ull << scale) < V) ++scale;
-        const uint64_t ta = (uint64_t)(s.a * 18446744073709551616.0);
-        const uint64_t tb = (uint64_t)((s.a + s.b) * 18446744073709551616.0);
-        const uint64_t tc = (uint64_t)((s.a + s.b + s.c) * 18446744073709551616.0);
-        perm = permutation(V, gg_mix64(s.seed ^ 0x5045524dull));
-        GCHK(mem.alloc(&d_perm, V * 4));
-        GCHK(hipMemcpy(d_perm, perm.data(), V * 4, hipMemcpyHostToDevice));
-        hipLaunchKernelGGL(rmat_pairs, dim3(grid_of(pairs)), dim3(kBlk), 0, st, V, scale, ta, tb, tc, s.seed, d_perm,
-                           pairs, k0, cb);
-        GCHK(hipGetLastError());
+        in_part += hist[q];
+        M += hist[q];
     }
-    // sort (row, col) keys; the sentinel's low 2*cb bits are all ones
-    rocprim::double_buffer<uint64_t> db(k0, k1);
+    row0.push_back(V);
+    off.push_back(M);
+    const uint32_t n_parts = (uint32_t)row0.size() - 1;
+    uint64_t max_part = 0;
+    for (uint32_t q = 0; q < n_parts; ++q) max_part = std::max(max_part, off[q + 1] - off[q]);
+    if (max_part >= (1ull << 32)) {
+        *err = "generator: a row bucket holds >= 2^32 adjacency entries";
+        return -22;
+    }
+    uint64_t* keys = nullptr;
+    uint64_t* alt = nullptr;
+    uint64_t* d_row0 = nullptr;
+    GCHK(mem.alloc(&keys, M * 8));
+    GCHK(mem.alloc(&d_row0, row0.size() * 8));
+    GCHK(hipMemcpy(d_row0, row0.data(), row0.size() * 8, hipMemcpyHostToDevice));
+    unsigned long long* d_cur = d_hist + kBuckets;
+    GCHK(hipMemcpy(d_cur, off.data(), n_parts * 8, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(emit_keys, dim3(gblocks), dim3(kBlk), 0, st, g, pairs, cb, n_parts, d_row0, d_cur, keys);
+    GCHK(hipGetLastError());
+    GCHK(hipStreamSynchronize(st));
+    if (d_perm) mem.release(d_perm);
+    // sort each part's slice by (row, col): the parts are row ranges in order,
+    // so the whole array ends up sorted
+    GCHK(mem.alloc(&alt, max_part * 8));
     size_t tmp_bytes = 0;
-    GCHK(rocprim::radix_sort_keys(nullptr, tmp_bytes, db, M, 0, 2 * cb, st));
     void* tmp = nullptr;
-    GCHK(mem.alloc(&tmp, tmp_bytes));
-    GCHK(rocprim::radix_sort_keys(tmp, tmp_bytes, db, M, 0, 2 * cb, st));
+    {
+        rocprim::double_buffer<uint64_t> db(keys, alt);
+        GCHK(rocprim::radix_sort_keys(nullptr, tmp_bytes, db, (size_t)max_part, 0, 2 * cb, st));
+        GCHK(mem.alloc(&tmp, tmp_bytes));
+    }
+    for (uint32_t q = 0; q < n_parts; ++q) {
+        const uint64_t n = off[q + 1] - off[q];
+        if (n < 2) continue;
+        rocprim::double_buffer<uint64_t> db(keys + off[q], alt);
+        size_t tb = tmp_bytes;
+        GCHK(rocprim::radix_sort_keys(tmp, tb, db, (size_t)n, 0, 2 * cb, st));
+        if (db.current() != keys + off[q])
+            GCHK(hipMemcpyAsync(keys + off[q], db.current(), n * 8, hipMemcpyDeviceToDevice, st));
+    }
     GCHK(hipStreamSynchronize(st));
     mem.release(tmp);
-    if (d_perm) mem.release(d_perm);
-    uint64_t* keys = db.current();
-    mem.release(keys == k0 ? (void*)k1 : (void*)k0);
+    mem.release(alt);
     // CSR of the distinct (row, col) keys
     int64_t* first = nullptr;
     int64_t* cnt = nullptr;

@@ -29,9 +29,13 @@ class Workload:
     enable_sync: bool = True
     windows: list = field(default_factory=list)  # ("seeded", r0, r1, epoch_seed)
     max_rounds: int = 400
+    gen: dict | None = None  # on-device generator spec of the same graph (Engine.generate kwargs)
 
     def apply(self, eng):
-        eng.topology(self.topo)
+        if self.topo is None:  # device_gen: the graph is built in HBM (gossip_gen.h)
+            eng.generate(**self.gen)
+        else:
+            eng.topology(self.topo)
         self.apply_events(eng)
 
     def apply_events(self, eng):
@@ -92,30 +96,40 @@ def c1(partition: bool = False, rounds: int = 260, seed: int = BASE_SEED + 1):
     return wl, reads
 
 
-def c2(V: int = 1 << 20, K: int = 1024) -> Workload:
+# device_gen=True: no host CSR; Workload.apply builds the same graph on the
+# device (gossip_gen.h, bit-identical to the host builder)
+
+def c2(V: int = 1 << 20, K: int = 1024, device_gen: bool = False) -> Workload:
     """1M-node tree4, 1024 concurrent messages (1 Kbit sets), sync on, no partitions."""
     seed = BASE_SEED + 2
-    return Workload("C2", T.tree(V, 4), K, uniform_injections(V, K, seed), seed)
+    gen = dict(kind="tree", n=V, k=4)
+    return Workload("C2", None if device_gen else T.tree(V, 4), K, uniform_injections(V, K, seed), seed,
+                    gen=gen)
 
 
-def c3(V: int = 10_000_000, K: int = 1024) -> Workload:
+def c3(V: int = 10_000_000, K: int = 1024, device_gen: bool = False) -> Workload:
     """Random 8-regular, seeded random bisection in rounds [2,12) then healed, sync on."""
     seed = BASE_SEED + 3
-    return Workload("C3", T.random_regular(V, 8, seed), K, uniform_injections(V, K, seed), seed,
-                    windows=[("seeded", 2, 12, seed ^ 0x5EED)])
+    gen = dict(kind="random_regular", n=V, k=8, seed=seed)
+    return Workload("C3", None if device_gen else T.random_regular(V, 8, seed), K,
+                    uniform_injections(V, K, seed), seed, windows=[("seeded", 2, 12, seed ^ 0x5EED)], gen=gen)
 
 
-def c4(V: int = 100_000_000, K: int = 4096) -> Workload:
+def c4(V: int = 100_000_000, K: int = 4096, device_gen: bool = False) -> Workload:
     """R-MAT (.57,.19,.19,.05) edge factor 16, symmetrized; 4096 messages."""
     seed = BASE_SEED + 4
-    return Workload("C4", T.rmat(V, 16, seed=seed), K, uniform_injections(V, K, seed), seed)
+    gen = dict(kind="rmat", n=V, k=16, seed=seed, a=0.57, b=0.19, c=0.19)
+    return Workload("C4", None if device_gen else T.rmat(V, 16, seed=seed), K, uniform_injections(V, K, seed),
+                    seed, gen=gen)
 
 
-def c5(side: int = 32768, K: int = 64) -> Workload:
+def c5(side: int = 32768, K: int = 64, device_gen: bool = False) -> Workload:
     """side^2 grid + 1 long-range link per node (small world); 64 messages."""
     seed = BASE_SEED + 5
     V = side * side
-    return Workload("C5", T.grid_links(side, seed), K, uniform_injections(V, K, seed), seed)
+    gen = dict(kind="grid_links", n=side, seed=seed)
+    return Workload("C5", None if device_gen else T.grid_links(side, seed), K, uniform_injections(V, K, seed),
+                    seed, gen=gen)
 
 
 def by_name(name: str, **kw) -> Workload:

@@ -5,6 +5,7 @@ builders that define the graphs (host/topology.cpp).
    host builder's row_ptr and col exactly — every kind, edge sizes (1- and
    2-node trees, 2x2 grids, regular graphs small enough for self loops and
    duplicate pairs, R-MAT with rejection at non-power-of-two V and with hubs),
+   the multi-part sort plan forced to tiny parts (full-size C5 needs 4 parts),
    and full-size C2 (2^20-node tree4) and a 2^20-node grid.
 2. Same episodes: an engine whose topology was generated on the device and one
    given the host CSR through gg_topology run identical seeded episodes
@@ -53,6 +54,24 @@ CASES = [
 
 @pytest.mark.parametrize("kind,n,k,seed", CASES, ids=[f"{c[0]}-{c[1]}-{c[2]}" for c in CASES])
 def test_generated_csr_equals_host_builder(hip_lib, kind, n, k, seed):
+    host = HOST[kind](n, k, seed)
+    e, nnz = _generate(hip_lib, kind, n, k, seed)
+    got = e.export_topology()
+    assert nnz == host.nnz
+    assert np.array_equal(got.row_ptr, host.row_ptr)
+    assert np.array_equal(got.col, host.col)
+
+
+MULTI = [("random_regular", 5000, 8, 14), ("rmat", 1 << 14, 16, 25), ("grid_links", 101, 0, 34),
+         ("rmat", 3, 16, 22)]
+
+
+@pytest.mark.parametrize("part_keys", [1, 1000, 20000])
+@pytest.mark.parametrize("kind,n,k,seed", MULTI, ids=[f"{c[0]}-{c[1]}" for c in MULTI])
+def test_generated_csr_in_many_sort_parts(hip_lib, monkeypatch, kind, n, k, seed, part_keys):
+    """The row-range part plan (one radix sort per part, < 2^32 keys each at
+    full size) forced down to tiny parts: same CSR as the host builder."""
+    monkeypatch.setenv("GG_GEN_PART_KEYS", str(part_keys))
     host = HOST[kind](n, k, seed)
     e, nnz = _generate(hip_lib, kind, n, k, seed)
     got = e.export_topology()

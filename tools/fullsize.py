@@ -48,6 +48,9 @@ def main():
     ap.add_argument("--max-rounds", type=int, default=200)
     ap.add_argument("--sample", type=int, default=20000)
     ap.add_argument("--no-sync", action="store_true")
+    ap.add_argument("--device-gen", action="store_true",
+                    help="build the graph in HBM (gossip_gen.h) instead of on the host; the CSR is "
+                         "exported back only for the host-side facts")
     ap.add_argument("--json")
     args = ap.parse_args()
     import torch
@@ -59,13 +62,19 @@ def main():
     if args.lanes:
         kw["K"] = args.lanes
     t0 = time.time()
-    wl = by_name(args.config, **kw)
+    wl = by_name(args.config, device_gen=args.device_gen, **kw)
     if args.no_sync:
         wl.enable_sync = False
-    topo = wl.topo
-    V, K = topo.n_nodes, len(wl.injections)
-    log(f"{wl.name}: V={V} E={topo.nnz} K={K} W={wl.n_lanes} sync={wl.enable_sync} "
-        f"windows={[w[:3] for w in wl.windows]} (built in {time.time() - t0:.1f}s)")
+    K = len(wl.injections)
+    if wl.topo is not None:
+        V = wl.topo.n_nodes
+        log(f"{wl.name}: V={V} E={wl.topo.nnz} K={K} W={wl.n_lanes} sync={wl.enable_sync} "
+            f"windows={[w[:3] for w in wl.windows]} (host CSR built in {time.time() - t0:.1f}s)")
+    else:
+        g = wl.gen
+        V = g["n"] * g["n"] if g["kind"] == "grid_links" else g["n"]
+        log(f"{wl.name}: V={V} K={K} W={wl.n_lanes} sync={wl.enable_sync} "
+            f"windows={[w[:3] for w in wl.windows]} (graph built on the device: {g})")
     free0 = torch.cuda.mem_get_info(0)[0]
     t1 = time.time()
     eng = Engine(V, wl.n_lanes, seed=wl.seed, sync_base=wl.sync_base, sync_jitter=wl.sync_jitter,
@@ -73,7 +82,14 @@ def main():
     wl.apply(eng)
     torch.cuda.synchronize()
     footprint = free0 - torch.cuda.mem_get_info(0)[0]
-    log(f"engine ready in {time.time() - t1:.1f}s, HBM footprint {footprint / 2**30:.2f} GiB")
+    ready_s = time.time() - t1
+    log(f"engine ready in {ready_s:.1f}s ({'device-built graph' if wl.topo is None else 'host CSR upload'}), "
+        f"HBM footprint {footprint / 2**30:.2f} GiB")
+    if wl.topo is None:
+        t = time.time()
+        wl.topo = eng.export_topology()
+        log(f"exported the generated CSR for the host facts in {time.time() - t:.1f}s (E={wl.topo.nnz})")
+    topo = wl.topo
 
     # host-side facts for the properties
     t2 = time.time()
@@ -162,7 +178,8 @@ def main():
     out = {"config": wl.name, "nodes": V, "edges": int(topo.nnz), "lanes": wl.n_lanes, "messages": K,
            "rounds": R, "rounds_to_full_delivery": last_deliv + 1, "deliveries": dl,
            "episode_s": el, "deliveries_per_s": dl / el, "device_ms": eng.step_device_ms(),
-           "hbm_footprint_GiB": footprint / 2**30, "inter_node_msgs": msgs, "msgs_per_op": msgs / K,
+           "hbm_footprint_GiB": footprint / 2**30,
+           "topology_source": "device generator" if args.device_gen else "host CSR", "engine_ready_s": ready_s, "inter_node_msgs": msgs, "msgs_per_op": msgs / K,
            "kernels": kinds, "oracle": bool(ref), "properties_failed": fails}
     log(json.dumps(out))
     if args.json:
