@@ -40,7 +40,6 @@ namespace gg_gen {
 namespace {
 
 constexpr unsigned kBlk = 256;
-constexpr uint64_t kSentinel = ~0ull;
 
 struct DevRng {  // the host builders' splitmix64 stream (host/topology.cpp:28-35)
     uint64_t s;
@@ -107,16 +106,16 @@ __device__ __forceinline__ bool pair_at(const GenParams& g, uint64_t slot, uint6
 }
 
 __global__ void tree_csr(uint64_t V, uint32_t k, int64_t* rp, uint32_t* col, uint32_t col_or) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > V) return;
-    // row i starts after the i-1 parent links of rows 1..i-1 and the
-    // min(V-1, i*k) child links of rows 0..i-1 (ggh_tree, host/topology.cpp:121)
-    const int64_t start = (int64_t)(i ? i - 1 : 0) + (int64_t)std::min<uint64_t>(V - 1, i * k);
-    rp[i] = i == V ? (int64_t)(2 * (V - 1)) : start;
-    if (i == V) return;
-    int64_t p = start;
-    if (i > 0) col[p++] = (uint32_t)((i - 1) / k) | col_or;
-    for (uint64_t c = i * k + 1; c <= i * k + k && c < V; ++c) col[p++] = (uint32_t)c | col_or;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= V; i += (uint64_t)gridDim.x * blockDim.x) {
+        // row i starts after the i-1 parent links of rows 1..i-1 and the
+        // min(V-1, i*k) child links of rows 0..i-1 (ggh_tree, host/topology.cpp:121)
+        const int64_t start = (int64_t)(i ? i - 1 : 0) + (int64_t)std::min<uint64_t>(V - 1, i * k);
+        rp[i] = i == V ? (int64_t)(2 * (V - 1)) : start;
+        if (i == V) continue;
+        int64_t p = start;
+        if (i > 0) col[p++] = (uint32_t)((i - 1) / k) | col_or;
+        for (uint64_t c = i * k + 1; c <= i * k + k && c < V; ++c) col[p++] = (uint32_t)c | col_or;
+    }
 }
 
 constexpr int kBuckets = 1024;  // row buckets of the part plan
@@ -175,47 +174,39 @@ __global__ __launch_bounds__(kBlk) void emit_keys(GenParams g, uint64_t pairs, u
 // first[r] = index of the first sorted key of row r (rows without keys take the
 // next row's index); first[V] = M
 __global__ void row_bounds(const uint64_t* keys, uint64_t M, uint64_t V, uint32_t cb, int64_t* first) {
-    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k > M) return;
-    auto row = [&](uint64_t i) -> uint64_t {
-        if (i >= M) return V;
-        const uint64_t key = keys[i];
-        return key == kSentinel ? V : key >> cb;
-    };
-    const uint64_t r = row(k);
-    const uint64_t prev = k ? row(k - 1) : 0;
-    const uint64_t lo = k ? prev + 1 : 0;
-    for (uint64_t q = lo; q <= r && q <= V; ++q) first[q] = (int64_t)k;
+    auto row = [&](uint64_t i) -> uint64_t { return i >= M ? V : keys[i] >> cb; };
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= M; k += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = row(k);
+        const uint64_t lo = k ? row(k - 1) + 1 : 0;
+        for (uint64_t q = lo; q <= r && q <= V; ++q) first[q] = (int64_t)k;
+    }
 }
 
 __global__ void row_count(const uint64_t* keys, const int64_t* first, uint64_t V, int64_t* cnt) {
-    const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v > V) return;
-    if (v == V) {
-        cnt[V] = 0;
-        return;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v <= V; v += (uint64_t)gridDim.x * blockDim.x) {
+        int64_t c = 0;
+        uint64_t last = ~0ull;  // never a key: rows are < 2^cb - 1
+        if (v < V)
+            for (int64_t i = first[v]; i < first[v + 1]; ++i) {
+                const uint64_t key = keys[i];
+                c += key != last;
+                last = key;
+            }
+        cnt[v] = c;
     }
-    int64_t c = 0;
-    uint64_t last = kSentinel;
-    for (int64_t i = first[v]; i < first[v + 1]; ++i) {
-        const uint64_t key = keys[i];
-        c += key != last;
-        last = key;
-    }
-    cnt[v] = c;
 }
 
 __global__ void row_write(const uint64_t* keys, const int64_t* first, const int64_t* rp, uint64_t V, uint32_t cb,
                           uint32_t col_or, uint32_t* col) {
-    const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= V) return;
     const uint64_t cmask = (1ull << cb) - 1;
-    int64_t p = rp[v];
-    uint64_t last = kSentinel;
-    for (int64_t i = first[v]; i < first[v + 1]; ++i) {
-        const uint64_t key = keys[i];
-        if (key != last) col[p++] = (uint32_t)(key & cmask) | col_or;
-        last = key;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V; v += (uint64_t)gridDim.x * blockDim.x) {
+        int64_t p = rp[v];
+        uint64_t last = ~0ull;
+        for (int64_t i = first[v]; i < first[v + 1]; ++i) {
+            const uint64_t key = keys[i];
+            if (key != last) col[p++] = (uint32_t)(key & cmask) | col_or;
+            last = key;
+        }
     }
 }
 
@@ -233,7 +224,10 @@ __global__ void degree_max(const int64_t* rp, uint64_t V, unsigned long long* ou
     if (threadIdx.x == 0) atomicMax(out, s[0]);
 }
 
-unsigned grid_of(uint64_t n) { return (unsigned)((n + kBlk - 1) / kBlk); }
+// Grids are capped and every kernel strides: a dispatch's grid size in
+// work-items is a 32-bit field, so 2^32 or more threads (6.4e9 keys at C5)
+// cannot be launched one per item.
+unsigned grid_of(uint64_t n) { return (unsigned)std::min<uint64_t>((n + kBlk - 1) / kBlk, 1u << 16); }
 
 // host/topology.cpp:100-106 (the permutation is part of the graph's definition)
 std::vector<uint32_t> permutation(uint64_t V, uint64_t seed) {
@@ -360,7 +354,7 @@ int build_csr(const gg_gen_spec& s, hipStream_t st, uint32_t col_or, Csr* out, s
     unsigned long long* d_hist = nullptr;
     GCHK(mem.alloc(&d_hist, (kBuckets + kMaxParts) * 8));
     GCHK(hipMemsetAsync(d_hist, 0, kBuckets * 8, st));
-    const unsigned gblocks = (unsigned)std::min<uint64_t>(grid_of(pairs), 4096);
+    const unsigned gblocks = std::min(grid_of(pairs), 4096u);
     hipLaunchKernelGGL(bucket_hist, dim3(gblocks), dim3(kBlk), 0, st, g, pairs, bshift, d_hist);
     GCHK(hipGetLastError());
     std::vector<unsigned long long> hist(kBuckets);
