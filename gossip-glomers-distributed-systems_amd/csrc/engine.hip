@@ -600,8 +600,9 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     if (a.n_own) {
         {
             // grid-stride over the nodes; a capped grid keeps the launch cheap in
-            // dense lean rounds, where it is a no-op (GG_PREP_BLOCKS: A/B knob)
-            static const uint64_t prep_cap = getenv("GG_PREP_BLOCKS") ? (uint64_t)atoi(getenv("GG_PREP_BLOCKS")) : 4096;
+            // dense lean rounds, where it is a no-op (C2 A/B: 1024 blocks 1.99 ms/episode,
+            // 4096 2.02, 256 2.10; GG_PREP_BLOCKS overrides)
+            static const uint64_t prep_cap = getenv("GG_PREP_BLOCKS") ? (uint64_t)atoi(getenv("GG_PREP_BLOCKS")) : 1024;
             const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((a.n_own + gg::kBlock - 1) / gg::kBlock, prep_cap));
             dim3 grid((unsigned)blocks), block(gg::kBlock);
             if (syncw_prep) {
