@@ -1262,11 +1262,12 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
 }
 
 // gossip_gen.h: the spec's graph built in HBM (csrc/generate.hip) and installed
-// as gg_topology would install the host builder's CSR: single engine, symmetric,
-// so the in-lists are the rows themselves with every entry reciprocal.
+// as gg_topology would install the host builder's CSR. Single engine:
+// symmetric, so the in-lists are the rows themselves with every entry
+// reciprocal and nothing crosses PCIe. Sharded: built on the device, then the
+// host partition path of gg_topology.
 int gg_topology_generate(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_out) {
     if (!e || !spec) return GG_EINVAL;
-    if (e->world != 1) return e->fail(GG_EINVAL, "gg_topology_generate: sharded engines take gg_topology");
     if (gg_gen::spec_nodes(*spec) != e->V) return e->fail(GG_EINVAL, "generator node count != engine n_nodes");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
@@ -1274,6 +1275,23 @@ int gg_topology_generate(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_ou
     e->have_topo = false;
     gg_gen::Csr g{};
     std::string err;
+    if (e->world != 1) {
+        // sharded: every rank builds the whole graph on its own device (no host
+        // generator), then takes the host path for the locality order, ghosts
+        // and send lists, which need the whole graph on the host anyway
+        int rc = gg_gen::build_csr(*spec, e->stream, 0u, &g, &err);
+        if (rc) return e->fail(rc, err);
+        std::vector<int64_t> rp(e->V + 1);
+        std::vector<int32_t> col(g.nnz);
+        hipError_t h1 = hipMemcpy(rp.data(), g.row_ptr, (e->V + 1) * 8, hipMemcpyDeviceToHost);
+        hipError_t h2 = g.nnz ? hipMemcpy(col.data(), g.col, g.nnz * 4, hipMemcpyDeviceToHost) : hipSuccess;
+        (void)hipFree(g.row_ptr);
+        (void)hipFree(g.col);
+        HIPCHK(h1);
+        HIPCHK(h2);
+        if (nnz_out) *nnz_out = g.nnz;
+        return gg_topology(e, rp.data(), col.data(), g.nnz);
+    }
     int rc = gg_gen::build_csr(*spec, e->stream, gg::kRecipBit, &g, &err);
     if (rc) return e->fail(rc, err);
     e->d_in_ptr = g.row_ptr;

@@ -16,8 +16,10 @@
  * to theirs (tests/test_gpu_generate.py). All generated graphs are symmetric.
  *
  * Only the HIP library exports these entry points (the CPU oracle takes the
- * host builders' CSR through gg_topology). Single-engine (world == 1) only:
- * sharded engines take the whole graph through gg_topology.
+ * host builders' CSR through gg_topology). A single engine (world == 1) keeps
+ * the graph in HBM end to end; a sharded engine builds it on its device, then
+ * copies it to the host for gg_topology's partition step (locality order,
+ * ghosts, send lists), so no rank runs the host generator.
  */
 #ifndef GOSSIP_GEN_H_
 #define GOSSIP_GEN_H_
@@ -51,7 +53,7 @@ typedef struct {
  * receives the number of directed adjacency entries. */
 int gg_topology_generate(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_out);
 
-/* Copy the installed topology back as CSR (single engine): row v = the nodes
+/* Copy the installed topology back as CSR (single engine only): row v = the nodes
  * that send to v, ascending — for a symmetric topology, topology[v] itself.
  * row_ptr has n_nodes + 1 entries; col holds cap entries (GG_EINVAL if the
  * graph has more; *nnz_out is set either way). col may be NULL to query nnz. */

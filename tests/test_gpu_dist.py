@@ -103,3 +103,62 @@ def test_sharded_equals_single(hip_lib, world):
         allown = np.sort(np.concatenate(owned_all))
         assert np.array_equal(allown, np.arange(sc.topo.n_nodes)), k
         single.close()
+
+
+def _gen_worker(rank, world, port, lib, spec, W, inj, rounds, q):
+    import torch
+    import torch.distributed as dist
+
+    from ggamd.dist import ShardedRunner
+    from ggamd.engine import Engine
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        e = Engine(spec["V"], W, seed=3, sync_base=6, sync_jitter=4, device=0, rank=rank, world=world, library=lib)
+        e.generate(**spec["gen"])
+        for n, v, r in inj:
+            e.broadcast(n, v, r)
+        stats = ShardedRunner(e, torch.device("cuda", 0)).step(rounds)
+        owned = e.dist_owned()
+        q.put((rank, stats, owned, e.read_bits_nodes(owned)))
+        e.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["grid_links", "tree"])
+def test_sharded_engine_with_device_generated_topology(hip_lib, kind):
+    """gg_topology_generate on a sharded engine (device build, host partition
+    step) equals one engine given the host builder's CSR."""
+    from ggamd import topology as T
+    from ggamd.engine import Engine
+    from ggamd.workload import uniform_injections
+    if kind == "grid_links":
+        spec = {"V": 40 * 40, "gen": dict(kind="grid_links", n=40, seed=77)}
+        topo = T.grid_links(40, 77)
+    else:
+        spec = {"V": 3000, "gen": dict(kind="tree", n=3000, k=4)}
+        topo = T.tree(3000, 4)
+    W, rounds, world = 128, 24, 2
+    inj = uniform_injections(spec["V"], 100, 5)
+    ref = Engine(spec["V"], W, seed=3, sync_base=6, sync_jitter=4, device=0, library=hip_lib)
+    ref.topology(topo)
+    for n, v, r in inj:
+        ref.broadcast(n, v, r)
+    want = ref.step(rounds)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gen_worker, args=(r, world, port, hip_lib, spec, W, inj, rounds, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    stats = res[0][1]
+    d = diff_stats(stats, want)
+    assert not d, d[:10]
+    bits = ref.read_bits()
+    for _, _, owned, got in res:
+        assert np.array_equal(got, bits[owned])
