@@ -1010,6 +1010,10 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
     }
     const bool dense = dense_round(a);
     const uint32_t n_items = dense ? (uint32_t)a.n_own : a.n_work[1];
+    if ((uint64_t)blockIdx.x * NGB >= n_items) {  // sparse round: no item reaches this block
+        noop_exit(a, K_STREAM, t_start);
+        return;
+    }
     // per-lane counts that fit 32 bits stay 32-bit (register budget)
     uint32_t c_new = 0, c_active = 0, c_gathers = 0, c_nact = 0;
     unsigned long long c_fwd = 0, c_hash = 0, c_bytes = 0;
@@ -1305,6 +1309,10 @@ void expand_stream1(RoundArgs a) {
     }
     const bool dense = dense_round(a);
     const uint32_t n_items = dense ? (uint32_t)a.n_own : a.n_work[1];
+    if ((uint64_t)blockIdx.x * kBlock >= n_items) {  // sparse round: no item reaches this block
+        noop_exit(a, K_STREAM, t_start);
+        return;
+    }
     uint32_t c_new = 0, c_active = 0, c_gathers = 0, c_nact = 0;
     unsigned long long c_fwd = 0, c_hash = 0, c_bytes = 0;
     const uint32_t stride = gridDim.x * kBlock;
