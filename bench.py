@@ -8,8 +8,10 @@ timers on, no partitions; the episode is reset -> inject -> lockstep rounds
 until the round after the last delivery (quiescence, fixed during warmup).
 `value` = all (node,msg) deliveries of the timed episodes on all ranks / the
 max-over-ranks wall time. On N GPUs the tree has N * 2^20 nodes, vertex-range
-sharded (locality order), with one RCCL all-to-all of ghost payloads per round ("scaling":
-"weak").
+sharded (locality order), with one exchange of ghost payloads per round ("scaling":
+"weak"): the engine's own grouped RCCL send/recv on its stream (checked once
+against torch's all_to_all_single during warmup, which it falls back to on a
+mismatch; GG_DIST_TRANSPORT=torch forces that), named in config["exchange"].
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
 For N > 1 launch under torch.distributed.run (one process per GPU).
@@ -128,17 +130,38 @@ def main():
             return eng.step(n, raw=True)  # dicts built after the timed region
         return runner.step(n, reduce=False)
 
-    # warmup 0: find the quiescence round with per-round global counts
+    # warmup 0: find the quiescence round with per-round global counts (sharded:
+    # over torch's all_to_all_single, the reference for the engine exchange check)
+    engine_xch = runner is not None and runner.engine_comm
+    if engine_xch:
+        runner.engine_comm = False
     eng.reset()
     inject(eng, inj)
     R = 0
+    ref = []
     while True:
         st = runner.step(1)[0] if runner else eng.step(1)[0]
+        ref.append(st)
         R += 1
         if st["new_bits"] == 0 and R > 1:
             break
         if R > 400:
             raise RuntimeError("no quiescence within 400 rounds")
+    if engine_xch:
+        # one episode over the engine-owned RCCL exchange must reproduce every
+        # round's global counters; the reduced counts are identical on every
+        # rank, so all ranks take the same decision
+        from ggamd.engine import COUNT_FIELDS
+        runner.engine_comm = True
+        eng.reset()
+        inject(eng, inj)
+        chk = runner.step(R)
+        if any(a[f] != b[f] for a, b in zip(ref, chk) for f in COUNT_FIELDS):
+            runner.engine_comm = False
+            runner.transport = "torch all_to_all_single (engine exchange failed its check)"
+            if rank == 0:
+                print("bench: engine RCCL exchange disagrees with all_to_all_single; using torch",
+                      file=sys.stderr)
 
     event_ms = []
 
@@ -225,6 +248,7 @@ def main():
                 "inter_node_msgs_per_step": msgs,
                 "msgs_per_op": msgs / K,
                 "parallelism": f"vertex-range x{world}" if world > 1 else "single GPU",
+                "exchange": runner.transport if runner is not None else None,
                 "shard": dinfo,
             },
             "roofline": {

@@ -15,7 +15,9 @@
 // exclusion, `:52`). Local rows: the owned nodes first, then (sharded mode,
 // from ghost0 on) read-only ghost copies of the remote nodes adjacent to them,
 // refreshed every round by the exchange (pack_ghosts / unpack_ghosts).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -24,6 +26,7 @@
 #include <map>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <unordered_map>
 #include <vector>
 
@@ -214,6 +217,8 @@ struct gg_engine {
     BatchKey graph_key;
     bool graph_broken = false;
 
+    ncclComm_t comm = nullptr;  // engine-owned RCCL communicator (gg_dist_comm_init)
+
     int fail(int code, const std::string& m) {
         err = m;
         return code;
@@ -280,9 +285,13 @@ void gg_engine::free_topology() {
     have_topo = false;
 }
 
+static void rccl_destroy(ncclComm_t c);
+
 gg_engine::~gg_engine() {
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
+    if (comm) rccl_destroy(comm);
+    comm = nullptr;
     free_topology();
     dfree(d_counters);
     dfree(d_inj);
@@ -1598,6 +1607,140 @@ int gg_dist_flush(gg_engine* e, gg_round_stats* out, uint64_t cap, uint64_t* n_o
     if (cap < n) return e->fail(GG_EINVAL, "stats buffer too small");
     for (uint64_t i = 0; i < n; ++i) out[i] = e->dist_done[i];
     e->dist_done.clear();
+    return GG_OK;
+}
+
+// ---- engine-owned RCCL exchange ------------------------------------------------
+// The ghost exchange as grouped ncclSend/ncclRecv on the engine stream, one pair
+// per peer rank with a non-empty segment (sizes match pairwise: rank p's send
+// segment to q is q's receive segment from p). The RCCL entry points are
+// resolved at run time from the copy already loaded in the process (PyTorch's,
+// when it drives the ranks; same soname), else librccl.so.1 (or GG_RCCL_LIB),
+// so a process never holds two RCCL builds.
+}  // extern "C"
+namespace {
+struct RcclApi {
+    bool ok = false;
+    std::string why;
+    ncclResult_t (*get_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    const char* (*errstr)(ncclResult_t) = nullptr;
+};
+
+RcclApi load_rccl() {
+    RcclApi r;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) {
+        const char* path = getenv("GG_RCCL_LIB");
+        h = dlopen(path && *path ? path : "librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    }
+    if (!h) {
+        r.why = std::string("RCCL not loadable: ") + dlerror();
+        return r;
+    }
+    bool all = true;
+    auto get = [&](auto& fn, const char* name) {
+        fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+        if (!fn) {
+            all = false;
+            r.why = std::string("RCCL symbol missing: ") + name;
+        }
+    };
+    get(r.get_id, "ncclGetUniqueId");
+    get(r.init_rank, "ncclCommInitRank");
+    get(r.destroy, "ncclCommAbort");  // local teardown: no wait on peers at exit
+    get(r.send, "ncclSend");
+    get(r.recv, "ncclRecv");
+    get(r.group_start, "ncclGroupStart");
+    get(r.group_end, "ncclGroupEnd");
+    get(r.errstr, "ncclGetErrorString");
+    r.ok = all;
+    return r;
+}
+
+const RcclApi& rccl() {
+    static const RcclApi api = load_rccl();
+    return api;
+}
+}  // namespace
+
+// (the engine stream is synchronised first, so no operation of ours is pending)
+static void rccl_destroy(ncclComm_t c) {
+    if (rccl().ok) (void)rccl().destroy(c);
+}
+extern "C" {
+
+#define NCCLCHK(x)                                                                         \
+    do {                                                                                   \
+        ncclResult_t r_ = (x);                                                             \
+        if (r_ != ncclSuccess) return e->fail(GG_EIO, std::string(#x) + ": " + rccl().errstr(r_)); \
+    } while (0)
+
+int gg_dist_comm_available(char* why, uint64_t cap) {
+    const RcclApi& r = rccl();
+    if (why && cap) {
+        std::snprintf(why, cap, "%s", r.ok ? "" : r.why.c_str());
+    }
+    return r.ok ? GG_OK : GG_EIO;
+}
+
+int gg_dist_comm_id(uint8_t* id_out) {
+    if (!id_out) return GG_EINVAL;
+    const RcclApi& r = rccl();
+    if (!r.ok) return GG_EIO;
+    ncclUniqueId id;
+    if (r.get_id(&id) != ncclSuccess) return GG_EIO;
+    std::memcpy(id_out, &id, sizeof(id));
+    return GG_OK;
+}
+
+int gg_dist_comm_init(gg_engine* e, const uint8_t* id_in) {
+    if (!e || !id_in) return GG_EINVAL;
+    if (e->world < 2) return e->fail(GG_EINVAL, "not a sharded engine (world == 1)");
+    if (e->comm) return e->fail(GG_EINVAL, "communicator already set");
+    const RcclApi& r = rccl();
+    if (!r.ok) return e->fail(GG_EIO, r.why);
+    HIPCHK(hipSetDevice(e->device));
+    ncclUniqueId id;
+    std::memcpy(&id, id_in, sizeof(id));
+    ncclComm_t c = nullptr;
+    NCCLCHK(r.init_rank(&c, (int)e->world, id, (int)e->rank));
+    e->comm = c;
+    return GG_OK;
+}
+
+int gg_dist_step(gg_engine* e, uint32_t n_rounds) {
+    if (!e) return GG_EINVAL;
+    if (!e->comm) return e->fail(GG_EINVAL, "no communicator (gg_dist_comm_init)");
+    const RcclApi& r = rccl();
+    for (uint32_t k = 0; k < n_rounds; ++k) {
+        gg_exchange x{};
+        int rc = gg_dist_round_begin(e, &x);
+        if (rc) return rc;
+        const uint64_t pb = x.send_total / std::max<uint64_t>(1, e->send_off[e->world]);
+        const uint64_t pr = x.recv_total / std::max<uint64_t>(1, e->recv_off[e->world]);
+        if (x.send_bytes[e->rank])  // own segment (empty by construction): a local copy
+            HIPCHK(hipMemcpyAsync((uint8_t*)x.recv + e->recv_off[e->rank] * pr,
+                                  (const uint8_t*)x.send + e->send_off[e->rank] * pb, x.send_bytes[e->rank],
+                                  hipMemcpyDeviceToDevice, e->stream));
+        NCCLCHK(r.group_start());
+        for (uint32_t q = 0; q < e->world; ++q) {
+            if (q == e->rank) continue;
+            if (x.send_bytes[q])
+                NCCLCHK(r.send((const uint8_t*)x.send + e->send_off[q] * pb, x.send_bytes[q], ncclUint8, (int)q,
+                               e->comm, e->stream));
+            if (x.recv_bytes[q])
+                NCCLCHK(r.recv((uint8_t*)x.recv + e->recv_off[q] * pr, x.recv_bytes[q], ncclUint8, (int)q, e->comm,
+                               e->stream));
+        }
+        NCCLCHK(r.group_end());
+        if ((rc = gg_dist_round_end(e, nullptr))) return rc;
+    }
     return GG_OK;
 }
 

@@ -13,16 +13,22 @@ network delivery of every forward/push/read/read_ok crossing a shard boundary
     all_to_all_single     -> per-peer byte counts from the engine
     gg_dist_round_end     -> unpack kernel into this rank's ghost rows
 
-On GPUs the backend is "nccl" (= RCCL over xGMI on ROCm): the collective is
-enqueued on the engine's own HIP stream (torch.cuda.ExternalStream), so a
-multi-round step runs without host synchronisation and the per-round counters
-are collected once at the end (gg_dist_flush) and summed over ranks with one
-all_reduce. With "gloo" (CPU tests, or several ranks sharing one GPU in the GPU
+On GPUs the backend is "nccl" (= RCCL over xGMI on ROCm). By default `step`
+hands the exchange to the engine: rank 0 makes an RCCL unique id, torch
+broadcasts it, every engine opens its own communicator (gg_dist_comm_init) and
+gg_dist_step(n) runs n rounds with grouped ncclSend/ncclRecv of the non-empty
+segments on the engine stream, with no Python and no cross-stream event hop per
+round. GG_DIST_TRANSPORT=torch (or transport="torch") keeps the per-round
+all_to_all_single through torch instead, enqueued on the engine's own HIP stream
+(torch.cuda.ExternalStream). Either way a multi-round step runs without host
+synchronisation and the per-round counters are collected once at the end
+(gg_dist_flush) and summed over ranks with one all_reduce. With "gloo" (CPU tests, or several ranks sharing one GPU in the GPU
 tests) the payloads are staged through host memory.
 """
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 import torch
@@ -49,7 +55,7 @@ def _view(ptr: int, nbytes: int, on_device: bool, device: torch.device) -> torch
 
 
 class ShardedRunner:
-    def __init__(self, eng: Engine, device: torch.device, group=None):
+    def __init__(self, eng: Engine, device: torch.device, group=None, transport: str | None = None):
         self.eng = eng
         self.device = device
         self.group = group
@@ -59,6 +65,28 @@ class ShardedRunner:
         self.nccl = dist.get_backend(group) == "nccl"
         self._views = {}   # (ptr, bytes, on_device) -> tensor view of engine memory
         self._streams = {}  # stream ptr -> torch.cuda.ExternalStream
+        want = transport or os.environ.get("GG_DIST_TRANSPORT", "engine")
+        if want not in ("engine", "torch"):
+            raise ValueError(f"transport {want!r}: 'engine' or 'torch'")
+        self.engine_comm = self.nccl and want == "engine" and self._init_engine_comm()
+        self.transport = "engine RCCL send/recv" if self.engine_comm else (
+            "torch all_to_all_single" if self.nccl else "gloo via host")
+
+    def _init_engine_comm(self) -> bool:
+        """Open the engine's own RCCL communicator if every rank can (agreed by
+        an all_reduce first, so no rank waits in a collective init alone)."""
+        ok, why = self.eng.dist_comm_available()
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        if int(flag.item()) == 0:
+            return False
+        uid = torch.zeros(128, dtype=torch.uint8, device=self.device)
+        if self.rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(self.eng.dist_comm_id()), dtype=torch.uint8))
+        src = 0 if self.group is None else dist.get_global_rank(self.group, 0)
+        dist.broadcast(uid, src=src, group=self.group)
+        self.eng.dist_comm_init(uid.cpu().numpy().tobytes())
+        return True
 
     def _view(self, ptr, nbytes, on_dev):
         key = (ptr, nbytes, on_dev)
@@ -107,8 +135,11 @@ class ShardedRunner:
         return self.eng.dist_round_end(wait=wait)
 
     def step(self, n_rounds: int, reduce: bool = True) -> list[dict]:
-        for _ in range(n_rounds):
-            self.round(wait=False)
+        if self.engine_comm:
+            self.eng.dist_step(n_rounds)
+        else:
+            for _ in range(n_rounds):
+                self.round(wait=False)
         local = self.eng.dist_flush()
         return self.reduce(local) if reduce else local
 

@@ -108,6 +108,7 @@ GG_SYMBOLS = [
     "gg_current_round", "gg_step_device_ms", "gg_read", "gg_read_bits", "gg_delivery_rounds", "gg_reset",
     "gg_read_bits_nodes", "gg_delivery_rounds_nodes",
     "gg_dist_round_begin", "gg_dist_round_end", "gg_dist_flush", "gg_dist_owned", "gg_dist_info",
+    "gg_dist_comm_available", "gg_dist_comm_id", "gg_dist_comm_init", "gg_dist_step",
 ]
 
 _LIBS: dict[str, C.CDLL] = {}
@@ -147,6 +148,10 @@ def load_library(path: str) -> C.CDLL:
     lib.gg_dist_owned.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]
     lib.gg_dist_info.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_uint64)]
     lib.gg_read_bits_nodes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+    lib.gg_dist_comm_available.argtypes = [C.c_char_p, C.c_uint64]
+    lib.gg_dist_comm_id.argtypes = [C.c_void_p]
+    lib.gg_dist_comm_init.argtypes = [C.c_void_p, C.c_void_p]
+    lib.gg_dist_step.argtypes = [C.c_void_p, C.c_uint32]
     lib.gg_delivery_rounds_nodes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
     if hasattr(lib, "gg_topology_generate"):
         lib.gg_topology_generate.argtypes = [C.c_void_p, P(GGGenSpec), P(C.c_uint64)]
@@ -351,6 +356,28 @@ class Engine:
         s = GGRoundStats()
         self._ok(self.lib.gg_dist_round_end(self.h, C.byref(s)))
         return stats_dict(s)
+
+    def dist_comm_available(self) -> tuple[bool, str]:
+        """Do the RCCL entry points resolve in this process (engine-owned exchange)?"""
+        buf = C.create_string_buffer(256)
+        rc = self.lib.gg_dist_comm_available(buf, 256)
+        return rc == 0, buf.value.decode()
+
+    def dist_comm_id(self) -> bytes:
+        buf = (C.c_uint8 * 128)()
+        rc = self.lib.gg_dist_comm_id(buf)
+        if rc:
+            raise RuntimeError(f"gg_dist_comm_id failed ({rc})")
+        return bytes(buf)
+
+    def dist_comm_init(self, uid: bytes) -> None:
+        assert len(uid) == 128
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self._ok(self.lib.gg_dist_comm_init(self.h, buf))
+
+    def dist_step(self, n_rounds: int) -> None:
+        """n sharded rounds with the engine's own RCCL exchange; counters pending (dist_flush)."""
+        self._ok(self.lib.gg_dist_step(self.h, n_rounds))
 
     def dist_flush(self) -> list[dict]:
         n = C.c_uint64(0)

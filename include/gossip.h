@@ -184,6 +184,21 @@ int gg_dist_info(const gg_engine* e, uint64_t* n_own, uint64_t* n_ghost, uint64_
 /* Original ids of the owned nodes (n_out = count, even if > cap). */
 int gg_dist_owned(const gg_engine* e, uint32_t* nodes, uint64_t cap, uint64_t* n_out);
 
+/* Engine-owned exchange over RCCL (GPU engines): the rounds run without a caller
+ * collective. Every rank of the sharded job passes the same 128-byte id (rank 0
+ * makes it with gg_dist_comm_id and the caller broadcasts it); gg_dist_comm_init
+ * is collective (all ranks call it together). gg_dist_step(n) then enqueues n
+ * rounds, each gg_dist_round_begin + grouped ncclSend/ncclRecv of the non-empty
+ * segments on the engine stream + gg_dist_round_end(NULL); counters stay pending
+ * for gg_dist_flush. Replaces the per-round all_to_all_single the caller would
+ * issue (the network delivery of every cross-shard message, broadcast.go:55,99,106,120).
+ * gg_dist_comm_available: 0 if the RCCL entry points resolve in this process
+ * (why = reason otherwise); the CPU oracle library has no RCCL and returns GG_EIO. */
+int gg_dist_comm_available(char* why, uint64_t cap);
+int gg_dist_comm_id(uint8_t* id_out /* 128 bytes */);
+int gg_dist_comm_init(gg_engine* e, const uint8_t* id /* 128 bytes */);
+int gg_dist_step(gg_engine* e, uint32_t n_rounds);
+
 /* gg_read_bits / gg_delivery_rounds for a list of owned nodes (any engine). */
 int gg_read_bits_nodes(gg_engine* e, const uint32_t* nodes, uint64_t n, uint64_t* out);
 int gg_delivery_rounds_nodes(gg_engine* e, const uint32_t* nodes, uint64_t n, int32_t* out);

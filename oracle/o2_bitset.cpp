@@ -635,6 +635,16 @@ int gg_dist_flush(gg_engine* e, gg_round_stats* out, uint64_t cap, uint64_t* n_o
     return GG_OK;
 }
 
+// The engine-owned RCCL exchange is GPU-only: the oracle's ranks exchange
+// through the caller (gg_dist_round_begin/end) and these report GG_EIO.
+int gg_dist_comm_available(char* why, uint64_t cap) {
+    if (why && cap) std::snprintf(why, cap, "%s", "CPU oracle: no RCCL");
+    return GG_EIO;
+}
+int gg_dist_comm_id(uint8_t*) { return GG_EIO; }
+int gg_dist_comm_init(gg_engine* e, const uint8_t*) { return e ? e->fail(GG_EIO, "CPU oracle: no RCCL") : GG_EINVAL; }
+int gg_dist_step(gg_engine* e, uint32_t) { return e ? e->fail(GG_EIO, "CPU oracle: no RCCL") : GG_EINVAL; }
+
 static bool owned(const gg_engine* e, uint64_t a, uint64_t b) { return a <= b && a >= e->lo && b <= e->hi; }
 
 int gg_read(gg_engine* e, uint32_t node, int64_t* out, uint64_t cap, uint64_t* n_out) {

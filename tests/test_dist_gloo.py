@@ -86,3 +86,19 @@ def test_random_three_ranks(cpu_lib):
     rnd = random.Random(11)
     sc = random_scenario(rnd, max_v=200, W=64, rounds=45)
     _check(cpu_lib, sc, world=3)
+
+
+def test_oracle_has_no_rccl(cpu_lib):
+    """The CPU oracle exports the engine-owned exchange symbols but has no RCCL:
+    each reports GG_EIO, so a caller falls back to its own collective."""
+    from ggamd.engine import Engine, GGError
+    e = Engine(16, 64, library=cpu_lib, rank=0, world=2)
+    ok, why = e.dist_comm_available()
+    assert not ok and "no RCCL" in why
+    with pytest.raises(RuntimeError):
+        e.dist_comm_id()
+    with pytest.raises(GGError):
+        e.dist_comm_init(bytes(128))
+    with pytest.raises(GGError):
+        e.dist_step(1)
+    e.close()

@@ -162,3 +162,29 @@ def test_sharded_engine_with_device_generated_topology(hip_lib, kind):
     bits = ref.read_bits()
     for _, _, owned, got in res:
         assert np.array_equal(got, bits[owned])
+
+
+def test_engine_rccl_plumbing():
+    """The engine-owned exchange (gg_dist_comm_*, gg_dist_step) in one process:
+    RCCL resolves from the copy torch loaded, a unique id comes back, and the
+    error paths hold (a world-1 engine cannot open a communicator; a sharded
+    engine without one cannot step). Two ranks on one device are refused by
+    RCCL itself (tools/nccl_probe.py), so the grouped send/recv runs only in the
+    driver's multi-GPU bench; its segments are the ones the gloo tests above
+    move and check."""
+    import torch  # noqa: F401  (loads torch's RCCL, as the bench does)
+
+    from ggamd.engine import Engine, GGError, HIP_LIB, Topology
+    e1 = Engine(64, 64, device=0, library=HIP_LIB)
+    ok, why = e1.dist_comm_available()
+    assert ok, why
+    uid = e1.dist_comm_id()
+    assert len(uid) == 128 and any(uid)
+    with pytest.raises(GGError):
+        e1.dist_comm_init(uid)
+    e2 = Engine(64, 64, device=0, rank=0, world=2, library=HIP_LIB)
+    e2.topology(Topology.from_rows([sorted({(v + 1) % 64, (v + 63) % 64}) for v in range(64)]))
+    with pytest.raises(GGError, match="no communicator"):
+        e2.dist_step(1)
+    e1.close()
+    e2.close()
