@@ -102,3 +102,27 @@ def test_oracle_has_no_rccl(cpu_lib):
     with pytest.raises(GGError):
         e.dist_step(1)
     e.close()
+
+
+def test_runner_transport_choice(cpu_lib):
+    """ShardedRunner picks the engine-owned exchange only on nccl; gloo moves the
+    payloads through the caller; an unknown transport name is an error."""
+    import torch.distributed as dist
+
+    from ggamd.dist import ShardedRunner
+    from ggamd.engine import Engine
+    dist.init_process_group("gloo", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{_free_port()}")
+    try:
+        e = Engine(16, 64, library=cpu_lib)
+        r = ShardedRunner(e, torch_device_cpu())
+        assert not r.engine_comm and r.transport == "gloo via host"
+        with pytest.raises(ValueError):
+            ShardedRunner(e, torch_device_cpu(), transport="mpi")
+        e.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def torch_device_cpu():
+    import torch
+    return torch.device("cpu")
