@@ -1729,16 +1729,19 @@ int gg_dist_step(gg_engine* e, uint32_t n_rounds) {
                                   (const uint8_t*)x.send + e->send_off[e->rank] * pb, x.send_bytes[e->rank],
                                   hipMemcpyDeviceToDevice, e->stream));
         NCCLCHK(r.group_start());
-        for (uint32_t q = 0; q < e->world; ++q) {
+        ncclResult_t first = ncclSuccess;  // the group is always closed, even after a failed call
+        for (uint32_t q = 0; q < e->world && first == ncclSuccess; ++q) {
             if (q == e->rank) continue;
             if (x.send_bytes[q])
-                NCCLCHK(r.send((const uint8_t*)x.send + e->send_off[q] * pb, x.send_bytes[q], ncclUint8, (int)q,
-                               e->comm, e->stream));
-            if (x.recv_bytes[q])
-                NCCLCHK(r.recv((uint8_t*)x.recv + e->recv_off[q] * pr, x.recv_bytes[q], ncclUint8, (int)q, e->comm,
-                               e->stream));
+                first = r.send((const uint8_t*)x.send + e->send_off[q] * pb, x.send_bytes[q], ncclUint8, (int)q,
+                               e->comm, e->stream);
+            if (first == ncclSuccess && x.recv_bytes[q])
+                first = r.recv((uint8_t*)x.recv + e->recv_off[q] * pr, x.recv_bytes[q], ncclUint8, (int)q, e->comm,
+                               e->stream);
         }
-        NCCLCHK(r.group_end());
+        const ncclResult_t ge = r.group_end();
+        NCCLCHK(first);
+        NCCLCHK(ge);
         if ((rc = gg_dist_round_end(e, nullptr))) return rc;
     }
     return GG_OK;
