@@ -1,19 +1,30 @@
 #!/usr/bin/env python3
 """Benchmark: (node,msg) deliveries/s of the gossip-propagation engine.
 
-One *step* = one full propagation episode of config C2 (BASELINE.json
-configs[1]): a 4-ary tree (Maelstrom `tree4`) of 2^20 nodes per GPU, K = 1024
-fresh messages broadcast by clients at seeded uniform nodes in round 0, sync
-timers on, no partitions; the episode is reset -> inject -> lockstep rounds
-until the round after the last delivery (quiescence, fixed during warmup).
-`value` = all (node,msg) deliveries of the timed episodes on all ranks / the
-max-over-ranks wall time. On N GPUs the tree has N * 2^20 nodes, vertex-range
-sharded (locality order), with one exchange of ghost payloads per round ("scaling":
-"weak"): the engine's own grouped RCCL send/recv on its stream (checked once
-against torch's all_to_all_single during warmup, which it falls back to on a
-mismatch; GG_DIST_TRANSPORT=torch forces that), named in config["exchange"].
+One *step* = one full propagation episode: reset -> the clients' broadcasts ->
+lockstep rounds until the round after the last delivery (quiescence, fixed
+during warmup). `value` = all (node,msg) deliveries of the timed episodes on
+all ranks / the max-over-ranks wall time.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+--config C2 (default; BASELINE.json configs[1]): a 4-ary tree (Maelstrom
+  `tree4`) of 2^20 nodes per GPU, K = 1024 fresh messages broadcast by clients
+  at seeded uniform nodes in round 0, sync timers on, no partitions. On N GPUs
+  the tree has N * 2^20 nodes, vertex-range sharded (locality order) with one
+  exchange of ghost payloads per round ("scaling": "weak"): the engine's own
+  grouped RCCL send/recv on its stream.
+--config C4 (configs[3], the 100M-node config the >= 6x scaling target is
+  quoted on): R-MAT (.57,.19,.19,.05), edge factor 16, 10^8 nodes, K = 4096
+  messages in round 0. Strong scaling: the graph is fixed and the ranks split
+  the 4096 message lanes (gg_config.lane_groups = N): every GPU holds the whole
+  CSR (13 GB of its 288 GB) and 4096/N lanes of every node, so a round needs no
+  exchange at all; the per-round counters are summed with one all_reduce after
+  the timed episodes.
+
+N > 1: after the timed region rank 0 runs one episode of a single unsharded
+engine over the whole graph on its own GPU and every round's global counters
+must equal it, else the run exits with status 1.
+
+Usage: python bench.py [--config C2|C4] [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
 For N > 1 launch under torch.distributed.run (one process per GPU).
 """
 from __future__ import annotations
@@ -33,19 +44,20 @@ import numpy as np  # noqa: E402
 METRIC = "(node,msg) deliveries/sec at 1/2/4/8 GPUs; % of HBM roofline; msgs/op"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
-
 KERNELS = {"prep": "round_prep", "expand": "expand_round", "stream": "expand_stream"}
 TRAFFIC_JSON = os.path.join(REPO, "profiles", "traffic.json")
+CPU_LIB = os.path.join(REPO, "oracle", "_build", "libgossip_cpu.so")
 
 
-def pmc_traffic(kernel: str):
+def pmc_traffic(kernel: str, config: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (tools/traffic.py: FETCH_SIZE and WRITE_SIZE in separate passes over this
     same bench command, FETCH_SIZE doubled for gfx950). None if not profiled."""
     try:
-        import json as _j
-        d = _j.load(open(TRAFFIC_JSON))
+        d = json.load(open(TRAFFIC_JSON))
     except (OSError, ValueError):
+        return None, None
+    if d.get("config", "C2") != config:
         return None, None
     for name, ent in d.get("kernels", {}).items():
         if name.split("(")[0].split("<")[0].split("::")[-1] == kernel:
@@ -67,15 +79,21 @@ def next_pow2(x: int) -> int:
     return p
 
 
+def cpu_counts():
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return os.cpu_count() or 1, aff or 1
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C2", choices=["C2", "C4"])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--nodes-per-gpu", type=int, default=1 << 20)
-    ap.add_argument("--lanes", type=int, default=1024)
+    ap.add_argument("--nodes", type=int, help="C2: nodes per GPU (2^20); C4: nodes (10^8)")
+    ap.add_argument("--lanes", type=int, help="C2: 1024; C4: 4096")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-episodes", type=int, default=2)
+    ap.add_argument("--no-check", action="store_true", help="skip the N > 1 single-engine check")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 "
                     "(nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
     args = ap.parse_args()
@@ -84,16 +102,14 @@ def main():
     import torch.distributed as dist
 
     from ggamd import topology as T
-    from ggamd.engine import Engine
-    from ggamd.engine import stats_dict
+    from ggamd.engine import COUNT_FIELDS, Engine, stats_dict
     from ggamd.workload import BASE_SEED, inject, injection_arrays, uniform_injections
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+    if world != args.gpus and world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
     if args.backend == "gloo":  # rehearsal: every rank on the one visible GPU
         local = 0
     torch.cuda.set_device(local)
@@ -104,19 +120,6 @@ def main():
         else:
             dist.init_process_group(args.backend)
 
-    V = args.nodes_per_gpu * world
-    K = args.lanes
-    seed = BASE_SEED + 2
-    topo = T.tree(V, 4)
-    inj = uniform_injections(V, K, seed)
-    inj_arr = injection_arrays(inj)  # converted once, outside the timed loop
-    eng = Engine(V, K, seed=seed, enable_sync=True, device=local, rank=rank, world=world)
-    eng.topology(topo)
-    runner = None
-    if world > 1:
-        from ggamd.dist import ShardedRunner
-        runner = ShardedRunner(eng, device)
-
     def barrier():
         if world > 1:
             if args.backend == "nccl":
@@ -125,43 +128,71 @@ def main():
                 dist.barrier()
         torch.cuda.synchronize()
 
+    def allreduce_i64(vals, op=None):
+        t = torch.tensor(vals, dtype=torch.int64, device=device if args.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=op or dist.ReduceOp.SUM)
+        return t.cpu().tolist()
+
+    cfg = args.config
+    free0 = torch.cuda.mem_get_info(local)[0]
+    t_setup = time.perf_counter()
+    runner = None
+    if cfg == "C2":
+        V = (args.nodes or (1 << 20)) * world
+        K = args.lanes or 1024
+        seed = BASE_SEED + 2
+        topo = T.tree(V, 4)
+        gen = None
+        E = int(topo.nnz)
+        eng = Engine(V, K, seed=seed, enable_sync=True, device=local, rank=rank, world=world)
+        eng.topology(topo)
+        if world > 1:
+            from ggamd.dist import ShardedRunner
+            runner = ShardedRunner(eng, device)
+        parallelism = f"vertex-range x{world}" if world > 1 else "single GPU"
+        scaling = "weak"
+        workload = ("C2: tree4 of 2^20 nodes per GPU, 1024 messages broadcast in round 0 at seeded uniform "
+                    "nodes, sync on, no partitions; one step = one episode to quiescence")
+    else:
+        V = args.nodes or 100_000_000
+        K = args.lanes or 4096
+        seed = BASE_SEED + 4
+        topo = None
+        gen = dict(kind="rmat", n=V, k=16, seed=seed, a=0.57, b=0.19, c=0.19)
+        eng = Engine(V, K, seed=seed, enable_sync=True, device=local, rank=rank, world=world,
+                     lane_groups=world)
+        E = eng.generate(**gen)  # the whole graph in this GPU's HBM (gossip_gen.h)
+        parallelism = f"message lanes x{world} (every GPU: whole graph, {K // world} lanes)" \
+            if world > 1 else "single GPU"
+        scaling = "strong"
+        workload = (f"C4: R-MAT (.57,.19,.19,.05) edge factor 16, symmetrized, {V} nodes, {K} messages "
+                    "broadcast in round 0 at seeded uniform nodes, sync on, no partitions; graph built "
+                    "in HBM by the on-device generator; one step = one episode to quiescence")
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t_setup
+    hbm_bytes = free0 - torch.cuda.mem_get_info(local)[0]
+    inj = uniform_injections(V, K, seed)
+    inj_arr = injection_arrays(inj)  # converted once, outside the timed loop
+
     def run_rounds(n):
         if runner is None:
             return eng.step(n, raw=True)  # dicts built after the timed region
         return runner.step(n, reduce=False)
 
-    # warmup 0: find the quiescence round with per-round global counts (sharded:
-    # over torch's all_to_all_single, the reference for the engine exchange check)
-    engine_xch = runner is not None and runner.engine_comm
-    if engine_xch:
-        runner.engine_comm = False
+    # warmup 0: the quiescence round R from per-round global counts
     eng.reset()
-    inject(eng, inj)
+    inject(eng, inj_arr)
     R = 0
-    ref = []
     while True:
         st = runner.step(1)[0] if runner else eng.step(1)[0]
-        ref.append(st)
+        nb = st["new_bits"]
+        if world > 1 and runner is None:  # lane groups: sum over the ranks
+            nb = allreduce_i64([nb])[0]
         R += 1
-        if st["new_bits"] == 0 and R > 1:
+        if nb == 0 and R > 1:
             break
         if R > 400:
             raise RuntimeError("no quiescence within 400 rounds")
-    if engine_xch:
-        # one episode over the engine-owned RCCL exchange must reproduce every
-        # round's global counters; the reduced counts are identical on every
-        # rank, so all ranks take the same decision
-        from ggamd.engine import COUNT_FIELDS
-        runner.engine_comm = True
-        eng.reset()
-        inject(eng, inj)
-        chk = runner.step(R)
-        if any(a[f] != b[f] for a, b in zip(ref, chk) for f in COUNT_FIELDS):
-            runner.engine_comm = False
-            runner.transport = "torch all_to_all_single (engine exchange failed its check)"
-            if rank == 0:
-                print("bench: engine RCCL exchange disagrees with all_to_all_single; using torch",
-                      file=sys.stderr)
 
     event_ms = []
 
@@ -188,27 +219,25 @@ def main():
     if runner is None:
         local_stats = [[stats_dict(a[i]) for i in range(R)] for a in local_stats]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=device if args.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        per_ep = [runner.reduce(s) for s in local_stats]
+        elapsed = float(allreduce_i64([int(elapsed * 1e9)], dist.ReduceOp.MAX)[0]) / 1e9
+        per_ep = [reduce_counts(s, allreduce_i64, COUNT_FIELDS) for s in local_stats]
     else:
         per_ep = local_stats
     deliveries = sum(s["new_bits"] for ep in per_ep for s in ep)
-    msgs = sum(s["fwd_sent"] + s["pushes"] + s["acks"] + s["reads"] + s["read_oks"]
-               for s in per_ep[-1])
+    msgs = sum(s["fwd_sent"] + s["pushes"] + s["acks"] + s["reads"] + s["read_oks"] for s in per_ep[-1])
+
     # roofline of the dominant kernel: per-kind device times (first block start
     # to last block end of each launch, stamped by the kernels) and the bytes
-    # each launch had to move (counted by the kernels)
-    dinfo = eng.dist_info() if world > 1 else None
-    if world > 1:
+    # each launch had to move (counted by the kernels); this rank's
+    dinfo = None
+    if runner is not None:
+        dinfo = eng.dist_info()
         owned = eng.dist_owned().astype(np.int64)
         n_own = int(owned.size)
         E_own = int((topo.row_ptr[owned + 1] - topo.row_ptr[owned]).sum())
     else:
-        n_own, E_own = V, int(topo.nnz)
-    nwp = next_pow2(K // 64)
+        n_own, E_own = V, E
+    nwp = next_pow2(K // 64 // (world if cfg == "C4" else 1))
     rounds_local = [s for ep in local_stats for s in ep]
     kinds = {}
     for kind, name in KERNELS.items():
@@ -220,9 +249,38 @@ def main():
     dom = max(kinds, key=lambda k: kinds[k]["total_ms"])
     D = kinds[dom]
     achieved = D["GBps"]
-    traffic, traffic_src = pmc_traffic(D["kernel"])
+    traffic, traffic_src = pmc_traffic(D["kernel"], cfg)
     round_ms = sum(s["kernel_ms"] for s in rounds_local)
     round_bytes = sum(s["prep_bytes"] + s["expand_bytes"] + s["stream_bytes"] for s in rounds_local)
+    xbytes = None
+    if runner is not None:  # payload bytes this rank sent per round (mean over the timed rounds)
+        xbytes = sum(s["sent_bytes"] for s in rounds_local) / len(rounds_local)
+
+    # N > 1: the sharded job must reproduce one unsharded engine, round by round
+    check = None
+    if world > 1 and not args.no_check:
+        bad = 0
+        if rank == 0:
+            eng.close()  # free this rank's shard before building the whole graph
+            ref = Engine(V, K, seed=seed, enable_sync=True, device=local)
+            if gen is None:
+                ref.topology(topo)
+            else:
+                ref.generate(**gen)
+            inject(ref, inj_arr)
+            want = ref.step(R)
+            ref.close()
+            diffs = [f"round {a['round']} {f}: sharded {a[f]} != single {b[f]}"
+                     for a, b in zip(per_ep[-1], want) for f in COUNT_FIELDS if a[f] != b[f]]
+            bad = len(diffs)
+            if diffs:
+                print("bench: sharded run differs from the single engine:", diffs[:8], file=sys.stderr)
+        bad = allreduce_i64([bad])[0]
+        check = "every round's global counters equal one unsharded engine" if bad == 0 else "FAILED"
+        if bad:
+            if world > 1:
+                dist.destroy_process_group()
+            raise SystemExit(1)
 
     if rank == 0:
         value = deliveries / elapsed
@@ -235,21 +293,25 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic (seeded tree4 topology, seeded client broadcasts)",
+            "data": f"synthetic (seeded {'tree4' if cfg == 'C2' else 'R-MAT'} topology, seeded client broadcasts)",
             "config": {
-                "workload": "C2: tree4 of 2^20 nodes per GPU, 1024 messages broadcast in round 0 "
-                            "at seeded uniform nodes, sync on, no partitions; one step = one "
-                            "episode to quiescence",
-                "nodes": V, "edges": int(topo.nnz), "lanes": K, "rounds_per_step": R,
+                "workload": workload,
+                "nodes": V, "edges": E, "lanes": K, "rounds_per_step": R,
                 "deliveries_per_step": deliveries // args.steps,
                 "inter_node_msgs_per_step": msgs,
                 "msgs_per_op": msgs / K,
-                "parallelism": f"vertex-range x{world}" if world > 1 else "single GPU",
-                "exchange": runner.transport if runner is not None else None,
+                "parallelism": parallelism,
+                "exchange": (runner.transport if runner is not None else
+                             ("none: lane groups never exchange; one all_reduce of the counters "
+                              "after the timed episodes" if world > 1 else None)),
+                "exchange_bytes_per_round_rank0": xbytes,
                 "shard": dinfo,
+                "hbm_bytes_rank0": hbm_bytes,
+                "setup_s_rank0": setup_s,
+                "check": check,
             },
             "roofline": {
                 "bound": "hbm",
@@ -268,42 +330,122 @@ def main():
                           "block end of that kernel, stamped by every block (no-op launches included, as in "
                           "rocprofv3's average); cross-check: HIP events around each step's launch sequence "
                           "on the engine stream",
-                "kernels": {k: {kk: v for kk, v in d.items()} for k, d in kinds.items()},
+                "kernels": {k: dict(d) for k, d in kinds.items()},
                 "round_GBps": round_bytes / (round_ms * 1e-3) / 1e9 if round_ms > 0 else 0.0,
                 "event_ms_per_step": (sum(event_ms) / len(event_ms)) if event_ms else None,
                 "stamp_ms_per_step": round_ms / args.steps,
             },
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(topo, inj, V, K, seed, R, args.cpu_episodes)
+        if world == 1 and not args.no_cpu_baseline and os.path.exists(CPU_LIB):
+            out["cpu_baseline"] = cpu_baseline(cfg, topo, inj, V, K, seed, R)
         print(json.dumps(out), flush=True)
     if world > 1:
         barrier()
         dist.destroy_process_group()
 
 
-def cpu_baseline(topo, inj, V, K, seed, R, episodes):
-    """The O2 bitset oracle (same semantics, CPU restatement of the reference
-    handlers) timed on this host's cores over `episodes` full C2 episodes."""
+def reduce_counts(stats, allreduce_i64, fields):
+    """Sum one episode's per-round counters over the ranks (seen_hash mod 2^64)."""
+    M = (1 << 64) - 1
+    flat = []
+    for s in stats:
+        for f in fields:
+            v = s[f] & M
+            flat.append(v - (1 << 64) if v >= (1 << 63) else v)
+    tot = allreduce_i64(flat)
+    out, k = [], 0
+    for s in stats:
+        d = dict(s)
+        for f in fields:
+            d[f] = tot[k] & M
+            k += 1
+        out.append(d)
+    return out
+
+
+def cpu_baseline(cfg, topo, inj, V, K, seed, R):
+    """The oracle restatements on this host's cores (reported beside the GPU
+    number, not the target). Legs: O2 (bitset, C++) on the box's CPU share, O2
+    on one thread, and O1 (message-level literal restatement of the handlers,
+    Python) on C1 per inter-node message — the cost of the reference's own
+    per-message Send/handler path in kind. Each leg is a bounded sample."""
+    from ggamd import topology as T
     from ggamd.engine import Engine
-    from ggamd.workload import inject
-    lib = os.path.join(REPO, "oracle", "_build", "libgossip_cpu.so")
-    if not os.path.exists(lib):
-        return None
-    threads = min(16, os.cpu_count() or 1)
-    os.environ["GG_CPU_THREADS"] = str(threads)
-    e = Engine(V, K, seed=seed, enable_sync=True, library=lib)
-    e.topology(topo)
-    dl = 0
+    from ggamd.workload import BASE_SEED, inject, uniform_injections
+    host_cpus, affinity = cpu_counts()
+    threads = min(16, affinity)  # the box's CPU share for one GPU
+
+    def o2_episodes(topo_, inj_, V_, K_, seed_, thr, budget_s, rounds=None):
+        os.environ["GG_CPU_THREADS"] = str(thr)
+        e = Engine(V_, K_, seed=seed_, enable_sync=True, library=CPU_LIB)
+        e.topology(topo_)
+        dl, eps, t0 = 0, 0, time.perf_counter()
+        while True:
+            e.reset()
+            inject(e, inj_)
+            if rounds is None:  # to quiescence
+                r = 0
+                while True:
+                    s = e.step(1)[0]
+                    dl += s["new_bits"]
+                    r += 1
+                    if s["new_bits"] == 0 and r > 1:
+                        break
+                rounds = r
+            else:
+                dl += sum(s["new_bits"] for s in e.step(rounds))
+            eps += 1
+            if time.perf_counter() - t0 >= budget_s:
+                break
+        dt = time.perf_counter() - t0
+        e.close()
+        return dl / dt, eps, rounds, dt
+
+    if cfg == "C2":
+        v_all, n_all, r_all, _ = o2_episodes(topo, inj, V, K, seed, threads, 8.0, R)
+        sample_all = f"{n_all} full C2 episodes ({r_all} rounds each)"
+        v_one, n_one, r_one, _ = o2_episodes(topo, inj, V, K, seed, 1, 6.0, R)
+        sample_one = f"{n_one} full C2 episode(s) on one thread"
+    else:  # C4: R-MAT samples of the same generator (the 10^8-node graph needs ~150 GB of host state)
+        Va = 1 << 20
+        ta = T.rmat(Va, 16, seed=seed)
+        v_all, n_all, r_all, _ = o2_episodes(ta, uniform_injections(Va, K, seed), Va, K, seed, threads, 1.0)
+        sample_all = f"{n_all} episode(s) to quiescence ({r_all} rounds) of the same R-MAT generator at 2^20 nodes"
+        V1 = 1 << 17
+        t1 = T.rmat(V1, 16, seed=seed)
+        v_one, n_one, r_one, _ = o2_episodes(t1, uniform_injections(V1, K, seed), V1, K, seed, 1, 1.0)
+        sample_one = f"{n_one} episode(s) ({r_one} rounds) of the R-MAT generator at 2^17 nodes on one thread"
+    o1 = o1_c1_leg()
+    return {"value": v_all, "unit": "deliveries/s", "cores": threads, "kind": "port",
+            "sample": f"O2 bitset oracle (oracle/o2_bitset.cpp, -O3, AVX-512 host) on {threads} threads: "
+                      f"{sample_all}",
+            "host_cpus": host_cpus, "affinity_cpus": affinity,
+            "single_thread": {"value": v_one, "unit": "deliveries/s", "cores": 1, "sample": sample_one},
+            "o1_per_message": o1}
+
+
+def o1_c1_leg():
+    """O1 (oracle/o1_literal.py: every Send/Reply/RPC a message object through an
+    in-memory network, handlers restated statement by statement) on config C1:
+    inter-node messages and deliveries per second of one thread."""
+    sys.path.insert(0, REPO)
+    from oracle.o1_literal import O1Network
+    from ggamd.workload import c1
+    wl, _ = c1()
+    o = O1Network(25, wl.n_lanes, wl.seed, wl.sync_base, wl.sync_jitter, wl.enable_sync)
+    o.topology(wl.topo.rows())
+    for n, v, r in wl.injections:
+        o.broadcast(int(n), int(v), int(r))
     t0 = time.perf_counter()
-    for _ in range(episodes):
-        e.reset()
-        inject(e, inj)
-        dl += sum(s["new_bits"] for s in e.step(R))
+    st = o.step(wl.max_rounds)
     dt = time.perf_counter() - t0
-    return {"value": dl / dt, "unit": "deliveries/s", "cores": threads, "kind": "port",
-            "sample": f"{episodes} full C2 episodes ({R} rounds each) of the O2 bitset oracle"}
+    msgs = sum(s["fwd_sent"] + s["pushes"] + s["acks"] + s["reads"] + s["read_oks"] for s in st)
+    dl = sum(s["new_bits"] for s in st)
+    return {"value": msgs / dt, "unit": "inter-node messages/s", "cores": 1,
+            "deliveries_per_s": dl / dt, "messages": msgs, "seconds": dt,
+            "sample": f"C1 (25-node tree4, {len(wl.injections)} client broadcasts over 200 rounds, sync on), "
+                      f"{wl.max_rounds} rounds through O1's message-level network"}
 
 
 if __name__ == "__main__":

@@ -141,6 +141,11 @@ struct gg_engine {
     hipStream_t stream = nullptr;
     uint64_t V = 0, nw = 0, nwp = 0;
     uint32_t rank = 0, world = 1;
+    // 2-D sharding: world = L lane groups x P vertex parts; this engine holds lane
+    // words [w0, w0 + nw) of nw_g (its lane group lgrp) for the nodes of part `part`
+    uint32_t L = 1, P = 1, lgrp = 0, part = 0;
+    uint64_t nw_g = 0, w0 = 0;
+    uint32_t peer_rank(uint32_t q) const { return lgrp * P + q; }
     uint64_t n_own = 0, ghost0 = 0, n_ghost = 0, rows = 0;  // local rows: own, then ghosts
     std::vector<uint32_t> gid;     // [rows] original id of each local row (~0u: padding)
     std::vector<uint32_t> loc_of;  // [V] local row of an owned node, ~0u otherwise (sharded)
@@ -157,6 +162,7 @@ struct gg_engine {
     std::vector<uint64_t> xsend_bytes, xrecv_bytes;
     uint32_t dist_k = 0;                       // pending rounds (counter slots in use)
     std::vector<int64_t> dist_round_of;        // round of each pending slot
+    std::vector<uint64_t> dist_sent;           // payload bytes sent in each pending slot
     std::vector<gg_round_stats> dist_done;     // folded, not yet flushed
     size_t inj_off = 0;                        // pinned injection ring offset (async rounds)
     uint32_t quiet = 0;                        // trailing rounds without new bits (gg_step)
@@ -321,9 +327,9 @@ int reset_device_state(gg_engine* e) {
     // run to quiescence. Single engine only: ghost rows follow remote rounds.
     // After exactly one quiet round r only the buffers of round r-1 (parity
     // dirty_parity = (r+1) & 1, recorded by gg_reset) can hold non-zero rows.
-    if (!(e->world == 1 && e->quiet >= 2)) {
+    if (!(e->P == 1 && e->quiet >= 2)) {
         for (int b = 0; b < 2; ++b) {
-            if (e->world == 1 && e->quiet == 1 && b != e->dirty_parity) continue;
+            if (e->P == 1 && e->quiet == 1 && b != e->dirty_parity) continue;
             seg(e->d_F[b], rowbytes, 0);  // F rows are zero unless ACT
             seg(e->d_flg[b], e->rows, 0);
         }
@@ -335,7 +341,7 @@ int reset_device_state(gg_engine* e) {
     seg(e->d_tile_cand, e->tile_bytes, 0);
     seg(e->d_act, 16, 0);
     const uint64_t n_own = e->n_own;
-    if (e->d_dr) seg(e->d_dr, n_own * e->cfg.n_lanes * 4, ~0ull);
+    if (e->d_dr) seg(e->d_dr, n_own * e->nw * 64 * 4, ~0ull);
     ra.sync_next = e->d_sync_next;
     ra.sync_k = e->d_sync_k;
     ra.n_own = n_own;
@@ -565,10 +571,6 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.sstate = e->d_sstate;
     a.ibits = e->d_ibits;
     a.n_mchunks = e->n_mchunks;
-    {
-        static const uint32_t ablate = getenv("GG_ABLATE") ? (uint32_t)atoi(getenv("GG_ABLATE")) : 0u;
-        a.ablate = ablate;  // diagnostic timing only
-    }
     a.fired_m1 = e->d_fired[(r - 1) & 3];
     a.fired_m2 = e->d_fired[(r - 2) & 3];
     a.fired_m3 = e->d_fired[(r - 3) & 3];
@@ -589,7 +591,9 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.own0 = 0;
     a.lo = 0;
     a.nwp = (uint32_t)e->nwp;
-    a.nw = (uint32_t)e->nw;
+    a.nw = (uint32_t)e->nw_g;
+    a.word0 = (uint32_t)e->w0;
+    a.count_nodes = e->lgrp == 0 ? 1u : 0u;
     a.round = r;
     a.seed = e->cfg.seed;
     a.sync_base = e->cfg.sync_base_ticks;
@@ -655,7 +659,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             const uint64_t n = a.n_own * e->nw;
             hipLaunchKernelGGL(gg::track_delivery, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream,
                                a.F_cur, a.flg_cur, e->d_dr, a.n_own, a.own0, (uint32_t)e->nwp, (uint32_t)e->nw,
-                               e->cfg.n_lanes, (int32_t)r);
+                               (uint32_t)(e->nw * 64), (int32_t)r);
             HIPCHK(hipGetLastError());
         }
     }
@@ -689,6 +693,7 @@ void fold_stats(gg_engine* e, const unsigned long long* slots, int64_t round, gg
     s->prep_bytes = c[gg::kBytes0 + gg::K_PREP];
     s->expand_bytes = c[gg::kBytes0 + gg::K_EXPAND];
     s->stream_bytes = c[gg::kBytes0 + gg::K_STREAM];
+    s->sent_bytes = 0;
     s->round = round;
     s->new_bits = c[gg::C_NEW];
     s->fwd_sent = c[gg::C_FWD_SENT];
@@ -749,7 +754,8 @@ size_t pack_injections(gg_engine* e, int64_t r0, uint32_t n, std::vector<size_t>
         const size_t b = tmp.size();
         for (const auto& x : it->second) {
             const uint32_t l = local_row(e, x.node);
-            if (l != ~0u) tmp.emplace_back(l, x.lane);
+            const uint64_t wd = x.lane >> 6;  // another lane group's value: not this engine's
+            if (l != ~0u && wd >= e->w0 && wd < e->w0 + e->nw) tmp.emplace_back(l, x.lane - 64 * (uint32_t)e->w0);
         }
         std::stable_sort(tmp.begin() + b, tmp.end(),
                          [](const auto& p, const auto& q) { return p.first < q.first; });
@@ -937,16 +943,24 @@ int gg_create(const gg_config* cfg, gg_engine** out) {
     if (cfg->n_lanes == 0 || cfg->n_lanes % 64 || cfg->n_lanes > 8192) return GG_EINVAL;
     if (cfg->enable_sync && cfg->sync_base_ticks == 0) return GG_EINVAL;
     if (cfg->world == 0 || cfg->rank >= cfg->world) return GG_EINVAL;
+    const uint32_t L = cfg->lane_groups ? cfg->lane_groups : 1u;
+    if (cfg->world % L || L > cfg->n_lanes / 64) return GG_EINVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GG_EIO;
     auto* e = new gg_engine();
     e->cfg = *cfg;
     e->lanes.init(cfg->n_lanes);
     e->V = cfg->n_nodes;
-    e->nw = cfg->n_lanes / 64;
-    e->nwp = next_pow2((uint32_t)e->nw);
     e->rank = cfg->rank;
     e->world = cfg->world;
+    e->L = L;
+    e->P = cfg->world / L;
+    e->lgrp = cfg->rank / e->P;
+    e->part = cfg->rank % e->P;
+    e->nw_g = cfg->n_lanes / 64;
+    e->w0 = e->nw_g * e->lgrp / L;
+    e->nw = e->nw_g * (e->lgrp + 1) / L - e->w0;
+    e->nwp = next_pow2((uint32_t)e->nw);
     if (cfg->device >= 0) {
         e->device = cfg->device;
         if (hipSetDevice(e->device) != hipSuccess) { delete e; return GG_EIO; }
@@ -1049,7 +1063,7 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     for (int b = 0; b < 4; ++b) HIPCHK(hipMalloc(&e->d_fired[b], e->rows / 8));
     HIPCHK(hipMalloc(&e->d_sync_next, std::max<uint64_t>(1, n_own) * 4));
     HIPCHK(hipMalloc(&e->d_sync_k, std::max<uint64_t>(1, n_own) * 4));
-    if (e->cfg.flags & GG_TRACK_DELIVERY) HIPCHK(hipMalloc(&e->d_dr, std::max<uint64_t>(1, n_own) * e->cfg.n_lanes * 4));
+    if (e->cfg.flags & GG_TRACK_DELIVERY) HIPCHK(hipMalloc(&e->d_dr, std::max<uint64_t>(1, n_own) * e->nw * 64 * 4));
     e->have_topo = true;
     e->quiet = 0;  // fresh buffers: clear everything
     e->dist_k = 0;
@@ -1122,7 +1136,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     }
     // ---- partition (sharded): a locality order of the nodes cut into
     // edge-balanced contiguous ranges; rank p owns order[plo[p] .. plo[p+1])
-    const uint32_t Wd = e->world;
+    const uint32_t Wd = e->P;  // vertex parts of this engine's lane group
     std::vector<uint32_t> order;    // position -> node (empty: identity)
     std::vector<uint64_t> plo;      // [Wd+1] position ranges
     std::vector<uint32_t> owner;    // node -> rank (sharded)
@@ -1132,26 +1146,28 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
         plo = {0, V};
     }
     auto node_at = [&](uint64_t pos) -> uint32_t { return order.empty() ? (uint32_t)pos : order[pos]; };
-    const uint64_t n_own = plo[e->rank + 1] - plo[e->rank];
+    const uint64_t n_own = plo[e->part + 1] - plo[e->part];
     e->n_own = n_own;
     e->loc_of.clear();
     e->gid.clear();
     std::vector<uint32_t> ghosts;                     // ghost nodes in local ghost order
     std::vector<std::vector<uint32_t>> sendl(Wd);     // owned local rows per destination
+    e->send_off.assign(Wd + 1, 0);
+    e->recv_off.assign(Wd + 1, 0);
     if (Wd > 1) {
         e->loc_of.assign(V, ~0u);
-        for (uint64_t i = 0; i < n_own; ++i) e->loc_of[node_at(plo[e->rank] + i)] = (uint32_t)i;
+        for (uint64_t i = 0; i < n_own; ++i) e->loc_of[node_at(plo[e->part] + i)] = (uint32_t)i;
         // ghosts: remote nodes adjacent (in or out) to owned ones; send lists:
         // owned nodes adjacent to each remote rank. Both sorted by node id, so
         // rank q's receive order from p equals p's send order to q.
         std::vector<std::vector<uint32_t>> gfrom(Wd);
         std::vector<uint32_t> peers;
         for (uint64_t i = 0; i < n_own; ++i) {
-            const uint32_t v = node_at(plo[e->rank] + i);
+            const uint32_t v = node_at(plo[e->part] + i);
             peers.clear();
             auto visit = [&](uint32_t u) {
                 const uint32_t q = owner[u];
-                if (q == e->rank) return;
+                if (q == e->part) return;
                 gfrom[q].push_back(u);
                 peers.push_back(q);
             };
@@ -1161,8 +1177,6 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
             peers.erase(std::unique(peers.begin(), peers.end()), peers.end());
             for (uint32_t q : peers) sendl[q].push_back(v);
         }
-        e->send_off.assign(Wd + 1, 0);
-        e->recv_off.assign(Wd + 1, 0);
         for (uint32_t q = 0; q < Wd; ++q) {
             auto& g = gfrom[q];
             std::sort(g.begin(), g.end());
@@ -1181,7 +1195,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     std::unordered_map<uint32_t, uint32_t> ghost_row;  // ghost node -> local row
     if (Wd > 1) {
         e->gid.assign(e->rows, ~0u);
-        for (uint64_t i = 0; i < n_own; ++i) e->gid[i] = node_at(plo[e->rank] + i);
+        for (uint64_t i = 0; i < n_own; ++i) e->gid[i] = node_at(plo[e->part] + i);
         ghost_row.reserve(ghosts.size() * 2);
         for (uint64_t k = 0; k < ghosts.size(); ++k) {
             e->gid[e->ghost0 + k] = ghosts[k];
@@ -1197,7 +1211,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     // (ascending receiver id: callback order) with local-row columns
     std::vector<int64_t> iptr(n_own + 1, 0), optr(n_own + 1, 0);
     for (uint64_t i = 0; i < n_own; ++i) {
-        const uint32_t v = node_at(plo[e->rank] + i);
+        const uint32_t v = node_at(plo[e->part] + i);
         iptr[i + 1] = iptr[i] + (tin[v + 1] - tin[v]);
         optr[i + 1] = optr[i] + (row_ptr[v + 1] - row_ptr[v]);
     }
@@ -1205,7 +1219,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     std::vector<int64_t> gcnt(e->n_ghost + 1, 0);
     auto build_rows = [&](uint64_t lo, uint64_t hi) {
         for (uint64_t i = lo; i < hi; ++i) {
-            const uint32_t v = node_at(plo[e->rank] + i);
+            const uint32_t v = node_at(plo[e->part] + i);
             const int32_t* ob = col + row_ptr[v];
             const int32_t* oe = col + row_ptr[v + 1];
             for (int64_t k = 0; k < tin[v + 1] - tin[v]; ++k) {
@@ -1284,7 +1298,7 @@ int gg_topology_generate(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_ou
     e->have_topo = false;
     gg_gen::Csr g{};
     std::string err;
-    if (e->world != 1) {
+    if (e->P != 1) {
         // sharded: every rank builds the whole graph on its own device (no host
         // generator), then takes the host path for the locality order, ghosts
         // and send lists, which need the whole graph on the host anyway
@@ -1329,7 +1343,7 @@ int gg_topology_generate(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_ou
 int gg_topology_export(gg_engine* e, int64_t* row_ptr, int32_t* col, uint64_t cap, uint64_t* nnz_out) {
     if (!e || !row_ptr) return GG_EINVAL;
     if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
-    if (e->world != 1) return e->fail(GG_EINVAL, "gg_topology_export: single engine only");
+    if (e->P != 1) return e->fail(GG_EINVAL, "gg_topology_export: vertex-sharded engine");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
     if (nnz_out) *nnz_out = e->n_in_edges;
@@ -1421,7 +1435,7 @@ int64_t gg_current_round(const gg_engine* e) { return e ? e->round : -1; }
 int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
     if (!e) return GG_EINVAL;
     if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
-    if (e->world != 1) return e->fail(GG_EINVAL, "sharded engine: use gg_dist_round_begin/end");
+    if (e->P != 1) return e->fail(GG_EINVAL, "vertex-sharded engine: use gg_dist_round_begin/end");
     HIPCHK(hipSetDevice(e->device));
     int rc = materialize_windows(e);
     if (rc) return rc;
@@ -1482,7 +1496,7 @@ int gg_dist_info(const gg_engine* e, uint64_t* n_own, uint64_t* n_ghost, uint64_
     if (!e || !e->have_topo) return GG_EINVAL;
     if (n_own) *n_own = e->n_own;
     if (n_ghost) *n_ghost = e->n_ghost;
-    if (n_send) *n_send = e->send_off.empty() ? 0 : e->send_off[e->world];
+    if (n_send) *n_send = e->send_off.empty() ? 0 : e->send_off[e->P];
     return GG_OK;
 }
 
@@ -1504,6 +1518,7 @@ static int fold_pending(gg_engine* e) {
     for (uint32_t k = 0; k < e->dist_k; ++k) {
         gg_round_stats s;
         fold_stats(e, e->h_counters + (size_t)k * gg::kSlots * gg::kCounters, e->dist_round_of[k], &s);
+        s.sent_bytes = e->dist_sent[k];
         e->dist_done.push_back(s);
     }
     e->dist_k = 0;
@@ -1539,7 +1554,7 @@ int gg_dist_round_begin(gg_engine* e, gg_exchange* x) {
     // next round may read remote sets: sync callbacks and push edges)
     const bool with_set = e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks;
     const uint64_t pb = exchange_stride(e->nwp, with_set);
-    const uint64_t n_send = e->send_off[e->world];
+    const uint64_t n_send = e->send_off[e->P];
     if (n_send) {
         const uint64_t chunks = n_send * (pb / 16);
         const unsigned blocks = (unsigned)std::min<uint64_t>((chunks + gg::kBlock - 1) / gg::kBlock, 4096);
@@ -1550,18 +1565,20 @@ int gg_dist_round_begin(gg_engine* e, gg_exchange* x) {
     }
     e->xsend_bytes.assign(e->world, 0);
     e->xrecv_bytes.assign(e->world, 0);
-    for (uint32_t q = 0; q < e->world; ++q) {
-        e->xsend_bytes[q] = (e->send_off[q + 1] - e->send_off[q]) * pb;
-        e->xrecv_bytes[q] = (e->recv_off[q + 1] - e->recv_off[q]) * pb;
+    for (uint32_t q = 0; q < e->P; ++q) {  // peers: the parts of this lane group
+        e->xsend_bytes[e->peer_rank(q)] = (e->send_off[q + 1] - e->send_off[q]) * pb;
+        e->xrecv_bytes[e->peer_rank(q)] = (e->recv_off[q + 1] - e->recv_off[q]) * pb;
     }
     if (e->dist_round_of.size() < kMaxBatch) e->dist_round_of.resize(kMaxBatch);
+    if (e->dist_sent.size() < kMaxBatch) e->dist_sent.resize(kMaxBatch);
     e->dist_round_of[e->dist_k] = r;
+    e->dist_sent[e->dist_k] = n_send * pb;
     x->send = e->d_xsend;
     x->recv = e->d_xrecv;
     x->send_bytes = e->xsend_bytes.data();
     x->recv_bytes = e->xrecv_bytes.data();
     x->send_total = n_send * pb;
-    x->recv_total = e->recv_off[e->world] * pb;
+    x->recv_total = e->recv_off[e->P] * pb;
     x->on_device = 1;
     x->stream = (void*)e->stream;
     e->dist_open = true;
@@ -1722,22 +1739,19 @@ int gg_dist_step(gg_engine* e, uint32_t n_rounds) {
         gg_exchange x{};
         int rc = gg_dist_round_begin(e, &x);
         if (rc) return rc;
-        const uint64_t pb = x.send_total / std::max<uint64_t>(1, e->send_off[e->world]);
-        const uint64_t pr = x.recv_total / std::max<uint64_t>(1, e->recv_off[e->world]);
-        if (x.send_bytes[e->rank])  // own segment (empty by construction): a local copy
-            HIPCHK(hipMemcpyAsync((uint8_t*)x.recv + e->recv_off[e->rank] * pr,
-                                  (const uint8_t*)x.send + e->send_off[e->rank] * pb, x.send_bytes[e->rank],
-                                  hipMemcpyDeviceToDevice, e->stream));
+        const uint64_t pb = x.send_total / std::max<uint64_t>(1, e->send_off[e->P]);
+        const uint64_t pr = x.recv_total / std::max<uint64_t>(1, e->recv_off[e->P]);
         NCCLCHK(r.group_start());
         ncclResult_t first = ncclSuccess;  // the group is always closed, even after a failed call
-        for (uint32_t q = 0; q < e->world && first == ncclSuccess; ++q) {
-            if (q == e->rank) continue;
-            if (x.send_bytes[q])
-                first = r.send((const uint8_t*)x.send + e->send_off[q] * pb, x.send_bytes[q], ncclUint8, (int)q,
+        for (uint32_t q = 0; q < e->P && first == ncclSuccess; ++q) {
+            if (q == e->part) continue;  // own segment: empty by construction
+            const uint32_t pr_q = e->peer_rank(q);
+            if (x.send_bytes[pr_q])
+                first = r.send((const uint8_t*)x.send + e->send_off[q] * pb, x.send_bytes[pr_q], ncclUint8,
+                               (int)pr_q, e->comm, e->stream);
+            if (first == ncclSuccess && x.recv_bytes[pr_q])
+                first = r.recv((uint8_t*)x.recv + e->recv_off[q] * pr, x.recv_bytes[pr_q], ncclUint8, (int)pr_q,
                                e->comm, e->stream);
-            if (first == ncclSuccess && x.recv_bytes[q])
-                first = r.recv((uint8_t*)x.recv + e->recv_off[q] * pr, x.recv_bytes[q], ncclUint8, (int)q, e->comm,
-                               e->stream);
         }
         const ncclResult_t ge = r.group_end();
         NCCLCHK(first);
@@ -1793,7 +1807,11 @@ static int read_bits_rows(gg_engine* e, const uint32_t* nodes, uint64_t n, uint6
     HIPCHK(hipSetDevice(e->device));
     std::vector<uint64_t> h;
     if ((rc = copy_rows(e, lo, hi, h))) return rc;
-    for (uint64_t k = 0; k < n; ++k) std::memcpy(out + k * e->nw, h.data() + (rows[k] - lo) * e->nwp, e->nw * 8);
+    // whole-job words per node; a lane-group engine fills only its own words
+    for (uint64_t k = 0; k < n; ++k) {
+        if (e->L > 1) std::memset(out + k * e->nw_g, 0, e->nw_g * 8);
+        std::memcpy(out + k * e->nw_g + e->w0, h.data() + (rows[k] - lo) * e->nwp, e->nw * 8);
+    }
     return GG_OK;
 }
 
@@ -1805,10 +1823,13 @@ static int delivery_rows(gg_engine* e, const uint32_t* nodes, uint64_t n, int32_
     if (rc) return rc;
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
-    const uint64_t W = e->cfg.n_lanes;
-    std::vector<int32_t> h((hi - lo) * W);
-    if (!h.empty()) HIPCHK(hipMemcpy(h.data(), e->d_dr + lo * W, h.size() * 4, hipMemcpyDeviceToHost));
-    for (uint64_t k = 0; k < n; ++k) std::memcpy(out + k * W, h.data() + (rows[k] - lo) * W, W * 4);
+    const uint64_t W = e->cfg.n_lanes, Wl = e->nw * 64;  // whole-job lanes, this engine's lanes
+    std::vector<int32_t> h((hi - lo) * Wl);
+    if (!h.empty()) HIPCHK(hipMemcpy(h.data(), e->d_dr + lo * Wl, h.size() * 4, hipMemcpyDeviceToHost));
+    for (uint64_t k = 0; k < n; ++k) {
+        if (e->L > 1) std::fill(out + k * W, out + (k + 1) * W, -1);
+        std::memcpy(out + k * W + 64 * e->w0, h.data() + (rows[k] - lo) * Wl, Wl * 4);
+    }
     return GG_OK;
 }
 
@@ -1820,11 +1841,11 @@ static std::vector<uint32_t> node_range(uint32_t a, uint32_t b) {
 
 int gg_read(gg_engine* e, uint32_t node, int64_t* out, uint64_t cap, uint64_t* n_out) {
     if (!e || !e->have_topo) return GG_EINVAL;
-    std::vector<uint64_t> h(e->nw);
+    std::vector<uint64_t> h(e->nw_g);
     int rc = read_bits_rows(e, &node, 1, h.data());
     if (rc) return rc;
-    std::vector<int64_t> vals;
-    for (uint64_t j = 0; j < e->nw; ++j) {
+    std::vector<int64_t> vals;  // a lane-group engine: the values of its own lanes
+    for (uint64_t j = 0; j < e->nw_g; ++j) {
         uint64_t x = h[j];
         while (x) {
             const int b = __builtin_ctzll(x);

@@ -168,15 +168,18 @@ struct RoundArgs {
     uint64_t ghost0, n_ghost;   // sharded: ghost rows ghost0 .. ghost0+n_ghost-1
     const int64_t* gout_ptr;    // [n_ghost+1] per ghost: the owned nodes it sends to
     const uint32_t* gout_col;
-    uint32_t nwp, nw;
+    uint32_t nwp;               // words per local row (power of two >= this engine's lane words)
+    uint32_t nw, word0;         // seen_hash index of local word j of node g: g * nw + word0 + j
+                                // (nw = words per node of the whole job; word0 = this engine's
+                                // first lane word: non-zero when ranks split the lanes)
+    uint32_t count_nodes;       // count node-level events (reads, read_oks, their drops, timers):
+                                // 1 on exactly one engine per node (lane group 0)
     uint32_t tile_nodes;        // NG of the expand kernel
     int32_t symmetric;          // out-lists == in-lists
     uint64_t n_edges;           // in_col entries of this engine
     uint64_t rows;              // replica rows
     int32_t stream_ok;          // lean round (no sync events in expand, no masks) with nwp >= 2:
                                 // expand_stream takes it when it is dense (dense_round)
-    uint32_t ablate;            // DIAGNOSTIC timing builds only (GG_ABLATE): 1 no row stores,
-                                // 2 no sender-row gathers, 4 no own-row loads, 8 no hash; results invalid
     int64_t round;
     uint64_t seed;
     uint32_t sync_base, sync_jitter;
@@ -494,10 +497,11 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
     unsigned long long acc[C_NUM];
 #pragma unroll
     for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
-    acc[C_READS] = c_reads;
-    acc[C_READ_OKS] = c_read_oks;
-    acc[C_DROPPED] = c_dropped;
-    acc[C_FIRED] = c_fired;
+    // node-level events happen once per node, not once per lane group
+    acc[C_READS] = a.count_nodes ? c_reads : 0;
+    acc[C_READ_OKS] = a.count_nodes ? c_read_oks : 0;
+    acc[C_DROPPED] = a.count_nodes ? c_dropped : 0;
+    acc[C_FIRED] = a.count_nodes ? c_fired : 0;
     acc[C_BYTES] = c_bytes;
     flush_counters(a, acc, s_red, t_start, K_PREP);
 }
@@ -657,7 +661,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
             lds_barrier();
 
             if (zm && !ca) {  // only the stale F row to clear
-                if (!(a.ablate & 1)) {
+                {
                     Row<WPL> z;
 #pragma unroll
                     for (int w = 0; w < WPL; ++w) z.w[w] = 0;
@@ -685,12 +689,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                 unsigned long long cb_new = 0, cb_new_deliv = 0, cb_new_ackdrop = 0;
                 unsigned long long push_sent = 0, push_deliv = 0, push_ackdrop = 0;
                 auto load_own = [&]() {
-                    if (a.ablate & 4) {
-#pragma unroll
-                        for (int w = 0; w < WPL; ++w) sp.w[w] = 0;
-                    } else {
-                        sp = load_row<WPL>(a.base + rep * a.nwp + off);
-                    }
+                    sp = load_row<WPL>(a.base + rep * a.nwp + off);
                     if (lag) {
                         const Row<WPL> f = load_row<WPL>(a.F_prev + rep * a.nwp + off);
 #pragma unroll
@@ -888,17 +887,16 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                     for (int w = 0; w < WPL; ++w) {
                         F.w[w] = S.w[w] & ~sp.w[w];
                         T += __popcll(F.w[w]);
-                        if (F.w[w] && !(a.ablate & 8)) {  // seen_hash delta of a changed word
-                            const uint64_t idx = g * a.nw + off + w;
+                        if (F.w[w]) {  // seen_hash delta of a changed word
+                            const uint64_t idx = g * a.nw + a.word0 + off + w;
                             c_hash += gg_word_hash(idx, S.w[w]) - (sp.w[w] ? gg_word_hash(idx, sp.w[w]) : 0ull);
                         }
                     }
                     const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
-                    if ((any || zm) && !(a.ablate & 1)) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
+                    if (any || zm) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
                     if (zm && lg == 0) a.zmark[rep] = 0;
                     nrows += (any || zm) ? 1 : 0;
-                    if (a.ablate & 1) {
-                    } else if (keep) {
+                    if (keep) {
                         if (lag) store_row<WPL>(a.base + rep * a.nwp + off, sp);
                         nrows += lag ? 1 : 0;
                     } else if (any || lag) {
@@ -937,7 +935,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                     Row<WPL> z;     // clear its stale F row (rows of inactive nodes are zero)
 #pragma unroll
                     for (int w = 0; w < WPL; ++w) z.w[w] = 0;
-                    if (!(a.ablate & 1)) store_row<WPL>(a.F_cur + rep * a.nwp + off, z);
+                    store_row<WPL>(a.F_cur + rep * a.nwp + off, z);
                     if (lg == 0) a.zmark[rep] = 0;
                     nrows++;
                 }
@@ -1041,12 +1039,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
     };
     auto fetch_meta = [&](uint32_t n, Meta& m) {
         m.node = n;
-        if (n < a.n_own && (a.ablate & 64)) {  // diagnostic: synthetic metadata
-            m.p0 = 2 * (int64_t)n;
-            m.deg = 2;
-            m.ca = 0;
-            m.fl = 0;
-        } else if (n < a.n_own) {
+        if (n < a.n_own) {
             m.p0 = a.in_ptr[n];
             m.deg = (uint32_t)(a.in_ptr[n + 1] - m.p0);
             m.ca = a.cand[a.own0 + n];      // CA_INJ: client broadcasts this round
@@ -1064,7 +1057,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
     auto fetch_cols = [&](const Meta& m, uint32_t (&c)[D]) {
 #pragma unroll
         for (int b = 0; b < D; ++b)
-            c[b] = ((uint32_t)b < m.deg) ? ((a.ablate & 32) ? (uint32_t)((m.p0 + b) / 2) : a.in_col[m.p0 + b]) : 0u;
+            c[b] = ((uint32_t)b < m.deg) ? a.in_col[m.p0 + b] : 0u;
     };
 
     uint32_t k = blockIdx.x * NGB + threadIdx.x / G;
@@ -1084,7 +1077,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         const uint64_t rep = a.own0 + i;
         // (a) DMA node i's own row and its first D sender rows (masked rounds:
         // and the words of the window bitmaps covering its first D in-edges)
-        if (!hub && !(a.ablate & 4)) dma16((const void*)(a.base + rep * a.nwp + off), my + D * 1024);
+        if (!hub) dma16((const void*)(a.base + rep * a.nwp + off), my + D * 1024);
         uint64_t mw[3][2];
         if constexpr (MASKW) {
 #pragma unroll
@@ -1096,7 +1089,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         }
 #pragma unroll
         for (int b = 0; b < D; ++b) {
-            if ((uint32_t)b < m0.deg && !(a.ablate & 2))
+            if ((uint32_t)b < m0.deg)
                 dma16((const void*)(a.F_prev + (uint64_t)(c0[b] & kColMask) * a.nwp + off), my + b * 1024);
         }
         // (b) prefetch: columns of item k+stride, row pointers of item k+2*stride,
@@ -1222,18 +1215,16 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         for (int w = 0; w < WPL; ++w) {
             F.w[w] = S.w[w] & ~sp.w[w];
             T += __popcll(F.w[w]);
-            if (F.w[w] && !(a.ablate & 8)) {
-                const uint64_t idx = g * a.nw + off + w;
+            if (F.w[w]) {
+                const uint64_t idx = g * a.nw + a.word0 + off + w;
                 c_hash += gg_word_hash(idx, S.w[w]) - (sp.w[w] ? gg_word_hash(idx, sp.w[w]) : 0ull);
             }
         }
         const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
         const bool zm = (m0.fl & FL_ACT) != 0;  // F row of round r-2 in this buffer
-        if (!(a.ablate & 1)) {
-            if (any || zm) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
-            if (any) store_row<WPL>(a.base + rep * a.nwp + off, S);
-        }
-        if (lg == 0 && !(a.ablate & 16)) {
+        if (any || zm) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
+        if (any) store_row<WPL>(a.base + rep * a.nwp + off, S);
+        if (lg == 0) {
             if (any || m0.fl) a.flg_cur[rep] = any ? FL_ACT : 0;
             if (m0.ca) a.cand[rep] = 0;
         }
@@ -1411,7 +1402,7 @@ void expand_stream1(RoundArgs a) {
             const uint64_t F = S & ~sp;
             const uint32_t T = (uint32_t)__popcll(F);
             if (F) {
-                const uint64_t idx = gid_of(a, i) * a.nw;
+                const uint64_t idx = gid_of(a, i) * a.nw + a.word0;
                 c_hash += gg_word_hash(idx, S) - (sp ? gg_word_hash(idx, sp) : 0ull);
             }
             const bool any = F != 0;
@@ -1738,7 +1729,7 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
             F.w[w] = S.w[w] & ~sp.w[w];
             T += __popcll(F.w[w]);
             if (F.w[w]) {
-                const uint64_t idx = g * a.nw + off + w;
+                const uint64_t idx = g * a.nw + a.word0 + off + w;
                 c_hash += gg_word_hash(idx, S.w[w]) - (sp.w[w] ? gg_word_hash(idx, sp.w[w]) : 0ull);
             }
         }
@@ -1960,7 +1951,7 @@ __global__ __launch_bounds__(kBlock) void hub_finish(RoundArgs a) {
                 F.w[w] = S.w[w] & ~sp.w[w];
                 T += __popcll(F.w[w]);
                 if (F.w[w]) {
-                    const uint64_t idx = g * a.nw + off + w;
+                    const uint64_t idx = g * a.nw + a.word0 + off + w;
                     c_hash += gg_word_hash(idx, S.w[w]) - (sp.w[w] ? gg_word_hash(idx, sp.w[w]) : 0ull);
                 }
             }

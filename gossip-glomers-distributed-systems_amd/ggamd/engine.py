@@ -39,6 +39,7 @@ class GGConfig(C.Structure):
         ("device", C.c_int32),
         ("rank", C.c_uint32),
         ("world", C.c_uint32),
+        ("lane_groups", C.c_uint32),
     ]
 
 
@@ -65,6 +66,7 @@ class GGRoundStats(C.Structure):
         ("prep_bytes", C.c_uint64),
         ("expand_bytes", C.c_uint64),
         ("stream_bytes", C.c_uint64),
+        ("sent_bytes", C.c_uint64),
     ]
 
 
@@ -98,7 +100,7 @@ GEN_SYMBOLS = ["gg_topology_generate", "gg_topology_export"]  # HIP library only
 
 STAT_FIELDS = [f for f, _ in GGRoundStats._fields_]
 DIAG_FIELDS = ("round", "kernel_ms", "work_rows", "work_gathers", "prep_ms", "expand_ms", "stream_ms",
-               "prep_bytes", "expand_bytes", "stream_bytes")
+               "prep_bytes", "expand_bytes", "stream_bytes", "sent_bytes")
 COUNT_FIELDS = [f for f in STAT_FIELDS if f not in DIAG_FIELDS]
 
 GG_SYMBOLS = [
@@ -197,18 +199,20 @@ class Engine:
 
     def __init__(self, n_nodes: int, n_lanes: int, *, seed: int = 0, sync_base: int = 20,
                  sync_jitter: int = 10, enable_sync: bool = True, track_delivery: bool = False,
-                 device: int = -1, rank: int = 0, world: int = 1, library: str | None = None):
+                 device: int = -1, rank: int = 0, world: int = 1, lane_groups: int = 1,
+                 library: str | None = None):
         self.lib = load_library(library or HIP_LIB)
         self.library = os.path.abspath(library or HIP_LIB)
         cfg = GGConfig(n_nodes, n_lanes, GG_TRACK_DELIVERY if track_delivery else 0, seed,
-                       sync_base, sync_jitter, 1 if enable_sync else 0, device, rank, world)
+                       sync_base, sync_jitter, 1 if enable_sync else 0, device, rank, world, lane_groups)
         h = C.c_void_p()
         rc = self.lib.gg_create(C.byref(cfg), C.byref(h))
         if rc != 0:
             raise GGError(rc, "gg_create failed")
         self.h = h
         self.V, self.W, self.nw = n_nodes, n_lanes, n_lanes // 64
-        self.rank, self.world = rank, world
+        self.rank, self.world, self.lane_groups = rank, world, lane_groups
+        self.parts = world // max(1, lane_groups)
 
     def close(self):
         if getattr(self, "h", None):

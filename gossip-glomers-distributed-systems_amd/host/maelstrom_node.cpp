@@ -325,12 +325,15 @@ public:
                 std::sort(vals.begin(), vals.end());
                 vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
             }
-            std::string extra = ",\"messages\":[";
+            // ReadResponse.Messages starts as a nil slice (broadcast.go:125): an
+            // empty read marshals as null, not []
+            std::string extra = ",\"messages\":";
+            if (vals.empty()) extra += "null";
             for (size_t k = 0; k < vals.size(); ++k) {
-                if (k) extra.push_back(',');
+                extra.push_back(k ? ',' : '[');
                 extra += std::to_string(vals[k]);
             }
-            extra.push_back(']');
+            if (!vals.empty()) extra.push_back(']');
             return reply(d, s, msg_id, "read_ok", extra, status);
         }
         if (t == "broadcast_ok") return true;  // main.go:38-40
@@ -365,9 +368,11 @@ private:
         quote(o, from);
         o += ",\"dest\":";
         quote(o, to);
-        o += ",\"body\":{\"type\":\"";
+        // the pinned maelstrom library's Reply re-marshals the body as a Go map,
+        // so body keys come out in alphabetical order: in_reply_to, messages, type
+        o += ",\"body\":{\"in_reply_to\":" + std::to_string(in_reply_to) + extra + ",\"type\":\"";
         o += type;
-        o += "\",\"in_reply_to\":" + std::to_string(in_reply_to) + extra + "}}\n";
+        o += "\"}}\n";
         fwrite(o.data(), 1, o.size(), stdout);
         fflush(stdout);
         if (opt_.log) fprintf(stderr, "Sent %s", o.c_str());

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 2
+#define GG_ABI_VERSION 3
 
 #define GG_OK 0
 #define GG_EIO (-5)
@@ -76,6 +76,13 @@ typedef struct {
     int32_t device;             /* HIP device ordinal; -1 = current device */
     uint32_t rank;              /* sharded mode: this engine's rank (0 if single) */
     uint32_t world;             /* sharded mode: number of engines (1 = single) */
+    uint32_t lane_groups;       /* sharded mode: the ranks split the message lanes into this many
+                                   groups of whole 64-lane words (0 or 1: every rank has every lane).
+                                   world = lane_groups * parts; rank = group * parts + part. Ranks of
+                                   one group split the nodes into `parts` vertex ranges (below); ranks
+                                   of different groups never exchange anything (a value's propagation
+                                   depends on no other value), so lane_groups == world needs no
+                                   exchange at all and such an engine runs with gg_step. */
 } gg_config;
 
 typedef struct {
@@ -100,6 +107,7 @@ typedef struct {
     uint64_t prep_bytes;     /*   algorithmic bytes each kind had to move this round */
     uint64_t expand_bytes;   /*   (DESIGN.md §4), counted by the kernels */
     uint64_t stream_bytes;
+    uint64_t sent_bytes;     /*   sharded: payload bytes this engine sent to other ranks */
 } gg_round_stats;
 
 /* Inter-node messages of a round = fwd_sent + pushes + acks + reads + read_oks. */

@@ -54,11 +54,13 @@ struct Injection {
 struct Acc {  // per-thread counters
     uint64_t new_bits = 0, fwd_sent = 0, fwd_deliv = 0, pushes = 0, push_deliv = 0;
     uint64_t reads = 0, read_oks = 0, dropped = 0, fired = 0, hash = 0;
+    uint64_t node_dropped = 0;  // dropped reads / read_oks (node-level, not per lane)
     uint64_t next_acks = 0, next_ackdrop = 0;
     void add(const Acc& o) {
         new_bits += o.new_bits; fwd_sent += o.fwd_sent; fwd_deliv += o.fwd_deliv;
         pushes += o.pushes; push_deliv += o.push_deliv; reads += o.reads;
         read_oks += o.read_oks; dropped += o.dropped; fired += o.fired; hash += o.hash;
+        node_dropped += o.node_dropped;
         next_acks += o.next_acks; next_ackdrop += o.next_ackdrop;
     }
 };
@@ -72,6 +74,11 @@ struct gg_engine {
     std::string err;
     uint64_t V = 0, nw = 0;
     uint32_t rank = 0, world = 1;
+    // 2-D sharding (gg_config.lane_groups): L lane groups x P vertex parts; this
+    // engine holds lane words [w0, w0 + nw) of nw_g for the nodes of part `part`
+    uint32_t L = 1, P = 1, lgrp = 0, part = 0;
+    uint64_t nw_g = 0, w0 = 0;
+    uint32_t peer_rank(uint32_t q) const { return lgrp * P + q; }
     uint64_t lo = 0, hi = 0, slice = 0;    // owned range, rows per rank slice
     std::vector<uint64_t> rank_lo;         // [world+1]
     bool have_topo = false, symmetric = true;
@@ -99,6 +106,7 @@ struct gg_engine {
     std::vector<uint8_t> xsend, xrecv;
     std::vector<uint64_t> xsend_bytes, xrecv_bytes;
     std::vector<gg_round_stats> dist_pending;
+    uint64_t xsend_sent = 0;  // payload bytes of the open round
 
     int fail(int code, const std::string& m) { err = m; return code; }
 
@@ -151,9 +159,9 @@ struct gg_engine {
 void gg_engine::compute_round(Acc& total) {
     const int64_t r = round;
     const uint64_t n_own = hi - lo;
-    const uint64_t own0 = (uint64_t)rank * slice;
+    const uint64_t own0 = (uint64_t)part * slice;
     const bool sync = cfg.enable_sync != 0;
-    const uint32_t W = cfg.n_lanes;
+    const uint32_t W = (uint32_t)(nw * 64);  // this engine's lanes
     std::vector<uint64_t>& sp_all = seen[(r + 1) & 1];  // seen_prev (round r-1)
     std::vector<uint64_t>& sc_all = seen[r & 1];        // seen_cur
     std::vector<uint64_t>& Fp_all = F[(r + 1) & 1];
@@ -168,8 +176,9 @@ void gg_engine::compute_round(Acc& total) {
     {
         auto it = inj.find(r);
         if (it != inj.end()) {
-            for (const auto& x : it->second)
-                if (x.node >= lo && x.node < hi) inj_by_node[x.node].push_back(x.lane);
+            for (const auto& x : it->second)  // owned nodes, this lane group's values
+                if (x.node >= lo && x.node < hi && (x.lane >> 6) >= w0 && (x.lane >> 6) < w0 + nw)
+                    inj_by_node[x.node].push_back(x.lane - 64 * (uint32_t)w0);
             inj.erase(it);
         }
     }
@@ -195,7 +204,7 @@ void gg_engine::compute_round(Acc& total) {
                 const uint64_t u = global_of(urep);
                 if (sync && fired_at(r - 1, urep) && !masked(r - 1, u, g)) {  // read arrives
                     a.read_oks++;                                             // HandleRead :131
-                    if (masked(r, g, u)) a.dropped++;
+                    if (masked(r, g, u)) a.node_dropped++;
                 }
                 if (masked(r - 1, u, g)) continue;                            // dropped in flight
                 const bool push = sync && fired_at(r - 3, urep) && !masked(r - 3, u, g) &&
@@ -251,7 +260,7 @@ void gg_engine::compute_round(Acc& total) {
                 uint64_t f = S[j] & ~sp[j];
                 fc[j] = f;
                 Tn += popc(f);
-                if (S[j]) a.hash += gg_word_hash(g * nw + j, S[j]);
+                if (S[j]) a.hash += gg_word_hash(g * nw_g + w0 + j, S[j]);
                 if (f && !dr.empty()) {
                     uint64_t x = f;
                     while (x) {
@@ -291,7 +300,7 @@ void gg_engine::compute_round(Acc& total) {
             if (sync && r == sync_next[i]) {
                 a.fired++;
                 a.reads += deg;                                          // RPC read :120
-                a.dropped += mdrop;
+                a.node_dropped += mdrop;
                 firedw[t].push_back(rep);
                 sync_k[i]++;
                 sync_next[i] = r + gg_sync_interval(cfg.seed, g, sync_k[i], cfg.sync_base_ticks,
@@ -307,6 +316,11 @@ void gg_engine::compute_round(Acc& total) {
         for (auto& x : th) x.join();
     }
     for (int t = 0; t < T; ++t) {
+        if (lgrp != 0) {  // node-level events are counted by lane group 0 only
+            accs[t].reads = accs[t].read_oks = accs[t].fired = accs[t].node_dropped = 0;
+        }
+        accs[t].dropped += accs[t].node_dropped;
+        accs[t].node_dropped = 0;
         total.add(accs[t]);
         for (uint64_t rep : firedw[t]) fired[r & 3][rep >> 6] |= 1ull << (rep & 63);
     }
@@ -325,12 +339,20 @@ int gg_create(const gg_config* cfg, gg_engine** out) {
     if (cfg->n_lanes == 0 || cfg->n_lanes % 64 || cfg->n_lanes > 8192) return GG_EINVAL;
     if (cfg->enable_sync && cfg->sync_base_ticks == 0) return GG_EINVAL;
     if (cfg->world == 0 || cfg->rank >= cfg->world) return GG_EINVAL;
+    const uint32_t L = cfg->lane_groups ? cfg->lane_groups : 1u;
+    if (cfg->world % L || L > cfg->n_lanes / 64) return GG_EINVAL;
     auto* e = new gg_engine();
     e->cfg = *cfg;
     e->V = cfg->n_nodes;
-    e->nw = cfg->n_lanes / 64;
     e->rank = cfg->rank;
     e->world = cfg->world;
+    e->L = L;
+    e->P = cfg->world / L;
+    e->lgrp = cfg->rank / e->P;
+    e->part = cfg->rank % e->P;
+    e->nw_g = cfg->n_lanes / 64;
+    e->w0 = e->nw_g * e->lgrp / L;
+    e->nw = e->nw_g * (e->lgrp + 1) / L - e->w0;
     unsigned hc = std::thread::hardware_concurrency();
     e->threads = hc ? (int)hc : 1;
     if (const char* s = getenv("GG_CPU_THREADS")) e->threads = std::max(1, atoi(s));
@@ -373,7 +395,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     }
     e->symmetric = sym;
     // edge-balanced vertex ranges over the in-lists (pull work)
-    const uint32_t Wd = e->world;
+    const uint32_t Wd = e->P;  // vertex parts of this lane group
     e->rank_lo.assign(Wd + 1, V);
     e->rank_lo[0] = 0;
     {
@@ -388,8 +410,8 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     uint64_t maxrows = 0;
     for (uint32_t p = 0; p < Wd; ++p) maxrows = std::max<uint64_t>(maxrows, e->rank_lo[p + 1] - e->rank_lo[p]);
     e->slice = std::max<uint64_t>(64, (maxrows + 63) / 64 * 64);
-    e->lo = e->rank_lo[e->rank];
-    e->hi = e->rank_lo[e->rank + 1];
+    e->lo = e->rank_lo[e->part];
+    e->hi = e->rank_lo[e->part + 1];
     const uint64_t n_own = e->hi - e->lo;
     // owned rows with replica column ids
     e->in_ptr.assign(n_own + 1, 0);
@@ -421,7 +443,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     for (int b = 0; b < 4; ++b) e->fired[b].assign(rows / 64, 0);
     e->sync_next.assign(n_own, 0);
     e->sync_k.assign(n_own, 0);
-    if (e->cfg.flags & GG_TRACK_DELIVERY) e->dr.assign(n_own * e->cfg.n_lanes, -1);
+    if (e->cfg.flags & GG_TRACK_DELIVERY) e->dr.assign(n_own * e->nw * 64, -1);
     else e->dr.clear();
     e->have_topo = true;
     e->reset_state();
@@ -509,12 +531,13 @@ static void fill_stats(gg_engine* e, const Acc& a, gg_round_stats* s) {
     s->work_gathers = 0;
     s->prep_ms = s->expand_ms = s->stream_ms = 0.0;
     s->prep_bytes = s->expand_bytes = s->stream_bytes = 0;
+    s->sent_bytes = e->dist_open ? e->xsend_sent : 0;
 }
 
 int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
     if (!e) return GG_EINVAL;
     if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
-    if (e->world != 1) return e->fail(GG_EINVAL, "sharded engine: use gg_dist_round_begin/end");
+    if (e->P != 1) return e->fail(GG_EINVAL, "vertex-sharded engine: use gg_dist_round_begin/end");
     for (uint32_t k = 0; k < n; ++k) {
         Acc a;
         e->compute_round(a);
@@ -538,8 +561,8 @@ int gg_dist_info(const gg_engine* e, uint64_t* n_own, uint64_t* n_ghost, uint64_
     if (!e || !e->have_topo) return GG_EINVAL;
     const uint64_t n = e->hi - e->lo;
     if (n_own) *n_own = n;
-    if (n_ghost) *n_ghost = e->world > 1 ? e->V - n : 0;  // full replicas
-    if (n_send) *n_send = e->world > 1 ? n * (e->world - 1) : 0;
+    if (n_ghost) *n_ghost = e->P > 1 ? e->V - n : 0;  // full replicas
+    if (n_send) *n_send = e->P > 1 ? n * (e->P - 1) : 0;
     return GG_OK;
 }
 
@@ -562,22 +585,23 @@ int gg_dist_round_begin(gg_engine* e, gg_exchange* x) {
     e->dist_acc = Acc();
     e->compute_round(e->dist_acc);
     const int64_t r = e->round;
-    const uint64_t pb = node_payload(e), n_own = e->hi - e->lo, own0 = (uint64_t)e->rank * e->slice;
+    const uint64_t pb = node_payload(e), n_own = e->hi - e->lo, own0 = (uint64_t)e->part * e->slice;
     e->xsend_bytes.assign(e->world, 0);
     e->xrecv_bytes.assign(e->world, 0);
     uint64_t st = 0, rt = 0;
-    for (uint32_t q = 0; q < e->world; ++q) {
-        if (q == e->rank) continue;
-        e->xsend_bytes[q] = n_own * pb;
-        e->xrecv_bytes[q] = (e->rank_lo[q + 1] - e->rank_lo[q]) * pb;
-        st += e->xsend_bytes[q];
-        rt += e->xrecv_bytes[q];
+    for (uint32_t q = 0; q < e->P; ++q) {  // peers: the other parts of this lane group
+        if (q == e->part) continue;
+        e->xsend_bytes[e->peer_rank(q)] = n_own * pb;
+        e->xrecv_bytes[e->peer_rank(q)] = (e->rank_lo[q + 1] - e->rank_lo[q]) * pb;
+        st += n_own * pb;
+        rt += (e->rank_lo[q + 1] - e->rank_lo[q]) * pb;
     }
     e->xsend.assign(std::max<uint64_t>(1, st), 0);
+    e->xsend_sent = st;
     e->xrecv.assign(std::max<uint64_t>(1, rt), 0);
     uint8_t* p = e->xsend.data();
-    for (uint32_t q = 0; q < e->world; ++q) {
-        if (q == e->rank) continue;
+    for (uint32_t q = 0; q < e->P; ++q) {
+        if (q == e->part) continue;
         for (uint64_t i = 0; i < n_own; ++i, p += pb) {
             const uint64_t rep = own0 + i;
             std::memcpy(p, &e->seen[r & 1][rep * e->nw], e->nw * 8);
@@ -602,8 +626,8 @@ int gg_dist_round_end(gg_engine* e, gg_round_stats* out) {
     const int64_t r = e->round;
     const uint64_t pb = node_payload(e);
     const uint8_t* p = e->xrecv.data();
-    for (uint32_t q = 0; q < e->world; ++q) {
-        if (q == e->rank) continue;
+    for (uint32_t q = 0; q < e->P; ++q) {
+        if (q == e->part) continue;
         for (uint64_t g = e->rank_lo[q]; g < e->rank_lo[q + 1]; ++g, p += pb) {
             const uint64_t rep = (uint64_t)q * e->slice + (g - e->rank_lo[q]);
             std::memcpy(&e->seen[r & 1][rep * e->nw], p, e->nw * 8);
@@ -650,15 +674,15 @@ static bool owned(const gg_engine* e, uint64_t a, uint64_t b) { return a <= b &&
 int gg_read(gg_engine* e, uint32_t node, int64_t* out, uint64_t cap, uint64_t* n_out) {
     if (!e || !e->have_topo) return GG_EINVAL;
     if (!owned(e, node, (uint64_t)node + 1)) return e->fail(GG_EINVAL, "node not owned by this engine");
-    const uint64_t rep = (uint64_t)e->rank * e->slice + (node - e->lo);
+    const uint64_t rep = (uint64_t)e->part * e->slice + (node - e->lo);
     const auto& sc = e->seen[(e->round + 1) & 1];  // last completed round
-    std::vector<int64_t> vals;
+    std::vector<int64_t> vals;  // a lane-group engine: the values of its own lanes
     for (uint64_t j = 0; j < e->nw; ++j) {
         uint64_t x = sc[rep * e->nw + j];
         while (x) {
             int b = __builtin_ctzll(x);
             x &= x - 1;
-            uint64_t lane = j * 64 + b;
+            uint64_t lane = (e->w0 + j) * 64 + b;
             if (lane < e->lane_value.size()) vals.push_back(e->lane_value[lane]);
         }
     }
@@ -673,8 +697,11 @@ int gg_read_bits(gg_engine* e, uint32_t a, uint32_t b, uint64_t* out) {
     if (!e || !e->have_topo || !out) return GG_EINVAL;
     if (!owned(e, a, b)) return e->fail(GG_EINVAL, "range not owned by this engine");
     const auto& sc = e->seen[(e->round + 1) & 1];
-    const uint64_t rep = (uint64_t)e->rank * e->slice + (a - e->lo);
-    std::memcpy(out, &sc[rep * e->nw], (uint64_t)(b - a) * e->nw * 8);
+    const uint64_t rep = (uint64_t)e->part * e->slice + (a - e->lo);
+    for (uint64_t k = 0; k < (uint64_t)(b - a); ++k) {  // whole-job words, own window filled
+        std::fill(out + k * e->nw_g, out + (k + 1) * e->nw_g, 0ull);
+        std::memcpy(out + k * e->nw_g + e->w0, &sc[(rep + k) * e->nw], e->nw * 8);
+    }
     return GG_OK;
 }
 
@@ -682,16 +709,19 @@ int gg_delivery_rounds(gg_engine* e, uint32_t a, uint32_t b, int32_t* out, uint6
     if (!e || !e->have_topo || !out) return GG_EINVAL;
     if (e->dr.empty()) return e->fail(GG_EINVAL, "GG_TRACK_DELIVERY not enabled");
     if (!owned(e, a, b)) return e->fail(GG_EINVAL, "range not owned by this engine");
-    const uint64_t n = (uint64_t)(b - a) * e->cfg.n_lanes;
+    const uint64_t W = e->cfg.n_lanes, Wl = e->nw * 64;
+    const uint64_t n = (uint64_t)(b - a) * W;
     if (cap < n) return e->fail(GG_EINVAL, "output buffer too small");
-    std::memcpy(out, &e->dr[(a - e->lo) * e->cfg.n_lanes], n * 4);
+    std::fill(out, out + n, -1);
+    for (uint64_t k = 0; k < (uint64_t)(b - a); ++k)
+        std::memcpy(out + k * W + 64 * e->w0, &e->dr[(a - e->lo + k) * Wl], Wl * 4);
     return GG_OK;
 }
 
 int gg_read_bits_nodes(gg_engine* e, const uint32_t* nodes, uint64_t n, uint64_t* out) {
     if (!e || !e->have_topo || (n && (!nodes || !out))) return GG_EINVAL;
     for (uint64_t k = 0; k < n; ++k) {
-        int rc = gg_read_bits(e, nodes[k], nodes[k] + 1, out + k * e->nw);
+        int rc = gg_read_bits(e, nodes[k], nodes[k] + 1, out + k * e->nw_g);
         if (rc) return rc;
     }
     return GG_OK;

@@ -24,7 +24,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, lib, sc, q):
+def _worker(rank, world, port, lib, sc, q, lane_groups=1):
     import torch.distributed as dist
 
     from ggamd.dist import ShardedRunner
@@ -33,7 +33,7 @@ def _worker(rank, world, port, lib, sc, q):
                             world_size=world)
     try:
         import torch
-        e = make_engine(lib, sc, rank=rank, world=world)
+        e = make_engine(lib, sc, rank=rank, world=world, lane_groups=lane_groups)
         r = ShardedRunner(e, torch.device("cpu"))
         stats = r.step(sc.rounds)
         owned = e.dist_owned()
@@ -44,11 +44,11 @@ def _worker(rank, world, port, lib, sc, q):
         dist.destroy_process_group()
 
 
-def _run_dist(lib, sc, world=2):
+def _run_dist(lib, sc, world=2, lane_groups=1):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, lib, sc, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, lib, sc, q, lane_groups)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
@@ -69,6 +69,36 @@ def _check(lib, sc, world=2):
         assert np.array_equal(dr, single.delivery_rounds_nodes(owned))
     allown = np.sort(np.concatenate([x[2] for x in res]))
     assert np.array_equal(allown, np.arange(sc.topo.n_nodes))  # a partition of the nodes
+
+
+def _check_lanes(lib, sc, world, lane_groups):
+    """2-D sharding: lane groups x vertex parts. Counters summed over every rank,
+    node sets OR-ed and delivery rounds max-ed over the lane groups of a node's
+    owners equal the single engine."""
+    single = make_engine(lib, sc)
+    s1 = single.step(sc.rounds)
+    res = _run_dist(lib, sc, world, lane_groups)
+    V = sc.topo.n_nodes
+    bits = np.zeros((V, sc.W // 64), np.uint64)
+    dr = np.full((V, sc.W), -1, np.int32)
+    for rank, stats, owned, b, d in res:
+        assert not diff_stats(s1, stats), (rank, diff_stats(s1, stats)[:10])
+        o = owned.astype(np.int64)
+        bits[o] |= b
+        dr[o] = np.maximum(dr[o], d)
+    assert np.array_equal(bits, single.read_bits())
+    assert np.array_equal(dr, single.delivery_rounds())
+
+
+@pytest.mark.parametrize("world,groups", [(2, 2), (3, 3), (4, 2)])
+def test_lane_groups(cpu_lib, world, groups):
+    rnd = random.Random(world * 10 + groups)
+    sc = random_scenario(rnd, max_v=200, W=256, rounds=45)
+    _check_lanes(cpu_lib, sc, world, groups)
+
+
+def test_lane_groups_c1_partition(cpu_lib):
+    _check_lanes(cpu_lib, c1_scenario(partition=True, rounds=120), 2, 2)
 
 
 def test_c1_two_ranks(cpu_lib):

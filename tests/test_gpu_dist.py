@@ -30,17 +30,18 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, lib, scenarios, q):
+def _worker(rank, world, port, lib, scenarios, q, lane_groups=1, env=None):
     import torch
     import torch.distributed as dist
 
     from ggamd.dist import ShardedRunner
+    os.environ.update(env or {})
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         out = []
         dev = torch.device("cuda", 0)
         for sc in scenarios:
-            e = make_engine(lib, sc, rank=rank, world=world, device=0)
+            e = make_engine(lib, sc, rank=rank, world=world, device=0, lane_groups=lane_groups)
             r = ShardedRunner(e, dev)
             half = sc.rounds // 2
             stats = r.step(half) + r.step(sc.rounds - half)  # two flushes
@@ -48,18 +49,26 @@ def _worker(rank, world, port, lib, scenarios, q):
             out.append((stats, owned, e.read_bits_nodes(owned), e.delivery_rounds_nodes(owned)))
             e.close()
         q.put((rank, out))
+    except BaseException as exc:  # report instead of leaving the parent waiting
+        q.put((rank, f"rank {rank} failed: {exc!r}"))
+        raise
     finally:
         dist.destroy_process_group()
 
 
-def _run(lib, scenarios, world):
+def _run(lib, scenarios, world, lane_groups=1, env=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, lib, scenarios, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, lib, scenarios, q, lane_groups, env))
+             for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=240) for _ in range(world))
+    res = {}
+    for _ in range(world):
+        r, got = q.get(timeout=150)
+        assert not isinstance(got, str), got
+        res[r] = got
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -103,6 +112,101 @@ def test_sharded_equals_single(hip_lib, world):
         allown = np.sort(np.concatenate(owned_all))
         assert np.array_equal(allown, np.arange(sc.topo.n_nodes)), k
         single.close()
+
+
+def _rmat_scenarios():
+    """R-MAT graphs with hubs: with GG_HUB_DEG=24 the high in-degree nodes take
+    hub_chunks/hub_finish and the high out-degree senders hub_mark, now with ghost
+    senders in their in-lists and ghost receivers in their out-lists."""
+    from ggamd import topology as T
+    from ggamd.workload import uniform_injections
+    rm = T.rmat(4096, 16, seed=21)
+    rm2 = T.rmat(3000, 8, seed=22)
+    return [Scenario(rm, 256, 24, uniform_injections(4096, 256, 8), seed=13, sync_base=30, sync_jitter=3),
+            Scenario(rm2, 128, 40, uniform_injections(3000, 100, 9), seed=14, sync_base=8, sync_jitter=4)]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_rmat_hubs_equals_single(hip_lib, world):
+    env = {"GG_HUB_DEG": "24"}
+    scs = _rmat_scenarios()
+    res = _run(hip_lib, scs, world, env=env)
+    old = os.environ.get("GG_HUB_DEG")
+    os.environ.update(env)
+    try:
+        for k, sc in enumerate(scs):
+            single = make_engine(hip_lib, sc, device=0)
+            s1 = single.step(sc.rounds)
+            for rank in range(world):
+                stats, owned, bits, dr = res[rank][k]
+                d = diff_stats(s1, stats)
+                assert not d, (k, rank, d[:10])
+                assert np.array_equal(bits, single.read_bits_nodes(owned)), (k, rank)
+                assert np.array_equal(dr, single.delivery_rounds_nodes(owned)), (k, rank)
+            single.close()
+    finally:
+        if old is None:
+            os.environ.pop("GG_HUB_DEG", None)
+        else:
+            os.environ["GG_HUB_DEG"] = old
+
+
+@pytest.mark.parametrize("world,groups", [(2, 2), (4, 2), (3, 3)])
+def test_lane_groups_equal_single(hip_lib, world, groups):
+    """2-D sharding on the GPU (gg_config.lane_groups): lane groups x vertex
+    parts. Counters summed over all ranks equal one engine; node sets OR-ed and
+    delivery rounds max-ed over a node's owners equal its set and rounds."""
+    scs = [sc for sc in _scenarios() + _rmat_scenarios()[:1] if sc.W // 64 >= groups][:4]
+    assert len(scs) >= 2
+    res = _run(hip_lib, scs, world, lane_groups=groups, env={"GG_HUB_DEG": "24"})
+    old = os.environ.get("GG_HUB_DEG")
+    os.environ["GG_HUB_DEG"] = "24"
+    try:
+        for k, sc in enumerate(scs):
+            single = make_engine(hip_lib, sc, device=0)
+            s1 = single.step(sc.rounds)
+            V = sc.topo.n_nodes
+            bits = np.zeros((V, sc.W // 64), np.uint64)
+            dr = np.full((V, sc.W), -1, np.int32)
+            for rank in range(world):
+                stats, owned, b, d = res[rank][k]
+                assert not diff_stats(s1, stats), (k, rank, diff_stats(s1, stats)[:10])
+                o = owned.astype(np.int64)
+                bits[o] |= b
+                dr[o] = np.maximum(dr[o], d)
+            assert np.array_equal(bits, single.read_bits()), k
+            assert np.array_equal(dr, single.delivery_rounds()), k
+            single.close()
+    finally:
+        if old is None:
+            os.environ.pop("GG_HUB_DEG", None)
+        else:
+            os.environ["GG_HUB_DEG"] = old
+
+
+def test_lane_group_engine_steps_without_exchange(hip_lib):
+    """lane_groups == world: no vertex parts, so every rank steps on its own
+    (gg_step, graph-captured batches) and the summed counters equal one engine."""
+    from ggamd import topology as T
+    from ggamd.workload import uniform_injections
+    topo = T.random_regular(5000, 8, seed=3)
+    sc = Scenario(topo, 512, 30, uniform_injections(5000, 500, 4), seed=5, sync_base=12, sync_jitter=4)
+    single = make_engine(hip_lib, sc, device=0)
+    want = single.step(sc.rounds)
+    tot = None
+    for rank in range(4):
+        e = make_engine(hip_lib, sc, device=0, rank=rank, world=4, lane_groups=4)
+        st = e.step(sc.rounds)
+        if tot is None:
+            tot = [dict(x) for x in st]
+        else:
+            for a, b in zip(tot, st):
+                for f in a:
+                    if f != "round" and isinstance(a[f], int):
+                        a[f] = (a[f] + b[f]) & ((1 << 64) - 1)
+        e.close()
+    assert not diff_stats(want, tot), diff_stats(want, tot)[:10]
+    single.close()
 
 
 def _gen_worker(rank, world, port, lib, spec, W, inj, rounds, q):

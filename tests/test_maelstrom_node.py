@@ -4,7 +4,8 @@ host/maelstrom_node.cpp): the reference node's handler surface
 process over the C ABI. CPU tests drive it with the oracle library O2
 (--engine; test-only), the GPU test with the HIP engine it loads by default.
 
-Checked: reply shapes (`in_reply_to`, `*_ok` types, src/dest swapped), a
+Checked: reply shapes (`in_reply_to`, `*_ok` types, src/dest swapped, the
+library's key order, `"messages":null` for an empty read), a
 client broadcast visible at once at its node (the reference's map) and at
 every node after hop-distance rounds, read results equal to the engine's own
 gg_read after the same broadcasts and rounds, the no-op `broadcast_ok`, the
@@ -34,7 +35,8 @@ def _need():
 def run(lines, *args):
     p = subprocess.run([BIN, *args], input="".join(json.dumps(x) + "\n" for x in lines),
                        capture_output=True, text=True, timeout=60)
-    return p.returncode, [json.loads(x) for x in p.stdout.splitlines()], p.stderr
+    run.raw = p.stdout.splitlines()
+    return p.returncode, [json.loads(x) for x in run.raw], p.stderr
 
 
 def msg(src, dest, body):
@@ -70,9 +72,14 @@ def test_protocol_shapes():
         assert o["body"]["in_reply_to"] == x["body"]["msg_id"]
     assert out[50]["body"] == {"type": "broadcast_ok", "in_reply_to": 7}
     assert out[51]["body"]["messages"] == [1000]   # at its node at once
-    assert out[52]["body"]["messages"] == []       # not yet propagated
+    assert out[52]["body"]["messages"] is None     # not yet propagated: null (broadcast.go:125)
     assert out[53]["body"]["messages"] == [1000]   # tree4 of 25: within 8 rounds
     assert out[53]["src"] == "n24" and out[53]["body"]["in_reply_to"] == 10
+    # wire order of the pinned library: Message struct fields, then the body
+    # re-marshalled as a map (alphabetical keys)
+    assert run.raw[52] == '{"src":"n24","dest":"c1","body":{"in_reply_to":9,"messages":null,"type":"read_ok"}}'
+    assert run.raw[53] == '{"src":"n24","dest":"c1","body":{"in_reply_to":10,"messages":[1000],"type":"read_ok"}}'
+    assert run.raw[50] == '{"src":"n3","dest":"c1","body":{"in_reply_to":7,"type":"broadcast_ok"}}'
 
 
 def test_unknown_type_exits_1():
@@ -124,7 +131,7 @@ def _equivalence(engine_args, ref_lib, device=None):
                 pending.setdefault(v, []).append(value)
             else:
                 lines.append(msg("c1", f"n{v}", {"type": "read", "msg_id": mid}))
-                want.append(sorted(set(ref.read(v)) | set(pending.get(v, []))))
+                want.append(sorted(set(ref.read(v)) | set(pending.get(v, []))) or None)
         lines.append(msg("c0", "n0", {"type": "tick"}))
         ref.step(1)
         pending = {}

@@ -3,9 +3,8 @@
 //
 // Builds a 4-ary tree CSR (V nodes), random node sets and frontier rows, marks
 // every node active (ACT) and candidate, and times expand_round_lean on the
-// same inputs repeatedly (inputs restored before every launch) under
-// diagnostic ablations (GG_ABLATE semantics: 1 no row stores, 2 no sender-row
-// gathers, 4 no own-row loads). Reports time and effective bytes.
+// same inputs repeatedly (inputs restored before every launch). Reports time
+// and effective bytes.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../include -I../gossip-glomers-distributed-systems_amd/csrc tools/kbench.hip
 #include <hip/hip_runtime.h>
 
@@ -108,8 +107,7 @@ int main(int argc, char** argv) {
     const double bytes = 8.0 * (V + 1) + 4.0 * E + 2.0 * V + E + E * w + 3.0 * V * w;
     printf("V=%llu E=%llu rows %llu B, algorithmic bytes/round %.1f MB\n", (unsigned long long)V,
            (unsigned long long)E, (unsigned long long)w, bytes / 1e6);
-    for (uint32_t abl : {0u}) {
-        a.ablate = abl;
+    {
         a.stream_ok = 0;  // sparse path over every tile
         float best = 1e30f, sum = 0;
         for (int r = 0; r < reps; ++r) {
@@ -126,12 +124,11 @@ int main(int argc, char** argv) {
             best = std::min(best, ms);
             sum += ms;
         }
-        printf("ablate=%u  best %.4f ms  mean %.4f ms  -> %.0f GB/s algorithmic\n", abl, best, sum / reps,
+        printf("round  best %.4f ms  mean %.4f ms  -> %.0f GB/s algorithmic\n", best, sum / reps,
                bytes / (best * 1e-3) / 1e9);
     }
     // streaming kernel (the dense-round path of the library for WPL == 2)
-    for (uint32_t abl : {0u, 15u, 31u, 47u, 79u, 63u, 127u, 111u, 95u}) {
-        a.ablate = abl;
+    {
         a.stream_ok = 1;
         for (int blocks : {1024}) {
             float best = 1e30f, sum = 0;
@@ -148,7 +145,7 @@ int main(int argc, char** argv) {
                 best = std::min(best, ms);
                 sum += ms;
             }
-            printf("stream blocks=%d ablate=%u  best %.4f ms  mean %.4f ms  -> %.0f GB/s algorithmic\n", blocks, abl,
+            printf("stream blocks=%d  best %.4f ms  mean %.4f ms  -> %.0f GB/s algorithmic\n", blocks,
                    best, sum / reps, bytes / (best * 1e-3) / 1e9);
         }
     }
