@@ -159,7 +159,28 @@ struct gg_engine {
     uint32_t* d_gout_col = nullptr;
     uint8_t* d_xsend = nullptr;
     uint8_t* d_xrecv = nullptr;
-    std::vector<uint64_t> xsend_bytes, xrecv_bytes;
+    // filtered exchange (expand_kernels.hpp pack_ghosts): per-part segment
+    // capacity offsets (bytes, [P+1]), pack tiles, per-gout-edge send entry,
+    // set-need marks, per-ghost F arrival stamps, per-peer counters and sizes
+    std::vector<uint64_t> xsoff, xroff;
+    uint64_t* d_xsoff = nullptr;
+    uint64_t* d_xroff = nullptr;
+    uint32_t* d_gfirst = nullptr;
+    gg::XchgTile* d_xtiles = nullptr;
+    uint32_t n_xtiles = 0;
+    uint32_t* d_gout_sidx = nullptr;
+    uint8_t* d_needmark = nullptr;
+    uint32_t* d_stamp = nullptr;
+    uint32_t* d_xcnt = nullptr;
+    unsigned long long* d_segbytes = nullptr;  // [2P]: bytes to each part, bytes from each part
+    unsigned long long* h_segbytes = nullptr;  // pinned copy
+    unsigned long long* d_payload = nullptr;   // [kMaxBatch] payload bytes of each pending round
+    uint32_t xstride = 16;
+    // exact-size directions (their sizes travel first, one host wait per round),
+    // decided per direction from its capacity, which both ends compute alike
+    std::vector<uint8_t> xexact_s, xexact_r;   // [P] to / from each part
+    bool xexact = false;                       // any exact direction
+    std::vector<uint64_t> xsend_bytes, xrecv_bytes, xsend_off, xrecv_off;  // [world]
     uint32_t dist_k = 0;                       // pending rounds (counter slots in use)
     std::vector<int64_t> dist_round_of;        // round of each pending slot
     std::vector<uint64_t> dist_sent;           // payload bytes sent in each pending slot
@@ -284,6 +305,19 @@ void gg_engine::free_topology() {
     dfree(d_gout_col);
     dfree(d_xsend);
     dfree(d_xrecv);
+    dfree(d_xsoff);
+    dfree(d_xroff);
+    dfree(d_gfirst);
+    dfree(d_xtiles);
+    dfree(d_gout_sidx);
+    dfree(d_needmark);
+    dfree(d_stamp);
+    dfree(d_xcnt);
+    dfree(d_segbytes);
+    dfree(d_payload);
+    if (h_segbytes) (void)hipHostFree(h_segbytes);
+    h_segbytes = nullptr;
+    n_xtiles = 0;
     for (auto& w : windows) {
         dfree(w.d_grp);
         dfree(w.d_ebits);
@@ -342,9 +376,14 @@ int reset_device_state(gg_engine* e) {
     seg(e->d_act, 16, 0);
     const uint64_t n_own = e->n_own;
     if (e->d_dr) seg(e->d_dr, n_own * e->nw * 64 * 4, ~0ull);
+    if (e->d_stamp) seg(e->d_stamp, (e->n_ghost + 1) / 2 * 8, ~0ull);
+    if (e->d_needmark) seg(e->d_needmark, (e->send_off[e->P] + 7) / 8 * 8, 0);
+    if (e->d_xcnt) seg(e->d_xcnt, (e->P + 1) / 2 * 8, 0);
     ra.sync_next = e->d_sync_next;
     ra.sync_k = e->d_sync_k;
     ra.n_own = n_own;
+    ra.ghost0 = e->ghost0;
+    ra.n_ghost = e->n_ghost;
     ra.gid = e->d_gid;
     ra.seed = e->cfg.seed;
     ra.sync_base = e->cfg.sync_base_ticks;
@@ -836,13 +875,6 @@ int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& o
 }
 
 
-// Payload bytes of one node in the exchange (pack_ghosts layout): F row, set
-// row when `with_set`, 16-byte tail; rows padded to 16 bytes.
-uint64_t exchange_stride(uint64_t nwp, bool with_set) {
-    const uint64_t rowc = nwp / 2 + (nwp & 1);
-    return (rowc * (with_set ? 2 : 1) + 1) * 16;
-}
-
 // Edge-balanced cut of a node order into `parts` contiguous ranges (weight of a
 // node: in-degree + 1, the pull work of its row).
 void balanced_ranges(uint64_t V, const int64_t* tin, const std::vector<uint32_t>& order, uint32_t parts,
@@ -1061,8 +1093,8 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
         HIPCHK(hipMalloc(&e->d_flg[b], e->rows));
     }
     for (int b = 0; b < 4; ++b) HIPCHK(hipMalloc(&e->d_fired[b], e->rows / 8));
-    HIPCHK(hipMalloc(&e->d_sync_next, std::max<uint64_t>(1, n_own) * 4));
-    HIPCHK(hipMalloc(&e->d_sync_k, std::max<uint64_t>(1, n_own) * 4));
+    HIPCHK(hipMalloc(&e->d_sync_next, e->rows * 4));  // owned nodes' and ghosts' timers
+    HIPCHK(hipMalloc(&e->d_sync_k, e->rows * 4));
     if (e->cfg.flags & GG_TRACK_DELIVERY) HIPCHK(hipMalloc(&e->d_dr, std::max<uint64_t>(1, n_own) * e->nw * 64 * 4));
     e->have_topo = true;
     e->quiet = 0;  // fresh buffers: clear everything
@@ -1152,6 +1184,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     e->gid.clear();
     std::vector<uint32_t> ghosts;                     // ghost nodes in local ghost order
     std::vector<std::vector<uint32_t>> sendl(Wd);     // owned local rows per destination
+    std::vector<std::vector<uint32_t>> send_ids(Wd);  // the same, original ids (ascending)
     e->send_off.assign(Wd + 1, 0);
     e->recv_off.assign(Wd + 1, 0);
     if (Wd > 1) {
@@ -1182,6 +1215,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
             std::sort(g.begin(), g.end());
             g.erase(std::unique(g.begin(), g.end()), g.end());
             std::sort(sendl[q].begin(), sendl[q].end());
+            send_ids[q] = sendl[q];
             for (auto& v : sendl[q]) v = e->loc_of[v];  // node -> owned local row
             ghosts.insert(ghosts.end(), g.begin(), g.end());
             e->recv_off[q + 1] = e->recv_off[q] + g.size();
@@ -1277,9 +1311,74 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
         HIPCHK(hipMalloc(&e->d_gout_col, std::max<size_t>(1, gocol.size()) * 4));
         if (!gocol.empty())
             HIPCHK(hipMemcpy(e->d_gout_col, gocol.data(), gocol.size() * 4, hipMemcpyHostToDevice));
-        const uint64_t pb = exchange_stride(e->nwp, true);
-        HIPCHK(hipMalloc(&e->d_xsend, std::max<uint64_t>(16, e->send_off[Wd] * pb)));
-        HIPCHK(hipMalloc(&e->d_xrecv, std::max<uint64_t>(16, e->recv_off[Wd] * pb)));
+        // filtered exchange: the send entry of every ghost -> owned edge (the
+        // owned node's position in the send list to the ghost's part), pack tiles,
+        // segment capacities (header + an F and an S entry per send-list node)
+        std::vector<uint32_t> gsidx(gocol.size());
+        {
+            uint32_t p = 0;
+            for (uint64_t g = 0; g < e->n_ghost; ++g) {
+                while (g >= e->recv_off[p + 1]) ++p;
+                const auto& ids = send_ids[p];
+                for (int64_t k = gcnt[g]; k < gcnt[g + 1]; ++k) {
+                    const uint32_t id = e->gid[gocol[k]];
+                    const auto it = std::lower_bound(ids.begin(), ids.end(), id);
+                    if (it == ids.end() || *it != id) return e->fail(GG_EIO, "internal: ghost edge without a send entry");
+                    gsidx[k] = (uint32_t)(e->send_off[p] + (it - ids.begin()));
+                }
+            }
+        }
+        HIPCHK(hipMalloc(&e->d_gout_sidx, std::max<size_t>(1, gsidx.size()) * 4));
+        if (!gsidx.empty())
+            HIPCHK(hipMemcpy(e->d_gout_sidx, gsidx.data(), gsidx.size() * 4, hipMemcpyHostToDevice));
+        e->xstride = (uint32_t)(e->nwp >= 2 ? 16 + 8 * e->nwp : 16);
+        e->xsoff.assign(Wd + 1, 0);
+        e->xroff.assign(Wd + 1, 0);
+        std::vector<gg::XchgTile> tiles;
+        for (uint32_t q = 0; q < Wd; ++q) {
+            const uint64_t ns = e->send_off[q + 1] - e->send_off[q], nr = e->recv_off[q + 1] - e->recv_off[q];
+            e->xsoff[q + 1] = e->xsoff[q] + (ns ? 16 + 2 * ns * e->xstride : 0);
+            e->xroff[q + 1] = e->xroff[q] + (nr ? 16 + 2 * nr * e->xstride : 0);
+            for (uint64_t k0 = e->send_off[q]; k0 < e->send_off[q + 1]; k0 += gg::kBlock)
+                tiles.push_back({q, (uint32_t)k0, (uint32_t)std::min<uint64_t>(gg::kBlock, e->send_off[q + 1] - k0),
+                                 (uint32_t)e->send_off[q]});
+        }
+        e->n_xtiles = (uint32_t)tiles.size();
+        HIPCHK(hipMalloc(&e->d_xtiles, std::max<size_t>(1, tiles.size()) * sizeof(gg::XchgTile)));
+        if (!tiles.empty())
+            HIPCHK(hipMemcpy(e->d_xtiles, tiles.data(), tiles.size() * sizeof(gg::XchgTile), hipMemcpyHostToDevice));
+        std::vector<uint32_t> gfirst(Wd + 1);
+        for (uint32_t q = 0; q <= Wd; ++q) gfirst[q] = (uint32_t)e->recv_off[q];
+        HIPCHK(hipMalloc(&e->d_gfirst, (Wd + 1) * 4));
+        HIPCHK(hipMemcpy(e->d_gfirst, gfirst.data(), (Wd + 1) * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMalloc(&e->d_xsoff, (Wd + 1) * 8));
+        HIPCHK(hipMemcpy(e->d_xsoff, e->xsoff.data(), (Wd + 1) * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMalloc(&e->d_xroff, (Wd + 1) * 8));
+        HIPCHK(hipMemcpy(e->d_xroff, e->xroff.data(), (Wd + 1) * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMalloc(&e->d_needmark, (e->send_off[Wd] + 7) / 8 * 8 + 8));
+        HIPCHK(hipMalloc(&e->d_stamp, (e->n_ghost + 1) / 2 * 8 + 8));
+        HIPCHK(hipMalloc(&e->d_xcnt, (Wd + 1) / 2 * 8 + 8));
+        HIPCHK(hipMalloc(&e->d_segbytes, 2 * Wd * 8));
+        HIPCHK(hipHostMalloc(&e->h_segbytes, 2 * Wd * 8));
+        HIPCHK(hipMalloc(&e->d_payload, kMaxBatch * 8));
+        HIPCHK(hipMalloc(&e->d_xsend, std::max<uint64_t>(16, e->xsoff[Wd])));
+        HIPCHK(hipMalloc(&e->d_xrecv, std::max<uint64_t>(16, e->xroff[Wd])));
+        // a direction whose static capacity exceeds GG_XCHG_EXACT_BYTES (default
+        // 4 MiB) sends its exact size first and then only the used bytes (one host
+        // wait per round); GG_XCHG_MODE=exact|static forces every direction
+        const char* mode = getenv("GG_XCHG_MODE");
+        uint64_t lim = 4ull << 20;
+        if (const char* l = getenv("GG_XCHG_EXACT_BYTES")) lim = strtoull(l, nullptr, 10);
+        e->xexact_s.assign(Wd, 0);
+        e->xexact_r.assign(Wd, 0);
+        e->xexact = false;
+        for (uint32_t q = 0; q < Wd; ++q) {
+            const uint64_t cs = e->xsoff[q + 1] - e->xsoff[q], cr = e->xroff[q + 1] - e->xroff[q];
+            const bool force = mode && !strcmp(mode, "exact"), never = mode && !strcmp(mode, "static");
+            e->xexact_s[q] = cs && !never && (force || cs > lim);
+            e->xexact_r[q] = cr && !never && (force || cr > lim);
+            e->xexact |= e->xexact_s[q] || e->xexact_r[q];
+        }
     }
     return finish_topology(e, iptr.data(), sym ? nullptr : optr.data());
 }
@@ -1513,12 +1612,14 @@ static int fold_pending(gg_engine* e) {
     if (e->dist_k) {
         const size_t slot = (size_t)gg::kSlots * gg::kCounters;
         HIPCHK(hipMemcpyAsync(e->h_counters, e->d_counters, e->dist_k * slot * 8, hipMemcpyDeviceToHost, e->stream));
+        if (e->d_payload)
+            HIPCHK(hipMemcpyAsync(e->dist_sent.data(), e->d_payload, e->dist_k * 8, hipMemcpyDeviceToHost, e->stream));
     }
     HIPCHK(hipStreamSynchronize(e->stream));
     for (uint32_t k = 0; k < e->dist_k; ++k) {
         gg_round_stats s;
         fold_stats(e, e->h_counters + (size_t)k * gg::kSlots * gg::kCounters, e->dist_round_of[k], &s);
-        s.sent_bytes = e->dist_sent[k];
+        s.sent_bytes = e->d_payload ? e->dist_sent[k] : 0;
         e->dist_done.push_back(s);
     }
     e->dist_k = 0;
@@ -1526,7 +1627,13 @@ static int fold_pending(gg_engine* e) {
     return GG_OK;
 }
 
-int gg_dist_round_begin(gg_engine* e, gg_exchange* x) {
+}  // extern "C"
+
+// One sharded round up to the exchange: the round's kernels, then (vertex
+// parts) the pack of this round's ghost payloads. host_sizes: in exact mode,
+// wait for the pack and return the segment sizes (the caller-driven exchange);
+// the engine's own RCCL exchange moves the sizes on the device instead.
+static int dist_begin(gg_engine* e, gg_exchange* x, bool host_sizes) {
     if (!e || !x) return GG_EINVAL;
     if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
     if (e->world < 2) return e->fail(GG_EINVAL, "not a sharded engine (world == 1): use gg_step");
@@ -1550,53 +1657,107 @@ int gg_dist_round_begin(gg_engine* e, gg_exchange* x) {
     unsigned long long* ctr = e->d_counters + e->dist_k * slot;
     HIPCHK(hipMemsetAsync(ctr, 0, slot * 8, e->stream));
     if ((rc = enqueue_round(e, d_inj, (uint32_t)total, ctr))) return rc;
-    // ghost payloads of this round: F rows, flags, fired bits (+ sets while the
-    // next round may read remote sets: sync callbacks and push edges)
-    const bool with_set = e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks;
-    const uint64_t pb = exchange_stride(e->nwp, with_set);
-    const uint64_t n_send = e->send_off[e->P];
-    if (n_send) {
-        const uint64_t chunks = n_send * (pb / 16);
-        const unsigned blocks = (unsigned)std::min<uint64_t>((chunks + gg::kBlock - 1) / gg::kBlock, 4096);
-        hipLaunchKernelGGL(gg::pack_ghosts, dim3(blocks), dim3(gg::kBlock), 0, e->stream, e->d_F[r & 1], e->d_base,
-                           e->d_flg[r & 1], e->d_fired[r & 3], e->d_send_idx, n_send, (uint32_t)e->nwp,
-                           with_set ? 1 : 0, e->d_xsend);
-        HIPCHK(hipGetLastError());
-    }
-    e->xsend_bytes.assign(e->world, 0);
-    e->xrecv_bytes.assign(e->world, 0);
-    for (uint32_t q = 0; q < e->P; ++q) {  // peers: the parts of this lane group
-        e->xsend_bytes[e->peer_rank(q)] = (e->send_off[q + 1] - e->send_off[q]) * pb;
-        e->xrecv_bytes[e->peer_rank(q)] = (e->recv_off[q + 1] - e->recv_off[q]) * pb;
-    }
+    const uint32_t P = e->P;
     if (e->dist_round_of.size() < kMaxBatch) e->dist_round_of.resize(kMaxBatch);
     if (e->dist_sent.size() < kMaxBatch) e->dist_sent.resize(kMaxBatch);
     e->dist_round_of[e->dist_k] = r;
-    e->dist_sent[e->dist_k] = n_send * pb;
+    e->xsend_bytes.assign(e->world, 0);
+    e->xrecv_bytes.assign(e->world, 0);
+    e->xsend_off.assign(e->world, 0);
+    e->xrecv_off.assign(e->world, 0);
+    if (P > 1) {
+        // sets may be read in r+1 by callbacks (fired in r-1) and pushes (fired in r-2)
+        const bool sync = e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks + 1;
+        if (sync && e->n_ghost) {
+            hipLaunchKernelGGL(gg::mark_set_needs, dim3((unsigned)((e->n_ghost + 255) / 256)), dim3(256), 0,
+                               e->stream, e->d_fired[(r - 1) & 3], e->d_gout_ptr, e->d_gout_sidx, e->ghost0,
+                               e->n_ghost, e->d_needmark);
+            HIPCHK(hipGetLastError());
+        }
+        if (e->n_xtiles) {
+            gg::PackArgs pa{};
+            pa.F_cur = e->d_F[r & 1];
+            pa.base = e->d_base;
+            pa.flg_cur = e->d_flg[r & 1];
+            pa.fired_m2 = e->d_fired[(r - 2) & 3];
+            pa.needmark = e->d_needmark;
+            pa.send_idx = e->d_send_idx;
+            pa.tiles = e->d_xtiles;
+            pa.n_tiles = e->n_xtiles;
+            pa.cnt = e->d_xcnt;
+            pa.out = e->d_xsend;
+            pa.seg_off = e->d_xsoff;
+            pa.nwp = (uint32_t)e->nwp;
+            pa.stride = e->xstride;
+            pa.sync = sync ? 1 : 0;
+            hipLaunchKernelGGL(gg::pack_ghosts, dim3(std::min<uint32_t>(e->n_xtiles, 4096)), dim3(gg::kBlock), 0,
+                               e->stream, pa);
+            HIPCHK(hipGetLastError());
+        }
+        hipLaunchKernelGGL(gg::finish_pack, dim3(1), dim3(64), 0, e->stream, e->d_xcnt, e->d_xsend, e->d_xsoff, P,
+                           e->part, e->xstride, e->d_segbytes, e->d_payload + e->dist_k);
+        HIPCHK(hipGetLastError());
+        for (uint32_t q = 0; q < P; ++q) {  // peers: the parts of this lane group
+            const uint32_t pr = e->peer_rank(q);
+            e->xsend_off[pr] = e->xsoff[q];
+            e->xrecv_off[pr] = e->xroff[q];
+            e->xsend_bytes[pr] = e->xsoff[q + 1] - e->xsoff[q];
+            e->xrecv_bytes[pr] = e->xroff[q + 1] - e->xroff[q];
+        }
+        if (e->xexact && host_sizes) {
+            HIPCHK(hipMemcpyAsync(e->h_segbytes, e->d_segbytes, P * 8, hipMemcpyDeviceToHost, e->stream));
+            HIPCHK(hipStreamSynchronize(e->stream));
+            for (uint32_t q = 0; q < P; ++q)
+                if (e->xexact_s[q]) e->xsend_bytes[e->peer_rank(q)] = e->h_segbytes[q];
+        }
+    }
     x->send = e->d_xsend;
     x->recv = e->d_xrecv;
     x->send_bytes = e->xsend_bytes.data();
     x->recv_bytes = e->xrecv_bytes.data();
-    x->send_total = n_send * pb;
-    x->recv_total = e->recv_off[e->P] * pb;
+    x->send_off = e->xsend_off.data();
+    x->recv_off = e->xrecv_off.data();
+    x->send_total = P > 1 ? e->xsoff[P] : 0;
+    x->recv_total = P > 1 ? e->xroff[P] : 0;
     x->on_device = 1;
+    x->exact = (P > 1 && e->xexact) ? 1 : 0;
     x->stream = (void*)e->stream;
     e->dist_open = true;
     return GG_OK;
 }
+
+extern "C" {
+
+int gg_dist_round_begin(gg_engine* e, gg_exchange* x) { return dist_begin(e, x, true); }
 
 int gg_dist_round_end(gg_engine* e, gg_round_stats* out) {
     if (!e || !e->dist_open) return GG_EINVAL;
     HIPCHK(hipSetDevice(e->device));
     const int64_t r = e->round;
     if (e->n_ghost) {
-        const bool with_set = e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks;
-        const uint64_t chunks = e->n_ghost * (exchange_stride(e->nwp, with_set) / 16);
-        const unsigned blocks = (unsigned)std::max<uint64_t>(
-            1, std::min<uint64_t>((chunks + gg::kBlock - 1) / gg::kBlock, 4096));
-        hipLaunchKernelGGL(gg::unpack_ghosts, dim3(blocks), dim3(gg::kBlock), 0, e->stream, e->d_F[r & 1], e->d_base,
-                           e->d_flg[r & 1], e->d_fired[r & 3], e->d_act + (r & 3), e->d_xrecv, e->n_ghost,
-                           e->ghost0, (uint32_t)e->nwp, with_set ? 1 : 0);
+        gg::UnpackArgs ua{};
+        ua.F_cur = e->d_F[r & 1];
+        ua.base = e->d_base;
+        ua.flg_cur = e->d_flg[r & 1];
+        ua.stamp = e->d_stamp;
+        ua.act_cur = e->d_act + (r & 3);
+        ua.in = e->d_xrecv;
+        ua.seg_off = e->d_xroff;
+        ua.gfirst = e->d_gfirst;
+        ua.parts = e->P;
+        ua.self = e->part;
+        ua.ghost0 = e->ghost0;
+        ua.n_ghost = e->n_ghost;
+        ua.nwp = (uint32_t)e->nwp;
+        ua.stride = e->xstride;
+        ua.round = (uint32_t)r;
+        const uint64_t cap = 2 * e->n_ghost * (e->nwp >= 2 ? 1 + e->nwp / 2 : 1);  // 16-byte pieces, at most
+        const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((cap + gg::kBlock - 1) / gg::kBlock, 2048));
+        hipLaunchKernelGGL(gg::unpack_ghosts, dim3(blocks), dim3(gg::kBlock), 0, e->stream, ua);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(gg::clear_stale_ghosts, dim3((unsigned)((e->n_ghost + 255) / 256)), dim3(256), 0, e->stream,
+                           e->d_F[r & 1], e->d_flg[r & 1], e->d_stamp, e->ghost0, e->n_ghost, (uint32_t)e->nwp,
+                           (uint32_t)r);
         HIPCHK(hipGetLastError());
     }
     e->dist_k++;
@@ -1735,27 +1896,56 @@ int gg_dist_step(gg_engine* e, uint32_t n_rounds) {
     if (!e) return GG_EINVAL;
     if (!e->comm) return e->fail(GG_EINVAL, "no communicator (gg_dist_comm_init)");
     const RcclApi& r = rccl();
+    const uint32_t P = e->P;
+    auto peer = [&](uint32_t q) {  // shares edges with part q (capacities are non-zero both ways)
+        return q != e->part && e->xsoff.size() > q + 1 && e->xsoff[q + 1] > e->xsoff[q];
+    };
     for (uint32_t k = 0; k < n_rounds; ++k) {
         gg_exchange x{};
-        int rc = gg_dist_round_begin(e, &x);
+        int rc = dist_begin(e, &x, false);
         if (rc) return rc;
-        const uint64_t pb = x.send_total / std::max<uint64_t>(1, e->send_off[e->P]);
-        const uint64_t pr = x.recv_total / std::max<uint64_t>(1, e->recv_off[e->P]);
-        NCCLCHK(r.group_start());
-        ncclResult_t first = ncclSuccess;  // the group is always closed, even after a failed call
-        for (uint32_t q = 0; q < e->P && first == ncclSuccess; ++q) {
-            if (q == e->part) continue;  // own segment: empty by construction
-            const uint32_t pr_q = e->peer_rank(q);
-            if (x.send_bytes[pr_q])
-                first = r.send((const uint8_t*)x.send + e->send_off[q] * pb, x.send_bytes[pr_q], ncclUint8,
-                               (int)pr_q, e->comm, e->stream);
-            if (first == ncclSuccess && x.recv_bytes[pr_q])
-                first = r.recv((uint8_t*)x.recv + e->recv_off[q] * pr, x.recv_bytes[pr_q], ncclUint8, (int)pr_q,
-                               e->comm, e->stream);
+        if (P > 1) {
+            std::vector<uint64_t> sb(P, 0), rb(P, 0);
+            for (uint32_t q = 0; q < P; ++q) {
+                sb[q] = e->xsoff[q + 1] - e->xsoff[q];
+                rb[q] = e->xroff[q + 1] - e->xroff[q];
+            }
+            if (e->xexact) {
+                // exact directions: this round's segment size first (8 bytes), then one wait
+                NCCLCHK(r.group_start());
+                ncclResult_t first = ncclSuccess;
+                for (uint32_t q = 0; q < P && first == ncclSuccess; ++q) {
+                    if (q == e->part) continue;
+                    if (e->xexact_s[q])
+                        first = r.send(e->d_segbytes + q, 1, ncclUint64, (int)e->peer_rank(q), e->comm, e->stream);
+                    if (first == ncclSuccess && e->xexact_r[q])
+                        first = r.recv(e->d_segbytes + P + q, 1, ncclUint64, (int)e->peer_rank(q), e->comm, e->stream);
+                }
+                const ncclResult_t ge = r.group_end();
+                NCCLCHK(first);
+                NCCLCHK(ge);
+                HIPCHK(hipMemcpyAsync(e->h_segbytes, e->d_segbytes, 2 * P * 8, hipMemcpyDeviceToHost, e->stream));
+                HIPCHK(hipStreamSynchronize(e->stream));
+                for (uint32_t q = 0; q < P; ++q) {
+                    if (e->xexact_s[q]) sb[q] = e->h_segbytes[q];
+                    if (e->xexact_r[q]) rb[q] = e->h_segbytes[P + q];
+                    if (sb[q] > e->xsoff[q + 1] - e->xsoff[q] || rb[q] > e->xroff[q + 1] - e->xroff[q])
+                        return e->fail(GG_EIO, "exchange segment larger than its capacity");
+                }
+            }
+            NCCLCHK(r.group_start());
+            ncclResult_t first = ncclSuccess;  // the group is always closed, even after a failed call
+            for (uint32_t q = 0; q < P && first == ncclSuccess; ++q) {
+                if (!peer(q)) continue;  // own part / no shared edges: nothing either way
+                const int pr_q = (int)e->peer_rank(q);
+                if (sb[q]) first = r.send(e->d_xsend + e->xsoff[q], sb[q], ncclUint8, pr_q, e->comm, e->stream);
+                if (first == ncclSuccess && rb[q])
+                    first = r.recv(e->d_xrecv + e->xroff[q], rb[q], ncclUint8, pr_q, e->comm, e->stream);
+            }
+            const ncclResult_t ge = r.group_end();
+            NCCLCHK(first);
+            NCCLCHK(ge);
         }
-        const ncclResult_t ge = r.group_end();
-        NCCLCHK(first);
-        NCCLCHK(ge);
         if ((rc = gg_dist_round_end(e, nullptr))) return rc;
     }
     return GG_OK;

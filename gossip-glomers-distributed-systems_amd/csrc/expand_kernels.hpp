@@ -154,8 +154,8 @@ struct RoundArgs {
     const uint64_t* fired_m2;
     const uint64_t* fired_m3;
     uint64_t* fired_cur;        // round r (written whole by round_prep)
-    int32_t* sync_next;         // [n_own]
-    uint32_t* sync_k;
+    int32_t* sync_next;         // [rows] sync timers of the owned nodes and (sharded) of the
+    uint32_t* sync_k;           // ghosts: every engine runs its ghosts' timers itself
     const uint8_t* grp[5];      // partition groups of rounds r-3..r+1 (nullptr: no window)
     const uint64_t* ebits[5];   // the same windows as in-edge bitmaps: bit e = the two ends of
                                 // in-edge e are in different groups (masked streaming rounds)
@@ -463,17 +463,33 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
             }
         }
     }
-    if constexpr (SYNCW) {  // sender states of the ghost rows
-        if (a.sstate) {  // whole waves over 64 consecutive ghost rows (ghost0 % 64 == 0)
-            const uint64_t gw = (a.n_ghost + 63) / 64 * 64;
-            for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < gw; g += stride) {
-                const uint64_t row = a.ghost0 + g;
-                uint8_t st = 0;
-                if (g < a.n_ghost) {
+    if constexpr (SYNCW) {
+        // ghost rows (sharded; whole waves over 64 consecutive ghost rows, ghost0 %
+        // 64 == 0): the ghosts' own sync timers — the same pure function of (seed,
+        // node id, k) their owner runs, so no fired bit crosses the exchange; not
+        // counted here (the owner counts its reads) — and their sender states
+        const uint64_t gw = (a.n_ghost + 63) / 64 * 64;
+        for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < gw; g += stride) {
+            const uint64_t row = a.ghost0 + g;
+            uint8_t st = 0;
+            bool fire = false;
+            if (g < a.n_ghost) {
+                if ((int64_t)a.sync_next[row] == a.round) {
+                    fire = true;
+                    const uint32_t kk = a.sync_k[row] + 1;
+                    a.sync_k[row] = kk;
+                    a.sync_next[row] = (int32_t)(a.round + gg_sync_interval(a.seed, gid_of(a, row), kk, a.sync_base,
+                                                                            a.sync_jitter));
+                }
+                if (a.sstate) {
                     st = (uint8_t)((a.flg_prev[row] & (FL_ACT | FL_LAG)) | (bit_at(a.fired_m2, row) ? SE_FM2 : 0) |
                                    (bit_at(a.fired_m3, row) ? SE_FM3 : 0));
                     a.sstate[row] = st;
                 }
+            }
+            const unsigned long long fw = __ballot(fire);
+            if ((threadIdx.x & 63) == 0) a.fired_cur[row >> 6] = fw;
+            if (a.sstate) {
                 const unsigned long long iw = __ballot(st != 0);
                 if ((threadIdx.x & 63) == 0) a.ibits[row >> 6] = iw;
             }
@@ -2044,7 +2060,7 @@ __global__ void fold_slots(const unsigned long long* ctr, unsigned long long* ou
 
 // Episode reset: fill up to kResetSegs arrays (8-byte words) and start the
 // sync timers, in one launch.
-constexpr int kResetSegs = 16;
+constexpr int kResetSegs = 20;
 struct ResetSeg {
     uint64_t* p;
     uint64_t n;    // 8-byte words
@@ -2055,7 +2071,7 @@ struct ResetArgs {
     int n_seg;
     int32_t* sync_next;
     uint32_t* sync_k;
-    uint64_t n_own;
+    uint64_t n_own, ghost0, n_ghost;  // timers: owned rows and ghost rows
     const uint32_t* gid;
     uint64_t seed;
     uint32_t sync_base, sync_jitter;
@@ -2079,7 +2095,8 @@ __global__ __launch_bounds__(kBlock) void reset_state(ResetArgs ra) {
         }
         for (uint64_t w = pieces * kPiece + t0; w < s.n; w += stride) s.p[w] = s.val;
     }
-    for (uint64_t i = t0; i < ra.n_own; i += stride) {
+    for (uint64_t t = t0; t < ra.n_own + ra.n_ghost; t += stride) {
+        const uint64_t i = t < ra.n_own ? t : ra.ghost0 + (t - ra.n_own);
         ra.sync_k[i] = 0;
         ra.sync_next[i] = (int32_t)gg_sync_interval(ra.seed, ra.gid ? (uint64_t)ra.gid[i] : i, 0, ra.sync_base,
                                                     ra.sync_jitter);
@@ -2118,80 +2135,241 @@ __global__ void build_edge_mask(const int64_t* in_ptr, const uint32_t* in_col, u
 }
 
 // ---------------------------------------------------------------------------
-// Sharded exchange. Payload slot of one node (stride bytes, 16-byte aligned):
-// its F row, its set row (base, when the round ships sets), then a 16-byte tail
-// {flag byte, sync-fired byte}. pack_ghosts writes the slots of the owned rows
-// listed in idx (concatenated per destination rank); unpack_ghosts writes slot
-// k into ghost row ghost0 + k (ghosts are numbered in receive order), rebuilds
-// the ghost words of the fired bitmap and counts the active ghosts into the
-// act ring (next round's dense/sparse choice).
-__global__ __launch_bounds__(kBlock) void pack_ghosts(const uint64_t* F_cur, const uint64_t* base,
-                                                      const uint8_t* flg_cur, const uint64_t* fired_cur,
-                                                      const uint32_t* idx, uint64_t n, uint32_t nwp,
-                                                      int32_t with_set, uint8_t* out) {
-    const uint64_t rowc = nwp / 2 + (nwp & 1);           // 16-byte chunks of a row (nwp=1: 1)
-    const uint64_t chunks = rowc * (with_set ? 2 : 1) + 1;
-    const uint64_t stride = chunks * 16;
-    const uint64_t total = n * chunks;
-    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-         t += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = t / chunks, c = t % chunks;
-        const uint64_t row = idx[k];
-        uint8_t* dst = out + k * stride + c * 16;
-        if (c < rowc * (with_set ? 2 : 1)) {
-            const uint64_t* src = (c < rowc ? F_cur : base) + row * nwp + (c % rowc) * 2;
+// Sharded exchange: only what a peer reads next round crosses.
+// After its round-r kernels, engine p sends peer q, for the owned nodes q holds
+// as ghosts (q's send list, `send_idx`):
+//   kind F  the node's F row, if it is ACT in round r (non-zero: it forwards
+//           these bits in r+1, broadcast.go:55; only first receipts cross, :64-76)
+//   kind S  the node's whole set (base | F when LAG, folded here), if q reads it
+//           in r+1: the node pushes in r+1 (it fired in r-2, :104-108) or a
+//           neighbour on q runs its sync callback in r+1 (fired in r-1; marked by
+//           mark_set_needs from p's own copy of that ghost's timer, :97-101)
+// Sync timers are not exchanged: every engine runs its ghosts' timers itself.
+// Segment for one peer (at a fixed capacity offset): a 16-byte header
+// {entries, payload bytes}, then entries of `stride` bytes: a 16-byte head
+// {position in the send list | XK_SET, 0, row word when nwp == 1} and the row
+// (nwp >= 2). A quiet round sends headers only.
+constexpr uint32_t XK_SET = 0x80000000u;
+
+struct XchgTile {
+    uint32_t peer;   // part index of the destination
+    uint32_t k0;     // first send entry of the tile (global send-list index)
+    uint32_t n;      // entries (<= kBlock), all for `peer`
+    uint32_t first;  // first send entry of `peer`
+};
+
+struct PackArgs {
+    const uint64_t* F_cur;
+    const uint64_t* base;
+    const uint8_t* flg_cur;
+    const uint64_t* fired_m2;   // round r-2: owned pushers of round r+1 (SYNC only)
+    uint8_t* needmark;          // [n_send] set read by a callback on the peer in r+1 (cleared here)
+    const uint32_t* send_idx;   // [n_send] owned local row of each send entry
+    const XchgTile* tiles;
+    uint32_t n_tiles;
+    uint32_t* cnt;              // [parts] entries written per peer this round
+    uint8_t* out;
+    const uint64_t* seg_off;    // [parts] byte offset of each peer's segment in `out`
+    uint32_t nwp, stride;
+    int32_t sync;               // sets may be read next round
+};
+
+__global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
+    __shared__ uint32_t s_row[2 * kBlock], s_head[2 * kBlock];
+    __shared__ uint32_t s_cnt[kBlock / 64];
+    __shared__ uint32_t s_base, s_tot;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t cpe = x.nwp >= 2 ? 1 + x.nwp / 2 : 1;  // 16-byte chunks per entry
+    for (uint32_t ti = blockIdx.x; ti < x.n_tiles; ti += gridDim.x) {
+        const XchgTile t = x.tiles[ti];
+        const uint32_t k = t.k0 + threadIdx.x;
+        const bool valid = threadIdx.x < t.n;
+        const uint32_t u = valid ? x.send_idx[k] : 0u;
+        const uint8_t fl = valid ? x.flg_cur[u] : (uint8_t)0;
+        const bool fa = (fl & FL_ACT) != 0;
+        bool sn = false;
+        if (valid && x.sync) {
+            const bool nm = x.needmark[k] != 0;
+            if (nm) x.needmark[k] = 0;
+            sn = nm || bit_at(x.fired_m2, u);
+        }
+        const uint32_t c = (fa ? 1u : 0u) + (sn ? 1u : 0u);
+        uint32_t incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) s_cnt[wave] = incl;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0;
+            for (int w = 0; w < kBlock / 64; ++w) {
+                const uint32_t v = s_cnt[w];
+                s_cnt[w] = tot;
+                tot += v;
+            }
+            s_tot = tot;
+            s_base = tot ? atomicAdd(&x.cnt[t.peer], tot) : 0u;
+        }
+        __syncthreads();
+        uint32_t pos = s_cnt[wave] + incl - c;
+        const uint32_t idx = k - t.first;
+        if (fa) {
+            s_row[pos] = u;
+            s_head[pos] = idx;
+            ++pos;
+        }
+        if (sn) {
+            s_row[pos] = u | ((fl & FL_LAG) ? XK_SET : 0u);  // bit 31: fold F into the set
+            s_head[pos] = idx | XK_SET;
+        }
+        __syncthreads();
+        uint8_t* seg = x.out + x.seg_off[t.peer] + 16 + (uint64_t)s_base * x.stride;
+        for (uint32_t e = threadIdx.x; e < s_tot * cpe; e += kBlock) {
+            const uint32_t j = e / cpe, ch = e % cpe;
+            const uint32_t hd = s_head[j], rr = s_row[j];
+            const bool set = (hd & XK_SET) != 0, lag = (rr & XK_SET) != 0;
+            const uint64_t u2 = rr & ~XK_SET;
+            uint8_t* dst = seg + (uint64_t)j * x.stride + ch * 16;
             ulonglong2 v;
-            v.x = src[0];
-            v.y = nwp > 1 ? src[1] : 0ull;
-            *reinterpret_cast<ulonglong2*>(dst) = v;
-        } else {
-            ulonglong2 v;
-            v.x = (uint64_t)flg_cur[row] | ((uint64_t)((fired_cur[row >> 6] >> (row & 63)) & 1ull) << 8);
-            v.y = 0;
+            if (ch == 0) {  // head (+ the row word when nwp == 1)
+                v.x = hd;
+                v.y = 0;
+                if (x.nwp == 1) v.y = set ? (x.base[u2] | (lag ? x.F_cur[u2] : 0ull)) : x.F_cur[u2];
+            } else {
+                const uint64_t o = u2 * x.nwp + 2 * (ch - 1);
+                if (set) {
+                    v = *reinterpret_cast<const ulonglong2*>(x.base + o);
+                    if (lag) {
+                        const ulonglong2 f = *reinterpret_cast<const ulonglong2*>(x.F_cur + o);
+                        v.x |= f.x;
+                        v.y |= f.y;
+                    }
+                } else {
+                    v = *reinterpret_cast<const ulonglong2*>(x.F_cur + o);
+                }
+            }
             *reinterpret_cast<ulonglong2*>(dst) = v;
         }
+        __syncthreads();  // LDS reuse
     }
 }
 
-__global__ __launch_bounds__(kBlock) void unpack_ghosts(uint64_t* F_cur, uint64_t* base, uint8_t* flg_cur,
-                                                        uint64_t* fired_cur, uint32_t* act_cur,
-                                                        const uint8_t* in, uint64_t n, uint64_t ghost0,
-                                                        uint32_t nwp, int32_t with_set) {
-    const uint64_t rowc = nwp / 2 + (nwp & 1);
-    const uint64_t chunks = rowc * (with_set ? 2 : 1) + 1;
-    const uint64_t stride = chunks * 16;
-    const uint64_t total = n * chunks;
-    uint32_t nact = 0;
-    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-         t += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = t / chunks, c = t % chunks;
-        const uint64_t row = ghost0 + k;
-        const uint8_t* src = in + k * stride + c * 16;
-        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(src);
-        if (c < rowc * (with_set ? 2 : 1)) {
-            uint64_t* dst = (c < rowc ? F_cur : base) + row * nwp + (c % rowc) * 2;
-            dst[0] = v.x;
-            if (nwp > 1) dst[1] = v.y;
-        } else {
-            const uint8_t f = (uint8_t)(v.x & 0xff);
-            flg_cur[row] = f;
-            nact += (f & FL_ACT) ? 1u : 0u;
+// After pack_ghosts: each peer's header, its byte count for an exact-size
+// exchange, the round's payload bytes; counters reset for the next round.
+__global__ void finish_pack(uint32_t* cnt, uint8_t* out, const uint64_t* seg_off, uint32_t parts, uint32_t self,
+                            uint32_t stride, unsigned long long* seg_bytes, unsigned long long* payload) {
+    const uint32_t q = threadIdx.x;
+    unsigned long long pay = 0;
+    if (q < parts) {
+        const uint32_t n = cnt[q];
+        const bool peer = q != self && seg_off[q + 1] > seg_off[q];  // segments with capacity only
+        if (peer) {
+            ulonglong2 h;
+            h.x = n;
+            h.y = (unsigned long long)n * stride;
+            *reinterpret_cast<ulonglong2*>(out + seg_off[q]) = h;
+            pay = (unsigned long long)n * stride;
         }
+        seg_bytes[q] = peer ? 16 + (unsigned long long)n * stride : 0ull;
+        cnt[q] = 0;
     }
-    // fired words of the ghost rows (ghost0 is a multiple of 64)
-    const uint64_t nwords = (n + 63) / 64;
-    for (uint64_t wi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; wi < nwords;
-         wi += (uint64_t)gridDim.x * blockDim.x) {
-        unsigned long long word = 0;
-        for (uint64_t b = 0; b < 64 && wi * 64 + b < n; ++b) {
-            const uint64_t k = wi * 64 + b;
-            const uint8_t fb = in[k * stride + (chunks - 1) * 16 + 1];
-            word |= (unsigned long long)(fb & 1) << b;
+    pay = wave_sum(pay);
+    if (threadIdx.x == 0) *payload = pay;
+}
+
+// Sync rounds: ghosts that fired in r-1 run their callback in r+1 and read the
+// sets of their out-peers; mark those owned nodes' send entries for the
+// ghost's owner (gout_sidx: the send entry of each ghost -> owned edge).
+__global__ void mark_set_needs(const uint64_t* fired_m1, const int64_t* gout_ptr, const uint32_t* gout_sidx,
+                               uint64_t ghost0, uint64_t n_ghost, uint8_t* needmark) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_ghost || !bit_at(fired_m1, ghost0 + g)) return;
+    for (int64_t e = gout_ptr[g]; e < gout_ptr[g + 1]; ++e) needmark[gout_sidx[e]] = 1;
+}
+
+struct UnpackArgs {
+    uint64_t* F_cur;
+    uint64_t* base;
+    uint8_t* flg_cur;
+    uint32_t* stamp;             // [n_ghost] last round a ghost's F row arrived
+    uint32_t* act_cur;           // act ring slot of round r
+    const uint8_t* in;
+    const uint64_t* seg_off;     // [parts + 1] capacity offset of each source's segment
+    const uint32_t* gfirst;      // [parts + 1] first ghost index from each source part
+    uint32_t parts, self;
+    uint64_t ghost0, n_ghost;
+    uint32_t nwp, stride;
+    uint32_t round;
+};
+
+// Every received entry into its ghost row (kind F: F row, flag ACT, stamp;
+// kind S: the set into base).
+__global__ __launch_bounds__(kBlock) void unpack_ghosts(UnpackArgs x) {
+    __shared__ uint32_t s_src[64], s_pref[65];
+    const uint32_t cpe = x.nwp >= 2 ? 1 + x.nwp / 2 : 1;
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0, m = 0;
+        for (uint32_t p = 0; p < x.parts; ++p) {
+            if (p == x.self || x.seg_off[p + 1] == x.seg_off[p]) continue;
+            const uint32_t n = (uint32_t)*reinterpret_cast<const unsigned long long*>(x.in + x.seg_off[p]);
+            s_src[m] = p;
+            s_pref[m] = tot;
+            tot += n;
+            ++m;
         }
-        fired_cur[(ghost0 >> 6) + wi] = word;
+        s_pref[m] = tot;
+        s_src[63] = m;
+    }
+    __syncthreads();
+    const uint32_t m = s_src[63];
+    const uint64_t total = (uint64_t)s_pref[m] * cpe;
+    uint32_t nact = 0;
+    for (uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x; e < total; e += (uint64_t)gridDim.x * kBlock) {
+        const uint32_t j = (uint32_t)(e / cpe), ch = (uint32_t)(e % cpe);
+        uint32_t lo = 0, hi = m - 1;  // the source segment holding entry j
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (s_pref[mid] <= j) lo = mid;
+            else hi = mid - 1;
+        }
+        const uint32_t p = s_src[lo];
+        const uint8_t* ent = x.in + x.seg_off[p] + 16 + (uint64_t)(j - s_pref[lo]) * x.stride;
+        const uint32_t hd = *reinterpret_cast<const uint32_t*>(ent);
+        const bool set = (hd & XK_SET) != 0;
+        const uint64_t g = x.gfirst[p] + (hd & ~XK_SET);
+        const uint64_t row = x.ghost0 + g;
+        if (ch == 0) {
+            if (x.nwp == 1) {
+                const uint64_t w = *reinterpret_cast<const uint64_t*>(ent + 8);
+                if (set) x.base[row] = w;
+                else x.F_cur[row] = w;
+            }
+            if (!set) {
+                x.flg_cur[row] = FL_ACT;
+                x.stamp[g] = x.round;
+                ++nact;
+            }
+        } else {
+            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(ent + 16 * ch);
+            *reinterpret_cast<ulonglong2*>((set ? x.base : x.F_cur) + row * x.nwp + 2 * (ch - 1)) = v;
+        }
     }
     const unsigned long long s = wave_sum(nact);
-    if ((threadIdx.x & 63) == 0 && s) atomicAdd(act_cur, (uint32_t)s);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(x.act_cur, (uint32_t)s);
+}
+
+// Ghosts whose F row of round r-2 sits in this round's buffer and that sent no
+// F row this round: zero it (F rows are zero unless ACT) and clear the flag.
+__global__ void clear_stale_ghosts(uint64_t* F_cur, uint8_t* flg_cur, const uint32_t* stamp, uint64_t ghost0,
+                                   uint64_t n_ghost, uint32_t nwp, uint32_t round) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_ghost) return;
+    const uint64_t row = ghost0 + g;
+    if (!(flg_cur[row] & FL_ACT) || stamp[g] == round) return;
+    for (uint32_t w = 0; w < nwp; ++w) F_cur[row * nwp + w] = 0;
+    flg_cur[row] = 0;
 }
 
 }  // namespace gg

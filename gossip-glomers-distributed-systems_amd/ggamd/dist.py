@@ -104,34 +104,60 @@ class ShardedRunner:
         return s
 
     def round(self, wait: bool = False) -> dict | None:
+        """One sharded round with the exchange through torch.distributed: every
+        rank first tells every rank how many bytes it sends it (an all_to_all of
+        the sizes: the engine's segments carry only what the peer reads next
+        round), then the segments move point-to-point into the
+        receivers' fixed segment offsets."""
         x = self.eng.dist_round_begin()
+        W = self.world
         on_dev = bool(x.on_device)
-        ss = x.send_bytes[:self.world]
-        rs = x.recv_bytes[:self.world]
+        ss = [int(x.send_bytes[i]) for i in range(W)]
+        soff = [int(x.send_off[i]) for i in range(W)]
+        roff = [int(x.recv_off[i]) for i in range(W)]
+        ext = self._stream(x.stream)
+        size_dev = self.device if self.nccl else torch.device("cpu")
+        st = torch.tensor(ss, dtype=torch.int64, device=size_dev)
+        rt = torch.empty_like(st)
+        if self.nccl and ext is not None:
+            with torch.cuda.stream(ext):
+                dist.all_to_all_single(rt, st, group=self.group)
+        else:
+            dist.all_to_all_single(rt, st, group=self.group)
+        rs = rt.cpu().tolist()
+        for i in range(W):
+            x.recv_bytes[i] = rs[i]
+        if not any(ss) and not any(rs):
+            return self.eng.dist_round_end(wait=wait)
         send = self._view(x.send, x.send_total, on_dev)
         recv = self._view(x.recv, x.recv_total, on_dev)
-        ext = self._stream(x.stream)
-        if self.nccl:
-            assert on_dev, "nccl backend needs device buffers"
-            if ext is not None:
-                with torch.cuda.stream(ext):
-                    dist.all_to_all_single(recv, send, rs, ss, group=self.group)
-            else:
-                dist.all_to_all_single(recv, send, rs, ss, group=self.group)
-        elif on_dev:
-            # gloo with device buffers (several ranks on one GPU): stage via host
+        stage = on_dev and not self.nccl  # gloo with device buffers (ranks sharing one GPU): via host
+        if stage:
             if ext is not None:
                 ext.synchronize()
-            send_h = send.cpu()
-            recv_h = torch.empty(recv.numel(), dtype=torch.uint8)
-            dist.all_to_all_single(recv_h, send_h, rs, ss, group=self.group)
+            send_b, recv_b = send.cpu(), torch.empty(recv.numel(), dtype=torch.uint8)
+        else:
+            send_b, recv_b = send, recv
+        glob = (lambda r: r) if self.group is None else (lambda r: dist.get_global_rank(self.group, r))
+        ops = []
+        for q in range(W):
+            if ss[q]:
+                ops.append(dist.P2POp(dist.isend, send_b[soff[q]:soff[q] + ss[q]], glob(q), self.group))
+            if rs[q]:
+                ops.append(dist.P2POp(dist.irecv, recv_b[roff[q]:roff[q] + rs[q]], glob(q), self.group))
+        if self.nccl and ext is not None:
+            with torch.cuda.stream(ext):
+                for w in dist.batch_isend_irecv(ops):
+                    w.wait()
+        else:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        if stage:
             if ext is not None:
                 with torch.cuda.stream(ext):
-                    recv.copy_(recv_h)
+                    recv.copy_(recv_b)
             else:
-                recv.copy_(recv_h)
-        else:
-            dist.all_to_all_single(recv, send, rs, ss, group=self.group)
+                recv.copy_(recv_b)
         return self.eng.dist_round_end(wait=wait)
 
     def step(self, n_rounds: int, reduce: bool = True) -> list[dict]:

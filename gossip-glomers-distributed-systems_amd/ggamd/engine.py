@@ -76,9 +76,12 @@ class GGExchange(C.Structure):
         ("recv", C.c_void_p),
         ("send_bytes", C.POINTER(C.c_uint64)),
         ("recv_bytes", C.POINTER(C.c_uint64)),
+        ("send_off", C.POINTER(C.c_uint64)),
+        ("recv_off", C.POINTER(C.c_uint64)),
         ("send_total", C.c_uint64),
         ("recv_total", C.c_uint64),
         ("on_device", C.c_int32),
+        ("exact", C.c_int32),
         ("stream", C.c_void_p),
     ]
 

@@ -161,23 +161,34 @@ int gg_reset(gg_engine* e);
  * contiguous ranges, and keeps its range's nodes ("owned") plus read-only copies
  * of the remote nodes adjacent to them ("ghosts"). Results do not depend on the
  * order: claims still go by ascending original sender id. A round is
- *   gg_dist_round_begin -> caller moves the packed ghost payloads between ranks
- *                          (an all-to-all-v of bytes: send_bytes[q] from `send`
- *                          to rank q, recv_bytes[p] from rank p into `recv`, both
- *                          concatenated in rank order)
+ *   gg_dist_round_begin -> caller moves the ghost payloads between the ranks of
+ *                          its lane group (see gg_exchange)
  *   gg_dist_round_end   -> the engine unpacks the ghosts; per-rank counters are
  *                          summed over ranks by the caller.
+ * Only what a peer reads next round crosses: the F rows of owned
+ * nodes that learned something this round, and whole sets only where the peer's
+ * sync callback or a push reads them next round; sync timers are not exchanged
+ * (each engine runs its ghosts' timers). A quiet round moves segment headers only.
  * When `stream` is non-NULL the round's kernels are only enqueued on that HIP
  * stream; the caller enqueues its collective on the same stream and passes
  * out = NULL to gg_dist_round_end, then collects the counters of all pending
  * rounds with gg_dist_flush (no host synchronisation per round). */
 typedef struct {
-    void* send;                 /* packed payloads, [world] segments */
-    void* recv;
-    const uint64_t* send_bytes; /* [world] bytes to each rank this round */
-    const uint64_t* recv_bytes; /* [world] bytes from each rank this round */
-    uint64_t send_total, recv_total;
+    void* send;                 /* packed payloads: one segment per peer, at send_off[q] */
+    void* recv;                 /* the segment from rank p must land at recv_off[p] */
+    const uint64_t* send_bytes; /* [world] bytes to send to each rank this round */
+    uint64_t* recv_bytes;       /* [world] bytes to receive from each rank (see exact) */
+    const uint64_t* send_off;   /* [world] byte offset of the segment for rank q in send */
+    const uint64_t* recv_off;   /* [world] byte offset of the segment from rank p in recv */
+    uint64_t send_total, recv_total;  /* buffer capacities */
     int32_t on_device;          /* 1: send/recv are device memory of the engine's GPU */
+    int32_t exact;              /* 0: static sizes (the segment capacities): send_bytes and recv_bytes
+                                   are fixed and the segments are contiguous in rank order, so one
+                                   all-to-all-v with them moves the round. 1: send_bytes are this
+                                   round's exact sizes (the engine waited for its pack kernel): each
+                                   peer must learn the size it receives (e.g. an all-to-all of the
+                                   sizes; the caller writes them into recv_bytes) and the bytes must
+                                   land at recv_off (e.g. point-to-point receives into views). */
     void* stream;               /* hipStream_t the round was enqueued on (NULL: done on return) */
 } gg_exchange;
 

@@ -104,7 +104,7 @@ struct gg_engine {
     // sharded exchange (dense: every owned node's seen row, F row and fired
     // bit to every other rank; the HIP engine sends ghosts only)
     std::vector<uint8_t> xsend, xrecv;
-    std::vector<uint64_t> xsend_bytes, xrecv_bytes;
+    std::vector<uint64_t> xsend_bytes, xrecv_bytes, xsend_off, xrecv_off;
     std::vector<gg_round_stats> dist_pending;
     uint64_t xsend_sent = 0;  // payload bytes of the open round
 
@@ -609,10 +609,19 @@ int gg_dist_round_begin(gg_engine* e, gg_exchange* x) {
             p[2 * e->nw * 8] = e->fired_at(r, rep) ? 1 : 0;
         }
     }
+    e->xsend_off.assign(e->world, 0);  // segments contiguous in rank order (static sizes)
+    e->xrecv_off.assign(e->world, 0);
+    for (uint32_t q = 1; q < e->world; ++q) {
+        e->xsend_off[q] = e->xsend_off[q - 1] + e->xsend_bytes[q - 1];
+        e->xrecv_off[q] = e->xrecv_off[q - 1] + e->xrecv_bytes[q - 1];
+    }
     x->send = e->xsend.data();
     x->recv = e->xrecv.data();
     x->send_bytes = e->xsend_bytes.data();
     x->recv_bytes = e->xrecv_bytes.data();
+    x->send_off = e->xsend_off.data();
+    x->recv_off = e->xrecv_off.data();
+    x->exact = 0;
     x->send_total = st;
     x->recv_total = rt;
     x->on_device = 0;

@@ -94,10 +94,12 @@ def _scenarios():
     return out
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_equals_single(hip_lib, world):
+@pytest.mark.parametrize("world,mode", [(2, "static"), (3, "static"), (2, "exact"), (3, "exact")])
+def test_sharded_equals_single(hip_lib, world, mode):
+    """GG_XCHG_MODE: every exchange direction with static sizes (segment
+    capacities) or exact sizes (sizes first, then only the used bytes)."""
     scs = _scenarios()
-    res = _run(hip_lib, scs, world)
+    res = _run(hip_lib, scs, world, env={"GG_XCHG_MODE": mode})
     for k, sc in enumerate(scs):
         single = make_engine(hip_lib, sc, device=0)
         s1 = single.step(sc.rounds)
@@ -128,7 +130,7 @@ def _rmat_scenarios():
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_rmat_hubs_equals_single(hip_lib, world):
-    env = {"GG_HUB_DEG": "24"}
+    env = {"GG_HUB_DEG": "24", "GG_XCHG_MODE": "exact"}
     scs = _rmat_scenarios()
     res = _run(hip_lib, scs, world, env=env)
     old = os.environ.get("GG_HUB_DEG")
@@ -182,6 +184,29 @@ def test_lane_groups_equal_single(hip_lib, world, groups):
             os.environ.pop("GG_HUB_DEG", None)
         else:
             os.environ["GG_HUB_DEG"] = old
+
+
+@pytest.mark.parametrize("kind", ["tree", "random_regular"])
+def test_exchange_payload_follows_activity(hip_lib, kind):
+    """Only first receipts cross (broadcast.go:55,64-76): a rank's payload bytes
+    per round are positive while its boundary nodes learn values and exactly 0
+    once the network is quiet (no sync: no sets are ever read)."""
+    from ggamd import topology as T
+    from ggamd.workload import uniform_injections
+    V = 3000 if kind == "tree" else 4000
+    topo = T.tree(V, 4) if kind == "tree" else T.random_regular(V, 8, seed=12)
+    sc = Scenario(topo, 256, 40, uniform_injections(V, 200, 5), seed=9, enable_sync=False)
+    res = _run(hip_lib, [sc], 2, env={"GG_XCHG_MODE": "exact"})
+    single = make_engine(hip_lib, sc, device=0)
+    s1 = single.step(sc.rounds)
+    last = max(i for i, s in enumerate(s1) if s["new_bits"])
+    for rank in range(2):
+        stats = res[rank][0][0]
+        assert not diff_stats(s1, stats)
+        sent = [s["sent_bytes"] for s in stats]
+        assert all(b == 0 for b in sent[last + 1:]), sent
+        assert sum(sent[:last + 1]) > 0, sent
+    single.close()
 
 
 def test_lane_group_engine_steps_without_exchange(hip_lib):
