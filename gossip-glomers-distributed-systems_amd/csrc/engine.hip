@@ -960,6 +960,28 @@ void choose_partition(uint64_t V, const int64_t* row_ptr, const int32_t* col, co
     }
 }
 
+// Local row order of an unsharded engine: on a power-law graph (max in-degree
+// > 16 x the mean, or GG_ORDER=degree) the nodes by descending in-degree, ties
+// by id: the hubs, which most in-lists name (R-MAT at 2^22 nodes: the top 1% of
+// nodes hold 56% of all edge ends), share cache lines, DRAM pages and TLB
+// entries instead of being scattered over the whole F array by the generator's
+// random relabelling. Claim order is unaffected (in-lists stay ascending by
+// original id). Empty: keep the native order.
+std::vector<uint32_t> degree_order(uint64_t V, const int64_t* tin) {
+    const char* o = getenv("GG_ORDER");
+    if (o && !strcmp(o, "native")) return {};
+    uint64_t maxd = 0;
+    for (uint64_t v = 0; v < V; ++v) maxd = std::max<uint64_t>(maxd, (uint64_t)(tin[v + 1] - tin[v]));
+    const double mean = (double)tin[V] / (double)std::max<uint64_t>(1, V);
+    if (!(o && !strcmp(o, "degree")) && !((double)maxd > 16.0 * std::max(1.0, mean))) return {};
+    std::vector<uint64_t> pos(maxd + 2, 0);  // counting sort, descending degree, stable in id
+    for (uint64_t v = 0; v < V; ++v) pos[maxd - (uint64_t)(tin[v + 1] - tin[v]) + 1]++;
+    for (uint64_t d = 0; d <= maxd; ++d) pos[d + 1] += pos[d];
+    std::vector<uint32_t> order(V);
+    for (uint64_t v = 0; v < V; ++v) order[pos[maxd - (uint64_t)(tin[v + 1] - tin[v])]++] = (uint32_t)v;
+    return order;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1176,7 +1198,9 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
         choose_partition(V, row_ptr, col, tin, Wd, order, plo, owner);
     } else {
         plo = {0, V};
+        order = degree_order(V, tin);
     }
+    const bool perm = Wd > 1 || !order.empty();  // local rows != node ids
     auto node_at = [&](uint64_t pos) -> uint32_t { return order.empty() ? (uint32_t)pos : order[pos]; };
     const uint64_t n_own = plo[e->part + 1] - plo[e->part];
     e->n_own = n_own;
@@ -1187,9 +1211,11 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     std::vector<std::vector<uint32_t>> send_ids(Wd);  // the same, original ids (ascending)
     e->send_off.assign(Wd + 1, 0);
     e->recv_off.assign(Wd + 1, 0);
-    if (Wd > 1) {
+    if (perm) {
         e->loc_of.assign(V, ~0u);
         for (uint64_t i = 0; i < n_own; ++i) e->loc_of[node_at(plo[e->part] + i)] = (uint32_t)i;
+    }
+    if (Wd > 1) {
         // ghosts: remote nodes adjacent (in or out) to owned ones; send lists:
         // owned nodes adjacent to each remote rank. Both sorted by node id, so
         // rank q's receive order from p equals p's send order to q.
@@ -1226,20 +1252,21 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     e->ghost0 = Wd > 1 ? (n_own + 63) / 64 * 64 : n_own;
     e->rows = std::max<uint64_t>(64, (e->ghost0 + e->n_ghost + 63) / 64 * 64);
     if (e->rows > 0x7fffffffull) return e->fail(GG_EINVAL, "local rows exceed 2^31");
-    std::unordered_map<uint32_t, uint32_t> ghost_row;  // ghost node -> local row
-    if (Wd > 1) {
+    if (perm) {
         e->gid.assign(e->rows, ~0u);
         for (uint64_t i = 0; i < n_own; ++i) e->gid[i] = node_at(plo[e->part] + i);
-        ghost_row.reserve(ghosts.size() * 2);
-        for (uint64_t k = 0; k < ghosts.size(); ++k) {
-            e->gid[e->ghost0 + k] = ghosts[k];
-            ghost_row.emplace(ghosts[k], (uint32_t)(e->ghost0 + k));
-        }
+        for (uint64_t k = 0; k < ghosts.size(); ++k) e->gid[e->ghost0 + k] = ghosts[k];
     }
+    // local row of a node: owned, or a ghost (the ghosts from part q are ascending
+    // ids at ghost0 + recv_off[q]); read-only lookups, so rows build in parallel
     auto row_of = [&](uint32_t u) -> uint32_t {
-        if (Wd == 1) return u;
+        if (!perm) return u;
         const uint32_t l = e->loc_of[u];
-        return l != ~0u ? l : ghost_row.at(u);
+        if (l != ~0u) return l;
+        const uint32_t q = owner[u];
+        const uint32_t* g0 = ghosts.data() + e->recv_off[q];
+        const uint32_t* g1 = ghosts.data() + e->recv_off[q + 1];
+        return (uint32_t)(e->ghost0 + e->recv_off[q] + (std::lower_bound(g0, g1, u) - g0));
     };
     // ---- owned rows: in-lists (ascending sender id: claim order) and out-lists
     // (ascending receiver id: callback order) with local-row columns
@@ -1265,8 +1292,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
                 for (int64_t k = 0; k < row_ptr[v + 1] - row_ptr[v]; ++k) ocol[optr[i] + k] = row_of((uint32_t)ob[k]);
         }
     };
-    if (Wd == 1) host_parallel(n_own, build_rows);  // row_of is pure here
-    else build_rows(0, n_own);
+    host_parallel(n_own, build_rows);
     for (uint64_t k = 0; k < icol.size() && e->n_ghost; ++k) {
         const uint32_t ru = icol[k] & gg::kColMask;
         if (ru >= e->ghost0) gcnt[ru - e->ghost0 + 1]++;
@@ -1299,9 +1325,11 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
         HIPCHK(hipMemcpy(e->d_out_ptr, optr.data(), (n_own + 1) * 8, hipMemcpyHostToDevice));
         if (!ocol.empty()) HIPCHK(hipMemcpy(e->d_out_col, ocol.data(), ocol.size() * 4, hipMemcpyHostToDevice));
     }
-    if (Wd > 1) {
+    if (perm) {
         HIPCHK(hipMalloc(&e->d_gid, e->rows * 4));
         HIPCHK(hipMemcpy(e->d_gid, e->gid.data(), e->rows * 4, hipMemcpyHostToDevice));
+    }
+    if (Wd > 1) {
         std::vector<uint32_t> sidx;
         for (uint32_t q = 0; q < Wd; ++q) sidx.insert(sidx.end(), sendl[q].begin(), sendl[q].end());
         HIPCHK(hipMalloc(&e->d_send_idx, std::max<size_t>(1, sidx.size()) * 4));
@@ -1416,6 +1444,28 @@ int gg_topology_generate(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_ou
     }
     int rc = gg_gen::build_csr(*spec, e->stream, gg::kRecipBit, &g, &err);
     if (rc) return e->fail(rc, err);
+    e->rows = std::max<uint64_t>(64, (e->V + 63) / 64 * 64);
+    e->loc_of.clear();
+    e->gid.clear();
+    uint64_t dmax = 0;
+    if ((rc = gg_gen::max_degree(g.row_ptr, e->V, e->stream, &dmax, &err))) {
+        (void)hipFree(g.row_ptr);
+        (void)hipFree(g.col);
+        return e->fail(rc, err);
+    }
+    {  // degree_order's rule, on the device: power-law graphs get rows by descending degree
+        const char* o = getenv("GG_ORDER");
+        const double mean = (double)g.nnz / (double)std::max<uint64_t>(1, e->V);
+        const bool want = o && !strcmp(o, "degree") ? true
+                          : o && !strcmp(o, "native") ? false
+                                                      : (double)dmax > 16.0 * std::max(1.0, mean);
+        if (want && (rc = gg_gen::degree_reorder(&g, e->rows, e->stream, gg::kRecipBit, &e->d_gid, &e->gid,
+                                                 &e->loc_of, &err))) {
+            (void)hipFree(g.row_ptr);
+            (void)hipFree(g.col);
+            return e->fail(rc, err);
+        }
+    }
     e->d_in_ptr = g.row_ptr;
     e->d_in_col = g.col;
     e->d_out_ptr = g.row_ptr;
@@ -1424,13 +1474,8 @@ int gg_topology_generate(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_ou
     e->n_own = e->V;
     e->n_ghost = 0;
     e->ghost0 = e->V;
-    e->rows = std::max<uint64_t>(64, (e->V + 63) / 64 * 64);
-    e->loc_of.clear();
-    e->gid.clear();
     e->n_in_edges = g.nnz;
     if (nnz_out) *nnz_out = g.nnz;
-    uint64_t dmax = 0;
-    if ((rc = gg_gen::max_degree(g.row_ptr, e->V, e->stream, &dmax, &err))) return e->fail(rc, err);
     std::vector<int64_t> iptr;
     if (dmax > hub_threshold()) {  // hub chunks are planned on the host
         iptr.resize(e->V + 1);
@@ -1446,12 +1491,35 @@ int gg_topology_export(gg_engine* e, int64_t* row_ptr, int32_t* col, uint64_t ca
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
     if (nnz_out) *nnz_out = e->n_in_edges;
-    HIPCHK(hipMemcpy(row_ptr, e->d_in_ptr, (e->V + 1) * 8, hipMemcpyDeviceToHost));
+    const uint64_t V = e->V;
+    if (e->gid.empty()) {  // rows are node ids
+        HIPCHK(hipMemcpy(row_ptr, e->d_in_ptr, (V + 1) * 8, hipMemcpyDeviceToHost));
+        if (!col) return GG_OK;
+        if (cap < e->n_in_edges) return e->fail(GG_EINVAL, "col buffer too small");
+        if (e->n_in_edges) HIPCHK(hipMemcpy(col, e->d_in_col, e->n_in_edges * 4, hipMemcpyDeviceToHost));
+        host_parallel(e->n_in_edges, [&](uint64_t lo, uint64_t hi) {
+            for (uint64_t k = lo; k < hi; ++k) col[k] = (int32_t)((uint32_t)col[k] & gg::kColMask);
+        });
+        return GG_OK;
+    }
+    // degree-ordered rows: back to node ids (row v = local row loc_of[v], columns by gid)
+    std::vector<int64_t> ip(V + 1);
+    HIPCHK(hipMemcpy(ip.data(), e->d_in_ptr, (V + 1) * 8, hipMemcpyDeviceToHost));
+    row_ptr[0] = 0;
+    for (uint64_t v = 0; v < V; ++v) {
+        const uint32_t l = e->loc_of[v];
+        row_ptr[v + 1] = row_ptr[v] + (ip[l + 1] - ip[l]);
+    }
     if (!col) return GG_OK;
     if (cap < e->n_in_edges) return e->fail(GG_EINVAL, "col buffer too small");
-    if (e->n_in_edges) HIPCHK(hipMemcpy(col, e->d_in_col, e->n_in_edges * 4, hipMemcpyDeviceToHost));
-    host_parallel(e->n_in_edges, [&](uint64_t lo, uint64_t hi) {
-        for (uint64_t k = lo; k < hi; ++k) col[k] = (int32_t)((uint32_t)col[k] & gg::kColMask);
+    std::vector<uint32_t> ic(e->n_in_edges);
+    if (e->n_in_edges) HIPCHK(hipMemcpy(ic.data(), e->d_in_col, e->n_in_edges * 4, hipMemcpyDeviceToHost));
+    host_parallel(V, [&](uint64_t lo, uint64_t hi) {
+        for (uint64_t v = lo; v < hi; ++v) {
+            const uint32_t l = e->loc_of[v];
+            for (int64_t k = ip[l]; k < ip[l + 1]; ++k)
+                col[row_ptr[v] + (k - ip[l])] = (int32_t)e->gid[ic[k] & gg::kColMask];
+        }
     });
     return GG_OK;
 }
@@ -1951,56 +2019,72 @@ int gg_dist_step(gg_engine* e, uint32_t n_rounds) {
     return GG_OK;
 }
 
-// Sets of owned local rows [a, b) after the last completed round: base | F_last
-// where the row's flag says LAG.
-static int copy_rows(gg_engine* e, uint64_t a, uint64_t b, std::vector<uint64_t>& h) {
-    const uint64_t n = b - a;
-    h.resize(n * e->nwp);
-    if (!n) return GG_OK;
-    HIPCHK(hipStreamSynchronize(e->stream));
-    HIPCHK(hipMemcpy(h.data(), e->d_base + a * e->nwp, h.size() * 8, hipMemcpyDeviceToHost));
-    if (e->round == 0) return GG_OK;
-    const int last = (int)((e->round - 1) & 1);
-    std::vector<uint8_t> fl(n);
-    HIPCHK(hipMemcpy(fl.data(), e->d_flg[last] + a, n, hipMemcpyDeviceToHost));
-    std::vector<uint64_t> f(e->nwp);
-    for (uint64_t i = 0; i < n; ++i) {
-        if (!(fl[i] & gg::FL_LAG)) continue;
-        HIPCHK(hipMemcpy(f.data(), e->d_F[last] + (a + i) * e->nwp, e->nwp * 8, hipMemcpyDeviceToHost));
-        for (uint64_t j = 0; j < e->nwp; ++j) h[i * e->nwp + j] |= f[j];
-    }
-    return GG_OK;
-}
+}  // extern "C"
 
 // Local rows of owned nodes (GG_EINVAL if one is not owned).
-static int rows_of(gg_engine* e, const uint32_t* nodes, uint64_t n, std::vector<uint32_t>& rows, uint64_t& lo,
-                   uint64_t& hi) {
+static int rows_of(gg_engine* e, const uint32_t* nodes, uint64_t n, std::vector<uint32_t>& rows) {
     rows.resize(n);
-    lo = ~0ull;
-    hi = 0;
     for (uint64_t k = 0; k < n; ++k) {
         const uint32_t l = local_row(e, nodes[k]);
         if (l == ~0u || l >= e->n_own) return e->fail(GG_EINVAL, "node not owned by this engine");
         rows[k] = l;
-        lo = std::min<uint64_t>(lo, l);
-        hi = std::max<uint64_t>(hi, (uint64_t)l + 1);
     }
-    if (!n) lo = hi = 0;
+    return GG_OK;
+}
+
+// Gather rows[0..n) on the device, kChunk rows per pass: sets (base | F of the
+// last round where LAG) or delivery rounds; the rows may be anywhere in the
+// local order (degree-ordered or sharded engines).
+template <class T, class Launch>
+static int gather_chunks(gg_engine* e, const std::vector<uint32_t>& rows, uint64_t per_row, std::vector<T>& h,
+                         Launch&& launch) {
+    constexpr uint64_t kChunk = 1 << 20;
+    const uint64_t n = rows.size();
+    h.resize(n * per_row);
+    if (!n) return GG_OK;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    uint32_t* d_rows = nullptr;
+    T* d_out = nullptr;
+    const uint64_t c = std::min(n, kChunk);
+    hipError_t err = hipMalloc(&d_rows, c * 4);
+    if (err == hipSuccess) err = hipMalloc(&d_out, c * per_row * sizeof(T));
+    for (uint64_t k0 = 0; k0 < n && err == hipSuccess; k0 += kChunk) {
+        const uint64_t m = std::min(kChunk, n - k0);
+        err = hipMemcpyAsync(d_rows, rows.data() + k0, m * 4, hipMemcpyHostToDevice, e->stream);
+        if (err == hipSuccess) {
+            launch(d_rows, m, d_out);
+            err = hipGetLastError();
+        }
+        if (err == hipSuccess)
+            err = hipMemcpyAsync(h.data() + k0 * per_row, d_out, m * per_row * sizeof(T), hipMemcpyDeviceToHost,
+                                 e->stream);
+        if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+    }
+    if (d_rows) (void)hipFree(d_rows);
+    if (d_out) (void)hipFree(d_out);
+    HIPCHK(err);
     return GG_OK;
 }
 
 static int read_bits_rows(gg_engine* e, const uint32_t* nodes, uint64_t n, uint64_t* out) {
     std::vector<uint32_t> rows;
-    uint64_t lo, hi;
-    int rc = rows_of(e, nodes, n, rows, lo, hi);
+    int rc = rows_of(e, nodes, n, rows);
     if (rc) return rc;
     HIPCHK(hipSetDevice(e->device));
     std::vector<uint64_t> h;
-    if ((rc = copy_rows(e, lo, hi, h))) return rc;
+    const int last = (int)((e->round - 1) & 1);
+    const uint64_t* F = e->round ? e->d_F[last] : nullptr;
+    const uint8_t* fl = e->round ? e->d_flg[last] : nullptr;
+    rc = gather_chunks(e, rows, e->nwp, h, [&](const uint32_t* d_rows, uint64_t m, uint64_t* d_out) {
+        const uint64_t t = m * e->nwp;
+        hipLaunchKernelGGL(gg::gather_sets, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, e->stream, d_rows, m,
+                           e->d_base, F, fl, (uint32_t)e->nwp, d_out);
+    });
+    if (rc) return rc;
     // whole-job words per node; a lane-group engine fills only its own words
     for (uint64_t k = 0; k < n; ++k) {
         if (e->L > 1) std::memset(out + k * e->nw_g, 0, e->nw_g * 8);
-        std::memcpy(out + k * e->nw_g + e->w0, h.data() + (rows[k] - lo) * e->nwp, e->nw * 8);
+        std::memcpy(out + k * e->nw_g + e->w0, h.data() + k * e->nwp, e->nw * 8);
     }
     return GG_OK;
 }
@@ -2008,20 +2092,25 @@ static int read_bits_rows(gg_engine* e, const uint32_t* nodes, uint64_t n, uint6
 static int delivery_rows(gg_engine* e, const uint32_t* nodes, uint64_t n, int32_t* out) {
     if (!e->d_dr) return e->fail(GG_EINVAL, "GG_TRACK_DELIVERY not enabled");
     std::vector<uint32_t> rows;
-    uint64_t lo, hi;
-    int rc = rows_of(e, nodes, n, rows, lo, hi);
+    int rc = rows_of(e, nodes, n, rows);
     if (rc) return rc;
     HIPCHK(hipSetDevice(e->device));
-    HIPCHK(hipStreamSynchronize(e->stream));
     const uint64_t W = e->cfg.n_lanes, Wl = e->nw * 64;  // whole-job lanes, this engine's lanes
-    std::vector<int32_t> h((hi - lo) * Wl);
-    if (!h.empty()) HIPCHK(hipMemcpy(h.data(), e->d_dr + lo * Wl, h.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<int32_t> h;
+    rc = gather_chunks(e, rows, Wl, h, [&](const uint32_t* d_rows, uint64_t m, int32_t* d_out) {
+        const uint64_t t = m * Wl;
+        hipLaunchKernelGGL(gg::gather_rounds, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, e->stream, d_rows, m,
+                           e->d_dr, (uint32_t)Wl, d_out);
+    });
+    if (rc) return rc;
     for (uint64_t k = 0; k < n; ++k) {
         if (e->L > 1) std::fill(out + k * W, out + (k + 1) * W, -1);
-        std::memcpy(out + k * W + 64 * e->w0, h.data() + (rows[k] - lo) * Wl, Wl * 4);
+        std::memcpy(out + k * W + 64 * e->w0, h.data() + k * Wl, Wl * 4);
     }
     return GG_OK;
 }
+
+extern "C" {
 
 static std::vector<uint32_t> node_range(uint32_t a, uint32_t b) {
     std::vector<uint32_t> v;

@@ -2029,6 +2029,24 @@ __global__ __launch_bounds__(kBlock) void hub_mark(RoundArgs a) {
     if (threadIdx.x == 0) stamp(a, K_PREP, t_start);
 }
 
+// Host reads (gg_read_bits, gg_delivery_rounds): rows gathered by local row;
+// a set is base | F of the last round where that round's flag says LAG.
+__global__ void gather_sets(const uint32_t* rows, uint64_t n, const uint64_t* base, const uint64_t* F_last,
+                            const uint8_t* flg_last, uint32_t nwp, uint64_t* out) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * nwp) return;
+    const uint64_t k = t / nwp, j = t % nwp, r = rows[k];
+    uint64_t w = base[r * nwp + j];
+    if (flg_last && (flg_last[r] & FL_LAG)) w |= F_last[r * nwp + j];
+    out[t] = w;
+}
+
+__global__ void gather_rounds(const uint32_t* rows, uint64_t n, const int32_t* dr, uint32_t W, int32_t* out) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * W) return;
+    out[t] = dr[(uint64_t)rows[t / W] * W + t % W];
+}
+
 // First-seen round of every new bit (GG_TRACK_DELIVERY only; observation).
 __global__ void track_delivery(const uint64_t* F_cur, const uint8_t* flg_cur, int32_t* dr, uint64_t n_own,
                                uint64_t own0, uint32_t nwp, uint32_t nw, uint32_t W, int32_t round) {

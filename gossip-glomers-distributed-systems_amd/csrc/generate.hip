@@ -442,6 +442,110 @@ int build_csr(const gg_gen_spec& s, hipStream_t st, uint32_t col_or, Csr* out, s
     return 0;
 }
 
+namespace {
+
+__global__ void deg_keys(const int64_t* rp, uint64_t V, uint64_t* keys) {
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V; v += (uint64_t)gridDim.x * blockDim.x)
+        keys[v] = ((uint64_t)(0xffffffffu - (uint32_t)(rp[v + 1] - rp[v])) << 32) | v;  // descending degree, then id
+}
+
+__global__ void order_from_keys(const uint64_t* keys, const int64_t* rp, uint64_t V, uint64_t rows, uint32_t* gid,
+                                uint32_t* loc, int64_t* ndeg) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (i >= V) {
+            gid[i] = ~0u;  // padding rows
+            continue;
+        }
+        const uint32_t v = (uint32_t)(keys[i] & 0xffffffffu);
+        gid[i] = v;
+        loc[v] = (uint32_t)i;
+        ndeg[i] = rp[v + 1] - rp[v];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) ndeg[V] = 0;
+}
+
+// Column j of the reordered CSR: its row i (binary search in nrp), that row's
+// node v = gid[i], entry j - nrp[i] of v's old list, mapped to its local row.
+// Edge-parallel, so a 10^6-entry hub row costs no more than its share.
+__global__ void copy_reordered(const int64_t* rp, const uint32_t* col, const int64_t* nrp, const uint32_t* gid,
+                               const uint32_t* loc, uint64_t V, uint64_t nnz, uint32_t col_or, uint32_t* ncol) {
+    const uint32_t cmask = 0x7fffffffu;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nnz; j += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t lo = 0, hi = V - 1;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi + 1) >> 1;
+            if ((uint64_t)nrp[mid] <= j) lo = mid;
+            else hi = mid - 1;
+        }
+        const uint32_t v = gid[lo];
+        ncol[j] = loc[col[rp[v] + (int64_t)(j - (uint64_t)nrp[lo])] & cmask] | col_or;
+    }
+}
+
+}  // namespace
+
+int degree_reorder(Csr* g, uint64_t rows, hipStream_t st, uint32_t col_or, uint32_t** gid_out,
+                   std::vector<uint32_t>* gid_host, std::vector<uint32_t>* loc_host, std::string* err) {
+    const uint64_t V = g->V;
+    Scoped mem;
+    uint64_t* keys = nullptr;
+    uint64_t* alt = nullptr;
+    uint32_t* gid = nullptr;
+    uint32_t* loc = nullptr;
+    int64_t* ndeg = nullptr;
+    int64_t* nrp = nullptr;
+    uint32_t* ncol = nullptr;
+    GCHK(mem.alloc(&keys, V * 8));
+    GCHK(mem.alloc(&alt, V * 8));
+    hipLaunchKernelGGL(deg_keys, dim3(grid_of(V)), dim3(kBlk), 0, st, g->row_ptr, V, keys);
+    GCHK(hipGetLastError());
+    size_t tmp_bytes = 0;
+    void* tmp = nullptr;
+    {
+        rocprim::double_buffer<uint64_t> db(keys, alt);
+        GCHK(rocprim::radix_sort_keys(nullptr, tmp_bytes, db, (size_t)V, 0, 64, st));
+        GCHK(mem.alloc(&tmp, tmp_bytes));
+        GCHK(rocprim::radix_sort_keys(tmp, tmp_bytes, db, (size_t)V, 0, 64, st));
+        if (db.current() != keys) std::swap(keys, alt);
+    }
+    mem.release(tmp);
+    GCHK(mem.alloc(&gid, rows * 4));
+    GCHK(mem.alloc(&loc, V * 4));
+    GCHK(mem.alloc(&ndeg, (V + 1) * 8));
+    hipLaunchKernelGGL(order_from_keys, dim3(grid_of(rows)), dim3(kBlk), 0, st, keys, g->row_ptr, V, rows, gid, loc,
+                       ndeg);
+    GCHK(hipGetLastError());
+    mem.release(keys);
+    mem.release(alt);
+    GCHK(mem.alloc(&nrp, (V + 1) * 8));
+    tmp_bytes = 0;
+    GCHK(rocprim::exclusive_scan(nullptr, tmp_bytes, ndeg, nrp, (int64_t)0, V + 1, rocprim::plus<int64_t>(), st));
+    GCHK(mem.alloc(&tmp, tmp_bytes));
+    GCHK(rocprim::exclusive_scan(tmp, tmp_bytes, ndeg, nrp, (int64_t)0, V + 1, rocprim::plus<int64_t>(), st));
+    mem.release(tmp);
+    mem.release(ndeg);
+    GCHK(mem.alloc(&ncol, g->nnz * 4));
+    if (g->nnz) {
+        hipLaunchKernelGGL(copy_reordered, dim3(grid_of(g->nnz)), dim3(kBlk), 0, st, g->row_ptr, g->col, nrp, gid,
+                           loc, V, g->nnz, col_or, ncol);
+        GCHK(hipGetLastError());
+    }
+    gid_host->resize(rows);
+    loc_host->resize(V);
+    GCHK(hipMemcpyAsync(gid_host->data(), gid, rows * 4, hipMemcpyDeviceToHost, st));
+    GCHK(hipMemcpyAsync(loc_host->data(), loc, V * 4, hipMemcpyDeviceToHost, st));
+    GCHK(hipStreamSynchronize(st));
+    (void)hipFree(g->row_ptr);
+    (void)hipFree(g->col);
+    g->row_ptr = nrp;
+    g->col = ncol;
+    mem.keep(nrp);
+    mem.keep(ncol);
+    mem.keep(gid);
+    *gid_out = gid;
+    return 0;
+}
+
 int max_degree(const int64_t* d_rp, uint64_t V, hipStream_t st, uint64_t* out, std::string* err) {
     unsigned long long* d = nullptr;
     GCHK(hipMalloc(&d, 8));

@@ -198,3 +198,44 @@ def test_reset_after_quiet_rounds(hip_lib, cpu_lib, shift, extra_quiet):
     d = diff_stats(c.step(30), g.step(30))
     assert not d, d[:5]
     assert np.array_equal(c.read_bits(), g.read_bits())
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_degree_order_vs_o2(hip_lib, cpu_lib, monkeypatch, seed):
+    """GG_ORDER=degree: local rows by descending in-degree (the default on
+    power-law graphs). Results must not depend on the row order: random
+    directed/symmetric graphs with partitions and sync, and an R-MAT with hubs
+    through the device generator (gg_topology_generate's reorder), equal O2."""
+    monkeypatch.setenv("GG_ORDER", "degree")
+    rnd = random.Random(8100 + seed)
+    for _ in range(6):
+        _compare(random_scenario(rnd, max_v=200, W=128), hip_lib, cpu_lib)
+    monkeypatch.setenv("GG_HUB_DEG", "32")
+    topo = T.rmat(3000, 16, seed=seed + 5)
+    _compare(Scenario(topo, 256, 30, uniform_injections(3000, 256, seed), seed=seed, sync_base=12,
+                      sync_jitter=3, windows=[("seeded", 14, 18, 3)]), hip_lib, cpu_lib)
+
+
+def test_degree_order_device_generated(hip_lib, cpu_lib, monkeypatch):
+    """The device reorder of a generated R-MAT equals the host path (and O2),
+    and gg_topology_export maps the rows back to the generator's CSR."""
+    from ggamd.engine import Engine
+    monkeypatch.setenv("GG_HUB_DEG", "48")
+    monkeypatch.setenv("GG_ORDER", "degree")
+    V, W = 5000, 256
+    topo = T.rmat(V, 16, seed=33)
+    inj = uniform_injections(V, 200, 4)
+    out = []
+    for lib, gen in ((hip_lib, True), (cpu_lib, False)):
+        e = Engine(V, W, seed=2, sync_base=10, sync_jitter=4, library=lib, track_delivery=True)
+        if gen:
+            e.generate("rmat", V, k=16, seed=33, a=0.57, b=0.19, c=0.19)
+            ex = e.export_topology()
+            assert np.array_equal(ex.row_ptr, topo.row_ptr) and np.array_equal(ex.col, topo.col)
+        else:
+            e.topology(topo)
+        for n, v, r in inj:
+            e.broadcast(n, v, r)
+        out.append((e.step(25), e.read_bits(), e.delivery_rounds()))
+    assert not diff_stats(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][2], out[1][2])

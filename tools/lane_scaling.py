@@ -61,6 +61,7 @@ def main():
     ap.add_argument("--lanes", type=int, default=4096)
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--only-rank", type=int, help="time just this rank of each N (profiling)")
     ap.add_argument("--json")
     args = ap.parse_args()
     V, K = args.nodes, args.lanes
@@ -71,7 +72,7 @@ def main():
     R = None
     for N in [int(x) for x in args.ranks.split(",")]:
         tot, per = None, []
-        for r in range(N):
+        for r in ([args.only_rank] if args.only_rank is not None else range(N)):
             R, st, best, mean, gen_s, gbps = run_rank(V, K, r, N, args.steps, gen, inj, R)
             per.append({"rank": r, "episode_s": mean, "best_s": best, "gen_s": gen_s, "stream_GBps": gbps})
             print(f"N={N} rank {r}: episode {mean * 1e3:.1f} ms (best {best * 1e3:.1f}), stream {gbps:.0f} GB/s, "
@@ -83,6 +84,8 @@ def main():
                     for f in COUNT_FIELDS:
                         if f != "round":
                             a[f] = (a[f] + b[f]) & ((1 << 64) - 1)
+        if args.only_rank is not None:
+            continue
         if base is None:
             base = (tot, max(p["episode_s"] for p in per))
         diffs = [f"round {a['round']} {f}" for a, b in zip(tot, base[0]) for f in COUNT_FIELDS if a[f] != b[f]]
