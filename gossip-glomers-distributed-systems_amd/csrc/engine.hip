@@ -203,6 +203,9 @@ struct gg_engine {
     uint32_t* d_n_work = nullptr;    // [2] live tiles, candidate nodes
     uint32_t* d_nodes = nullptr;     // [n_own] candidate-node list (sparse lean rounds)
     uint32_t* d_act = nullptr;       // [4] ring: nodes that became active per round
+    unsigned long long* d_act_deg = nullptr;  // [4] ring: their out-degree sums
+    uint64_t* d_abits = nullptr;     // [rows/64] ACT bits of the previous round (flags-first rounds)
+    bool ff_ok = false;              // flags-first gathers allowed
     // hubs (see expand_kernels.hpp): in-edge chunks of high in-degree nodes,
     // out-edge chunks of high out-degree senders, per-chunk partial rows
     uint32_t hub_deg = 0;
@@ -295,6 +298,8 @@ void gg_engine::free_topology() {
     dfree(d_n_work);
     dfree(d_nodes);
     dfree(d_act);
+    dfree(d_act_deg);
+    dfree(d_abits);
     for (auto& p : d_fired) dfree(p);
     dfree(d_sync_next);
     dfree(d_sync_k);
@@ -374,6 +379,7 @@ int reset_device_state(gg_engine* e) {
     seg(e->d_zmark, e->rows, 0);
     seg(e->d_tile_cand, e->tile_bytes, 0);
     seg(e->d_act, 16, 0);
+    seg(e->d_act_deg, 32, 0);
     const uint64_t n_own = e->n_own;
     if (e->d_dr) seg(e->d_dr, n_own * e->nw * 64 * 4, ~0ull);
     if (e->d_stamp) seg(e->d_stamp, (e->n_ghost + 1) / 2 * 8, ~0ull);
@@ -589,6 +595,9 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.n_work = e->d_n_work;
     a.nodes = e->d_nodes;
     a.act = e->d_act;
+    a.act_deg = e->d_act_deg;
+    a.abits = e->d_abits;
+    a.ff_ok = e->ff_ok ? 1 : 0;
     a.tile_nodes = (uint32_t)e->tile_nodes;
     a.symmetric = e->symmetric ? 1 : 0;
     a.n_edges = e->n_in_edges;
@@ -685,6 +694,11 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         if (sync_stream) {
             launch_stream_sync(a, e->stream);
         } else if (a.stream_ok) {  // lean rounds: all nodes (dense) or the candidate list (sparse)
+            if (e->ff_ok && !maskw) {  // the sender bitmap of a flags-first round (the kernel decides)
+                const uint64_t blocks = std::min<uint64_t>((e->rows + gg::kBlock - 1) / gg::kBlock, 4096);
+                hipLaunchKernelGGL(gg::pack_act_bits, dim3((unsigned)blocks), dim3(gg::kBlock), 0, e->stream, a);
+                HIPCHK(hipGetLastError());
+            }
             launch_stream(a, maskw, e->stream);
             if (e->n_hubs) {
                 HIPCHK(hipGetLastError());
@@ -1109,6 +1123,14 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     HIPCHK(hipMalloc(&e->d_n_work, 2 * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->d_nodes, std::max<uint64_t>(1, n_own) * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->d_act, 4 * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&e->d_act_deg, 4 * 8));
+    // flags-first gathers (ff_round): rows of >= 64 B (the request-rate-bound
+    // regime) and a mean in-degree >= 4; GG_FLAGS_FIRST=0/1 overrides
+    {
+        const char* f = getenv("GG_FLAGS_FIRST");
+        e->ff_ok = f ? atoi(f) != 0 : (e->nwp >= 8 && e->n_in_edges >= 4 * std::max<uint64_t>(1, n_own));
+        if (e->ff_ok) HIPCHK(hipMalloc(&e->d_abits, e->rows / 8));
+    }
     HIPCHK(hipMalloc(&e->d_base, rowbytes));
     for (int b = 0; b < 2; ++b) {
         HIPCHK(hipMalloc(&e->d_F[b], rowbytes));

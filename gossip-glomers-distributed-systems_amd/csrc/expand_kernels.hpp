@@ -61,7 +61,7 @@ namespace gg {
 #define GG_STREAM_ROWS 6
 #endif
 #ifndef GG_STREAM_WAVES_PER_EU
-#define GG_STREAM_WAVES_PER_EU 5
+#define GG_STREAM_WAVES_PER_EU 4
 #endif
 constexpr int kStreamRows = GG_STREAM_ROWS;
 
@@ -90,6 +90,7 @@ enum Counter : int {
     C_DROPPED, C_FIRED, C_HASH, C_NEXT_ACKS, C_NEXT_ACKDROP, C_ACTIVE, C_GATHERS,
     C_NACT,   // nodes that became active (ACT) this round: next round's dense/sparse choice
     C_BYTES,  // algorithmic bytes the launch had to move, per kernel kind
+    C_NACTDEG,  // out-degree sum of those nodes: next round's flags-first choice
     C_NUM
 };
 // Kernel kinds with their own device clock stamps (s_memrealtime, 100 MHz) per
@@ -135,6 +136,9 @@ struct RoundArgs {
     uint32_t* n_work;           // [2]: live tiles, candidate nodes
     uint32_t* nodes;            // candidate nodes of a sparse lean round (compact_round; expand_stream)
     uint32_t* act;              // [4] ring: nodes that became active in round r (slot r&3)
+    unsigned long long* act_deg;  // [4] ring: their out-degree sum (edges carrying F rows next round)
+    uint64_t* abits;            // [rows/64] bit u: sender u is ACT in round r-1 (pack_act_bits; flags-first)
+    int32_t ff_ok;              // flags-first gathers allowed (engine choice: W/64 >= 8, mean degree >= 4)
     // hubs (lean rounds): owned nodes with in-degree > hub_deg skip expand_stream
     // and take hub_chunks + hub_finish; senders with out-degree > hub_deg are
     // marked by hub_mark instead of round_prep (0: no hubs)
@@ -240,6 +244,18 @@ __device__ __forceinline__ bool busy_round(const RoundArgs& a) {
 // and expand_round exits.
 __device__ __forceinline__ bool dense_round(const RoundArgs& a) { return a.stream_ok && busy_round(a); }
 
+// Flags-first streaming round: fewer than half of the in-edges name a sender
+// that was ACT last round (an F row that is not zero), so expand_stream looks
+// each sender up in the abits bitmap first and gathers only the rows of active
+// senders. Random row gathers of <= 128 B are capped by the memory system's
+// request rate (~50 G rows/s, tools/gather_bench.hip), and the bitmap (one bit
+// a node; in degree order its hub part stays in L2) replaces most of them: in
+// C4's round 2 about 6% of the candidates' in-edges carry data.
+__device__ __forceinline__ bool ff_round(const RoundArgs& a) {
+    return a.ff_ok && a.stream_ok && a.act_deg &&
+           2.0 * (double)a.act_deg[(a.round - 1) & 3] < (double)a.n_edges;
+}
+
 // Original node id of local row i (hashes, sync timers, partition groups).
 __device__ __forceinline__ uint64_t gid_of(const RoundArgs& a, uint64_t i) {
     return a.gid ? (uint64_t)a.gid[i] : a.lo + i;
@@ -344,6 +360,7 @@ __device__ __forceinline__ void flush_counters(const RoundArgs& a, unsigned long
         const int idx = threadIdx.x == C_BYTES ? kBytes0 + kind : (int)threadIdx.x;
         if (s) atomicAdd(&a.counters[(blockIdx.x % kSlots) * kCounters + idx], s);
         if (threadIdx.x == C_NACT && s) atomicAdd(&a.act[a.round & 3], (uint32_t)s);
+        if (threadIdx.x == C_NACTDEG && s && a.act_deg) atomicAdd(&a.act_deg[a.round & 3], s);
     }
     if (threadIdx.x == 0) stamp(a, kind, t_start);
 }
@@ -360,6 +377,7 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
     const bool dense = dense_round(a);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.act[(a.round + 1) & 3] = 0;  // next round's act slot
+        if (a.act_deg) a.act_deg[(a.round + 1) & 3] = 0;
         a.n_work[0] = a.n_work[1] = 0;  // compact_round runs after this kernel
     }
     if (!SYNCW && dense) {
@@ -630,6 +648,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
     const unsigned long long t_start = clock100();
     // always-live counters
     unsigned long long c_new = 0, c_fwd = 0, c_hash = 0, c_active = 0, c_gathers = 0, c_nact = 0, c_bytes = 0;
+    unsigned long long c_nactdeg = 0;
     // MASKW-only
     unsigned long long c_fwd_deliv = 0, c_push_deliv = 0, c_dropped = 0, c_next_ackdrop = 0;
     // SYNCW-only
@@ -921,6 +940,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                     }
                     if (lg == 0 && any) a.flg_cur[rep] = (uint8_t)(FL_ACT | (keep ? FL_LAG : 0));
                     c_nact += (lg == 0 && any) ? 1ull : 0ull;
+                    c_nactdeg += (lg == 0 && any) ? deg : 0ull;
 
                     // messages v sends in round r (rebroadcastAllExcept :50-57, pushes :106)
                     const unsigned long long fs = deg * T - cl_recip - cb_new;
@@ -982,6 +1002,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
     acc[C_ACTIVE] = c_active;
     acc[C_GATHERS] = c_gathers;
     acc[C_NACT] = c_nact;
+    acc[C_NACTDEG] = c_nactdeg;
     acc[C_BYTES] = c_bytes;
     flush_counters(a, acc, s_red, t_start, K_EXPAND);
 }
@@ -1010,6 +1031,28 @@ void expand_round_lean(RoundArgs a) {
 // without looking at sender flags, and a node nobody reached finds no new
 // bits. The node-local part of round_prep (stale F row of round r-2, flag
 // reset) is done here from the node's old flag byte.
+// Which of a batch's D senders (columns c, the first n valid) were ACT last
+// round (flags-first rounds): lane lg of the node group looks up senders lg,
+// lg + G, ... in the abits bitmap and a ballot assembles the group's D-bit
+// mask, which every lane of the group gets. All lanes of a group call it.
+template <int G, int D>
+__device__ __forceinline__ uint32_t active_senders(const uint64_t* abits, const uint32_t (&c)[D], uint32_t n, int lg,
+                                                   int gbase) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < (D + G - 1) / G; ++q) {
+        const int b = lg + q * G;
+        uint32_t col = 0;
+#pragma unroll
+        for (int bb = 0; bb < D; ++bb) col = (bb == b) ? c[bb] : col;
+        const bool act = b < D && (uint32_t)b < n && bit_at(abits, col & kColMask);
+        const unsigned long long w = __ballot(act);
+        const unsigned long long gm = (G >= 64) ? ~0ull : ((1ull << G) - 1ull);
+        m |= (uint32_t)((w >> gbase) & gm) << (q * G);
+    }
+    return m & ((1u << D) - 1u);
+}
+
 template <int G, int WPL, bool MASKW>
 __device__ __forceinline__ void stream_body(RoundArgs a) {
     static_assert(WPL == 2, "DMA slots hold 16 bytes per lane");
@@ -1028,13 +1071,16 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         noop_exit(a, K_STREAM, t_start);
         return;
     }
+    const bool ff = !MASKW && ff_round(a);  // flags-first gathers (block-uniform)
+    constexpr uint32_t kAllD = (1u << D) - 1u;
     // per-lane counts that fit 32 bits stay 32-bit (register budget)
-    uint32_t c_new = 0, c_active = 0, c_gathers = 0, c_nact = 0;
+    uint32_t c_new = 0, c_active = 0, c_gathers = 0, c_nact = 0, c_nactdeg = 0;
     unsigned long long c_fwd = 0, c_hash = 0, c_bytes = 0;
     unsigned long long c_fwd_deliv = 0, c_dropped = 0, c_next_ackdrop = 0;  // MASKW
     const int lg = threadIdx.x % G;
     const uint32_t off = (uint32_t)lg * WPL;
     const int gshift = (threadIdx.x & 63) / G * G;
+    const int gbase = (int)(threadIdx.x & 63) - lg;  // the node group's first lane in the wave
     const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
     uint8_t* const my = &s_slots[(threadIdx.x >> 6) * (D + 1) * 1024];
     const uint32_t lane16 = (threadIdx.x & 63) * 16;
@@ -1103,9 +1149,10 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
                 mw[q][1] = (eb && m0.deg) ? eb[(m0.p0 + D - 1) >> 6] : 0ull;
             }
         }
+        const uint32_t am0 = ff ? active_senders<G, D>(a.abits, c0, m0.deg, lg, gbase) : kAllD;
 #pragma unroll
         for (int b = 0; b < D; ++b) {
-            if ((uint32_t)b < m0.deg)
+            if ((uint32_t)b < m0.deg && ((am0 >> b) & 1u))
                 dma16((const void*)(a.F_prev + (uint64_t)(c0[b] & kColMask) * a.nwp + off), my + b * 1024);
         }
         // (b) prefetch: columns of item k+stride, row pointers of item k+2*stride,
@@ -1177,7 +1224,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         };
 #pragma unroll
         for (int b = 0; b < D; ++b) {
-            if ((uint32_t)b < m0.deg) {
+            if ((uint32_t)b < m0.deg && ((am0 >> b) & 1u)) {
                 const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(my + b * 1024 + lane16);
                 uint32_t mb = 0;
                 if constexpr (MASKW) {
@@ -1189,12 +1236,20 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             }
         }
         const int64_t p1 = m0.p0 + m0.deg;
+        if (MASKW) {
+            if (lg == 0) c_gathers += m0.deg;  // every sender row
+        } else if (lg == 0) {
+            c_gathers += __popc(am0 & (m0.deg >= (uint32_t)D ? kAllD : ((1u << m0.deg) - 1u)));
+        }
         for (int64_t e = m0.p0 + D; e < p1; e += D) {  // more than D senders
             uint32_t cb[D];
 #pragma unroll
+            for (int b = 0; b < D; ++b) cb[b] = e + b < p1 ? a.in_col[e + b] : 0u;
+            // flags-first: only the active senders' rows (bits looked up first)
+            const uint32_t am = ff ? active_senders<G, D>(a.abits, cb, (uint32_t)(p1 - e), lg, gbase) : kAllD;
+#pragma unroll
             for (int b = 0; b < D; ++b) {
-                cb[b] = e + b < p1 ? a.in_col[e + b] : 0u;
-                if (e + b < p1)
+                if (e + b < p1 && ((am >> b) & 1u))
                     dma16((const void*)(a.F_prev + (uint64_t)(cb[b] & kColMask) * a.nwp + off), my + b * 1024);
             }
             uint64_t ew[3][2];
@@ -1209,7 +1264,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             vm_drain();
 #pragma unroll
             for (int b = 0; b < D; ++b) {
-                if (e + b < p1) {
+                if (e + b < p1 && ((am >> b) & 1u)) {
                     const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(my + b * 1024 + lane16);
                     uint32_t mb = 0;
                     if constexpr (MASKW) {
@@ -1220,9 +1275,9 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
                     claim(x.x, x.y, cb[b], mb);
                 }
             }
+            if (!MASKW && lg == 0) c_gathers += __popc(am & ((p1 - e >= D) ? kAllD : ((1u << (uint32_t)(p1 - e)) - 1u)));
         }
         const unsigned long long nin = m0.deg;
-        c_gathers += (lg == 0) ? m0.deg : 0u;
         // new state
         Row<WPL> F;
         uint32_t T = 0;
@@ -1257,9 +1312,11 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         if (lg == 0) {
             c_active += 1;
             c_nact += any ? 1 : 0;
-            // row_ptr + cand + flag bytes + col, own row + sender rows, F / base / flag writes
-            c_bytes += (dense ? 0 : 4) + 8 + 2 + 4 * nin + (1 + nin) * rowb + ((any || zm) ? rowb : 0) +
-                       (any ? rowb + 1 : 0);
+            if constexpr (!MASKW) c_nactdeg += any ? (uint32_t)deg : 0u;  // masked rounds: no flags-first next
+            // row_ptr + cand + flag bytes + col (+ a sender bit, flags-first), own row + gathered
+            // sender rows, F / base / flag writes
+            c_bytes += (dense ? 0 : 4) + 8 + 2 + 4 * nin + (ff ? (nin + 7) / 8 : 0) + rowb +
+                       ((any || zm) ? rowb : 0) + (any ? rowb + 1 : 0);
         }
         }  // !hub
         m0 = m1;
@@ -1272,6 +1329,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
 #pragma unroll
     for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
     if constexpr (!MASKW) c_fwd_deliv = c_fwd;
+    c_bytes += (unsigned long long)c_gathers * rowb;  // the gathered sender rows
     acc[C_NEW] = c_new;
     acc[C_FWD_SENT] = c_fwd;
     acc[C_FWD_DELIV] = c_fwd_deliv;
@@ -1282,6 +1340,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
     acc[C_ACTIVE] = c_active;
     acc[C_GATHERS] = c_gathers;
     acc[C_NACT] = c_nact;
+    acc[C_NACTDEG] = c_nactdeg;
     acc[C_BYTES] = c_bytes;
     flush_counters(a, acc, s_red, t_start, K_STREAM);
 }
@@ -1321,7 +1380,7 @@ void expand_stream1(RoundArgs a) {
         return;
     }
     uint32_t c_new = 0, c_active = 0, c_gathers = 0, c_nact = 0;
-    unsigned long long c_fwd = 0, c_hash = 0, c_bytes = 0;
+    unsigned long long c_fwd = 0, c_hash = 0, c_bytes = 0, c_nactdeg = 0;
     const uint32_t stride = gridDim.x * kBlock;
 
     struct Meta {
@@ -1432,6 +1491,7 @@ void expand_stream1(RoundArgs a) {
             c_fwd += deg * (unsigned long long)T - cl_recip;
             c_active += 1;
             c_nact += any ? 1 : 0;
+            c_nactdeg += any ? deg : 0;
             c_bytes += (dense ? 0 : 4) + 8 + 2 + 4ull * nin + 8ull * (1 + nin) + ((any || zm) ? 8 : 0) + (any ? 9 : 0);
         }
         m0 = m1;
@@ -1451,6 +1511,7 @@ void expand_stream1(RoundArgs a) {
     acc[C_ACTIVE] = c_active;
     acc[C_GATHERS] = c_gathers;
     acc[C_NACT] = c_nact;
+    acc[C_NACTDEG] = c_nactdeg;
     acc[C_BYTES] = c_bytes;
     flush_counters(a, acc, s_red, t_start, K_STREAM);
 }
@@ -1574,7 +1635,7 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
     const bool dense = dense_round(a);
     const uint32_t n_items = dense ? (uint32_t)a.n_own : a.n_work[1];
     uint32_t c_new = 0, c_active = 0, c_gathers = 0, c_nact = 0;
-    unsigned long long c_fwd = 0, c_push = 0, c_hash = 0, c_bytes = 0;
+    unsigned long long c_fwd = 0, c_push = 0, c_hash = 0, c_bytes = 0, c_nactdeg = 0;
     const int lg = threadIdx.x % G;
     const uint32_t off = (uint32_t)lg * WPL;
     const int gshift = (threadIdx.x & 63) / G * G;
@@ -1768,6 +1829,7 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
             c_active += 1;
             c_gathers += nc;
             c_nact += any ? 1u : 0u;
+            c_nactdeg += any ? dout : 0ull;
             c_bytes += nrows * rowb + nextra + ((any || zm) ? 1 : 0);
         }
         n0 = n1;
@@ -1788,8 +1850,24 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
     acc[C_ACTIVE] = c_active;
     acc[C_GATHERS] = c_gathers;
     acc[C_NACT] = c_nact;
+    acc[C_NACTDEG] = c_nactdeg;
     acc[C_BYTES] = c_bytes;
     flush_counters(a, acc, s_red, t_start, K_STREAM);
+}
+
+// Flags-first rounds: the ACT bits of round r-1 (every local row: owned nodes
+// and ghosts) packed into abits, one word per wave (rows is a multiple of 64).
+__global__ __launch_bounds__(kBlock) void pack_act_bits(RoundArgs a) {
+    const unsigned long long t_start = clock100();
+    if (!ff_round(a)) {
+        noop_exit(a, K_PREP, t_start);
+        return;
+    }
+    for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < a.rows; t += (uint64_t)gridDim.x * kBlock) {
+        const unsigned long long w = __ballot((a.flg_prev[t] & FL_ACT) != 0);
+        if ((threadIdx.x & 63) == 0) a.abits[t >> 6] = w;
+    }
+    if (threadIdx.x == 0) stamp(a, K_PREP, t_start);
 }
 
 // ---------------------------------------------------------------------------
@@ -1855,6 +1933,7 @@ __global__ __launch_bounds__(kBlock) void hub_chunks(RoundArgs a) {
         return;
     }
     const bool dense = dense_round(a);
+    const bool ff = ff_round(a);  // flags-first: only active senders' rows
     const int j = threadIdx.x / G, lg = threadIdx.x % G;
     const uint64_t off = (uint64_t)lg * WPL;
     unsigned long long c_bytes = 0;
@@ -1871,10 +1950,15 @@ __global__ __launch_bounds__(kBlock) void hub_chunks(RoundArgs a) {
             uint32_t cb[D];
             Row<WPL> src[D];
 #pragma unroll
+            for (int b = 0; b < D; ++b) cb[b] = e + b < e1 ? a.in_col[e + b] : 0u;
+            bool act[D];
+#pragma unroll
+            for (int b = 0; b < D; ++b) act[b] = e + b < e1 && (!ff || bit_at(a.abits, cb[b] & kColMask));
+#pragma unroll
             for (int b = 0; b < D; ++b) {
-                cb[b] = e + b < e1 ? a.in_col[e + b] : 0u;
-                if (e + b < e1) {
+                if (act[b]) {
                     src[b] = load_row<WPL>(a.F_prev + (uint64_t)(cb[b] & kColMask) * a.nwp + off);
+                    if (lg == 0) c_bytes += 8ull * a.nwp;
                 } else {
 #pragma unroll
                     for (int w = 0; w < WPL; ++w) src[b].w[w] = 0;
@@ -1890,7 +1974,7 @@ __global__ __launch_bounds__(kBlock) void hub_chunks(RoundArgs a) {
                 }
             }
         }
-        if (lg == 0 && e1 > e0) c_bytes += (unsigned long long)(e1 - e0) * (4 + 8ull * a.nwp);
+        if (lg == 0 && e1 > e0) c_bytes += (unsigned long long)(e1 - e0) * 4 + (ff ? (e1 - e0 + 7) / 8 : 0);
         hub_block_reduce<G, WPL>(O, R, s_or, s_rc);
         if (j == 0) {
             uint64_t* dst = a.hscratch + c * 2 * a.nwp;
@@ -1923,6 +2007,7 @@ __global__ __launch_bounds__(kBlock) void hub_finish(RoundArgs a) {
     const int gshift = (threadIdx.x & 63) / G * G;
     const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
     unsigned long long c_new = 0, c_fwd = 0, c_hash = 0, c_active = 0, c_gathers = 0, c_nact = 0, c_bytes = 0;
+    unsigned long long c_nactdeg = 0;
     for (uint64_t h = blockIdx.x; h < a.n_hubs; h += gridDim.x) {
         const uint32_t i = a.hubs[h];
         const uint8_t ca = a.cand[i];
@@ -1986,6 +2071,7 @@ __global__ __launch_bounds__(kBlock) void hub_finish(RoundArgs a) {
                 c_active += 1;
                 c_gathers += nin;
                 c_nact += any ? 1 : 0;
+                c_nactdeg += any ? deg : 0;
                 c_bytes += 16 + 2 + (uint64_t)(c1 - c0) * 16 * a.nwp + 8 * a.nwp +
                            ((any || zm) ? 8 * a.nwp : 0) + (any ? 8 * a.nwp + 1 : 0);
             }
@@ -2003,6 +2089,7 @@ __global__ __launch_bounds__(kBlock) void hub_finish(RoundArgs a) {
     acc[C_ACTIVE] = c_active;
     acc[C_GATHERS] = c_gathers;
     acc[C_NACT] = c_nact;
+    acc[C_NACTDEG] = c_nactdeg;
     acc[C_BYTES] = c_bytes;
     flush_counters(a, acc, s_red, t_start, K_STREAM);
 }

@@ -1,0 +1,92 @@
+// gather_bench.hip — random whole-row gathers from a large table on MI355X
+// (tools only): rows/s and GB/s for row sizes 32..512 B, uniformly random or
+// power-law (row index = the top bits of a product of uniforms, hubs first),
+// into registers (G lanes x 16 B per row, K rows in flight per lane) — the
+// access shape of expand_stream's sender-row gathers at 8..64 lanes per node.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/gather_bench tools/gather_bench.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                    \
+    do {                                                                         \
+        hipError_t e_ = (x);                                                     \
+        if (e_ != hipSuccess) {                                                  \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));              \
+            exit(1);                                                             \
+        }                                                                        \
+    } while (0)
+
+template <int G, int K>
+__global__ __launch_bounds__(256) void gather(const uint4* table, const uint32_t* idx, uint64_t n_rows_idx,
+                                              uint4* out) {
+    const int lg = threadIdx.x % G;
+    const uint64_t groups = (uint64_t)gridDim.x * (256 / G);
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (uint64_t r0 = ((uint64_t)blockIdx.x * (256 / G) + threadIdx.x / G) * K; r0 < n_rows_idx; r0 += groups * K) {
+        uint32_t ix[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) ix[k] = r0 + k < n_rows_idx ? idx[r0 + k] : 0u;
+        uint4 v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k] = table[(uint64_t)ix[k] * G + lg];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            acc.x |= v[k].x;
+            acc.y |= v[k].y;
+            acc.z |= v[k].z;
+            acc.w |= v[k].w;
+        }
+    }
+    out[(uint64_t)blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
+template <int G, int K>
+double run(const uint4* table, const uint32_t* idx, uint64_t n, uint4* out, int blocks) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    hipLaunchKernelGGL((gather<G, K>), dim3(blocks), dim3(256), 0, 0, table, idx, n, out);
+    CK(hipEventRecord(a, 0));
+    for (int r = 0; r < 3; ++r) hipLaunchKernelGGL((gather<G, K>), dim3(blocks), dim3(256), 0, 0, table, idx, n, out);
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / 3;
+}
+
+int main(int argc, char** argv) {
+    const uint64_t n = 1ull << 27;
+    uint4* table;
+    uint32_t* idx;
+    uint4* out;
+    const uint64_t max_table = 8ull << 30;
+    CK(hipMalloc(&table, max_table));
+    CK(hipMemset(table, 1, max_table));
+    CK(hipMalloc(&idx, n * 4));
+    CK(hipMalloc(&out, 8192ull * 256 * 16));
+    std::vector<uint32_t> h(n);
+    // where does the row-request ceiling sit? table in L2 (2 MB), in the
+    // Infinity Cache (64 MB) or in HBM (8 GB); rows in flight per lane K
+    for (uint64_t tb : {2ull << 20, 64ull << 20, 8ull << 30}) {
+        for (int rb : {64, 128}) {
+            const uint64_t rows = tb / rb;
+            uint64_t s = 88172645463325252ull + rb;
+            auto rnd = [&]() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; };
+            for (uint64_t i = 0; i < n; ++i) h[i] = (uint32_t)(rnd() % rows);
+            CK(hipMemcpy(idx, h.data(), n * 4, hipMemcpyHostToDevice));
+            for (int K : {2, 8, 16}) {
+                double ms = 0;
+                if (rb == 64) ms = K == 2 ? run<4, 2>(table, idx, n, out, 4096) : K == 8 ? run<4, 8>(table, idx, n, out, 4096) : run<4, 16>(table, idx, n, out, 4096);
+                else ms = K == 2 ? run<8, 2>(table, idx, n, out, 4096) : K == 8 ? run<8, 8>(table, idx, n, out, 4096) : run<8, 16>(table, idx, n, out, 4096);
+                printf("table %6llu MB rows %3d B K=%2d: %.1f G rows/s  %.0f GB/s\n", (unsigned long long)(tb >> 20), rb, K,
+                       n / (ms * 1e-3) / 1e9, n * (double)rb / (ms * 1e-3) / 1e9);
+                fflush(stdout);
+            }
+        }
+    }
+    return 0;
+}

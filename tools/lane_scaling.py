@@ -49,6 +49,11 @@ def run_rank(V, K, rank, world, steps, gen, inj, R=None):
         t = time.perf_counter()
         e.step(R, raw=True)
         times.append(time.perf_counter() - t)
+    if os.environ.get("LANE_ROUNDS"):
+        for s in ref:
+            print(f"  r{s['round']:2d} new {s['new_bits']:12d} rows {s['work_rows']:10d} gathers {s['work_gathers']:11d} "
+                  f"stream {s['stream_ms']:8.2f} ms {s['stream_bytes'] / 1e9:8.2f} GB prep {s['prep_ms']:.2f} ms",
+                  flush=True)
     stream_ms = sum(s["stream_ms"] for s in ref)
     stream_b = sum(s["stream_bytes"] for s in ref)
     e.close()
