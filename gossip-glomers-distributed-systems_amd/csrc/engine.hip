@@ -45,8 +45,11 @@ struct Window {
     bool seeded;
     uint64_t epoch_seed;
     std::vector<uint8_t> group;  // explicit: global node -> group
-    uint8_t* d_grp = nullptr;    // local-row groups on device
-    uint64_t* d_ebits = nullptr; // in-edge bitmap: ends in different groups (build_edge_mask)
+    bool edges = false;          // gg_set_partition: per-edge drops (overrides group windows)
+    std::vector<uint64_t> ebits; // ... as a bitmap over this engine's local in-edges
+    uint8_t* d_grp = nullptr;    // local-row groups on device (per-edge window: all zero)
+    uint64_t* d_ebits = nullptr; // in-edge bitmap: ends in different groups (build_edge_mask),
+                                 // or the per-edge window's bits
 };
 
 struct Injection {
@@ -150,6 +153,7 @@ struct gg_engine {
     std::vector<uint32_t> gid;     // [rows] original id of each local row (~0u: padding)
     std::vector<uint32_t> loc_of;  // [V] local row of an owned node, ~0u otherwise (sharded)
     bool have_topo = false, symmetric = true;
+    std::vector<int64_t> host_rp;  // vertex-sharded: the caller's row offsets (gg_set_partition)
     uint32_t* d_gid = nullptr;     // sharded only (single engine: row == id)
     // exchange: owned rows each rank needs (concatenated per destination) and
     // ghost counts per source rank; outgoing ghost edges (ghost -> owned receivers)
@@ -406,6 +410,13 @@ int materialize_windows(gg_engine* e) {
         if (w.d_grp) continue;
         any = true;
         HIPCHK(hipMalloc(&w.d_grp, e->rows));
+        if (w.edges) {  // the kernels take the bits; the groups only mark the window active
+            HIPCHK(hipMemset(w.d_grp, 0, e->rows));
+            HIPCHK(hipMalloc(&w.d_ebits, std::max<size_t>(1, w.ebits.size()) * 8));
+            if (!w.ebits.empty())
+                HIPCHK(hipMemcpy(w.d_ebits, w.ebits.data(), w.ebits.size() * 8, hipMemcpyHostToDevice));
+            continue;
+        }
         if (w.seeded) {
             const uint64_t valid = e->d_gid ? e->rows : e->n_own;
             hipLaunchKernelGGL(gg::fill_seeded_groups, dim3((unsigned)((e->rows + 255) / 256)), dim3(256), 0,
@@ -432,6 +443,8 @@ int materialize_windows(gg_engine* e) {
 }
 
 const Window* window_at(const gg_engine* e, int64_t r) {
+    for (const auto& w : e->windows)  // a per-edge window overrides a group window
+        if (w.edges && w.from <= r && r < w.to) return &w;
     for (const auto& w : e->windows)
         if (w.from <= r && r < w.to) return &w;
     return nullptr;
@@ -626,10 +639,12 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.sync_next = e->d_sync_next;
     a.sync_k = e->d_sync_k;
     bool maskw = false;
+    a.ewin = 0;
     for (int k = 0; k < 5; ++k) {
         const Window* w = window_at(e, r - 3 + k);
         a.grp[k] = w ? w->d_grp : nullptr;
         a.ebits[k] = w ? w->d_ebits : nullptr;
+        if (w && w->edges) a.ewin |= 1u << k;
         maskw |= a.grp[k] != nullptr;
     }
     a.inj = d_inj;
@@ -1177,6 +1192,11 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     }
     HIPCHK(hipStreamSynchronize(e->stream));
     e->free_topology();
+    if (e->P > 1) e->host_rp.assign(row_ptr, row_ptr + V + 1);
+    else e->host_rp.clear();
+    // per-edge windows are in the old topology's edge order
+    e->windows.erase(std::remove_if(e->windows.begin(), e->windows.end(), [](const Window& w) { return w.edges; }),
+                     e->windows.end());
     // symmetric (u lists v iff v lists u)? then the in-lists are the rows themselves
     bool sym = true;
     {
@@ -1445,6 +1465,9 @@ int gg_topology_generate(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_ou
     HIPCHK(hipStreamSynchronize(e->stream));
     e->free_topology();
     e->have_topo = false;
+    e->host_rp.clear();
+    e->windows.erase(std::remove_if(e->windows.begin(), e->windows.end(), [](const Window& w) { return w.edges; }),
+                     e->windows.end());
     gg_gen::Csr g{};
     std::string err;
     if (e->P != 1) {
@@ -1548,8 +1571,8 @@ int gg_topology_export(gg_engine* e, int64_t* row_ptr, int32_t* col, uint64_t ca
 
 static int add_window(gg_engine* e, int64_t a, int64_t b, Window&& w) {
     if (a >= b) return e->fail(GG_EINVAL, "empty partition window");
-    for (const auto& x : e->windows)
-        if (a < x.to && x.from < b) return e->fail(GG_EINVAL, "overlapping partition windows");
+    for (const auto& x : e->windows)  // per-edge windows may overlap group windows (and win)
+        if (x.edges == w.edges && a < x.to && x.from < b) return e->fail(GG_EINVAL, "overlapping partition windows");
     w.from = a;
     w.to = b;
     e->windows.push_back(std::move(w));
@@ -1561,6 +1584,60 @@ int gg_partition_seeded(gg_engine* e, int64_t a, int64_t b, uint64_t epoch_seed)
     Window w;
     w.seeded = true;
     w.epoch_seed = epoch_seed;
+    return add_window(e, a, b, std::move(w));
+}
+
+// Per-edge partition window (Maelstrom's partition nemesis as arbitrary cut
+// links; SURVEY.md Appendix A D7: an explicit per-edge bitset overrides the
+// seeded plan). The caller's E bits follow its CSR (entry k of row u = the link
+// u -> col[k]); a cut link drops messages both ways, so the topology and the
+// mask must be symmetric. Converted here to this engine's local in-edge order.
+int gg_set_partition(gg_engine* e, int64_t a, int64_t b, const uint64_t* bits) {
+    if (!e || !bits) return GG_EINVAL;
+    if (!e->have_topo) return e->fail(GG_EINVAL, "gg_set_partition: install the topology first");
+    if (!e->symmetric) return e->fail(GG_EINVAL, "gg_set_partition: per-edge windows need a symmetric topology");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    const uint64_t V = e->V, n_own = e->n_own;
+    std::vector<int64_t> ip(n_own + 1);
+    std::vector<uint32_t> ic(e->n_in_edges);
+    HIPCHK(hipMemcpy(ip.data(), e->d_in_ptr, (n_own + 1) * 8, hipMemcpyDeviceToHost));
+    if (e->n_in_edges) HIPCHK(hipMemcpy(ic.data(), e->d_in_col, e->n_in_edges * 4, hipMemcpyDeviceToHost));
+    auto gid = [&](uint64_t row) -> uint64_t { return e->gid.empty() ? row : e->gid[row]; };
+    // the caller's row offsets: every node's degree (sharded: kept from gg_topology)
+    std::vector<int64_t> crp;
+    const std::vector<int64_t>* rp = &e->host_rp;
+    if (e->host_rp.empty()) {
+        crp.assign(V + 1, 0);
+        for (uint64_t i = 0; i < n_own; ++i) crp[gid(i) + 1] = ip[i + 1] - ip[i];
+        for (uint64_t v = 0; v < V; ++v) crp[v + 1] += crp[v];
+        rp = &crp;
+    }
+    auto bit = [&](uint64_t k) { return (bits[k >> 6] >> (k & 63)) & 1ull; };
+    Window w;
+    w.seeded = false;
+    w.epoch_seed = 0;
+    w.edges = true;
+    w.ebits.assign((e->n_in_edges + 63) / 64, 0);
+    for (uint64_t i = 0; i < n_own; ++i) {
+        const uint64_t v = gid(i);
+        for (int64_t k = ip[i]; k < ip[i + 1]; ++k) {
+            if (!bit((uint64_t)((*rp)[v] + (k - ip[i])))) continue;
+            w.ebits[k >> 6] |= 1ull << (k & 63);
+            // symmetric mask: the reverse link u -> v (an owned u) must be cut too
+            const uint32_t ru = ic[k] & gg::kColMask;
+            if (ru >= n_own) continue;  // a ghost: its owner checks
+            const uint64_t u = gid(ru);
+            int64_t lo = ip[ru], hi = ip[ru + 1];
+            while (lo < hi) {  // u's list ascends by node id
+                const int64_t mid = (lo + hi) / 2;
+                if (gid(ic[mid] & gg::kColMask) < v) lo = mid + 1;
+                else hi = mid;
+            }
+            if (lo >= ip[ru + 1] || !bit((uint64_t)((*rp)[u] + (lo - ip[ru]))))
+                return e->fail(GG_EINVAL, "gg_set_partition: the mask is not symmetric");
+        }
+    }
     return add_window(e, a, b, std::move(w));
 }
 

@@ -162,7 +162,9 @@ struct RoundArgs {
     uint32_t* sync_k;           // ghosts: every engine runs its ghosts' timers itself
     const uint8_t* grp[5];      // partition groups of rounds r-3..r+1 (nullptr: no window)
     const uint64_t* ebits[5];   // the same windows as in-edge bitmaps: bit e = the two ends of
-                                // in-edge e are in different groups (masked streaming rounds)
+                                // in-edge e are in different groups (masked streaming rounds),
+                                // or the caller's per-edge mask (gg_set_partition windows)
+    uint32_t ewin;              // bit k: window k is per-edge (ebits[k] decides, not grp[k])
     const uint32_t* inj;        // (local node, lane) pairs sorted by node
     uint32_t n_inj;
     unsigned long long* counters;  // [kSlots][kCounters]
@@ -261,14 +263,18 @@ __device__ __forceinline__ uint64_t gid_of(const RoundArgs& a, uint64_t i) {
     return a.gid ? (uint64_t)a.gid[i] : a.lo + i;
 }
 
-// message from replica row ra to replica row rb in round (r-3+k) dropped?
+// message from replica row ra to replica row rb in round (r-3+k) dropped? e:
+// the edge between them (its position in rb's in-list or ra's out-list: the
+// same list on the symmetric topologies per-edge windows require).
 template <bool MASKW>
-__device__ __forceinline__ bool masked(const RoundArgs& a, int k, uint64_t ra, uint64_t rb) {
+__device__ __forceinline__ bool masked(const RoundArgs& a, int k, uint64_t ra, uint64_t rb, uint64_t e) {
     if constexpr (!MASKW) {
         return false;
     } else {
         const uint8_t* g = a.grp[k];
-        return g != nullptr && g[ra] != g[rb];
+        if (g == nullptr) return false;
+        if ((a.ewin >> k) & 1u) return bit_at(a.ebits[k], e);  // gg_set_partition window
+        return g[ra] != g[rb];
     }
 }
 
@@ -300,11 +306,11 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 // read reached v in r-3 and v's read_ok reached u in r-2), so v receives u's
 // whole round r-1 set.
 template <bool SYNCW, bool MASKW>
-__device__ __forceinline__ bool is_push(const RoundArgs& a, uint8_t ef, uint64_t u, uint64_t v) {
+__device__ __forceinline__ bool is_push(const RoundArgs& a, uint8_t ef, uint64_t u, uint64_t v, uint64_t e) {
     if constexpr (!SYNCW) {
         return false;
     } else {
-        return (ef & SE_FM3) && !masked<MASKW>(a, 0, u, v) && !masked<MASKW>(a, 1, v, u);
+        return (ef & SE_FM3) && !masked<MASKW>(a, 0, u, v, e) && !masked<MASKW>(a, 1, v, u, e);
     }
 }
 
@@ -450,9 +456,9 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                 if (fm1) {
                     for (int64_t e = o0; e < o1; ++e) {
                         const uint64_t w = a.out_col[e] & kColMask;
-                        if (masked<MASKW>(a, 2, rep, w)) continue;
+                        if (masked<MASKW>(a, 2, rep, w, e)) continue;
                         c_read_oks++;
-                        if (masked<MASKW>(a, 3, w, rep)) c_dropped++;
+                        if (masked<MASKW>(a, 3, w, rep, e)) c_dropped++;
                     }
                 }
                 // (5) the sync timer (main.go:42-51): read RPC to every neighbour (:119-121)
@@ -463,7 +469,7 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                     c_reads += (unsigned long long)(o1 - o0);
                     if constexpr (MASKW) {
                         for (int64_t e = o0; e < o1; ++e)
-                            c_dropped += masked<MASKW>(a, 3, rep, a.out_col[e] & kColMask) ? 1 : 0;
+                            c_dropped += masked<MASKW>(a, 3, rep, a.out_col[e] & kColMask, e) ? 1 : 0;
                     }
                     const uint32_t kk = a.sync_k[i] + 1;
                     a.sync_k[i] = kk;
@@ -633,7 +639,8 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
     constexpr int kSpec = GG_SPEC_BATCH;  // busy lean rounds (W = 64): (flag, row) pairs in flight per lane
     constexpr int kPre = 64;        // worklist entries preloaded per chunk
     constexpr bool LEAN = !SYNCW && !MASKW;
-    constexpr uint8_t L_PUSH = 1, L_LAG = 2;  // compacted-list flags
+    constexpr uint8_t L_PUSH = 1, L_LAG = 2, L_M3 = 4, L_M4 = 8;  // compacted-list flags (L_M3/L_M4: the
+                                                                  // windows of r, r+1 cut the edge)
     __shared__ int64_t s_ptr[NG + 1];
     __shared__ uint32_t s_col[kEdgeStage];
     __shared__ uint8_t s_ef[kEdgeStage];
@@ -748,7 +755,8 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                     }
                 };
                 // (2) first deliverer claims, ascending sender
-                auto claim = [&](const Row<WPL>& src, uint32_t c) {
+                // mb: bit 0 = v's forward of round r to u dropped, bit 1 = u's ack of r+1 dropped
+                auto claim = [&](const Row<WPL>& src, uint32_t c, uint32_t mb) {
                     unsigned long long pc = 0;
 #pragma unroll
                     for (int w = 0; w < WPL; ++w) {
@@ -759,10 +767,9 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                     if (c & kRecipBit) {
                         cl_recip += pc;
                         if constexpr (MASKW) {
-                            const uint64_t u = c & kColMask;
-                            if (!masked<MASKW>(a, 3, rep, u)) {
+                            if (!(mb & 1u)) {
                                 cl_deliv += pc;
-                                if (masked<MASKW>(a, 4, u, rep)) cl_ackdrop += pc;
+                                if (mb & 2u) cl_ackdrop += pc;
                             }
                         }
                     }
@@ -807,7 +814,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
 #pragma unroll
                             for (int b = 0; b < kSpec; ++b) {
                                 if (fb[b] & FL_ACT) {
-                                    claim(src[b], cb[b]);
+                                    claim(src[b], cb[b], 0u);
                                     c_gathers += (lg == 0) ? 1ull : 0ull;
                                 }
                             }
@@ -829,14 +836,17 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                             ef = sender_flags<SYNCW>(a, c & kColMask);
                         }
                         const uint64_t u = c & kColMask;
-                        const bool drop = masked<MASKW>(a, 2, u, rep);  // sent in r-1
+                        const uint64_t ei = (uint64_t)(eb + k);
+                        const bool drop = masked<MASKW>(a, 2, u, rep, ei);  // sent in r-1
                         if constexpr (SYNCW) keep |= (ef & SE_FM2) != 0;  // u's callback reads v now
-                        const bool p = !drop && is_push<SYNCW, MASKW>(a, ef, u, rep);
+                        const bool p = !drop && is_push<SYNCW, MASKW>(a, ef, u, rep, ei);
                         if (!drop && ((ef & SE_ACT) || p)) {
                             need = true;
                             if (staged) {  // every lane of the group writes the same entry
                                 s_col[k0 + m] = c;
-                                s_ef[k0 + m] = (p ? L_PUSH : 0) | ((ef & SE_LAG) ? L_LAG : 0);
+                                s_ef[k0 + m] = (p ? L_PUSH : 0) | ((ef & SE_LAG) ? L_LAG : 0) |
+                                               (masked<MASKW>(a, 3, rep, u, ei) ? L_M3 : 0) |
+                                               (masked<MASKW>(a, 4, u, rep, ei) ? L_M4 : 0);
                                 ++m;
                             }
                         }
@@ -850,12 +860,14 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                             nrows += (unsigned long long)m;
                             for (int b0 = 0; b0 < m; b0 += kBatch) {
                                 uint32_t cb[kBatch];
+                                uint8_t lfs[kBatch];
                                 Row<WPL> src[kBatch];
 #pragma unroll
                                 for (int b = 0; b < kBatch; ++b) {
                                     const bool v = b0 + b < m;
                                     cb[b] = v ? s_col[k0 + b0 + b] : 0u;
                                     const uint8_t lf = v ? s_ef[k0 + b0 + b] : 0;
+                                    lfs[b] = lf;
                                     if (v) {
                                         src[b] = sender_row(cb[b], lf & L_PUSH, lf & L_LAG);
                                     } else {
@@ -864,19 +876,22 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                                     }
                                 }
 #pragma unroll
-                                for (int b = 0; b < kBatch; ++b) claim(src[b], cb[b]);
+                                for (int b = 0; b < kBatch; ++b) claim(src[b], cb[b], (uint32_t)(lfs[b] >> 2));
                             }
                         } else {
                             for (int64_t k = k0; k < k1; ++k) {  // hub slow path
                                 const uint32_t c = a.in_col[eb + k];
                                 const uint64_t u = c & kColMask;
                                 const uint8_t ef = sender_flags<SYNCW>(a, u);
-                                if (masked<MASKW>(a, 2, u, rep)) continue;
-                                const bool p = is_push<SYNCW, MASKW>(a, ef, u, rep);
+                                const uint64_t ei = (uint64_t)(eb + k);
+                                if (masked<MASKW>(a, 2, u, rep, ei)) continue;
+                                const bool p = is_push<SYNCW, MASKW>(a, ef, u, rep, ei);
                                 if (!(ef & SE_ACT) && !p) continue;
                                 c_gathers += (lg == 0) ? 1ull : 0ull;
                                 nrows++;
-                                claim(sender_row(c, p, (ef & SE_LAG) != 0), c);
+                                claim(sender_row(c, p, (ef & SE_LAG) != 0), c,
+                                      (masked<MASKW>(a, 3, rep, u, ei) ? 1u : 0u) |
+                                          (masked<MASKW>(a, 4, u, rep, ei) ? 2u : 0u));
                             }
                         }
                         // (3) sync callback: v fired in r-2, read_oks of peers in ascending order
@@ -885,7 +900,7 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                                 const int64_t o0 = a.out_ptr[i], o1 = a.out_ptr[i + 1];
                                 for (int64_t e = o0; e < o1; ++e) {
                                     const uint64_t w = a.out_col[e] & kColMask;
-                                    if (masked<MASKW>(a, 1, rep, w) || masked<MASKW>(a, 2, w, rep)) continue;
+                                    if (masked<MASKW>(a, 1, rep, w, e) || masked<MASKW>(a, 2, w, rep, e)) continue;
                                     const Row<WPL> R =
                                         sender_row((uint32_t)w, true, (a.flg_prev[w] & FL_LAG) != 0);
                                     nrows++;
@@ -899,10 +914,10 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                                     }
                                     cb_new += pn;
                                     push_sent += pp;
-                                    if (!masked<MASKW>(a, 3, rep, w)) {
+                                    if (!masked<MASKW>(a, 3, rep, w, e)) {
                                         cb_new_deliv += pn;
                                         push_deliv += pp;
-                                        if (masked<MASKW>(a, 4, w, rep)) {
+                                        if (masked<MASKW>(a, 4, w, rep, e)) {
                                             cb_new_ackdrop += pn;
                                             push_ackdrop += pp;
                                         }
@@ -954,9 +969,9 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                             U = 0;
                             for (int64_t e = a.out_ptr[i]; e < a.out_ptr[i + 1]; ++e) {
                                 const uint64_t w = a.out_col[e] & kColMask;
-                                if (!masked<MASKW>(a, 3, rep, w)) {
+                                if (!masked<MASKW>(a, 3, rep, w, e)) {
                                     U++;
-                                    if (masked<MASKW>(a, 4, w, rep)) AD++;
+                                    if (masked<MASKW>(a, 4, w, rep, e)) AD++;
                                 }
                             }
                         }

@@ -108,7 +108,7 @@ COUNT_FIELDS = [f for f in STAT_FIELDS if f not in DIAG_FIELDS]
 
 GG_SYMBOLS = [
     "gg_abi_version", "gg_create", "gg_destroy", "gg_last_error", "gg_topology",
-    "gg_partition_seeded", "gg_partition_groups", "gg_broadcast", "gg_broadcast_many",
+    "gg_partition_seeded", "gg_partition_groups", "gg_set_partition", "gg_broadcast", "gg_broadcast_many",
     "gg_lane_of", "gg_step",
     "gg_current_round", "gg_step_device_ms", "gg_read", "gg_read_bits", "gg_delivery_rounds", "gg_reset",
     "gg_read_bits_nodes", "gg_delivery_rounds_nodes",
@@ -136,6 +136,7 @@ def load_library(path: str) -> C.CDLL:
     lib.gg_topology.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
     lib.gg_partition_seeded.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_uint64]
     lib.gg_partition_groups.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]
+    lib.gg_set_partition.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]
     lib.gg_broadcast.argtypes = [C.c_void_p, C.c_uint32, C.c_int64, C.c_int64]
     lib.gg_broadcast_many.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
     lib.gg_lane_of.argtypes = [C.c_void_p, C.c_int64]
@@ -264,6 +265,12 @@ class Engine:
 
     def partition_seeded(self, r0: int, r1: int, epoch_seed: int):
         self._ok(self.lib.gg_partition_seeded(self.h, r0, r1, epoch_seed))
+
+    def set_partition(self, r0: int, r1: int, bits):
+        """Per-edge window (gg_set_partition): one bit per adjacency entry of the
+        installed topology (CSR order; uint64 words), 1 = the link is cut both ways."""
+        b = np.ascontiguousarray(bits, np.uint64)
+        self._ok(self.lib.gg_set_partition(self.h, r0, r1, b.ctypes.data))
 
     def partition_groups(self, r0: int, r1: int, groups):
         g = np.ascontiguousarray(groups, np.uint8)

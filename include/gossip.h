@@ -14,7 +14,8 @@
  * gg_topology                 HandleTopology `broadcast/broadcast.go:36-48`
  *                             (every node keeps its own row; here: all rows at once)
  * gg_partition_seeded /       Maelstrom `--nemesis partition` (external harness,
- * gg_partition_groups         `README.md:18`): messages across groups are dropped
+ * gg_partition_groups /       `README.md:18`): messages across groups (or over cut
+ * gg_set_partition            links) are dropped; no retry (`broadcast.go:55`)
  * gg_broadcast                client `broadcast` -> HandleBroadcast `broadcast.go:59-79`
  * gg_step                     n lockstep rounds: every HandleBroadcast /
  *                             rebroadcastAllExcept (`:50-57`) / SyncBroadcast
@@ -127,6 +128,14 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
  * Seeded: group(v) = bisection bit from (seed, epoch_seed, v). */
 int gg_partition_seeded(gg_engine* e, int64_t round_from, int64_t round_to, uint64_t epoch_seed);
 int gg_partition_groups(gg_engine* e, int64_t round_from, int64_t round_to, const uint8_t* group);
+/* Per-edge window: edge_mask_bits holds one bit per
+ * adjacency entry in the caller's CSR order (entry k of row u = the link u -> col[k];
+ * 1 = cut): a message sent on a cut link in a round of [round_from, round_to) is
+ * dropped, both ways, so the topology and the mask must be symmetric (GG_EINVAL
+ * otherwise). Call after gg_topology (a new topology drops per-edge windows). A
+ * per-edge window overrides a group window for the rounds both cover; per-edge
+ * windows must not overlap each other. */
+int gg_set_partition(gg_engine* e, int64_t round_from, int64_t round_to, const uint64_t* edge_mask_bits);
 
 /* Client broadcast of `message` to `node`, delivered in `round` (>= current
  * round). The first broadcast of a value assigns it the next free lane. */

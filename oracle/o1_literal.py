@@ -155,6 +155,19 @@ class O1Network:
     def partition_groups(self, r0: int, r1: int, groups):
         self.windows.append((r0, r1, "groups", list(groups)))
 
+    def set_partition(self, r0: int, r1: int, bits):
+        """Per-edge window (gg_set_partition): bit k of `bits` (uint64 words) cuts
+        adjacency entry k in topology order (row u, then its neighbours); a cut
+        link drops messages both ways; it overrides a group window."""
+        cut, k = set(), 0
+        for nd in self.nodes:
+            for n in nd.neighbors:
+                if (int(bits[k >> 6]) >> (k & 63)) & 1:
+                    cut.add((nd.nid, n))
+                    cut.add((n, nd.nid))
+                k += 1
+        self.windows.append((r0, r1, "edges", frozenset(cut)))
+
     def broadcast(self, node: int, value: int, rnd: int):
         if value not in self.lanes:
             if len(self.lanes) >= self.W:
@@ -171,8 +184,11 @@ class O1Network:
         return payload[v]
 
     def masked(self, rnd: int, a: int, b: int) -> bool:
+        for win in self.windows:  # a per-edge window overrides a group window
+            if win[2] == "edges" and win[0] <= rnd < win[1]:
+                return (a, b) in win[3]
         for win in self.windows:
-            if win[0] <= rnd < win[1]:
+            if win[2] != "edges" and win[0] <= rnd < win[1]:
                 return self._group(win, a) != self._group(win, b)
         return False
 

@@ -44,6 +44,8 @@ struct Window {
     bool seeded;
     uint64_t epoch_seed;
     std::vector<uint8_t> group;  // global node -> group (explicit windows)
+    bool edges = false;          // gg_set_partition: cut links, in the caller's CSR order
+    std::vector<uint64_t> bits;
 };
 
 struct Injection {
@@ -83,6 +85,8 @@ struct gg_engine {
     std::vector<uint64_t> rank_lo;         // [world+1]
     bool have_topo = false, symmetric = true;
     // owned rows; columns are replica indices (rank * slice + offset)
+    std::vector<int64_t> crp;              // the caller's CSR (per-edge windows)
+    std::vector<int32_t> ccol;
     std::vector<int64_t> in_ptr, out_ptr;
     std::vector<uint32_t> in_col, out_col;
     std::vector<uint8_t> in_recip;
@@ -119,8 +123,10 @@ struct gg_engine {
         return (uint64_t)r * slice + (g - rank_lo[r]);
     }
     const Window* window_at(int64_t r) const {
+        for (const auto& w : windows)  // a per-edge window overrides a group window
+            if (w.edges && w.from <= r && r < w.to) return &w;
         for (const auto& w : windows)
-            if (w.from <= r && r < w.to) return &w;
+            if (!w.edges && w.from <= r && r < w.to) return &w;
         return nullptr;
     }
     int group_of(const Window* w, uint64_t g) const {
@@ -129,7 +135,14 @@ struct gg_engine {
     // message from global a to global b sent in round r dropped?
     bool masked(int64_t r, uint64_t a, uint64_t b) const {
         const Window* w = window_at(r);
-        return w && group_of(w, a) != group_of(w, b);
+        if (!w) return false;
+        if (w->edges) {  // the link a -> b (symmetric topology: it exists both ways)
+            const int32_t* r0 = ccol.data() + crp[a];
+            const int32_t* r1 = ccol.data() + crp[a + 1];
+            const uint64_t k = (uint64_t)crp[a] + (uint64_t)(std::lower_bound(r0, r1, (int32_t)b) - r0);
+            return (w->bits[k >> 6] >> (k & 63)) & 1ull;
+        }
+        return group_of(w, a) != group_of(w, b);
     }
     bool fired_at(int64_t r, uint64_t rep) const {
         if (r < 0) return false;
@@ -394,6 +407,10 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
                 if ((int64_t)tcol[tin[v] + k] != col[row_ptr[v] + k]) { sym = false; break; }
     }
     e->symmetric = sym;
+    e->crp.assign(row_ptr, row_ptr + V + 1);
+    e->ccol.assign(col, col + nnz);
+    e->windows.erase(std::remove_if(e->windows.begin(), e->windows.end(), [](const Window& w) { return w.edges; }),
+                     e->windows.end());
     // edge-balanced vertex ranges over the in-lists (pull work)
     const uint32_t Wd = e->P;  // vertex parts of this lane group
     e->rank_lo.assign(Wd + 1, V);
@@ -453,8 +470,8 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
 static int add_window(gg_engine* e, int64_t a, int64_t b, Window&& w) {
     if (!e) return GG_EINVAL;
     if (a >= b) return e->fail(GG_EINVAL, "empty partition window");
-    for (const auto& x : e->windows)
-        if (a < x.to && x.from < b) return e->fail(GG_EINVAL, "overlapping partition windows");
+    for (const auto& x : e->windows)  // per-edge windows may overlap group windows (and win)
+        if (x.edges == w.edges && a < x.to && x.from < b) return e->fail(GG_EINVAL, "overlapping partition windows");
     w.from = a;
     w.to = b;
     e->windows.push_back(std::move(w));
@@ -465,6 +482,28 @@ int gg_partition_seeded(gg_engine* e, int64_t a, int64_t b, uint64_t epoch_seed)
     Window w;
     w.seeded = true;
     w.epoch_seed = epoch_seed;
+    return add_window(e, a, b, std::move(w));
+}
+
+int gg_set_partition(gg_engine* e, int64_t a, int64_t b, const uint64_t* bits) {
+    if (!e || !bits) return GG_EINVAL;
+    if (!e->have_topo) return e->fail(GG_EINVAL, "gg_set_partition: install the topology first");
+    if (!e->symmetric) return e->fail(GG_EINVAL, "gg_set_partition: per-edge windows need a symmetric topology");
+    const uint64_t E = e->ccol.size();
+    Window w;
+    w.seeded = false;
+    w.epoch_seed = 0;
+    w.edges = true;
+    w.bits.assign(bits, bits + (E + 63) / 64);
+    auto bit = [&](uint64_t k) { return (bits[k >> 6] >> (k & 63)) & 1ull; };
+    for (uint64_t u = 0; u < e->V; ++u)
+        for (int64_t k = e->crp[u]; k < e->crp[u + 1]; ++k) {
+            const uint64_t v = (uint64_t)e->ccol[k];
+            const int32_t* r0 = e->ccol.data() + e->crp[v];
+            const int32_t* r1 = e->ccol.data() + e->crp[v + 1];
+            const uint64_t kr = (uint64_t)e->crp[v] + (uint64_t)(std::lower_bound(r0, r1, (int32_t)u) - r0);
+            if (bit((uint64_t)k) != bit(kr)) return e->fail(GG_EINVAL, "gg_set_partition: the mask is not symmetric");
+        }
     return add_window(e, a, b, std::move(w));
 }
 

@@ -20,6 +20,7 @@ class Scenario:
     sync_jitter: int = 10
     enable_sync: bool = True
     windows: list = field(default_factory=list)  # ("seeded", r0, r1, epoch) | ("groups", r0, r1, arr)
+    #                                              | ("edges", r0, r1, uint64 bit words over the CSR)
 
 
 def apply(eng, sc: Scenario):
@@ -28,6 +29,8 @@ def apply(eng, sc: Scenario):
     for w in sc.windows:
         if w[0] == "seeded":
             eng.partition_seeded(w[1], w[2], w[3])
+        elif w[0] == "edges":
+            eng.set_partition(w[1], w[2], w[3])
         else:
             eng.partition_groups(w[1], w[2], w[3])
     for n, v, r in sc.injections:
@@ -126,3 +129,36 @@ def c1_scenario(partition=False, rounds=260, seed=0x6A09E667F3BCC909 + 1) -> Sce
     W = ((val + 63) // 64) * 64
     windows = [("seeded", 50, 100, seed ^ 0xB15EC7)] if partition else []
     return Scenario(topo, W, rounds, inj, seed=seed, windows=windows)
+
+
+def symmetric_cut(topo: Topology, rnd: random.Random, p: float) -> np.ndarray:
+    """A random set of cut links as gg_set_partition bits: each undirected link
+    u-v is cut with probability p, its two adjacency entries together."""
+    E = topo.nnz
+    words = np.zeros((E + 63) // 64, np.uint64)
+    for u in range(topo.n_nodes):
+        for k in range(int(topo.row_ptr[u]), int(topo.row_ptr[u + 1])):
+            v = int(topo.col[k])
+            if v <= u or rnd.random() >= p:
+                continue
+            kr = int(topo.row_ptr[v]) + int(np.searchsorted(topo.col[topo.row_ptr[v]:topo.row_ptr[v + 1]], u))
+            for x in (k, kr):
+                words[x >> 6] |= np.uint64(1) << np.uint64(x & 63)
+    return words
+
+
+def symmetric_random_scenario(rnd: random.Random, max_v=60, W=None, rounds=50, edge_windows=2) -> Scenario:
+    """random_scenario on a symmetric topology, plus per-edge windows (some
+    overlapping its group windows, which they override)."""
+    sc = random_scenario(rnd, max_v=max_v, directed_p=0.0, W=W, rounds=rounds)
+    wins = list(sc.windows)
+    for _ in range(edge_windows):
+        a = rnd.randrange(0, 30)
+        wins.append(("edges", a, a + rnd.randrange(1, 10), symmetric_cut(sc.topo, rnd, rnd.choice([0.1, 0.3, 0.7]))))
+    ok = []
+    for w in wins:  # per-edge windows must not overlap each other
+        if w[0] == "edges" and any(x[0] == "edges" and w[1] < x[2] and x[1] < w[2] for x in ok):
+            continue
+        ok.append(w)
+    sc.windows = ok
+    return sc

@@ -156,3 +156,10 @@ def test_runner_transport_choice(cpu_lib):
 def torch_device_cpu():
     import torch
     return torch.device("cpu")
+
+
+def test_edge_windows_two_ranks(cpu_lib):
+    """gg_set_partition windows in a sharded job equal the single engine."""
+    from helpers import symmetric_random_scenario
+    sc = symmetric_random_scenario(random.Random(77), max_v=200, W=128, rounds=45)
+    _check(cpu_lib, sc)

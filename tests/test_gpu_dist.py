@@ -90,6 +90,10 @@ def _scenarios():
     out.append(Scenario(rr, 1024, 30, uniform_injections(4000, 1000, 7), seed=12, sync_base=10,
                         sync_jitter=5, windows=[("seeded", 2, 7, 5)]))
     out.append(c1_scenario(partition=True, rounds=120))
+    from helpers import symmetric_cut
+    grid2 = T.grid_links(40, seed=13)
+    out.append(Scenario(grid2, 128, 40, uniform_injections(1600, 100, 8), seed=11, sync_base=7, sync_jitter=3,
+                        windows=[("seeded", 3, 9, 5), ("edges", 5, 14, symmetric_cut(grid2, rnd, 0.3))]))
     del rnd
     return out
 

@@ -239,3 +239,27 @@ def test_degree_order_device_generated(hip_lib, cpu_lib, monkeypatch):
         out.append((e.step(25), e.read_bits(), e.delivery_rounds()))
     assert not diff_stats(out[0][0], out[1][0])
     assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][2], out[1][2])
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_edge_windows_vs_o2(hip_lib, cpu_lib, seed):
+    """gg_set_partition: per-edge windows (overriding overlapping group windows)
+    on random symmetric graphs, every lane width class; the masked streaming
+    kernel (lean rounds) and the tile kernel (sync rounds) both read the bits."""
+    from helpers import symmetric_random_scenario
+    rnd = random.Random(9100 + seed)
+    for W in (64, 128, 1024):
+        sc = symmetric_random_scenario(rnd, max_v=150, W=W, rounds=45)
+        _compare(sc, hip_lib, cpu_lib)
+
+
+def test_edge_window_c3_shape_vs_o2(hip_lib, cpu_lib):
+    """A 4K-node random 8-regular graph (C3's shape) with a seeded bisection and
+    an overlapping per-edge window that cuts 30% of the links, sync on."""
+    from helpers import symmetric_cut
+    topo = T.random_regular(4096, 8, seed=3)
+    bits = symmetric_cut(topo, random.Random(4), 0.3)
+    sc = Scenario(topo, 1024, 40, uniform_injections(4096, 1024, 3), seed=3, sync_base=8, sync_jitter=4,
+                  windows=[("seeded", 2, 12, 7), ("edges", 6, 16, bits)])
+    st, _ = _compare(sc, hip_lib, cpu_lib)
+    assert sum(s["dropped"] for s in st[12:16]) > 0

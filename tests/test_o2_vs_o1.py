@@ -64,3 +64,34 @@ def test_sync_disabled_and_no_injection(cpu_lib):
     sc.injections = []
     st = _compare(sc, cpu_lib)
     assert all(s["new_bits"] == 0 for s in st)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_o2_equals_o1_edge_windows(cpu_lib, seed):
+    """gg_set_partition (per-edge windows, overriding overlapping group windows):
+    O2 = O1 on random symmetric graphs with sync."""
+    from helpers import symmetric_random_scenario
+    rnd = random.Random(500 + seed)
+    sc = symmetric_random_scenario(rnd)
+    o1 = make_o1(sc)
+    o2 = make_engine(cpu_lib, sc)
+    d = diff_stats(o1.step(sc.rounds), o2.step(sc.rounds))
+    assert not d, d[:10]
+    for v in range(sc.topo.n_nodes):
+        assert o1.read(v) == o2.read(v)
+
+
+def test_edge_window_rejects_asymmetric(cpu_lib):
+    from ggamd.engine import Engine, GGError, Topology
+    import numpy as np
+    topo = Topology.from_rows([[1], [0, 2], [1]])
+    e = Engine(3, 64, library=cpu_lib)
+    e.topology(topo)
+    with pytest.raises(GGError):
+        e.set_partition(0, 5, np.array([0b1], np.uint64))  # cuts 0->1 but not 1->0
+    e.set_partition(0, 5, np.array([0b11], np.uint64))      # both entries of link 0-1
+    d = Topology.from_rows([[1], [], []])
+    e2 = Engine(3, 64, library=cpu_lib)
+    e2.topology(d)
+    with pytest.raises(GGError):
+        e2.set_partition(0, 5, np.array([0b1], np.uint64))  # directed topology
