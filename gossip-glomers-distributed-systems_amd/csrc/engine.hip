@@ -219,6 +219,9 @@ struct gg_engine {
     gg::HubChunk* d_hchunks = nullptr;
     gg::HubChunk* d_mchunks = nullptr;
     uint4* d_srec = nullptr;         // [2 n_own] sync records (streamed sync rounds), or none
+    uint8_t* d_pushb = nullptr;      // [out-edges] non-empty sync pushes of the last callbacks
+    uint32_t* d_rev = nullptr;       // [in-edges] sender's out-edge index (streamed sync rounds)
+    uint64_t n_out_edges = 0;
     uint8_t* d_sstate = nullptr;     // [rows] sender states (streamed sync rounds)
     uint64_t* d_ibits = nullptr;     // [rows/64] non-zero sender states
     bool sync_tiles = false;         // GG_SYNC_TILES=1: sync rounds on the tile path (A/B)
@@ -294,6 +297,8 @@ void gg_engine::free_topology() {
     dfree(d_hchunks);
     dfree(d_mchunks);
     dfree(d_srec);
+    dfree(d_pushb);
+    dfree(d_rev);
     dfree(d_sstate);
     dfree(d_ibits);
     dfree(d_hscratch);
@@ -629,6 +634,8 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.hscratch = e->d_hscratch;
     a.mchunks = e->d_mchunks;
     a.srec = e->d_srec;
+    a.pushb = e->d_pushb;
+    a.rev = e->d_rev;
     a.sstate = e->d_sstate;
     a.ibits = e->d_ibits;
     a.n_mchunks = e->n_mchunks;
@@ -1120,13 +1127,28 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     // streamed sync rounds need no in-hubs and two words per lane
     e->sync_tiles = getenv("GG_SYNC_TILES") && atoi(getenv("GG_SYNC_TILES")) != 0;
     dfree(e->d_srec);
+    dfree(e->d_pushb);
+    dfree(e->d_rev);
     dfree(e->d_sstate);
     dfree(e->d_ibits);
     if (e->cfg.enable_sync && e->n_hubs == 0 && e->nwp >= 2 && !e->sync_tiles && n_own) {
         HIPCHK(hipMalloc(&e->d_srec, 2 * n_own * sizeof(uint4)));
         HIPCHK(hipMalloc(&e->d_sstate, e->rows));
         HIPCHK(hipMalloc(&e->d_ibits, e->rows / 8));
+        if (e->n_in_edges) {  // receivers look up whether an owned pusher sent them anything
+            HIPCHK(hipMalloc(&e->d_rev, e->n_in_edges * 4));
+            const unsigned blocks = (unsigned)std::min<uint64_t>((n_own + 255) / 256, 4096);
+            hipLaunchKernelGGL(gg::build_rev, dim3(blocks), dim3(256), 0, e->stream, e->d_in_ptr, e->d_in_col,
+                               e->d_out_ptr, e->d_out_col, e->d_gid, n_own, e->d_rev);
+            HIPCHK(hipGetLastError());
+        }
     }
+    // non-empty pushes per out-edge, written by each sync callback (SyncBroadcast
+    // sends nothing for an empty difference): receivers of empty pushes are not
+    // candidates (GG_SYNC_ALLPUSH=1 keeps every push edge, for A/B)
+    if (e->cfg.enable_sync && e->n_out_edges && !(getenv("GG_SYNC_ALLPUSH") && atoi(getenv("GG_SYNC_ALLPUSH"))))
+        HIPCHK(hipMalloc(&e->d_pushb, e->n_out_edges));
+    if (!e->d_pushb) dfree(e->d_rev);
     const size_t rowbytes = e->rows * e->nwp * 8;
     e->tile_nodes = gg::kBlock / lanes_per_node((uint32_t)e->nwp);
     const uint64_t ntiles = (n_own + e->tile_nodes - 1) / e->tile_nodes;
@@ -1353,6 +1375,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     }
     // device buffers
     e->n_in_edges = icol.size();
+    e->n_out_edges = sym ? icol.size() : ocol.size();
     HIPCHK(hipMalloc(&e->d_in_ptr, (n_own + 1) * 8));
     HIPCHK(hipMalloc(&e->d_in_col, std::max<size_t>(1, icol.size()) * 4));
     HIPCHK(hipMemcpy(e->d_in_ptr, iptr.data(), (n_own + 1) * 8, hipMemcpyHostToDevice));
@@ -1520,6 +1543,7 @@ int gg_topology_generate(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_ou
     e->n_ghost = 0;
     e->ghost0 = e->V;
     e->n_in_edges = g.nnz;
+    e->n_out_edges = g.nnz;
     if (nnz_out) *nnz_out = g.nnz;
     std::vector<int64_t> iptr;
     if (dmax > hub_threshold()) {  // hub chunks are planned on the host

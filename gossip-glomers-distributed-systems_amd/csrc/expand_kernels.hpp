@@ -152,6 +152,11 @@ struct RoundArgs {
     const struct HubChunk* mchunks;  // out-edge chunks of high out-degree senders
     uint64_t n_mchunks;
     uint4* srec;                // [2 n_own] sync records (streamed sync rounds), or nullptr
+    uint8_t* pushb;             // [out-edges] 1: the node's sync callback (round r-1 for a pusher
+                                // of round r) pushed something to that peer (SyncBroadcast
+                                // :104-108 sends nothing for an empty difference); or nullptr
+    const uint32_t* rev;        // [in-edges] the sender's out-edge index of this edge (owned
+                                // senders; streamed sync rounds), or nullptr
     uint8_t* sstate;            // [rows] sender state of round r (round_prep; streamed sync rounds)
     uint64_t* ibits;            // [rows/64] bit: sstate non-zero (a cache-resident filter for it)
     const uint64_t* fired_m1;   // sync-fired bitmaps of rounds r-1, r-2, r-3
@@ -438,10 +443,13 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                     o0 = a.out_ptr[i];
                     o1 = a.out_ptr[i + 1];
                     if (a.hub_deg && o1 - o0 > (int64_t)a.hub_deg) o1 = o0;  // hub_mark does it
-                    c_bytes += 16 + 5 * (unsigned long long)(o1 - o0);
+                    // a pusher that is not active reaches only the peers it pushed to
+                    const bool only_pushed = !(f & FL_ACT) && a.pushb != nullptr;
+                    c_bytes += 16 + (only_pushed ? 6 : 5) * (unsigned long long)(o1 - o0);
                     for (int64_t e = o0; e < o1; ++e) {
                         const uint64_t w = a.out_col[e] & kColMask;
                         if (w >= a.n_own) continue;  // a ghost: its owner marks it
+                        if (only_pushed && !a.pushb[e]) continue;
                         a.cand[w] = CA_NODE;
                         if (!a.stream_ok) a.tile_cand[w / a.tile_nodes] = 1;
                     }
@@ -900,7 +908,10 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                                 const int64_t o0 = a.out_ptr[i], o1 = a.out_ptr[i + 1];
                                 for (int64_t e = o0; e < o1; ++e) {
                                     const uint64_t w = a.out_col[e] & kColMask;
-                                    if (masked<MASKW>(a, 1, rep, w, e) || masked<MASKW>(a, 2, w, rep, e)) continue;
+                                    if (masked<MASKW>(a, 1, rep, w, e) || masked<MASKW>(a, 2, w, rep, e)) {
+                                        if (a.pushb && lg == 0) a.pushb[e] = 0;  // no callback: no push
+                                        continue;
+                                    }
                                     const Row<WPL> R =
                                         sender_row((uint32_t)w, true, (a.flg_prev[w] & FL_LAG) != 0);
                                     nrows++;
@@ -911,6 +922,10 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                                         pn += __popcll(R.w[q2] & ~S.w[q2]);
                                         pp += __popcll(S.w[q2] & ~R.w[q2]);
                                         S.w[q2] |= R.w[q2];
+                                    }
+                                    if (a.pushb) {  // did this peer get any push (next round's receivers)
+                                        const bool nz = ((__ballot(pp != 0) >> gshift) & gmask) != 0;
+                                        if (lg == 0) a.pushb[e] = nz ? 1 : 0;
                                     }
                                     cb_new += pn;
                                     push_sent += pp;
@@ -1594,6 +1609,11 @@ __global__ __launch_bounds__(kBlock) void sync_records(RoundArgs a) {
 #pragma unroll
             for (int b = 0; b < B; ++b) f[b] = f[b] ? a.sstate[cb[b] & kColMask] : (uint8_t)0;
 #pragma unroll
+            for (int b = 0; b < B; ++b) {  // a push from an owned sender that sent nothing is no push
+                if ((f[b] & SE_FM3) && a.rev && (cb[b] & kColMask) < a.n_own && !a.pushb[a.rev[e0 + b]])
+                    f[b] &= (uint8_t)~SE_FM3;
+            }
+#pragma unroll
             for (int b = 0; b < B; ++b) {
                 keep |= (f[b] & SE_FM2) != 0;
                 if (f[b] & (FL_ACT | SE_FM3)) {
@@ -1759,6 +1779,11 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
 #pragma unroll
                 for (int b = 0; b < kCb; ++b) f[b] = e0 + b < p1 ? a.sstate[cb[b] & kColMask] : (uint8_t)0;
 #pragma unroll
+                for (int b = 0; b < kCb; ++b) {  // as sync_records: empty pushes are no pushes
+                    if ((f[b] & SE_FM3) && a.rev && (cb[b] & kColMask) < a.n_own && !a.pushb[a.rev[e0 + b]])
+                        f[b] &= (uint8_t)~SE_FM3;
+                }
+#pragma unroll
                 for (int b = 0; b < kCb; ++b) {
                     const uint64_t u = cb[b] & kColMask;
                     const bool push = f[b] & SE_FM3, con = f[b] & (FL_ACT | SE_FM3), slag = f[b] & FL_LAG;
@@ -1806,6 +1831,10 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
                         pn += __popcll(R[b].w[q] & ~S.w[q]);
                         pp += __popcll(S.w[q] & ~R[b].w[q]);
                         S.w[q] |= R[b].w[q];
+                    }
+                    if (a.pushb) {  // did this peer get any push (next round's receivers)
+                        const bool nz = ((__ballot(pp != 0) >> gshift) & gmask) != 0;
+                        if (lg == 0) a.pushb[o0 + e0 + b] = nz ? 1 : 0;
                     }
                     cb_new += pn;
                     push_sent += pp;
@@ -1868,6 +1897,31 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
     acc[C_NACTDEG] = c_nactdeg;
     acc[C_BYTES] = c_bytes;
     flush_counters(a, acc, s_red, t_start, K_STREAM);
+}
+
+// rev[k] for in-edge k (sender u -> v): the position of v in u's out-list, for
+// owned senders (streamed sync rounds read pushb through it); ~0u for ghosts.
+// Out-lists ascend by node id (gid), so a binary search by id.
+__global__ void build_rev(const int64_t* in_ptr, const uint32_t* in_col, const int64_t* out_ptr,
+                          const uint32_t* out_col, const uint32_t* gid, uint64_t n_own, uint32_t* rev) {
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n_own; v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t gv = gid ? gid[v] : v;
+        for (int64_t k = in_ptr[v]; k < in_ptr[v + 1]; ++k) {
+            const uint32_t u = in_col[k] & kColMask;
+            uint32_t r = ~0u;
+            if (u < n_own) {
+                int64_t lo = out_ptr[u], hi = out_ptr[u + 1];
+                while (lo < hi) {
+                    const int64_t mid = (lo + hi) >> 1;
+                    const uint32_t w = out_col[mid] & kColMask;
+                    if ((gid ? (uint64_t)gid[w] : (uint64_t)w) < gv) lo = mid + 1;
+                    else hi = mid;
+                }
+                r = (uint32_t)lo;
+            }
+            rev[k] = r;
+        }
+    }
 }
 
 // Flags-first rounds: the ACT bits of round r-1 (every local row: owned nodes
