@@ -85,10 +85,11 @@ struct BatchKey {
     int64_t r0 = -1;
     uint32_t m = 0;
     uint64_t inj_hash = 0;
+    uint64_t u_hash = 0;  // lanes_through of rounds r0-1 .. r0+m-1 (sync digest)
     size_t windows = 0;
     const void* inj_buf = nullptr;
     bool operator==(const BatchKey& o) const {
-        return r0 == o.r0 && m == o.m && inj_hash == o.inj_hash && windows == o.windows && inj_buf == o.inj_buf;
+        return r0 == o.r0 && m == o.m && inj_hash == o.inj_hash && u_hash == o.u_hash && windows == o.windows && inj_buf == o.inj_buf;
     }
 };
 
@@ -224,6 +225,12 @@ struct gg_engine {
     uint64_t n_out_edges = 0;
     uint8_t* d_sstate = nullptr;     // [rows] sender states (streamed sync rounds)
     uint64_t* d_ibits = nullptr;     // [rows/64] non-zero sender states
+    uint64_t* d_sat = nullptr;       // [rows/64] saturation digest (streamed sync rounds)
+    uint8_t* d_pushany = nullptr;    // [rows] a streamed callback pushed to some peer
+    uint2* d_nmeta = nullptr;        // [n_own] node list with the nodes' bytes (streamed sync rounds)
+    uint64_t* d_sat_new = nullptr;   // [rows/64] its bits found in the current round
+    std::vector<uint32_t> u_hist;    // u_hist[r]: lanes of this engine injected in rounds <= r
+    std::vector<uint64_t> u_bits;    // those lanes (nw words)
     bool sync_tiles = false;         // GG_SYNC_TILES=1: sync rounds on the tile path (A/B)
     uint64_t* d_hscratch = nullptr;
     uint64_t tile_nodes = 0, tile_bytes = 0;
@@ -301,6 +308,10 @@ void gg_engine::free_topology() {
     dfree(d_rev);
     dfree(d_sstate);
     dfree(d_ibits);
+    dfree(d_sat);
+    dfree(d_sat_new);
+    dfree(d_pushany);
+    dfree(d_nmeta);
     dfree(d_hscratch);
     n_hubs = n_hchunks = n_mchunks = 0;
     dfree(d_work);
@@ -389,6 +400,10 @@ int reset_device_state(gg_engine* e) {
     seg(e->d_tile_cand, e->tile_bytes, 0);
     seg(e->d_act, 16, 0);
     seg(e->d_act_deg, 32, 0);
+    if (e->d_sat) {
+        seg(e->d_sat, e->rows / 8, 0);
+        seg(e->d_sat_new, e->rows / 8, 0);
+    }
     const uint64_t n_own = e->n_own;
     if (e->d_dr) seg(e->d_dr, n_own * e->nw * 64 * 4, ~0ull);
     if (e->d_stamp) seg(e->d_stamp, (e->n_ghost + 1) / 2 * 8, ~0ull);
@@ -572,7 +587,7 @@ void launch_stream_sync_t(const gg::RoundArgs& a, hipStream_t s) {
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gg::expand_stream_sync<G>, gg::kBlock, 0);
         resident = std::max(1, cus) * std::max(1, per_cu);
     }
-    const uint64_t rb = std::min<uint64_t>((a.n_own + gg::kBlock - 1) / gg::kBlock, 16384);
+    const uint64_t rb = std::min<uint64_t>((a.n_own + gg::kBlock - 1) / gg::kBlock, 4096);
     hipLaunchKernelGGL(gg::sync_records, dim3((unsigned)std::max<uint64_t>(1, rb)), dim3(gg::kBlock), 0, s, a);
     const uint64_t ngb = gg::kBlock / G;
     uint64_t blocks = (a.n_own + ngb - 1) / ngb;
@@ -591,6 +606,40 @@ void launch_stream_sync(const gg::RoundArgs& a, hipStream_t s) {
         case 128: launch_stream_sync_t<64>(a, s); break;
         default: break;
     }
+}
+
+// Number of distinct lanes of this engine's word range broadcast in rounds
+// <= r (every engine sees every broadcast: gg_broadcast does not filter by
+// owner), extended round by round while the rounds' lists are still held.
+uint32_t lanes_through(gg_engine* e, int64_t r) {
+    if (r < 0) return 0;
+    if (e->u_bits.size() != e->nw) e->u_bits.assign(e->nw, 0);
+    while ((int64_t)e->u_hist.size() <= r) {
+        const int64_t q = (int64_t)e->u_hist.size();
+        uint32_t u = q ? e->u_hist.back() : 0;
+        auto it = e->inj.find(q);
+        if (it != e->inj.end())
+            for (const auto& x : it->second) {
+                const uint64_t wd = x.lane >> 6;
+                if (wd < e->w0 || wd >= e->w0 + e->nw) continue;
+                uint64_t& word = e->u_bits[wd - e->w0];
+                const uint64_t bit = 1ull << (x.lane & 63);
+                if (!(word & bit)) ++u;
+                word |= bit;
+            }
+        e->u_hist.push_back(u);
+    }
+    return e->u_hist[r];
+}
+
+// Round r runs the streamed sync kernels (sync_records + expand_stream_sync):
+// callbacks and pushes reach the expand, no partition window touches rounds
+// r-3..r+1, and the engine has the sync records.
+bool sync_stream_at(gg_engine* e, int64_t r) {
+    if (!e->cfg.enable_sync || !e->d_srec || r < (int64_t)e->cfg.sync_base_ticks + 2) return false;
+    for (int k = 0; k < 5; ++k)
+        if (window_at(e, r - 3 + k)) return false;
+    return true;
 }
 
 // Enqueue round e->round (kernels only). inj: device pairs for this round.
@@ -638,6 +687,12 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.rev = e->d_rev;
     a.sstate = e->d_sstate;
     a.ibits = e->d_ibits;
+    if (e->d_sat) {
+        a.sat = e->d_sat;
+        a.sat_new = e->d_sat_new;
+        a.usat = lanes_through(e, r);
+        a.sat_reset = (r == 0 || a.usat != lanes_through(e, r - 1)) ? 1u : 0u;
+    }
     a.n_mchunks = e->n_mchunks;
     a.fired_m1 = e->d_fired[(r - 1) & 3];
     a.fired_m2 = e->d_fired[(r - 2) & 3];
@@ -678,6 +733,12 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     // on symmetric graphs without hubs at W >= 128 (expand_stream<.., MASKW>)
     // streamed sync rounds (sync_records + expand_stream_sync): no masks, no in-hubs, nwp >= 2
     const bool sync_stream = syncw && !maskw && e->d_srec != nullptr;
+    a.nmeta = sync_stream ? e->d_nmeta : nullptr;
+    if (e->d_pushany) {  // streamed callbacks mark the receivers of their pushes for the next round
+        a.pushany = e->d_pushany;
+        a.mark_next = (sync_stream && sync_stream_at(e, r + 1)) ? 1u : 0u;
+        a.push_marked = (sync_stream && sync_stream_at(e, r - 1)) ? 1u : 0u;
+    }
     a.stream_ok = ((!syncw && (!maskw || (e->symmetric && e->n_hubs == 0 && e->nwp >= 2))) || sync_stream) ? 1 : 0;
 
     if (a.n_own) {
@@ -686,7 +747,10 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             // dense lean rounds, where it is a no-op (C2 A/B: 1024 blocks 1.99 ms/episode,
             // 4096 2.02, 256 2.10; GG_PREP_BLOCKS overrides)
             static const uint64_t prep_cap = getenv("GG_PREP_BLOCKS") ? (uint64_t)atoi(getenv("GG_PREP_BLOCKS")) : 1024;
-            const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((a.n_own + gg::kBlock - 1) / gg::kBlock, prep_cap));
+            // sync rounds do real work per node: a larger capped grid (each block's
+            // counter flush is a few same-address atomics, so not one block per 256 nodes)
+            const uint64_t blocks = std::max<uint64_t>(
+                1, std::min<uint64_t>((a.n_own + gg::kBlock - 1) / gg::kBlock, syncw_prep ? 4096 : prep_cap));
             dim3 grid((unsigned)blocks), block(gg::kBlock);
             if (syncw_prep) {
                 if (maskw) hipLaunchKernelGGL((gg::round_prep<true, true>), grid, block, 0, e->stream, a);
@@ -709,7 +773,8 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         }
         {
             const uint64_t groups = (a.n_own + 7) / 8;  // >= tile groups
-            hipLaunchKernelGGL(gg::compact_round, dim3((unsigned)((groups + gg::kBlock - 1) / gg::kBlock)),
+            const uint64_t per_block = (uint64_t)gg::kBlock * gg::kCompactQ;
+            hipLaunchKernelGGL(gg::compact_round, dim3((unsigned)((groups + per_block - 1) / per_block)),
                                dim3(gg::kBlock), 0, e->stream, a);
             HIPCHK(hipGetLastError());
         }
@@ -879,6 +944,11 @@ int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& o
     for (size_t t = 0; t < 2 * total; ++t) h = gg_mix64(h ^ e->h_inj[t]);
     for (size_t k = 0; k <= m; ++k) h = gg_mix64(h ^ off[k]);
     key.inj_hash = h;
+    if (e->d_sat) {
+        uint64_t u = gg_mix64(~0ull);
+        for (int64_t q = r0 - 1; q < r0 + (int64_t)m; ++q) u = gg_mix64(u ^ lanes_through(e, q));
+        key.u_hash = u;
+    }
     if (!(e->graph_exec && key == e->graph_key)) {
         if (e->graph_exec) (void)hipGraphExecDestroy(e->graph_exec);
         e->graph_exec = nullptr;
@@ -1131,10 +1201,20 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     dfree(e->d_rev);
     dfree(e->d_sstate);
     dfree(e->d_ibits);
+    dfree(e->d_sat);
+    dfree(e->d_sat_new);
+    dfree(e->d_pushany);
+    dfree(e->d_nmeta);
     if (e->cfg.enable_sync && e->n_hubs == 0 && e->nwp >= 2 && !e->sync_tiles && n_own) {
         HIPCHK(hipMalloc(&e->d_srec, 2 * n_own * sizeof(uint4)));
         HIPCHK(hipMalloc(&e->d_sstate, e->rows));
         HIPCHK(hipMalloc(&e->d_ibits, e->rows / 8));
+        HIPCHK(hipMalloc(&e->d_nmeta, n_own * sizeof(uint2)));
+        // saturation digest (GG_SYNC_DIGEST=0 turns it off, for A/B)
+        if (!(getenv("GG_SYNC_DIGEST") && atoi(getenv("GG_SYNC_DIGEST")) == 0)) {
+            HIPCHK(hipMalloc(&e->d_sat, e->rows / 8));
+            HIPCHK(hipMalloc(&e->d_sat_new, e->rows / 8));
+        }
         if (e->n_in_edges) {  // receivers look up whether an owned pusher sent them anything
             HIPCHK(hipMalloc(&e->d_rev, e->n_in_edges * 4));
             const unsigned blocks = (unsigned)std::min<uint64_t>((n_own + 255) / 256, 4096);
@@ -1149,6 +1229,7 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     if (e->cfg.enable_sync && e->n_out_edges && !(getenv("GG_SYNC_ALLPUSH") && atoi(getenv("GG_SYNC_ALLPUSH"))))
         HIPCHK(hipMalloc(&e->d_pushb, e->n_out_edges));
     if (!e->d_pushb) dfree(e->d_rev);
+    if (e->d_pushb && e->d_srec) HIPCHK(hipMalloc(&e->d_pushany, e->rows));
     const size_t rowbytes = e->rows * e->nwp * 8;
     e->tile_nodes = gg::kBlock / lanes_per_node((uint32_t)e->nwp);
     const uint64_t ntiles = (n_own + e->tile_nodes - 1) / e->tile_nodes;
@@ -1189,6 +1270,8 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     e->pend_acks = e->pend_ackdrop = 0;
     e->hash_total = 0;
     e->dist_open = false;
+    e->u_hist.clear();
+    e->u_bits.clear();
     return reset_device_state(e);
 }
 
@@ -2300,6 +2383,8 @@ int gg_reset(gg_engine* e) {
     e->pend_acks = e->pend_ackdrop = 0;
     e->hash_total = 0;
     e->dist_open = false;
+    e->u_hist.clear();
+    e->u_bits.clear();
     if (!e->have_topo) return GG_OK;
     HIPCHK(hipSetDevice(e->device));
     return reset_device_state(e);

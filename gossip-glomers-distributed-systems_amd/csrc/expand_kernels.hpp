@@ -158,7 +158,22 @@ struct RoundArgs {
     const uint32_t* rev;        // [in-edges] the sender's out-edge index of this edge (owned
                                 // senders; streamed sync rounds), or nullptr
     uint8_t* sstate;            // [rows] sender state of round r (round_prep; streamed sync rounds)
-    uint64_t* ibits;            // [rows/64] bit: sstate non-zero (a cache-resident filter for it)
+    uint64_t* ibits;            // [rows/64] bit: sstate has FL_ACT, FL_LAG or SE_FM3 (a
+                                // cache-resident filter in front of it; callbacks: fired_m2)
+    uint8_t* pushany;           // [rows] the node's sync callback (streamed) pushed to some peer
+    uint32_t push_marked;       // the streamed callbacks of r-1 marked their push receivers and
+                                // wrote pushany: round_prep skips the pushers' out-lists
+    uint32_t mark_next;         // this round's callbacks mark their push receivers for r+1
+    uint2* nmeta;               // streamed sync rounds: compact_round's node list as (node,
+                                // cand | flg_cur << 8 | sstate << 16), cand cleared; or nullptr
+    uint64_t* sat;              // [rows/64] saturation digest (streamed sync rounds, else nullptr):
+                                // bit = the row's seen set was, after some round r' < r, every
+                                // lane injected so far (|S| == usat) — exact: sets only grow
+                                // and hold injected lanes only, so it stays true until a new
+                                // lane is injected (sat_reset). Owned rows; ghosts stay 0.
+    uint64_t* sat_new;          // [rows/64] bits found this round (merged by the next round_prep)
+    uint32_t usat;              // lanes of this engine's range injected in rounds <= r
+    uint32_t sat_reset;         // usat grew this round: every digest bit is void
     const uint64_t* fired_m1;   // sync-fired bitmaps of rounds r-1, r-2, r-3
     const uint64_t* fired_m2;
     const uint64_t* fired_m3;
@@ -319,6 +334,19 @@ __device__ __forceinline__ bool is_push(const RoundArgs& a, uint8_t ef, uint64_t
     }
 }
 
+// Saturation digest: the G lanes of a node group that changed its set this
+// round count it; a full set (every lane injected so far) sets the node's bit
+// for the next rounds. Group-uniform call (shuffles stay inside the group).
+template <int G, int WPL>
+__device__ __forceinline__ void sat_mark(const RoundArgs& a, const Row<WPL>& S, uint64_t rep, int lg) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int w = 0; w < WPL; ++w) c += (uint32_t)__popcll(S.w[w]);
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (lg == 0 && c == a.usat) atomicOr(a.sat_new + (rep >> 6), 1ull << (rep & 63));
+}
+
 // Block reduction of C_NUM per-thread counters -> one atomic per counter per
 // block into slot blockIdx % 64.
 // Wait until every vector-memory op of this wave (loads, stores, LDS-DMA) is
@@ -391,6 +419,14 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
         if (a.act_deg) a.act_deg[(a.round + 1) & 3] = 0;
         a.n_work[0] = a.n_work[1] = 0;  // compact_round runs after this kernel
     }
+    if (a.sat) {  // last round's digest bits in (readers of this round see rounds < r only)
+        const uint64_t nw = (a.n_own + 63) / 64;
+        for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < nw; t += (uint64_t)gridDim.x * kBlock) {
+            const uint64_t w = (a.own0 >> 6) + t;
+            a.sat[w] = a.sat_reset ? 0ull : (a.sat[w] | a.sat_new[w]);
+            a.sat_new[w] = 0;
+        }
+    }
     if (!SYNCW && dense) {
         noop_exit(a, K_PREP, t_start);
         return;
@@ -398,7 +434,31 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
     unsigned long long c_reads = 0, c_read_oks = 0, c_dropped = 0, c_fired = 0, c_bytes = 0;
     const uint64_t nwords = (a.n_own + 63) / 64;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    // the per-node bytes of the next node are loaded before this node's stores:
+    // two nodes' worth of loads in flight per thread (the grid is capped)
+    struct PrepIn {
+        uint64_t w1, w2, w3;  // fired words of r-1, r-2, r-3
+        int32_t sn;           // sync_next
+        uint8_t f, fc, pa;    // flg_prev, flg_cur, pushany
+    };
+    auto load_in = [&](uint64_t i, PrepIn& p) {
+        p = PrepIn{};
+        if (i >= a.n_own) return;
+        const uint64_t rp = a.own0 + i;
+        p.f = a.flg_prev[rp];
+        if (!dense) p.fc = a.flg_cur[rp];
+        if constexpr (SYNCW) {
+            p.w1 = a.fired_m1[rp >> 6];
+            p.w2 = a.fired_m2[rp >> 6];
+            p.w3 = a.fired_m3[rp >> 6];
+            p.sn = a.sync_next[i];
+            if (a.push_marked) p.pa = a.pushany[rp];
+        }
+    };
+    PrepIn cur, nxt;
+    load_in((uint64_t)blockIdx.x * kBlock + threadIdx.x, cur);
     for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < nwords * 64; t += stride) {
+        load_in(t + stride, nxt);
         const uint64_t i = t;
         const bool valid = i < a.n_own;
         const uint64_t rep = a.own0 + i;
@@ -408,26 +468,24 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
             int64_t o0 = 0, o1 = 0;
             bool fm1 = false, fm2 = false, fm3 = false;
             if constexpr (SYNCW) {
-                fm1 = bit_at(a.fired_m1, rep);
-                fm2 = bit_at(a.fired_m2, rep);
-                fm3 = bit_at(a.fired_m3, rep);
-                if (a.sstate) {  // sender state for sync_records / expand_stream_sync
-                    st = (uint8_t)((a.flg_prev[rep] & (FL_ACT | FL_LAG)) | (fm2 ? SE_FM2 : 0) | (fm3 ? SE_FM3 : 0));
-                    a.sstate[rep] = st;
-                }
+                fm1 = (cur.w1 >> (rep & 63)) & 1;
+                fm2 = (cur.w2 >> (rep & 63)) & 1;
+                fm3 = (cur.w3 >> (rep & 63)) & 1;
+                if (a.sstate)  // sender state for sync_records / expand_stream_sync (stored below)
+                    st = (uint8_t)((cur.f & (FL_ACT | FL_LAG)) | (fm2 ? SE_FM2 : 0) | (fm3 ? SE_FM3 : 0));
             }
             if (!dense) {
-                const uint8_t f = a.flg_prev[rep];
+                const uint8_t f = cur.f;
                 // flg_cur still holds round r-2's flags: an F row written then is
                 // stale in this round's F buffer; the expand kernel zeroes it unless
                 // the node writes a new one, so F rows stay zero for inactive nodes.
                 if (a.stream_ok) {
                     // sparse lean round: expand_stream takes the node (it reads and
                     // rewrites the old flag byte itself); no tile flags (node list)
-                    if (a.flg_cur[rep] & FL_ACT) a.cand[rep] = CA_NODE;
+                    if (cur.fc & FL_ACT) a.cand[rep] = CA_NODE;
                     c_bytes += 2;
                 } else {
-                    if (a.flg_cur[rep] & FL_ACT) {
+                    if (cur.fc & FL_ACT) {
                         a.zmark[rep] = 1;
                         a.tile_cand[i / a.tile_nodes] = 1;
                     }
@@ -439,24 +497,44 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                     a.cand[rep] = CA_NODE;
                     if (!a.stream_ok) a.tile_cand[i / a.tile_nodes] = 1;
                 }
-                if ((f & FL_ACT) || fm3) {  // senders mark their (owned) receivers
+                if (!(f & FL_ACT) && fm3 && a.push_marked) {
+                    // the streamed callback of r-1 marked its push receivers itself
+                    if (!cur.pa) st &= (uint8_t)~SE_FM3;
+                    c_bytes += 1;
+                } else if ((f & FL_ACT) || fm3) {  // senders mark their (owned) receivers
                     o0 = a.out_ptr[i];
                     o1 = a.out_ptr[i + 1];
-                    if (a.hub_deg && o1 - o0 > (int64_t)a.hub_deg) o1 = o0;  // hub_mark does it
+                    const bool hub = a.hub_deg && o1 - o0 > (int64_t)a.hub_deg;
+                    if (hub) o1 = o0;  // hub_mark does it
                     // a pusher that is not active reaches only the peers it pushed to
                     const bool only_pushed = !(f & FL_ACT) && a.pushb != nullptr;
                     c_bytes += 16 + (only_pushed ? 6 : 5) * (unsigned long long)(o1 - o0);
-                    for (int64_t e = o0; e < o1; ++e) {
-                        const uint64_t w = a.out_col[e] & kColMask;
-                        if (w >= a.n_own) continue;  // a ghost: its owner marks it
-                        if (only_pushed && !a.pushb[e]) continue;
-                        a.cand[w] = CA_NODE;
-                        if (!a.stream_ok) a.tile_cand[w / a.tile_nodes] = 1;
+                    bool pushed = false;
+                    constexpr int B = 8;  // a batch of columns and push bytes in flight together
+                    for (int64_t e0 = o0; e0 < o1; e0 += B) {
+                        uint64_t w[B];
+                        uint8_t pb[B];
+#pragma unroll
+                        for (int b = 0; b < B; ++b) w[b] = e0 + b < o1 ? (uint64_t)(a.out_col[e0 + b] & kColMask) : ~0ull;
+#pragma unroll
+                        for (int b = 0; b < B; ++b) pb[b] = (only_pushed && e0 + b < o1) ? a.pushb[e0 + b] : (uint8_t)1;
+#pragma unroll
+                        for (int b = 0; b < B; ++b) {
+                            if (e0 + b >= o1 || !pb[b]) continue;
+                            pushed = true;
+                            if (w[b] >= a.n_own) continue;  // a ghost: its owner marks it
+                            a.cand[w[b]] = CA_NODE;
+                            if (!a.stream_ok) a.tile_cand[w[b] / a.tile_nodes] = 1;
+                        }
                     }
+                    // a push that reached no peer with anything is no push: its
+                    // receivers skip it, and nobody reads this node's set for it
+                    if (only_pushed && !pushed && !hub) st &= (uint8_t)~SE_FM3;
                 }
             }
             if constexpr (SYNCW) {
-                if (fm1 || (int64_t)a.sync_next[i] == a.round) {
+                if (a.sstate) a.sstate[rep] = st;
+                if (fm1 || (int64_t)cur.sn == a.round) {
                     o0 = a.out_ptr[i];
                     o1 = a.out_ptr[i + 1];
                 }
@@ -471,7 +549,7 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                 }
                 // (5) the sync timer (main.go:42-51): read RPC to every neighbour (:119-121)
                 c_bytes += 4;
-                if ((int64_t)a.sync_next[i] == a.round) {
+                if ((int64_t)cur.sn == a.round) {
                     fire = true;
                     c_fired++;
                     c_reads += (unsigned long long)(o1 - o0);
@@ -490,10 +568,11 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
             const unsigned long long word = __ballot(fire);
             if ((threadIdx.x & 63) == 0) a.fired_cur[(a.own0 + (i & ~63ull)) >> 6] = word;
             if (a.ibits) {
-                const unsigned long long iw = __ballot(st != 0);
+                const unsigned long long iw = __ballot((st & (FL_ACT | FL_LAG | SE_FM3)) != 0);
                 if ((threadIdx.x & 63) == 0) a.ibits[(a.own0 + (i & ~63ull)) >> 6] = iw;
             }
         }
+        cur = nxt;
     }
     if constexpr (SYNCW) {
         // ghost rows (sharded; whole waves over 64 consecutive ghost rows, ghost0 %
@@ -522,7 +601,7 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
             const unsigned long long fw = __ballot(fire);
             if ((threadIdx.x & 63) == 0) a.fired_cur[row >> 6] = fw;
             if (a.sstate) {
-                const unsigned long long iw = __ballot(st != 0);
+                const unsigned long long iw = __ballot((st & (FL_ACT | FL_LAG | SE_FM3)) != 0);
                 if ((threadIdx.x & 63) == 0) a.ibits[row >> 6] = iw;
             }
         }
@@ -564,10 +643,13 @@ __global__ void mark_injections(RoundArgs a) {
 }
 
 // Sparse rounds: the candidate nodes -> node list (lean rounds, expand_stream;
-// node-granular, so every node group gets the same share; one thread per 8
-// candidate bytes, a coalesced pass over them), or the live tiles -> work list
-// (expand_round; 8 tile flags per thread, cleared for the next round). Order is
+// node-granular, so every node group gets the same share; kCompactQ groups of 8
+// candidate bytes per thread, a coalesced pass over them), or the live tiles ->
+// work list (expand_round; 8 tile flags per group, cleared for the next round).
+// One atomic per block reserves the block's slots: same-address atomics are
+// serialised in L2, so blocks cover 8 KB of candidate bytes each. Order is
 // irrelevant: nodes/tiles are independent within a round and the counters are sums.
+constexpr int kCompactQ = 4;
 __global__ __launch_bounds__(kBlock) void compact_round(RoundArgs a) {
     __shared__ uint32_t s_cnt[kBlock / 64];
     __shared__ uint32_t s_base;
@@ -579,23 +661,37 @@ __global__ __launch_bounds__(kBlock) void compact_round(RoundArgs a) {
     const bool nodes = a.stream_ok != 0;
     const uint64_t NG = a.tile_nodes;
     const uint64_t ntiles = (a.n_own + NG - 1) / NG;
-    const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;  // 8-byte group
-    unsigned long long x = 0;  // 8 candidate bytes (nodes) or 8 tile flags (tiles)
+    const uint64_t q0 = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * kCompactQ;  // first 8-byte group
+    unsigned long long x[kCompactQ];  // 8 candidate bytes (nodes) or 8 tile flags (tiles) per group
     uint32_t c = 0;
-    if (nodes) {
-        const uint64_t n = q * 8;
-        if (n + 8 <= a.n_own) {  // own0 is a multiple of 64: aligned
-            x = *reinterpret_cast<const unsigned long long*>(a.cand + a.own0 + n);
-        } else {
-            for (uint64_t k = n; k < a.n_own; ++k) x |= (unsigned long long)a.cand[a.own0 + k] << (8 * (k - n));
+#pragma unroll
+    for (int j = 0; j < kCompactQ; ++j) {
+        const uint64_t q = q0 + j;
+        x[j] = 0;
+        if (nodes) {
+            const uint64_t n = q * 8;
+            if (n + 8 <= a.n_own) {  // own0 is a multiple of 64: aligned
+                x[j] = *reinterpret_cast<const unsigned long long*>(a.cand + a.own0 + n);
+            } else {
+                for (uint64_t k = n; k < a.n_own; ++k) x[j] |= (unsigned long long)a.cand[a.own0 + k] << (8 * (k - n));
+            }
+        } else if (q * 8 < ntiles) {
+            x[j] = *reinterpret_cast<const unsigned long long*>(a.tile_cand + q * 8);
         }
-    } else if (q * 8 < ntiles) {
-        x = *reinterpret_cast<const unsigned long long*>(a.tile_cand + q * 8);
-        if (x) *reinterpret_cast<unsigned long long*>(a.tile_cand + q * 8) = 0ull;
     }
-    {
+#pragma unroll
+    for (int j = 0; j < kCompactQ; ++j) {
+        const uint64_t q = q0 + j;
+        if (!x[j]) continue;
+        if (!nodes) {
+            *reinterpret_cast<unsigned long long*>(a.tile_cand + q * 8) = 0ull;
+        } else if (a.nmeta) {  // streamed sync rounds: sync_records does not touch the bytes
+            if (q * 8 + 8 <= a.n_own) *reinterpret_cast<unsigned long long*>(a.cand + a.own0 + q * 8) = 0ull;
+            else
+                for (uint64_t k = q * 8; k < a.n_own; ++k) a.cand[a.own0 + k] = 0;
+        }
         const unsigned long long lo7 = 0x7f7f7f7f7f7f7f7full;
-        c = (uint32_t)__popcll((((x & lo7) + lo7) | x) & ~lo7);  // non-zero bytes
+        c += (uint32_t)__popcll((((x[j] & lo7) + lo7) | x[j]) & ~lo7);  // non-zero bytes
     }
     // block exclusive scan of c
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -618,19 +714,29 @@ __global__ __launch_bounds__(kBlock) void compact_round(RoundArgs a) {
     }
     __syncthreads();
     uint32_t pos = s_base + s_cnt[wave] + incl - c;
-    for (int t = 0; t < 8; ++t) {
-        if (!((x >> (8 * t)) & 0xff)) continue;
-        if (nodes) {
-            a.nodes[pos++] = (uint32_t)(q * 8 + t);
-        } else {
-            const uint64_t tile = q * 8 + t;
-            const uint64_t n0 = tile * NG;
-            const uint64_t n1 = n0 + NG < a.n_own ? n0 + NG : a.n_own;
-            TileWork w;
-            w.tile = (uint32_t)tile;
-            w.eb = a.in_ptr[n0];
-            w.ne = (uint32_t)(a.in_ptr[n1] - w.eb);
-            a.work[pos++] = w;
+    for (int j = 0; j < kCompactQ; ++j) {
+        const uint64_t q = q0 + j;
+        for (int t = 0; t < 8; ++t) {
+            const uint32_t byte = (uint32_t)((x[j] >> (8 * t)) & 0xff);
+            if (!byte) continue;
+            if (nodes) {
+                const uint32_t node = (uint32_t)(q * 8 + t);
+                if (a.nmeta) {
+                    const uint64_t rep = a.own0 + node;
+                    a.nmeta[pos] = make_uint2(node, byte | ((uint32_t)a.flg_cur[rep] << 8) |
+                                                        ((uint32_t)a.sstate[rep] << 16));
+                }
+                a.nodes[pos++] = node;
+            } else {
+                const uint64_t tile = q * 8 + t;
+                const uint64_t n0 = tile * NG;
+                const uint64_t n1 = n0 + NG < a.n_own ? n0 + NG : a.n_own;
+                TileWork w;
+                w.tile = (uint32_t)tile;
+                w.eb = a.in_ptr[n0];
+                w.ne = (uint32_t)(a.in_ptr[n1] - w.eb);
+                a.work[pos++] = w;
+            }
         }
     }
     if (threadIdx.x == 0) stamp(a, K_PREP, t_start);
@@ -1325,6 +1431,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         const bool zm = (m0.fl & FL_ACT) != 0;  // F row of round r-2 in this buffer
         if (any || zm) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
         if (any) store_row<WPL>(a.base + rep * a.nwp + off, S);
+        if (any && a.sat_new) sat_mark<G, WPL>(a, S, rep, lg);
         if (lg == 0) {
             if (any || m0.fl) a.flg_cur[rep] = any ? FL_ACT : 0;
             if (m0.ca) a.cand[rep] = 0;
@@ -1572,6 +1679,9 @@ void expand_stream1(RoundArgs a) {
 constexpr uint32_t SR_DEG = 0x000fffffu;       // forward recipients (out-degree)
 constexpr int SR_NC = 20;                      // bits 20-21: recorded contributing senders
 constexpr uint32_t SR_SLOW = 1u << 22;         // more than 3 of them (or a huge degree): walk the in-list
+constexpr uint32_t SR_QUIET = 1u << 23;        // saturated, nothing arrives, every callback peer saturated:
+                                               // the set cannot change and no push has content
+constexpr uint32_t SR_SATV = 1u << 24;         // the node's set is saturated (sat digest)
 constexpr uint32_t SR_KEEP = 1u << 26;         // the node's set is read this round: base stays
 constexpr uint32_t SR_CB = 1u << 27;           // sync callback (fired in r-2)
 constexpr uint32_t SR_LAG = 1u << 28;          // base lacks F_prev
@@ -1585,74 +1695,131 @@ __global__ __launch_bounds__(kBlock) void sync_records(RoundArgs a) {
     const unsigned long long t_start = clock100();
     const bool dense = dense_round(a);
     const uint32_t n_items = dense ? (uint32_t)a.n_own : a.n_work[1];
+    // symmetric topology: the out-list is the in-list (same array), so a
+    // callback's peer checks ride on the in-list walk
+    const bool sym = a.out_col == a.in_col && a.out_ptr == a.in_ptr;
     unsigned long long c_bytes = 0;
     constexpr int B = 8;
     for (uint32_t k = blockIdx.x * kBlock + threadIdx.x; k < n_items; k += gridDim.x * kBlock) {
-        const uint32_t i = dense ? k : a.nodes[k];
-        const uint64_t rep = a.own0 + i;
-        const uint8_t ca = a.cand[rep];
-        const uint8_t fo = a.flg_cur[rep];
-        const uint8_t st = a.sstate[rep];
-        const int64_t p0 = a.in_ptr[i], p1 = a.in_ptr[i + 1];
-        const int64_t o0 = a.out_ptr[i], o1 = a.out_ptr[i + 1];
-        const uint64_t dout = (uint64_t)(o1 - o0);
-        if (ca) a.cand[rep] = 0;
-        bool keep = (st & SE_FM3) != 0;
-        uint32_t nc = 0, sbits = 0, col0 = 0, col1 = 0, col2 = 0;
-        for (int64_t e0 = p0; e0 < p1; e0 += B) {
-            uint32_t cb[B];
-            uint8_t f[B];
-#pragma unroll
-            for (int b = 0; b < B; ++b) cb[b] = e0 + b < p1 ? a.in_col[e0 + b] : 0u;
-#pragma unroll
-            for (int b = 0; b < B; ++b) f[b] = e0 + b < p1 ? (uint8_t)bit_at(a.ibits, cb[b] & kColMask) : (uint8_t)0;
-#pragma unroll
-            for (int b = 0; b < B; ++b) f[b] = f[b] ? a.sstate[cb[b] & kColMask] : (uint8_t)0;
-#pragma unroll
-            for (int b = 0; b < B; ++b) {  // a push from an owned sender that sent nothing is no push
-                if ((f[b] & SE_FM3) && a.rev && (cb[b] & kColMask) < a.n_own && !a.pushb[a.rev[e0 + b]])
-                    f[b] &= (uint8_t)~SE_FM3;
-            }
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                keep |= (f[b] & SE_FM2) != 0;
-                if (f[b] & (FL_ACT | SE_FM3)) {
-                    if (nc == 0) col0 = cb[b];
-                    else if (nc == 1) col1 = cb[b];
-                    else if (nc == 2) col2 = cb[b];
-                    if (nc < 3)
-                        sbits |= ((f[b] & SE_FM3) ? 1u << nc : 0u) | ((f[b] & FL_LAG) ? 8u << nc : 0u);
-                    ++nc;
-                }
-            }
+        uint32_t i;
+        uint8_t ca, fo, st;
+        if (dense) {
+            i = k;
+            ca = a.cand[a.own0 + i];
+            fo = a.flg_cur[a.own0 + i];
+            st = a.sstate[a.own0 + i];
+            if (ca) a.cand[a.own0 + i] = 0;
+        } else {  // compact_round packed the node's bytes and cleared its candidate byte
+            const uint2 m = a.nmeta[k];
+            i = m.x;
+            ca = (uint8_t)m.y;
+            fo = (uint8_t)(m.y >> 8);
+            st = (uint8_t)(m.y >> 16);
         }
-        uint32_t lagm = 0;
-        if (st & SE_FM2) {  // callback: which peers' base rows lag their F rows
-            const int64_t oe = o1 < o0 + 32 ? o1 : o0 + 32;
-            for (int64_t e0 = o0; e0 < oe; e0 += B) {
+        const uint64_t rep = a.own0 + i;
+        const int64_t p0 = a.in_ptr[i], p1 = a.in_ptr[i + 1];
+        const int64_t o0 = sym ? p0 : a.out_ptr[i], o1 = sym ? p1 : a.out_ptr[i + 1];
+        const uint64_t dout = (uint64_t)(o1 - o0);
+        const bool cbk = (st & SE_FM2) != 0;
+        const bool satv = a.sat && bit_at(a.sat, rep);
+        bool keep = (st & SE_FM3) != 0;
+        uint32_t nc = 0, sbits = 0, col0 = 0, col1 = 0, col2 = 0, lagm = 0;
+        bool quiet = false;
+        if (satv) {
+            // saturated: S is every lane injected so far and nothing that arrives
+            // (senders' sets are subsets of it) can change it, so senders are not
+            // looked up and keep does not matter (the base write is S either way).
+            // A callback still answers each peer: peers saturated too need nothing,
+            // the others are gathered for the push difference (and their LAG bit).
+            keep = false;
+            quiet = !(st & FL_LAG) && !(fo & FL_ACT) && !(ca & CA_INJ);
+            if (cbk) {
+                bool allsat = true;
+                for (int64_t e0 = o0; e0 < o1; e0 += B) {
+                    uint32_t w[B];
+                    bool sb[B];
+#pragma unroll
+                    for (int b = 0; b < B; ++b) w[b] = e0 + b < o1 ? (a.out_col[e0 + b] & kColMask) : 0u;
+#pragma unroll
+                    for (int b = 0; b < B; ++b) sb[b] = e0 + b >= o1 || bit_at(a.sat, w[b]);
+#pragma unroll
+                    for (int b = 0; b < B; ++b) {
+                        allsat &= sb[b];
+                        const int64_t pos = e0 - o0 + b;
+                        if (!sb[b] && pos < 32 && bit_at(a.ibits, w[b]) && (a.sstate[w[b]] & FL_LAG)) lagm |= 1u << pos;
+                    }
+                }
+                quiet = quiet && allsat;
+                c_bytes += 4ull * dout;
+            }
+        } else {
+            for (int64_t e0 = p0; e0 < p1; e0 += B) {
+                uint32_t cb[B];
                 uint8_t f[B];
 #pragma unroll
-                for (int b = 0; b < B; ++b) {
-                    const uint64_t w = e0 + b < oe ? (uint64_t)(a.out_col[e0 + b] & kColMask) : 0ull;
-                    f[b] = (e0 + b < oe && bit_at(a.ibits, w)) ? a.sstate[w] : (uint8_t)0;
+                for (int b = 0; b < B; ++b) cb[b] = e0 + b < p1 ? a.in_col[e0 + b] : 0u;
+                // in-neighbour u is a callback of this round (fired in r-2): it reads this set
+#pragma unroll
+                for (int b = 0; b < B; ++b) keep |= e0 + b < p1 && bit_at(a.fired_m2, cb[b] & kColMask);
+                // ibits: ACT, LAG or pushing senders only (sparse once sync rounds settle)
+#pragma unroll
+                for (int b = 0; b < B; ++b) f[b] = e0 + b < p1 ? (uint8_t)bit_at(a.ibits, cb[b] & kColMask) : (uint8_t)0;
+#pragma unroll
+                for (int b = 0; b < B; ++b) f[b] = f[b] ? a.sstate[cb[b] & kColMask] : (uint8_t)0;
+#pragma unroll
+                for (int b = 0; b < B; ++b) {  // a push from an owned sender that sent nothing is no push
+                    if ((f[b] & SE_FM3) && a.rev && (cb[b] & kColMask) < a.n_own && !a.pushb[a.rev[e0 + b]])
+                        f[b] &= (uint8_t)~SE_FM3;
+                }
+                if (sym && cbk) {  // the out-list is this list: the peers' LAG bits
+#pragma unroll
+                    for (int b = 0; b < B; ++b) {
+                        const int64_t pos = e0 - p0 + b;
+                        if (e0 + b < p1 && pos < 32 && (f[b] & FL_LAG)) lagm |= 1u << pos;
+                    }
                 }
 #pragma unroll
-                for (int b = 0; b < B; ++b) lagm |= (f[b] & FL_LAG) ? 1u << (e0 - o0 + b) : 0u;
+                for (int b = 0; b < B; ++b) {
+                    if (f[b] & (FL_ACT | SE_FM3)) {
+                        if (nc == 0) col0 = cb[b];
+                        else if (nc == 1) col1 = cb[b];
+                        else if (nc == 2) col2 = cb[b];
+                        if (nc < 3)
+                            sbits |= ((f[b] & SE_FM3) ? 1u << nc : 0u) | ((f[b] & FL_LAG) ? 8u << nc : 0u);
+                        ++nc;
+                    }
+                }
             }
-            c_bytes += 5ull * (uint64_t)(oe - o0);
+            c_bytes += 5ull * (uint64_t)(p1 - p0);
+            if (cbk && !sym) {  // which peers' base rows lag their F rows
+                const int64_t oe = o1 < o0 + 32 ? o1 : o0 + 32;
+                for (int64_t e0 = o0; e0 < oe; e0 += B) {
+                    uint8_t f[B];
+#pragma unroll
+                    for (int b = 0; b < B; ++b) {
+                        const uint64_t w = e0 + b < oe ? (uint64_t)(a.out_col[e0 + b] & kColMask) : 0ull;
+                        f[b] = (e0 + b < oe && bit_at(a.ibits, w)) ? a.sstate[w] : (uint8_t)0;
+                    }
+#pragma unroll
+                    for (int b = 0; b < B; ++b) lagm |= (f[b] & FL_LAG) ? 1u << (e0 - o0 + b) : 0u;
+                }
+                c_bytes += 5ull * (uint64_t)(oe - o0);
+            }
         }
         uint32_t x = (uint32_t)(dout < SR_DEG ? dout : SR_DEG);
         if (nc > 3 || dout >= SR_DEG) x |= SR_SLOW;
         else x |= nc << SR_NC;
         if (keep) x |= SR_KEEP;
-        if (st & SE_FM2) x |= SR_CB;
+        if (quiet) x |= SR_QUIET;
+        if (satv) x |= SR_SATV;
+        if (cbk) x |= SR_CB;
         if (st & FL_LAG) x |= SR_LAG;
         if (fo & FL_ACT) x |= SR_STALE;
         if (ca & CA_INJ) x |= SR_INJ;
         a.srec[2 * (uint64_t)i] = make_uint4(x, col0, col1, col2);
         a.srec[2 * (uint64_t)i + 1] = make_uint4((uint32_t)o0, (uint32_t)((uint64_t)o0 >> 32), lagm, sbits);
-        // row_ptr, out_ptr, own bytes, per in-edge: column + sender state; the record
-        c_bytes += 32 + 3 + (ca ? 1 : 0) + 5ull * (uint64_t)(p1 - p0) + 32;
+        // row_ptr (+ out_ptr), the node's bytes, the record
+        c_bytes += (sym ? 16 : 32) + (dense ? 3 + (ca ? 1 : 0) : 8) + 32;
     }
     unsigned long long acc[C_NUM];
 #pragma unroll
@@ -1700,6 +1867,7 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
         const uint64_t rep = a.own0 + i;
         const uint32_t x = r0.x;
         const bool lag = (x & SR_LAG) != 0, slow = (x & SR_SLOW) != 0, cbk = (x & SR_CB) != 0;
+        const bool quiet = (x & SR_QUIET) != 0, satv = (x & SR_SATV) != 0;
         const uint32_t nc = slow ? 0u : (x >> SR_NC) & 3u;
         const uint32_t sb = q0.w;
         const int64_t o0 = (int64_t)(((uint64_t)q0.y << 32) | q0.x);
@@ -1708,7 +1876,7 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
         // own row (+ its F row when base lags), the recorded senders' rows (F,
         // or base for pushes, + F when that base lags), the first callback
         // peers' columns: one round trip
-        Row<WPL> sp = row_at(a.base, rep);
+        Row<WPL> sp = quiet ? zero() : row_at(a.base, rep);
         const Row<WPL> of = lag ? row_at(a.F_prev, rep) : zero();
         const uint32_t cs[3] = {r0.y, r0.z, r0.w};
         Row<WPL> fr[3], br[3];
@@ -1722,13 +1890,28 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
         uint64_t pw[kCb];
 #pragma unroll
         for (int b = 0; b < kCb; ++b)
-            pw[b] = (cbk && (uint64_t)b < dout) ? (uint64_t)(a.out_col[o0 + b] & kColMask) : 0ull;
+            pw[b] = (cbk && !quiet && (uint64_t)b < dout) ? (uint64_t)(a.out_col[o0 + b] & kColMask) : 0ull;
         // next item's record, the item after's list entry
         const uint32_t n2 = node_of(k + 2 * stride);
         uint4 r1 = make_uint4(0, 0, 0, 0), q1 = r1;
         if (n1 < a.n_own) {
             r1 = a.srec[2 * (uint64_t)n1];
             q1 = a.srec[2 * (uint64_t)n1 + 1];
+        }
+        if (quiet) {  // nothing arrives, every read_ok equals the node's set: no change, no push
+            if (cbk && a.pushb && lg == 0) {
+                for (uint64_t e = 0; e < dout; ++e) a.pushb[o0 + e] = 0;
+                if (a.pushany) a.pushany[rep] = 0;
+            }
+            if (lg == 0) {
+                c_active += 1;
+                c_bytes += 32 + (cbk ? dout : 0);
+            }
+            n0 = n1;
+            n1 = n2;
+            r0 = r1;
+            q0 = q1;
+            continue;
         }
 
         sp.w[0] |= of.w[0];
@@ -1801,30 +1984,36 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
         }
         // (3) sync callback: v fired in r-2; read_oks of its peers, ascending peer
         unsigned long long cb_new = 0, push_sent = 0;
+        bool pushed = false;
         if (cbk) {
             const uint32_t lagm = q0.z;
             nextra += 16 + 4 * dout;
             for (uint64_t e0 = 0; e0 < dout; e0 += kCb) {
                 Row<WPL> R[kCb];
+                bool same[kCb];  // both sets saturated: the read_ok equals S, no row needed
 #pragma unroll
                 for (int b = 0; b < kCb; ++b) {
                     const uint64_t e = e0 + b;
+                    same[b] = satv && e < dout && bit_at(a.sat, pw[b]);
                     const bool slag = e >= 32 || ((lagm >> e) & 1u);
-                    R[b] = e < dout ? row_at(a.base, pw[b]) : zero();
-                    const Row<WPL> f = (e < dout && slag) ? row_at(a.F_prev, pw[b]) : zero();
+                    R[b] = (e < dout && !same[b]) ? row_at(a.base, pw[b]) : zero();
+                    const Row<WPL> f = (e < dout && !same[b] && slag) ? row_at(a.F_prev, pw[b]) : zero();
                     R[b].w[0] |= f.w[0];
                     R[b].w[1] |= f.w[1];
-                    nrows += e < dout ? (slag ? 2 : 1) : 0;
+                    nrows += (e < dout && !same[b]) ? (slag ? 2 : 1) : 0;
                 }
                 // columns of the next batch, in flight with these rows
+                uint64_t pc[kCb];
 #pragma unroll
                 for (int b = 0; b < kCb; ++b) {
                     const uint64_t e = e0 + kCb + b;
+                    pc[b] = pw[b];
                     pw[b] = e < dout ? (uint64_t)(a.out_col[o0 + e] & kColMask) : 0ull;
                 }
 #pragma unroll
                 for (int b = 0; b < kCb; ++b) {
                     if (e0 + b >= dout) continue;
+                    if (same[b]) R[b] = S;  // S is the saturated set throughout (only sets <= it arrive)
                     unsigned long long pn = 0, pp = 0;
 #pragma unroll
                     for (int q = 0; q < WPL; ++q) {
@@ -1834,13 +2023,19 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
                     }
                     if (a.pushb) {  // did this peer get any push (next round's receivers)
                         const bool nz = ((__ballot(pp != 0) >> gshift) & gmask) != 0;
-                        if (lg == 0) a.pushb[o0 + e0 + b] = nz ? 1 : 0;
+                        if (lg == 0) {
+                            a.pushb[o0 + e0 + b] = nz ? 1 : 0;
+                            pushed |= nz;
+                            // the receiver's candidate byte for round r+1 (round_prep skips the walk)
+                            if (nz && a.mark_next && pc[b] < a.n_own) a.cand[a.own0 + pc[b]] = CA_NODE;
+                        }
                     }
                     cb_new += pn;
                     push_sent += pp;
                 }
             }
         }
+        if (cbk && lg == 0 && a.pushany) a.pushany[rep] = pushed ? 1 : 0;
         // new state (as expand_round)
         Row<WPL> F;
         uint32_t T = 0;
@@ -1866,6 +2061,7 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
             nrows++;
         }
         if (lg == 0 && (any || zm)) a.flg_cur[rep] = any ? (uint8_t)(FL_ACT | (keep ? FL_LAG : 0)) : (uint8_t)0;
+        if (any && a.sat_new) sat_mark<G, WPL>(a, S, rep, lg);
         c_new += T;
         c_fwd += dout * (unsigned long long)T - cl_recip - cb_new;
         c_push += push_sent;
@@ -2234,7 +2430,7 @@ __global__ void fold_slots(const unsigned long long* ctr, unsigned long long* ou
 
 // Episode reset: fill up to kResetSegs arrays (8-byte words) and start the
 // sync timers, in one launch.
-constexpr int kResetSegs = 20;
+constexpr int kResetSegs = 24;
 struct ResetSeg {
     uint64_t* p;
     uint64_t n;    // 8-byte words

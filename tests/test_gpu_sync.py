@@ -76,3 +76,58 @@ def test_tree_long_sync(hip_lib, cpu_lib, path):
     inj = uniform_injections(4096, 512, 83) + [(n, 512 + v, 30) for n, v, _ in uniform_injections(4096, 100, 84)]
     sc = Scenario(topo, 1024, 60, inj, seed=85, sync_base=20, sync_jitter=10)
     _compare(sc, hip_lib, cpu_lib, path)
+
+
+def _digest_scenario():
+    """Converges early, then many quiet sync rounds (the saturation digest's
+    fast path), with new lanes broadcast late (digest reset), a value
+    re-broadcast at another node (same lane: no reset) and a partition-free
+    directed sprinkle of hubs-free random edges."""
+    topo = T.random_regular(4096, 8, seed=91)
+    inj = uniform_injections(4096, 200, 92)
+    inj += [(n, 200 + v, 44) for n, v, _ in uniform_injections(4096, 20, 93)]  # new lanes, mid-sync
+    inj += [(17, 5, 52), (4000, 210, 57)]  # values already known: no new lane
+    inj += [(n, 300 + v, 70) for n, v, _ in uniform_injections(4096, 3, 94)]
+    return Scenario(topo, 256, 100, inj, seed=95, sync_base=6, sync_jitter=5)
+
+
+def test_digest_quiet_rounds(hip_lib, cpu_lib, monkeypatch):
+    """Bit-exact with the digest on, and the digest is what saves the work:
+    the quiet sync rounds move far fewer bytes than with GG_SYNC_DIGEST=0."""
+    sc = _digest_scenario()
+    monkeypatch.setenv("GG_SYNC_TILES", "0")
+    _compare(sc, hip_lib, cpu_lib, "stream")
+    monkeypatch.setenv("GG_SYNC_DIGEST", "0")
+    off = make_engine(hip_lib, sc, device=0).step(sc.rounds)
+    monkeypatch.delenv("GG_SYNC_DIGEST")
+    on = make_engine(hip_lib, sc, device=0).step(sc.rounds)
+    assert not diff_stats(on, off)
+    late = range(32, 44)  # converged, before the late broadcasts
+    b_on = sum(on[r]["stream_bytes"] for r in late)
+    b_off = sum(off[r]["stream_bytes"] for r in late)
+    assert b_on < 0.5 * b_off, (b_on, b_off)
+
+
+def test_digest_lane_groups(hip_lib, cpu_lib, monkeypatch):
+    """Per lane group the digest counts that group's lanes only: the summed
+    counters of 2 and 4 lane groups equal the single engine's."""
+    from ggamd.engine import COUNT_FIELDS, Engine
+    monkeypatch.setenv("GG_SYNC_TILES", "0")
+    sc = _digest_scenario()
+    ref = make_engine(cpu_lib, sc).step(sc.rounds)
+    for L in (2, 4):
+        tot = None
+        for r in range(L):
+            e = make_engine(hip_lib, sc, track=False, device=0, rank=r, world=L, lane_groups=L)
+            st = e.step(sc.rounds)
+            e.close()
+            if tot is None:
+                tot = [dict(s) for s in st]
+            else:
+                for a, b in zip(tot, st):
+                    for f in COUNT_FIELDS:
+                        if f != "round":
+                            a[f] = (a[f] + b[f]) & ((1 << 64) - 1)
+        for a, b in zip(tot, ref):
+            for f in COUNT_FIELDS:
+                assert a[f] == b[f], (L, a["round"], f, a[f], b[f])
