@@ -229,10 +229,13 @@ __device__ __forceinline__ void set_lane_bit(Row<WPL>& S, uint32_t w, uint32_t b
 template <int WPL>
 __device__ __forceinline__ Row<WPL> load_row(const uint64_t* p) {
     Row<WPL> r;
-    if constexpr (WPL == 2) {
-        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(p);
-        r.w[0] = v.x;
-        r.w[1] = v.y;
+    if constexpr (WPL % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < WPL; k += 2) {
+            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(p + k);
+            r.w[k] = v.x;
+            r.w[k + 1] = v.y;
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < WPL; ++k) r.w[k] = p[k];
@@ -242,8 +245,9 @@ __device__ __forceinline__ Row<WPL> load_row(const uint64_t* p) {
 
 template <int WPL>
 __device__ __forceinline__ void store_row(uint64_t* p, const Row<WPL>& r) {
-    if constexpr (WPL == 2) {
-        *reinterpret_cast<ulonglong2*>(p) = make_ulonglong2(r.w[0], r.w[1]);
+    if constexpr (WPL % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < WPL; k += 2) *reinterpret_cast<ulonglong2*>(p + k) = make_ulonglong2(r.w[k], r.w[k + 1]);
     } else {
 #pragma unroll
         for (int k = 0; k < WPL; ++k) p[k] = r.w[k];
@@ -379,7 +383,7 @@ __device__ __forceinline__ void stamp(const RoundArgs& a, int kind, unsigned lon
 
 // A launch with nothing to do this round (the other kernel kind takes it).
 __device__ __forceinline__ void noop_exit(const RoundArgs& a, int kind, unsigned long long t_start) {
-    if (threadIdx.x == 0) stamp(a, kind, t_start);
+    if (threadIdx.x == 0 && blockIdx.x == 0) stamp(a, kind, t_start);  // one block's stamps suffice
 }
 
 __device__ __forceinline__ void flush_counters(const RoundArgs& a, unsigned long long (&acc)[C_NUM],
@@ -1058,9 +1062,9 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                     for (int w = 0; w < WPL; ++w) {
                         F.w[w] = S.w[w] & ~sp.w[w];
                         T += __popcll(F.w[w]);
-                        if (F.w[w]) {  // seen_hash delta of a changed word
+                        if (F.w[w]) {  // seen_hash: the round's new bits of a word
                             const uint64_t idx = g * a.nw + a.word0 + off + w;
-                            c_hash += gg_word_hash(idx, S.w[w]) - (sp.w[w] ? gg_word_hash(idx, sp.w[w]) : 0ull);
+                            c_hash += gg_word_hash(idx, F.w[w]);
                         }
                     }
                     const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
@@ -1424,7 +1428,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             T += __popcll(F.w[w]);
             if (F.w[w]) {
                 const uint64_t idx = g * a.nw + a.word0 + off + w;
-                c_hash += gg_word_hash(idx, S.w[w]) - (sp.w[w] ? gg_word_hash(idx, sp.w[w]) : 0ull);
+                c_hash += gg_word_hash(idx, F.w[w]);
             }
         }
         const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
@@ -1615,7 +1619,7 @@ void expand_stream1(RoundArgs a) {
             const uint32_t T = (uint32_t)__popcll(F);
             if (F) {
                 const uint64_t idx = gid_of(a, i) * a.nw + a.word0;
-                c_hash += gg_word_hash(idx, S) - (sp ? gg_word_hash(idx, sp) : 0ull);
+                c_hash += gg_word_hash(idx, F);
             }
             const bool any = F != 0;
             const bool zm = (m0.fl & FL_ACT) != 0;
@@ -2046,7 +2050,7 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
             T += __popcll(F.w[w]);
             if (F.w[w]) {
                 const uint64_t idx = g * a.nw + a.word0 + off + w;
-                c_hash += gg_word_hash(idx, S.w[w]) - (sp.w[w] ? gg_word_hash(idx, sp.w[w]) : 0ull);
+                c_hash += gg_word_hash(idx, F.w[w]);
             }
         }
         const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
@@ -2318,7 +2322,7 @@ __global__ __launch_bounds__(kBlock) void hub_finish(RoundArgs a) {
                 T += __popcll(F.w[w]);
                 if (F.w[w]) {
                     const uint64_t idx = g * a.nw + a.word0 + off + w;
-                    c_hash += gg_word_hash(idx, S.w[w]) - (sp.w[w] ? gg_word_hash(idx, sp.w[w]) : 0ull);
+                    c_hash += gg_word_hash(idx, F.w[w]);
                 }
             }
             const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;

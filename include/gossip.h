@@ -98,7 +98,7 @@ typedef struct {
     uint64_t read_oks;       /* `read_ok` replies to nodes sent (:131) */
     uint64_t dropped;        /* messages of every kind sent this round and dropped */
     uint64_t syncs_fired;    /* sync timers that fired this round */
-    uint64_t seen_hash;      /* order-free hash of every node's set */
+    uint64_t seen_hash;      /* fingerprint of every round's new bits so far */
     double kernel_ms;        /* device time of the round (0 for the CPU oracle) */
     uint64_t work_rows;      /* diagnostics, engine-specific (not part of parity): */
     uint64_t work_gathers;   /*   nodes that moved rows, sender rows gathered */

@@ -50,8 +50,9 @@ GG_HD uint32_t gg_part_group(uint64_t seed, uint64_t epoch_seed, uint64_t v) {
     return (uint32_t)(gg_mix64(gg_mix64(seed ^ GG_TAG_PART ^ epoch_seed) ^ v) & 1ull);
 }
 
-/* Contribution of one non-zero set word to seen_hash; word index
- * idx = v * (W/64) + j. seen_hash = sum (mod 2^64) over all non-zero words. */
+/* Contribution to seen_hash of one set word that gained bits in a round:
+ * word = the round's new bits of node v's word j, idx = v * (W/64) + j.
+ * seen_hash = sum (mod 2^64) over all rounds so far and all such words. */
 GG_HD uint64_t gg_word_hash(uint64_t idx, uint64_t word) {
     return gg_mix64(gg_mix64(idx ^ GG_TAG_HASH) ^ word);
 }

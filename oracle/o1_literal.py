@@ -140,6 +140,8 @@ class O1Network:
         self.first_seen: dict = {}  # (node, value) -> round
         self._ctr: Counters | None = None
         self._seq = 0
+        self._hash_total = 0  # seen_hash so far
+        self._prev_bits: list[list[int]] = [[0] * (n_lanes // 64) for _ in range(n_nodes)]
 
     # ---- setup -----------------------------------------------------------
 
@@ -356,13 +358,18 @@ class O1Network:
         return words
 
     def seen_hash(self) -> int:
+        """Delivery fingerprint: the sum (mod 2^64), over every
+        round so far and every set word that gained bits in it, of
+        word_hash(idx, the word's new bits); called once at the end of a round."""
         nw = self.W // 64
-        h = 0
         for v in range(self.V):
+            prev = self._prev_bits[v]
             for j, w in enumerate(self.bits(v)):
-                if w:
-                    h = (h + word_hash(v * nw + j, w)) & M64
-        return h
+                new = w & ~prev[j]
+                if new:
+                    self._hash_total = (self._hash_total + word_hash(v * nw + j, new)) & M64
+                prev[j] = w
+        return self._hash_total
 
     def delivery_rounds(self, v: int) -> list[int]:
         out = [-1] * self.W

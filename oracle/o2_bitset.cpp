@@ -102,6 +102,7 @@ struct gg_engine {
     std::map<int64_t, std::vector<Injection>> inj;
     int64_t round = 0;
     uint64_t pend_acks = 0, pend_ackdrop = 0;
+    uint64_t hash_total = 0;  // seen_hash: all rounds' new-bit words so far
     int threads = 1;
     bool dist_open = false;
     Acc dist_acc;
@@ -164,6 +165,7 @@ struct gg_engine {
         inj.clear();
         round = 0;
         pend_acks = pend_ackdrop = 0;
+        hash_total = 0;
         dist_open = false;
     }
     void compute_round(Acc& total);
@@ -273,7 +275,7 @@ void gg_engine::compute_round(Acc& total) {
                 uint64_t f = S[j] & ~sp[j];
                 fc[j] = f;
                 Tn += popc(f);
-                if (S[j]) a.hash += gg_word_hash(g * nw_g + w0 + j, S[j]);
+                if (f) a.hash += gg_word_hash(g * nw_g + w0 + j, f);
                 if (f && !dr.empty()) {
                     uint64_t x = f;
                     while (x) {
@@ -564,7 +566,8 @@ static void fill_stats(gg_engine* e, const Acc& a, gg_round_stats* s) {
     s->read_oks = a.read_oks;
     s->dropped = a.dropped + e->pend_ackdrop;
     s->syncs_fired = a.fired;
-    s->seen_hash = a.hash;
+    e->hash_total += a.hash;
+    s->seen_hash = e->hash_total;
     s->kernel_ms = 0.0;
     s->work_rows = 0;
     s->work_gathers = 0;
