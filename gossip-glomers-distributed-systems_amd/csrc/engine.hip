@@ -747,6 +747,12 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             // dense lean rounds, where it is a no-op (C2 A/B: 1024 blocks 1.99 ms/episode,
             // 4096 2.02, 256 2.10; GG_PREP_BLOCKS overrides)
             static const uint64_t prep_cap = getenv("GG_PREP_BLOCKS") ? (uint64_t)atoi(getenv("GG_PREP_BLOCKS")) : 1024;
+            if (e->d_sat && r == base + 2) {  // the digest's first bits (sat_scan)
+                const uint64_t thr = a.n_own * (e->nwp / 2);
+                hipLaunchKernelGGL(gg::sat_scan, dim3((unsigned)((thr + gg::kBlock - 1) / gg::kBlock)), dim3(gg::kBlock),
+                                   0, e->stream, e->d_base, a.n_own, (uint32_t)e->nwp, lanes_through(e, r - 1), e->d_sat);
+                HIPCHK(hipGetLastError());
+            }
             // sync rounds do real work per node: a larger capped grid (each block's
             // counter flush is a few same-address atomics, so not one block per 256 nodes)
             const uint64_t blocks = std::max<uint64_t>(

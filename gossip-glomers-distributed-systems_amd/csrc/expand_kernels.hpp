@@ -351,6 +351,31 @@ __device__ __forceinline__ void sat_mark(const RoundArgs& a, const Row<WPL>& S, 
     if (lg == 0 && c == a.usat) atomicOr(a.sat_new + (rep >> 6), 1ull << (rep & 63));
 }
 
+// The digest's first bits: one pass over every owned row at the start of the
+// first streamed sync round r (lean rounds before it have no LAG rows, so the
+// base row is the node's set after r-1, and they do not mark, keeping the
+// dense loop lean). cpn 16-byte chunks per row, one per lane; a wave covers
+// 64/cpn consecutive nodes, one word's worth of bits, and ORs them in at once.
+__global__ __launch_bounds__(kBlock) void sat_scan(const uint64_t* base, uint64_t n_own, uint32_t nwp, uint32_t usat,
+                                                   uint64_t* sat) {
+    const uint32_t cpn = nwp / 2;
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t node = t / cpn;
+    uint32_t c = 0;
+    if (node < n_own) {
+        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(base + node * nwp + (t % cpn) * 2);
+        c = (uint32_t)(__popcll(v.x) + __popcll(v.y));
+    }
+    for (uint32_t o = cpn / 2; o > 0; o >>= 1) c += __shfl_xor(c, (int)o, 64);
+    const unsigned long long m = __ballot(node < n_own && t % cpn == 0 && c == usat);
+    if ((threadIdx.x & 63) == 0) {
+        uint64_t bits = 0;  // lane k*cpn -> node bit k
+        for (uint32_t k = 0; k < 64 / cpn; ++k) bits |= ((m >> (k * cpn)) & 1ull) << k;
+        const uint64_t n0 = t / cpn;  // first node of the wave
+        if (bits) atomicOr(sat + (n0 >> 6), bits << (n0 & 63));
+    }
+}
+
 // Block reduction of C_NUM per-thread counters -> one atomic per counter per
 // block into slot blockIdx % 64.
 // Wait until every vector-memory op of this wave (loads, stores, LDS-DMA) is
@@ -1435,7 +1460,6 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         const bool zm = (m0.fl & FL_ACT) != 0;  // F row of round r-2 in this buffer
         if (any || zm) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
         if (any) store_row<WPL>(a.base + rep * a.nwp + off, S);
-        if (any && a.sat_new) sat_mark<G, WPL>(a, S, rep, lg);
         if (lg == 0) {
             if (any || m0.fl) a.flg_cur[rep] = any ? FL_ACT : 0;
             if (m0.ca) a.cand[rep] = 0;
