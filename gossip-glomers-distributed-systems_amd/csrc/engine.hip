@@ -153,6 +153,8 @@ struct gg_engine {
     uint64_t n_own = 0, ghost0 = 0, n_ghost = 0, rows = 0;  // local rows: own, then ghosts
     std::vector<uint32_t> gid;     // [rows] original id of each local row (~0u: padding)
     std::vector<uint32_t> loc_of;  // [V] local row of an owned node, ~0u otherwise (sharded)
+    bool range_mode = false;       // device-partitioned shard: owned nodes [range_lo, range_hi)
+    uint64_t range_lo = 0, range_hi = 0;  // are rows 0.. (no loc_of)
     bool have_topo = false, symmetric = true;
     std::vector<int64_t> host_rp;  // vertex-sharded: the caller's row offsets (gg_set_partition)
     uint32_t* d_gid = nullptr;     // sharded only (single engine: row == id)
@@ -885,6 +887,7 @@ int ensure_inj(gg_engine* e, size_t pairs) {
 // Local row of an owned node, ~0u if another engine owns it.
 uint32_t local_row(const gg_engine* e, uint64_t node) {
     if (node >= e->V) return ~0u;
+    if (e->range_mode) return node >= e->range_lo && node < e->range_hi ? (uint32_t)(node - e->range_lo) : ~0u;
     if (e->loc_of.empty()) return (uint32_t)node;
     return e->loc_of[node];
 }
@@ -1281,6 +1284,63 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     return reset_device_state(e);
 }
 
+// Exchange buffers of a vertex-sharded engine from its send/receive lists
+// (send_off, recv_off, n_ghost; d_send_idx, d_gout_* already on the device):
+// segment capacities (header + an F and an S entry per send-list node), pack
+// tiles, the size mode of every direction.
+static int setup_exchange(gg_engine* e) {
+    const uint32_t Wd = e->P;
+    e->xstride = (uint32_t)(e->nwp >= 2 ? 16 + 8 * e->nwp : 16);
+    e->xsoff.assign(Wd + 1, 0);
+    e->xroff.assign(Wd + 1, 0);
+    std::vector<gg::XchgTile> tiles;
+    for (uint32_t q = 0; q < Wd; ++q) {
+        const uint64_t ns = e->send_off[q + 1] - e->send_off[q], nr = e->recv_off[q + 1] - e->recv_off[q];
+        e->xsoff[q + 1] = e->xsoff[q] + (ns ? 16 + 2 * ns * e->xstride : 0);
+        e->xroff[q + 1] = e->xroff[q] + (nr ? 16 + 2 * nr * e->xstride : 0);
+        for (uint64_t k0 = e->send_off[q]; k0 < e->send_off[q + 1]; k0 += gg::kBlock)
+            tiles.push_back({q, (uint32_t)k0, (uint32_t)std::min<uint64_t>(gg::kBlock, e->send_off[q + 1] - k0),
+                             (uint32_t)e->send_off[q]});
+    }
+    e->n_xtiles = (uint32_t)tiles.size();
+    HIPCHK(hipMalloc(&e->d_xtiles, std::max<size_t>(1, tiles.size()) * sizeof(gg::XchgTile)));
+    if (!tiles.empty())
+        HIPCHK(hipMemcpy(e->d_xtiles, tiles.data(), tiles.size() * sizeof(gg::XchgTile), hipMemcpyHostToDevice));
+    std::vector<uint32_t> gfirst(Wd + 1);
+    for (uint32_t q = 0; q <= Wd; ++q) gfirst[q] = (uint32_t)e->recv_off[q];
+    HIPCHK(hipMalloc(&e->d_gfirst, (Wd + 1) * 4));
+    HIPCHK(hipMemcpy(e->d_gfirst, gfirst.data(), (Wd + 1) * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&e->d_xsoff, (Wd + 1) * 8));
+    HIPCHK(hipMemcpy(e->d_xsoff, e->xsoff.data(), (Wd + 1) * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&e->d_xroff, (Wd + 1) * 8));
+    HIPCHK(hipMemcpy(e->d_xroff, e->xroff.data(), (Wd + 1) * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&e->d_needmark, (e->send_off[Wd] + 7) / 8 * 8 + 8));
+    HIPCHK(hipMalloc(&e->d_stamp, (e->n_ghost + 1) / 2 * 8 + 8));
+    HIPCHK(hipMalloc(&e->d_xcnt, (Wd + 1) / 2 * 8 + 8));
+    HIPCHK(hipMalloc(&e->d_segbytes, 2 * Wd * 8));
+    HIPCHK(hipHostMalloc(&e->h_segbytes, 2 * Wd * 8));
+    HIPCHK(hipMalloc(&e->d_payload, kMaxBatch * 8));
+    HIPCHK(hipMalloc(&e->d_xsend, std::max<uint64_t>(16, e->xsoff[Wd])));
+    HIPCHK(hipMalloc(&e->d_xrecv, std::max<uint64_t>(16, e->xroff[Wd])));
+    // a direction whose static capacity exceeds GG_XCHG_EXACT_BYTES (default
+    // 4 MiB) sends its exact size first and then only the used bytes (one host
+    // wait per round); GG_XCHG_MODE=exact|static forces every direction
+    const char* mode = getenv("GG_XCHG_MODE");
+    uint64_t lim = 4ull << 20;
+    if (const char* l = getenv("GG_XCHG_EXACT_BYTES")) lim = strtoull(l, nullptr, 10);
+    e->xexact_s.assign(Wd, 0);
+    e->xexact_r.assign(Wd, 0);
+    e->xexact = false;
+    for (uint32_t q = 0; q < Wd; ++q) {
+        const uint64_t cs = e->xsoff[q + 1] - e->xsoff[q], cr = e->xroff[q + 1] - e->xroff[q];
+        const bool force = mode && !strcmp(mode, "exact"), never = mode && !strcmp(mode, "static");
+        e->xexact_s[q] = cs && !never && (force || cs > lim);
+        e->xexact_r[q] = cr && !never && (force || cr > lim);
+        e->xexact |= e->xexact_s[q] || e->xexact_r[q];
+    }
+    return GG_OK;
+}
+
 int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64_t nnz) {
     if (!e || !row_ptr || (nnz && !col)) return GG_EINVAL;
     HIPCHK(hipSetDevice(e->device));
@@ -1359,6 +1419,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     e->n_own = n_own;
     e->loc_of.clear();
     e->gid.clear();
+    e->range_mode = false;
     std::vector<uint32_t> ghosts;                     // ghost nodes in local ghost order
     std::vector<std::vector<uint32_t>> sendl(Wd);     // owned local rows per destination
     std::vector<std::vector<uint32_t>> send_ids(Wd);  // the same, original ids (ascending)
@@ -1513,54 +1574,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
         HIPCHK(hipMalloc(&e->d_gout_sidx, std::max<size_t>(1, gsidx.size()) * 4));
         if (!gsidx.empty())
             HIPCHK(hipMemcpy(e->d_gout_sidx, gsidx.data(), gsidx.size() * 4, hipMemcpyHostToDevice));
-        e->xstride = (uint32_t)(e->nwp >= 2 ? 16 + 8 * e->nwp : 16);
-        e->xsoff.assign(Wd + 1, 0);
-        e->xroff.assign(Wd + 1, 0);
-        std::vector<gg::XchgTile> tiles;
-        for (uint32_t q = 0; q < Wd; ++q) {
-            const uint64_t ns = e->send_off[q + 1] - e->send_off[q], nr = e->recv_off[q + 1] - e->recv_off[q];
-            e->xsoff[q + 1] = e->xsoff[q] + (ns ? 16 + 2 * ns * e->xstride : 0);
-            e->xroff[q + 1] = e->xroff[q] + (nr ? 16 + 2 * nr * e->xstride : 0);
-            for (uint64_t k0 = e->send_off[q]; k0 < e->send_off[q + 1]; k0 += gg::kBlock)
-                tiles.push_back({q, (uint32_t)k0, (uint32_t)std::min<uint64_t>(gg::kBlock, e->send_off[q + 1] - k0),
-                                 (uint32_t)e->send_off[q]});
-        }
-        e->n_xtiles = (uint32_t)tiles.size();
-        HIPCHK(hipMalloc(&e->d_xtiles, std::max<size_t>(1, tiles.size()) * sizeof(gg::XchgTile)));
-        if (!tiles.empty())
-            HIPCHK(hipMemcpy(e->d_xtiles, tiles.data(), tiles.size() * sizeof(gg::XchgTile), hipMemcpyHostToDevice));
-        std::vector<uint32_t> gfirst(Wd + 1);
-        for (uint32_t q = 0; q <= Wd; ++q) gfirst[q] = (uint32_t)e->recv_off[q];
-        HIPCHK(hipMalloc(&e->d_gfirst, (Wd + 1) * 4));
-        HIPCHK(hipMemcpy(e->d_gfirst, gfirst.data(), (Wd + 1) * 4, hipMemcpyHostToDevice));
-        HIPCHK(hipMalloc(&e->d_xsoff, (Wd + 1) * 8));
-        HIPCHK(hipMemcpy(e->d_xsoff, e->xsoff.data(), (Wd + 1) * 8, hipMemcpyHostToDevice));
-        HIPCHK(hipMalloc(&e->d_xroff, (Wd + 1) * 8));
-        HIPCHK(hipMemcpy(e->d_xroff, e->xroff.data(), (Wd + 1) * 8, hipMemcpyHostToDevice));
-        HIPCHK(hipMalloc(&e->d_needmark, (e->send_off[Wd] + 7) / 8 * 8 + 8));
-        HIPCHK(hipMalloc(&e->d_stamp, (e->n_ghost + 1) / 2 * 8 + 8));
-        HIPCHK(hipMalloc(&e->d_xcnt, (Wd + 1) / 2 * 8 + 8));
-        HIPCHK(hipMalloc(&e->d_segbytes, 2 * Wd * 8));
-        HIPCHK(hipHostMalloc(&e->h_segbytes, 2 * Wd * 8));
-        HIPCHK(hipMalloc(&e->d_payload, kMaxBatch * 8));
-        HIPCHK(hipMalloc(&e->d_xsend, std::max<uint64_t>(16, e->xsoff[Wd])));
-        HIPCHK(hipMalloc(&e->d_xrecv, std::max<uint64_t>(16, e->xroff[Wd])));
-        // a direction whose static capacity exceeds GG_XCHG_EXACT_BYTES (default
-        // 4 MiB) sends its exact size first and then only the used bytes (one host
-        // wait per round); GG_XCHG_MODE=exact|static forces every direction
-        const char* mode = getenv("GG_XCHG_MODE");
-        uint64_t lim = 4ull << 20;
-        if (const char* l = getenv("GG_XCHG_EXACT_BYTES")) lim = strtoull(l, nullptr, 10);
-        e->xexact_s.assign(Wd, 0);
-        e->xexact_r.assign(Wd, 0);
-        e->xexact = false;
-        for (uint32_t q = 0; q < Wd; ++q) {
-            const uint64_t cs = e->xsoff[q + 1] - e->xsoff[q], cr = e->xroff[q + 1] - e->xroff[q];
-            const bool force = mode && !strcmp(mode, "exact"), never = mode && !strcmp(mode, "static");
-            e->xexact_s[q] = cs && !never && (force || cs > lim);
-            e->xexact_r[q] = cr && !never && (force || cr > lim);
-            e->xexact |= e->xexact_s[q] || e->xexact_r[q];
-        }
+        if (int rc = setup_exchange(e)) return rc;
     }
     return finish_topology(e, iptr.data(), sym ? nullptr : optr.data());
 }
@@ -1570,6 +1584,75 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
 // symmetric, so the in-lists are the rows themselves with every entry
 // reciprocal and nothing crosses PCIe. Sharded: built on the device, then the
 // host partition path of gg_topology.
+}  // extern "C"
+
+// gg_topology_generate on a vertex-sharded engine: rank part of P owns the
+// contiguous node range [plo[part], plo[part+1]) (native order, cut at
+// multiples of 64) and builds only those rows of the generated graph, then
+// its ghosts, send lists and ghost -> owned lists on the device
+// (gg_gen::shard_csr): no rank holds the whole graph, in HBM or in host
+// memory (host memory: the rank's ghost ids and per-part offsets only).
+static int generate_sharded(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_out) {
+    const uint64_t V = e->V;
+    const uint32_t P = e->P;
+    std::vector<uint64_t> plo(P + 1);
+    for (uint32_t p = 0; p < P; ++p) plo[p] = std::min<uint64_t>(V, (V * p / P) / 64 * 64);
+    plo[P] = V;
+    const uint64_t lo = plo[e->part], hi = plo[e->part + 1];
+    gg_gen::Csr g{};
+    std::string err;
+    int rc = gg_gen::build_csr_rows(*spec, e->stream, 0u, lo, hi, &g, &err);
+    if (rc) return e->fail(rc, err);
+    const uint64_t n_own = hi - lo;
+    const uint64_t ghost0 = (n_own + 63) / 64 * 64;
+    gg_gen::Shard sh;
+    rc = gg_gen::shard_csr(&g, lo, hi, plo, ghost0, gg::kRecipBit, e->stream, &sh, &err);
+    if (rc) {
+        (void)hipFree(g.row_ptr);
+        (void)hipFree(g.col);
+        return e->fail(rc, err);
+    }
+    e->range_mode = true;
+    e->range_lo = lo;
+    e->range_hi = hi;
+    e->loc_of.clear();
+    e->symmetric = true;
+    e->n_own = n_own;
+    e->n_ghost = sh.n_ghost;
+    e->ghost0 = ghost0;
+    e->rows = std::max<uint64_t>(64, (ghost0 + sh.n_ghost + 63) / 64 * 64);
+    if (e->rows > 0x7fffffffull) return e->fail(GG_EINVAL, "local rows exceed 2^31");
+    e->gid.assign(e->rows, ~0u);
+    for (uint64_t i = 0; i < n_own; ++i) e->gid[i] = (uint32_t)(lo + i);
+    for (uint64_t k = 0; k < sh.n_ghost; ++k) e->gid[ghost0 + k] = sh.ghosts_host[k];
+    std::vector<uint32_t>().swap(sh.ghosts_host);
+    e->d_gid = sh.gid;
+    e->d_in_ptr = g.row_ptr;
+    e->d_in_col = g.col;
+    e->d_out_ptr = g.row_ptr;
+    e->d_out_col = g.col;
+    e->n_in_edges = g.nnz;
+    e->n_out_edges = g.nnz;
+    if (nnz_out) *nnz_out = g.nnz;  // this rank's rows
+    e->send_off = sh.send_off;
+    e->recv_off = sh.recv_off;
+    e->d_send_idx = sh.send_idx;
+    e->d_gout_ptr = sh.gout_ptr;
+    e->d_gout_col = sh.gout_col;
+    e->d_gout_sidx = sh.gout_sidx;
+    if ((rc = setup_exchange(e))) return rc;
+    uint64_t dmax = 0;
+    if ((rc = gg_gen::max_degree(g.row_ptr, n_own, e->stream, &dmax, &err))) return e->fail(rc, err);
+    std::vector<int64_t> iptr;
+    if (dmax > hub_threshold()) {  // hub chunks are planned on the host
+        iptr.resize(n_own + 1);
+        HIPCHK(hipMemcpy(iptr.data(), g.row_ptr, (n_own + 1) * 8, hipMemcpyDeviceToHost));
+    }
+    return finish_topology(e, iptr.empty() ? nullptr : iptr.data(), nullptr);
+}
+
+extern "C" {
+
 int gg_topology_generate(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_out) {
     if (!e || !spec) return GG_EINVAL;
     if (gg_gen::spec_nodes(*spec) != e->V) return e->fail(GG_EINVAL, "generator node count != engine n_nodes");
@@ -1582,23 +1665,8 @@ int gg_topology_generate(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_ou
                      e->windows.end());
     gg_gen::Csr g{};
     std::string err;
-    if (e->P != 1) {
-        // sharded: every rank builds the whole graph on its own device (no host
-        // generator), then takes the host path for the locality order, ghosts
-        // and send lists, which need the whole graph on the host anyway
-        int rc = gg_gen::build_csr(*spec, e->stream, 0u, &g, &err);
-        if (rc) return e->fail(rc, err);
-        std::vector<int64_t> rp(e->V + 1);
-        std::vector<int32_t> col(g.nnz);
-        hipError_t h1 = hipMemcpy(rp.data(), g.row_ptr, (e->V + 1) * 8, hipMemcpyDeviceToHost);
-        hipError_t h2 = g.nnz ? hipMemcpy(col.data(), g.col, g.nnz * 4, hipMemcpyDeviceToHost) : hipSuccess;
-        (void)hipFree(g.row_ptr);
-        (void)hipFree(g.col);
-        HIPCHK(h1);
-        HIPCHK(h2);
-        if (nnz_out) *nnz_out = g.nnz;
-        return gg_topology(e, rp.data(), col.data(), g.nnz);
-    }
+    if (e->P != 1) return generate_sharded(e, spec, nnz_out);
+    e->range_mode = false;
     int rc = gg_gen::build_csr(*spec, e->stream, gg::kRecipBit, &g, &err);
     if (rc) return e->fail(rc, err);
     e->rows = std::max<uint64_t>(64, (e->V + 63) / 64 * 64);
@@ -1709,6 +1777,9 @@ int gg_set_partition(gg_engine* e, int64_t a, int64_t b, const uint64_t* bits) {
     if (!e || !bits) return GG_EINVAL;
     if (!e->have_topo) return e->fail(GG_EINVAL, "gg_set_partition: install the topology first");
     if (!e->symmetric) return e->fail(GG_EINVAL, "gg_set_partition: per-edge windows need a symmetric topology");
+    if (e->P > 1 && e->host_rp.empty())
+        return e->fail(GG_EINVAL, "gg_set_partition: a shard built by gg_topology_generate holds no whole-graph "
+                                  "row offsets (use gg_topology, or seeded/group windows)");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
     const uint64_t V = e->V, n_own = e->n_own;

@@ -26,6 +26,7 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
 
 #include <algorithm>
 #include <cstdint>
@@ -56,6 +57,7 @@ struct GenParams {
     uint32_t scale;           // R-MAT: log2 of the sampling square
     uint64_t ta, tb, tc;      // R-MAT: quadrant thresholds (x < ta: a, < tb: b, < tc: c, else d)
     const uint32_t* perm;     // R-MAT: relabelling; regular: the k/2 permutations, [j*V + v]
+    uint64_t rlo, rhi;        // rows kept: [rlo, rhi) (a vertex-sharded rank's own rows)
 };
 
 __device__ __forceinline__ bool pair_at(const GenParams& g, uint64_t slot, uint64_t& a, uint64_t& b) {
@@ -105,13 +107,21 @@ __device__ __forceinline__ bool pair_at(const GenParams& g, uint64_t slot, uint6
     return a != b;
 }
 
-__global__ void tree_csr(uint64_t V, uint32_t k, int64_t* rp, uint32_t* col, uint32_t col_or) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= V; i += (uint64_t)gridDim.x * blockDim.x) {
-        // row i starts after the i-1 parent links of rows 1..i-1 and the
-        // min(V-1, i*k) child links of rows 0..i-1 (ggh_tree, host/topology.cpp:121)
-        const int64_t start = (int64_t)(i ? i - 1 : 0) + (int64_t)std::min<uint64_t>(V - 1, i * k);
-        rp[i] = i == V ? (int64_t)(2 * (V - 1)) : start;
-        if (i == V) continue;
+// row i starts after the i-1 parent links of rows 1..i-1 and the min(V-1, i*k)
+// child links of rows 0..i-1 (ggh_tree, host/topology.cpp:121)
+__host__ __device__ inline int64_t tree_row_start(uint64_t V, uint32_t k, uint64_t i) {
+    return i >= V ? (int64_t)(2 * (V - 1)) : (int64_t)(i ? i - 1 : 0) + (int64_t)std::min<uint64_t>(V - 1, i * k);
+}
+
+// rows [rlo, rhi) of the tree (row_ptr relative to row rlo's first entry)
+__global__ void tree_csr(uint64_t V, uint32_t k, uint64_t rlo, uint64_t rhi, int64_t* rp, uint32_t* col,
+                         uint32_t col_or) {
+    const int64_t s0 = tree_row_start(V, k, rlo);
+    for (uint64_t i = rlo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= rhi;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const int64_t start = tree_row_start(V, k, i) - s0;
+        rp[i - rlo] = start;
+        if (i == rhi) continue;
         int64_t p = start;
         if (i > 0) col[p++] = (uint32_t)((i - 1) / k) | col_or;
         for (uint64_t c = i * k + 1; c <= i * k + k && c < V; ++c) col[p++] = (uint32_t)c | col_or;
@@ -132,8 +142,8 @@ __global__ __launch_bounds__(kBlk) void bucket_hist(GenParams g, uint64_t pairs,
     for (uint64_t s = (uint64_t)blockIdx.x * kBlk + threadIdx.x; s < pairs; s += (uint64_t)gridDim.x * kBlk) {
         uint64_t a, b;
         if (!pair_at(g, s, a, b)) continue;
-        atomicAdd(&h[a >> bshift], 1u);
-        atomicAdd(&h[b >> bshift], 1u);
+        if (a >= g.rlo && a < g.rhi) atomicAdd(&h[(a - g.rlo) >> bshift], 1u);
+        if (b >= g.rlo && b < g.rhi) atomicAdd(&h[(b - g.rlo) >> bshift], 1u);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kBuckets; i += kBlk)
@@ -152,9 +162,9 @@ __global__ __launch_bounds__(kBlk) void emit_keys(GenParams g, uint64_t pairs, u
         uint64_t a = 0, b = 0;
         const bool ok = s < pairs && pair_at(g, s, a, b);
         for (int d = 0; d < 2; ++d) {
-            const uint64_t row = d ? b : a, colv = d ? a : b;
+            const uint64_t row = (d ? b : a) - g.rlo, colv = d ? a : b;  // row local to [rlo, rhi)
             int p = -1;
-            if (ok) {
+            if (ok && (d ? b : a) >= g.rlo && (d ? b : a) < g.rhi) {
                 p = 0;
                 while (p + 1 < (int)n_parts && row >= part_row0[p + 1]) ++p;
             }
@@ -279,28 +289,38 @@ struct Scoped {  // device allocations released on every exit path
 uint64_t spec_nodes(const gg_gen_spec& s) { return s.kind == GG_GEN_GRID_LINKS ? s.n * s.n : s.n; }
 
 int build_csr(const gg_gen_spec& s, hipStream_t st, uint32_t col_or, Csr* out, std::string* err) {
+    return build_csr_rows(s, st, col_or, 0, spec_nodes(s), out, err);
+}
+
+int build_csr_rows(const gg_gen_spec& s, hipStream_t st, uint32_t col_or, uint64_t rlo, uint64_t rhi, Csr* out,
+                   std::string* err) {
     const uint64_t V = spec_nodes(s);
     if (V == 0 || V > 0x7fffffffull) {
         *err = "generator: node count must be in [1, 2^31)";
         return -22;
     }
+    if (rlo > rhi || rhi > V) {
+        *err = "generator: row range outside [0, V]";
+        return -22;
+    }
+    const uint64_t n = rhi - rlo;  // rows built
     Scoped mem;
     int64_t* rp = nullptr;
     uint32_t* col = nullptr;
-    GCHK(mem.alloc(&rp, (V + 1) * 8));
+    GCHK(mem.alloc(&rp, (n + 1) * 8));
     if (s.kind == GG_GEN_TREE) {
         if (s.k == 0) {
             *err = "generator: tree arity must be >= 1";
             return -22;
         }
-        const uint64_t nnz = 2 * (V - 1);
+        const uint64_t nnz = (uint64_t)(tree_row_start(V, s.k, rhi) - tree_row_start(V, s.k, rlo));
         GCHK(mem.alloc(&col, nnz * 4));
-        hipLaunchKernelGGL(tree_csr, dim3(grid_of(V + 1)), dim3(kBlk), 0, st, V, s.k, rp, col, col_or);
+        hipLaunchKernelGGL(tree_csr, dim3(grid_of(n + 1)), dim3(kBlk), 0, st, V, s.k, rlo, rhi, rp, col, col_or);
         GCHK(hipGetLastError());
         GCHK(hipStreamSynchronize(st));
         mem.keep(rp);
         mem.keep(col);
-        *out = {rp, col, V, nnz};
+        *out = {rp, col, n, nnz};
         return 0;
     }
     // undirected pairs -> packed keys (row << cb | col), both directions
@@ -311,6 +331,8 @@ int build_csr(const gg_gen_spec& s, hipStream_t st, uint32_t col_or, Csr* out, s
     g.V = V;
     g.side = s.n;
     g.seed = s.seed;
+    g.rlo = rlo;
+    g.rhi = rhi;
     uint64_t pairs = 0;
     std::vector<uint32_t> perm;
     uint32_t* d_perm = nullptr;
@@ -350,7 +372,7 @@ int build_csr(const gg_gen_spec& s, hipStream_t st, uint32_t col_or, Csr* out, s
     uint64_t part_keys = kPartKeys;
     if (const char* e = getenv("GG_GEN_PART_KEYS")) part_keys = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     uint32_t bshift = 0;
-    while ((V - 1) >> bshift >= (uint64_t)kBuckets) ++bshift;
+    while (n > 1 && (n - 1) >> bshift >= (uint64_t)kBuckets) ++bshift;
     unsigned long long* d_hist = nullptr;
     GCHK(mem.alloc(&d_hist, (kBuckets + kMaxParts) * 8));
     GCHK(hipMemsetAsync(d_hist, 0, kBuckets * 8, st));
@@ -371,7 +393,7 @@ int build_csr(const gg_gen_spec& s, hipStream_t st, uint32_t col_or, Csr* out, s
         in_part += hist[q];
         M += hist[q];
     }
-    row0.push_back(V);
+    row0.push_back(n);
     off.push_back(M);
     const uint32_t n_parts = (uint32_t)row0.size() - 1;
     uint64_t max_part = 0;
@@ -417,28 +439,28 @@ int build_csr(const gg_gen_spec& s, hipStream_t st, uint32_t col_or, Csr* out, s
     // CSR of the distinct (row, col) keys
     int64_t* first = nullptr;
     int64_t* cnt = nullptr;
-    GCHK(mem.alloc(&first, (V + 1) * 8));
-    GCHK(mem.alloc(&cnt, (V + 1) * 8));
-    hipLaunchKernelGGL(row_bounds, dim3(grid_of(M + 1)), dim3(kBlk), 0, st, keys, M, V, cb, first);
+    GCHK(mem.alloc(&first, (n + 1) * 8));
+    GCHK(mem.alloc(&cnt, (n + 1) * 8));
+    hipLaunchKernelGGL(row_bounds, dim3(grid_of(M + 1)), dim3(kBlk), 0, st, keys, M, n, cb, first);
     GCHK(hipGetLastError());
-    hipLaunchKernelGGL(row_count, dim3(grid_of(V + 1)), dim3(kBlk), 0, st, keys, first, V, cnt);
+    hipLaunchKernelGGL(row_count, dim3(grid_of(n + 1)), dim3(kBlk), 0, st, keys, first, n, cnt);
     GCHK(hipGetLastError());
     tmp_bytes = 0;
-    GCHK(rocprim::exclusive_scan(nullptr, tmp_bytes, cnt, rp, (int64_t)0, V + 1, rocprim::plus<int64_t>(), st));
+    GCHK(rocprim::exclusive_scan(nullptr, tmp_bytes, cnt, rp, (int64_t)0, n + 1, rocprim::plus<int64_t>(), st));
     GCHK(mem.alloc(&tmp, tmp_bytes));
-    GCHK(rocprim::exclusive_scan(tmp, tmp_bytes, cnt, rp, (int64_t)0, V + 1, rocprim::plus<int64_t>(), st));
+    GCHK(rocprim::exclusive_scan(tmp, tmp_bytes, cnt, rp, (int64_t)0, n + 1, rocprim::plus<int64_t>(), st));
     int64_t nnz = 0;
-    GCHK(hipMemcpyAsync(&nnz, rp + V, 8, hipMemcpyDeviceToHost, st));
+    GCHK(hipMemcpyAsync(&nnz, rp + n, 8, hipMemcpyDeviceToHost, st));
     GCHK(hipStreamSynchronize(st));
     mem.release(tmp);
     mem.release(cnt);
     GCHK(mem.alloc(&col, (uint64_t)nnz * 4));
-    hipLaunchKernelGGL(row_write, dim3(grid_of(V)), dim3(kBlk), 0, st, keys, first, rp, V, cb, col_or, col);
+    hipLaunchKernelGGL(row_write, dim3(grid_of(n)), dim3(kBlk), 0, st, keys, first, rp, n, cb, col_or, col);
     GCHK(hipGetLastError());
     GCHK(hipStreamSynchronize(st));
     mem.keep(rp);
     mem.keep(col);
-    *out = {rp, col, V, (uint64_t)nnz};
+    *out = {rp, col, n, (uint64_t)nnz};
     return 0;
 }
 
@@ -561,6 +583,287 @@ int max_degree(const int64_t* d_rp, uint64_t V, hipStream_t st, uint64_t* out, s
     (void)hipFree(d);
     GCHK(e1);
     *out = h;
+    return 0;
+}
+
+
+// ---------------------------------------------------------------------------
+// Vertex-sharded ranks: one rank's own rows [lo, hi) of a symmetric generated
+// graph (build_csr_rows) -> its ghosts, send lists and ghost -> owned lists,
+// all on the device (nothing of the whole graph anywhere). Symmetric: owned u
+// is a ghost on part q iff u has a neighbour in q, so u's send list to q is
+// read off u's own row, in the same ascending-id order as q's ghosts from here.
+namespace {
+
+__device__ __forceinline__ uint32_t part_of(const uint64_t* plo, uint32_t P, uint64_t v) {
+    uint32_t lo = 0, hi = P;  // largest p with plo[p] <= v
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (plo[mid] <= v) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ uint64_t lower_bound32(const uint32_t* a, uint64_t n, uint32_t x) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (a[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// edge k's row (one thread per row)
+__global__ void edge_rows(const int64_t* rp, uint64_t n, uint32_t* erow) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) erow[k] = (uint32_t)i;
+}
+
+// remote columns (~0u for own rows' columns: they sort last)
+__global__ void remote_cols(const uint32_t* col, uint64_t m, uint64_t lo, uint64_t hi, uint32_t* out) {
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = col[k];
+        out[k] = (c >= lo && c < hi) ? ~0u : (uint32_t)c;
+    }
+}
+
+// send keys (part << 32 | owned row), ghost keys (ghost << 32 | owned row);
+// ~0 for an edge inside the part; per-part send counts come after the unique
+__global__ void cut_keys(const uint32_t* col, const uint32_t* erow, uint64_t m, uint64_t lo, uint64_t hi,
+                         const uint64_t* plo, uint32_t P, const uint32_t* ghosts, uint64_t n_ghost, uint64_t* skey,
+                         uint64_t* gkey, unsigned long long* gcnt) {
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = col[k];
+        if (c >= lo && c < hi) {
+            skey[k] = gkey[k] = ~0ull;
+            continue;
+        }
+        const uint64_t gi = lower_bound32(ghosts, n_ghost, (uint32_t)c);
+        skey[k] = ((uint64_t)part_of(plo, P, c) << 32) | erow[k];
+        gkey[k] = (gi << 32) | erow[k];
+        atomicAdd(&gcnt[gi], 1ull);
+    }
+}
+
+__global__ void send_counts(const uint64_t* skey, uint64_t n, unsigned long long* cnt) {
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
+        atomicAdd(&cnt[skey[k] >> 32], 1ull);
+    }
+}
+
+__global__ void low_words(const uint64_t* key, uint64_t n, uint32_t* out) {
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x)
+        out[k] = (uint32_t)key[k];
+}
+
+// ghost -> owned edge j: the owned row, and its entry in the send list to the
+// ghost's part (the list is ascending, so a binary search)
+__global__ void ghost_lists(const uint64_t* gkey, uint64_t m, const uint64_t* recv_off, const uint64_t* send_off,
+                            uint32_t P, const uint32_t* send_idx, uint32_t* gout_col, uint32_t* gout_sidx) {
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t g = gkey[j] >> 32;
+        const uint32_t u = (uint32_t)gkey[j];
+        const uint32_t p = part_of(recv_off, P, g);
+        gout_col[j] = u;
+        gout_sidx[j] = (uint32_t)(send_off[p] + lower_bound32(send_idx + send_off[p], send_off[p + 1] - send_off[p], u));
+    }
+}
+
+// columns -> local rows: own rows first, ghosts from ghost0 (| col_or)
+__global__ void remap_cols(uint32_t* col, uint64_t m, uint64_t lo, uint64_t hi, const uint32_t* ghosts,
+                           uint64_t n_ghost, uint64_t ghost0, uint32_t col_or) {
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = col[k];
+        const uint64_t r = (c >= lo && c < hi) ? c - lo : ghost0 + lower_bound32(ghosts, n_ghost, (uint32_t)c);
+        col[k] = (uint32_t)r | col_or;
+    }
+}
+
+// Every index the round kernels will follow, checked before any of them runs:
+// columns are own rows or ghost rows, receivers own rows, send entries in range.
+__global__ void check_shard(const int64_t* rp, uint64_t n, const uint32_t* col, uint64_t m, uint64_t ghost0,
+                            uint64_t n_ghost, const uint32_t* send_idx, uint64_t n_send, const int64_t* gout_ptr,
+                            const uint32_t* gout_col, const uint32_t* gout_sidx, uint64_t n_cut,
+                            unsigned long long* bad) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (uint64_t)gridDim.x * blockDim.x;
+    unsigned long long b = 0;
+    for (uint64_t k = t; k < m; k += st) {
+        const uint64_t c = col[k] & 0x7fffffffu;
+        b += !(c < n || (c >= ghost0 && c < ghost0 + n_ghost));
+    }
+    for (uint64_t i = t; i < n; i += st) b += rp[i + 1] < rp[i];
+    for (uint64_t k = t; k < n_send; k += st) b += send_idx[k] >= n;
+    for (uint64_t j = t; j < n_cut; j += st) b += gout_col[j] >= n || gout_sidx[j] >= n_send;
+    for (uint64_t g = t; g < n_ghost; g += st) b += gout_ptr[g + 1] < gout_ptr[g];
+    if (b) atomicAdd(bad, b);
+}
+
+// local row -> node id (owned: lo + row; ghosts from ghost0; ~0u padding)
+__global__ void fill_gid(uint64_t rows, uint64_t lo, uint64_t n_own, uint64_t ghost0, const uint32_t* ghosts,
+                         uint64_t n_ghost, uint32_t* gid) {
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (uint64_t)gridDim.x * blockDim.x)
+        gid[r] = r < n_own ? (uint32_t)(lo + r)
+                 : (r >= ghost0 && r < ghost0 + n_ghost) ? ghosts[r - ghost0] : ~0u;
+}
+
+template <class K>
+int sort_unique(K* keys, uint64_t n, int bits, hipStream_t st, uint64_t* n_unique, std::string* err) {
+    Scoped mem;
+    K* alt = nullptr;
+    GCHK(mem.alloc(&alt, n * sizeof(K)));
+    size_t tb = 0;
+    void* tmp = nullptr;
+    {
+        rocprim::double_buffer<K> db(keys, alt);
+        GCHK(rocprim::radix_sort_keys(nullptr, tb, db, (size_t)n, 0, bits, st));
+        GCHK(mem.alloc(&tmp, tb));
+        GCHK(rocprim::radix_sort_keys(tmp, tb, db, (size_t)n, 0, bits, st));
+        if (db.current() != keys) GCHK(hipMemcpyAsync(keys, db.current(), n * sizeof(K), hipMemcpyDeviceToDevice, st));
+    }
+    mem.release(tmp);
+    if (!n_unique) {
+        GCHK(hipStreamSynchronize(st));
+        return 0;
+    }
+    size_t* d_cnt = nullptr;
+    GCHK(mem.alloc(&d_cnt, sizeof(size_t)));
+    tb = 0;
+    GCHK(rocprim::unique(nullptr, tb, keys, alt, d_cnt, (size_t)n, rocprim::equal_to<K>(), st));
+    GCHK(mem.alloc(&tmp, tb));
+    GCHK(rocprim::unique(tmp, tb, keys, alt, d_cnt, (size_t)n, rocprim::equal_to<K>(), st));
+    size_t h = 0;
+    GCHK(hipMemcpyAsync(&h, d_cnt, sizeof(size_t), hipMemcpyDeviceToHost, st));
+    GCHK(hipMemcpyAsync(keys, alt, n * sizeof(K), hipMemcpyDeviceToDevice, st));
+    GCHK(hipStreamSynchronize(st));
+    *n_unique = h;
+    return 0;
+}
+
+}  // namespace
+
+int shard_csr(Csr* g, uint64_t lo, uint64_t hi, const std::vector<uint64_t>& plo, uint64_t ghost0, uint32_t col_or,
+              hipStream_t st, Shard* out, std::string* err) {
+    const uint64_t m = g->nnz, n = hi - lo;
+    const uint32_t P = (uint32_t)plo.size() - 1;
+    Scoped mem;
+    uint32_t* rc = nullptr;  // remote columns -> ghosts
+    uint32_t* erow = nullptr;
+    uint64_t* d_plo = nullptr;
+    GCHK(mem.alloc(&rc, m * 4));
+    GCHK(mem.alloc(&erow, m * 4));
+    GCHK(mem.alloc(&d_plo, plo.size() * 8));
+    GCHK(hipMemcpyAsync(d_plo, plo.data(), plo.size() * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(edge_rows, dim3(grid_of(n)), dim3(kBlk), 0, st, g->row_ptr, n, erow);
+    hipLaunchKernelGGL(remote_cols, dim3(grid_of(m)), dim3(kBlk), 0, st, g->col, m, lo, hi, rc);
+    GCHK(hipGetLastError());
+    uint64_t nu = 0;
+    if (int r = sort_unique(rc, m, 32, st, &nu, err)) return r;
+    std::vector<uint32_t> last(1, 0);
+    if (nu) GCHK(hipMemcpyAsync(last.data(), rc + nu - 1, 4, hipMemcpyDeviceToHost, st));
+    GCHK(hipStreamSynchronize(st));
+    const uint64_t n_ghost = (nu && last[0] == ~0u) ? nu - 1 : nu;
+    out->n_ghost = n_ghost;
+    out->ghosts_host.resize(n_ghost);
+    if (n_ghost) GCHK(hipMemcpyAsync(out->ghosts_host.data(), rc, n_ghost * 4, hipMemcpyDeviceToHost, st));
+    GCHK(hipStreamSynchronize(st));
+    out->recv_off.assign(P + 1, 0);
+    for (uint32_t q = 0; q <= P; ++q)
+        out->recv_off[q] = (uint64_t)(std::lower_bound(out->ghosts_host.begin(), out->ghosts_host.end(),
+                                                       (uint32_t)std::min<uint64_t>(plo[q], 0xffffffffull)) -
+                                      out->ghosts_host.begin());
+    out->recv_off[P] = n_ghost;
+    // cut edges: send keys and ghost keys
+    uint64_t* skey = nullptr;
+    uint64_t* gkey = nullptr;
+    unsigned long long* gcnt = nullptr;
+    GCHK(mem.alloc(&skey, m * 8));
+    GCHK(mem.alloc(&gkey, m * 8));
+    GCHK(mem.alloc(&gcnt, (n_ghost + 1) * 8));
+    GCHK(hipMemsetAsync(gcnt, 0, (n_ghost + 1) * 8, st));
+    hipLaunchKernelGGL(cut_keys, dim3(grid_of(m)), dim3(kBlk), 0, st, g->col, erow, m, lo, hi, d_plo, P, rc, n_ghost,
+                       skey, gkey, gcnt);
+    GCHK(hipGetLastError());
+    mem.release(erow);
+    // send lists: unique (part, row), ascending
+    uint64_t ns = 0;
+    if (int r = sort_unique(skey, m, 64, st, &ns, err)) return r;
+    std::vector<uint64_t> lastk(1, 0);
+    if (ns) GCHK(hipMemcpyAsync(lastk.data(), skey + ns - 1, 8, hipMemcpyDeviceToHost, st));
+    GCHK(hipStreamSynchronize(st));
+    if (ns && lastk[0] == ~0ull) --ns;
+    unsigned long long* scnt = nullptr;
+    GCHK(mem.alloc(&scnt, (P + 1) * 8));
+    GCHK(hipMemsetAsync(scnt, 0, (P + 1) * 8, st));
+    hipLaunchKernelGGL(send_counts, dim3(grid_of(ns)), dim3(kBlk), 0, st, skey, ns, scnt);
+    GCHK(hipGetLastError());
+    std::vector<unsigned long long> sc(P + 1);
+    GCHK(hipMemcpyAsync(sc.data(), scnt, (P + 1) * 8, hipMemcpyDeviceToHost, st));  // the stream is non-blocking:
+    GCHK(hipStreamSynchronize(st));                                                 // copies go on it, then wait
+    out->send_off.assign(P + 1, 0);
+    for (uint32_t q = 0; q < P; ++q) out->send_off[q + 1] = out->send_off[q] + sc[q];
+    GCHK(mem.alloc(&out->send_idx, ns * 4));
+    hipLaunchKernelGGL(low_words, dim3(grid_of(ns)), dim3(kBlk), 0, st, skey, ns, out->send_idx);
+    GCHK(hipGetLastError());
+    out->n_send = ns;
+    mem.release(skey);
+    // ghost -> owned lists: ghost keys sorted (every cut edge once)
+    if (int r = sort_unique<uint64_t>(gkey, m, 64, st, nullptr, err)) return r;
+    uint64_t n_cut = 0;
+    {
+        // the cut edges are the keys before the ~0 tail: their count = sum of gcnt
+        GCHK(mem.alloc(&out->gout_ptr, (n_ghost + 1) * 8));
+        size_t tb = 0;
+        void* tmp = nullptr;
+        GCHK(rocprim::exclusive_scan(nullptr, tb, (int64_t*)gcnt, out->gout_ptr, (int64_t)0, n_ghost + 1,
+                                     rocprim::plus<int64_t>(), st));
+        GCHK(mem.alloc(&tmp, tb));
+        GCHK(rocprim::exclusive_scan(tmp, tb, (int64_t*)gcnt, out->gout_ptr, (int64_t)0, n_ghost + 1,
+                                     rocprim::plus<int64_t>(), st));
+        int64_t h = 0;
+        GCHK(hipMemcpyAsync(&h, out->gout_ptr + n_ghost, 8, hipMemcpyDeviceToHost, st));
+        GCHK(hipStreamSynchronize(st));
+        mem.release(tmp);
+        n_cut = (uint64_t)h;
+    }
+    uint64_t* d_roff = nullptr;
+    uint64_t* d_soff = nullptr;
+    GCHK(mem.alloc(&d_roff, (P + 1) * 8));
+    GCHK(mem.alloc(&d_soff, (P + 1) * 8));
+    GCHK(hipMemcpyAsync(d_roff, out->recv_off.data(), (P + 1) * 8, hipMemcpyHostToDevice, st));
+    GCHK(hipMemcpyAsync(d_soff, out->send_off.data(), (P + 1) * 8, hipMemcpyHostToDevice, st));
+    GCHK(mem.alloc(&out->gout_col, n_cut * 4));
+    GCHK(mem.alloc(&out->gout_sidx, n_cut * 4));
+    hipLaunchKernelGGL(ghost_lists, dim3(grid_of(n_cut)), dim3(kBlk), 0, st, gkey, n_cut, d_roff, d_soff, P,
+                       out->send_idx, out->gout_col, out->gout_sidx);
+    GCHK(hipGetLastError());
+    out->n_cut = n_cut;
+    // columns -> local rows, and the row -> node map
+    hipLaunchKernelGGL(remap_cols, dim3(grid_of(m)), dim3(kBlk), 0, st, g->col, m, lo, hi, rc, n_ghost, ghost0, col_or);
+    GCHK(hipGetLastError());
+    const uint64_t rows = std::max<uint64_t>(64, (ghost0 + n_ghost + 63) / 64 * 64);
+    GCHK(mem.alloc(&out->gid, rows * 4));
+    hipLaunchKernelGGL(fill_gid, dim3(grid_of(rows)), dim3(kBlk), 0, st, rows, lo, n, ghost0, rc, n_ghost, out->gid);
+    GCHK(hipGetLastError());
+    unsigned long long* d_bad = nullptr;
+    GCHK(mem.alloc(&d_bad, 8));
+    GCHK(hipMemsetAsync(d_bad, 0, 8, st));
+    hipLaunchKernelGGL(check_shard, dim3(std::min(grid_of(m), 4096u)), dim3(kBlk), 0, st, g->row_ptr, n, g->col, m,
+                       ghost0, n_ghost, out->send_idx, ns, out->gout_ptr, out->gout_col, out->gout_sidx, n_cut, d_bad);
+    GCHK(hipGetLastError());
+    unsigned long long bad = 0;
+    GCHK(hipMemcpyAsync(&bad, d_bad, 8, hipMemcpyDeviceToHost, st));
+    GCHK(hipStreamSynchronize(st));
+    if (bad || out->send_off[P] != ns) {
+        *err = "shard_csr: " + std::to_string(bad) + " inconsistent indices";
+        return -5;
+    }
+    mem.keep(out->send_idx);
+    mem.keep(out->gout_ptr);
+    mem.keep(out->gout_col);
+    mem.keep(out->gout_sidx);
+    mem.keep(out->gid);
     return 0;
 }
 

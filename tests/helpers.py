@@ -21,11 +21,16 @@ class Scenario:
     enable_sync: bool = True
     windows: list = field(default_factory=list)  # ("seeded", r0, r1, epoch) | ("groups", r0, r1, arr)
     #                                              | ("edges", r0, r1, uint64 bit words over the CSR)
+    gen: dict | None = None  # the same graph as an on-device generator spec (Engine.generate kwargs)
 
 
-def apply(eng, sc: Scenario):
-    """Feed a scenario to an Engine (C ABI) or an O1Network (same method names)."""
-    eng.topology(sc.topo if isinstance(eng, Engine) else sc.topo.rows())
+def apply(eng, sc: Scenario, generate: bool = False):
+    """Feed a scenario to an Engine (C ABI) or an O1Network (same method names);
+    generate: build the graph with the on-device generator (sc.gen)."""
+    if generate:
+        eng.generate(**sc.gen)
+    else:
+        eng.topology(sc.topo if isinstance(eng, Engine) else sc.topo.rows())
     for w in sc.windows:
         if w[0] == "seeded":
             eng.partition_seeded(w[1], w[2], w[3])
@@ -37,11 +42,11 @@ def apply(eng, sc: Scenario):
         eng.broadcast(int(n), int(v), int(r))
 
 
-def make_engine(lib: str, sc: Scenario, track=True, **kw) -> Engine:
+def make_engine(lib: str, sc: Scenario, track=True, generate=False, **kw) -> Engine:
     e = Engine(sc.topo.n_nodes, sc.W, seed=sc.seed, sync_base=sc.sync_base,
                sync_jitter=sc.sync_jitter, enable_sync=sc.enable_sync, track_delivery=track,
                library=lib, **kw)
-    apply(e, sc)
+    apply(e, sc, generate)
     return e
 
 

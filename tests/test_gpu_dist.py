@@ -30,7 +30,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, lib, scenarios, q, lane_groups=1, env=None):
+def _worker(rank, world, port, lib, scenarios, q, lane_groups=1, env=None, generate=False):
     import torch
     import torch.distributed as dist
 
@@ -41,7 +41,7 @@ def _worker(rank, world, port, lib, scenarios, q, lane_groups=1, env=None):
         out = []
         dev = torch.device("cuda", 0)
         for sc in scenarios:
-            e = make_engine(lib, sc, rank=rank, world=world, device=0, lane_groups=lane_groups)
+            e = make_engine(lib, sc, rank=rank, world=world, device=0, lane_groups=lane_groups, generate=generate)
             r = ShardedRunner(e, dev)
             half = sc.rounds // 2
             stats = r.step(half) + r.step(sc.rounds - half)  # two flushes
@@ -56,11 +56,11 @@ def _worker(rank, world, port, lib, scenarios, q, lane_groups=1, env=None):
         dist.destroy_process_group()
 
 
-def _run(lib, scenarios, world, lane_groups=1, env=None):
+def _run(lib, scenarios, world, lane_groups=1, env=None, generate=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, lib, scenarios, q, lane_groups, env))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, lib, scenarios, q, lane_groups, env, generate))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -321,3 +321,42 @@ def test_engine_rccl_plumbing():
         e2.dist_step(1)
     e1.close()
     e2.close()
+
+
+def _gen_scenarios():
+    """Generated graphs: the same graphs as the host builders (gossip_gen.h)."""
+    from ggamd import topology as T
+    from ggamd.workload import uniform_injections
+    return [
+        Scenario(T.grid_links(48, seed=31), 64, 45, uniform_injections(48 * 48, 64, 32), seed=33, sync_base=8,
+                 sync_jitter=4, windows=[("seeded", 3, 9, 7)], gen=dict(kind="grid_links", n=48, seed=31)),
+        Scenario(T.tree(3001, 4), 256, 40, uniform_injections(3001, 200, 34), seed=35, sync_base=6, sync_jitter=3,
+                 gen=dict(kind="tree", n=3001, k=4)),
+        Scenario(T.random_regular(4000, 8, seed=36), 1024, 30, uniform_injections(4000, 900, 37), seed=38,
+                 sync_base=10, sync_jitter=5, gen=dict(kind="random_regular", n=4000, k=8, seed=36)),
+        Scenario(T.rmat(4096, 16, seed=39), 256, 24, uniform_injections(4096, 256, 40), seed=41, sync_base=9,
+                 sync_jitter=3, gen=dict(kind="rmat", n=4096, k=16, seed=39, a=0.57, b=0.19, c=0.19)),
+    ]
+
+
+@pytest.mark.parametrize("world,mode", [(2, "static"), (3, "exact"), (4, "static")])
+def test_device_partition_equals_single(hip_lib, world, mode):
+    """gg_topology_generate on vertex-sharded engines: every rank builds only
+    its node range of the generated graph and its ghosts / send lists on the
+    device (gg_gen::shard_csr). Counters summed over ranks, and every owned
+    node's set and delivery rounds, equal one engine on the host-built graph."""
+    scs = _gen_scenarios()
+    res = _run(hip_lib, scs, world, env={"GG_XCHG_MODE": mode, "GG_HUB_DEG": "40"}, generate=True)
+    for k, sc in enumerate(scs):
+        single = make_engine(hip_lib, sc, device=0)
+        s1 = single.step(sc.rounds)
+        owned_all = []
+        for rank in range(world):
+            stats, owned, bits, dr = res[rank][k]
+            d = diff_stats(s1, stats)
+            assert not d, (k, rank, d[:10])
+            assert np.array_equal(bits, single.read_bits_nodes(owned)), (k, rank)
+            assert np.array_equal(dr, single.delivery_rounds_nodes(owned)), (k, rank)
+            owned_all.append(owned)
+        assert np.array_equal(np.sort(np.concatenate(owned_all)), np.arange(sc.topo.n_nodes)), k
+        single.close()
