@@ -228,6 +228,8 @@ struct gg_engine {
     uint8_t* d_sstate = nullptr;     // [rows] sender states (streamed sync rounds)
     uint64_t* d_ibits = nullptr;     // [rows/64] non-zero sender states
     uint64_t* d_sat = nullptr;       // [rows/64] saturation digest (streamed sync rounds)
+    uint64_t* d_pend = nullptr;      // batched gossip: [rows][nwp] pending values
+    uint32_t* d_pend_src = nullptr;  // batched gossip: [rows] who delivered them
     uint8_t* d_pushany = nullptr;    // [rows] a streamed callback pushed to some peer
     uint2* d_nmeta = nullptr;        // [n_own] node list with the nodes' bytes (streamed sync rounds)
     uint64_t* d_sat_new = nullptr;   // [rows/64] its bits found in the current round
@@ -314,6 +316,8 @@ void gg_engine::free_topology() {
     dfree(d_sat_new);
     dfree(d_pushany);
     dfree(d_nmeta);
+    dfree(d_pend);
+    dfree(d_pend_src);
     dfree(d_hscratch);
     n_hubs = n_hchunks = n_mchunks = 0;
     dfree(d_work);
@@ -405,6 +409,10 @@ int reset_device_state(gg_engine* e) {
     if (e->d_sat) {
         seg(e->d_sat, e->rows / 8, 0);
         seg(e->d_sat_new, e->rows / 8, 0);
+    }
+    if (e->d_pend) {
+        seg(e->d_pend, e->rows * e->nwp * 8, 0);
+        seg(e->d_pend_src, e->rows * 4, ~0ull);
     }
     const uint64_t n_own = e->n_own;
     if (e->d_dr) seg(e->d_dr, n_own * e->nw * 64 * 4, ~0ull);
@@ -634,6 +642,27 @@ uint32_t lanes_through(gg_engine* e, int64_t r) {
     return e->u_hist[r];
 }
 
+template <int G, int WPL>
+void launch_batched_t(const gg::RoundArgs& a, hipStream_t s) {
+    const uint64_t groups = a.n_own, per = gg::kBlock / G;
+    const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((groups + per - 1) / per, 8192));
+    hipLaunchKernelGGL((gg::expand_batched<G, WPL>), dim3(blocks), dim3(gg::kBlock), 0, s, a);
+}
+
+void launch_batched(const gg::RoundArgs& a, hipStream_t s) {
+    switch (a.nwp) {
+        case 1: launch_batched_t<1, 1>(a, s); break;
+        case 2: launch_batched_t<1, 2>(a, s); break;
+        case 4: launch_batched_t<2, 2>(a, s); break;
+        case 8: launch_batched_t<4, 2>(a, s); break;
+        case 16: launch_batched_t<8, 2>(a, s); break;
+        case 32: launch_batched_t<16, 2>(a, s); break;
+        case 64: launch_batched_t<32, 2>(a, s); break;
+        case 128: launch_batched_t<64, 2>(a, s); break;
+        default: break;
+    }
+}
+
 // Round r runs the streamed sync kernels (sync_records + expand_stream_sync):
 // callbacks and pushes reach the expand, no partition window touches rounds
 // r-3..r+1, and the engine has the sync records.
@@ -736,6 +765,20 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     // streamed sync rounds (sync_records + expand_stream_sync): no masks, no in-hubs, nwp >= 2
     const bool sync_stream = syncw && !maskw && e->d_srec != nullptr;
     a.nmeta = sync_stream ? e->d_nmeta : nullptr;
+    if (e->cfg.batch_ticks) {  // batched gossip: one kernel over every node
+        a.pend = e->d_pend;
+        a.pend_src = e->d_pend_src;
+        a.batch_tick = (r + 1) % (int64_t)e->cfg.batch_ticks == 0 ? 1u : 0u;
+        if (n_inj) {
+            hipLaunchKernelGGL(gg::mark_injections, dim3((n_inj + 255) / 256), dim3(256), 0, e->stream, a);
+            HIPCHK(hipGetLastError());
+        }
+        a.dr = e->d_dr;  // first-seen rounds are written by the kernel (F rows hold batches here)
+        a.dr_w = (uint32_t)(e->nw * 64);
+        if (a.n_own) launch_batched(a, e->stream);
+        HIPCHK(hipGetLastError());
+        return GG_OK;
+    }
     if (e->d_pushany) {  // streamed callbacks mark the receivers of their pushes for the next round
         a.pushany = e->d_pushany;
         a.mark_next = (sync_stream && sync_stream_at(e, r + 1)) ? 1u : 0u;
@@ -1114,6 +1157,7 @@ int gg_create(const gg_config* cfg, gg_engine** out) {
     if (cfg->world == 0 || cfg->rank >= cfg->world) return GG_EINVAL;
     const uint32_t L = cfg->lane_groups ? cfg->lane_groups : 1u;
     if (cfg->world % L || L > cfg->n_lanes / 64) return GG_EINVAL;
+    if (cfg->batch_ticks && (cfg->enable_sync || cfg->world != 1)) return GG_EINVAL;  // batched: single, no sync
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GG_EIO;
     auto* e = new gg_engine();
@@ -1214,6 +1258,12 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     dfree(e->d_sat_new);
     dfree(e->d_pushany);
     dfree(e->d_nmeta);
+    dfree(e->d_pend);
+    dfree(e->d_pend_src);
+    if (e->cfg.batch_ticks) {
+        HIPCHK(hipMalloc(&e->d_pend, e->rows * e->nwp * 8));
+        HIPCHK(hipMalloc(&e->d_pend_src, e->rows * 4));
+    }
     if (e->cfg.enable_sync && e->n_hubs == 0 && e->nwp >= 2 && !e->sync_tiles && n_own) {
         HIPCHK(hipMalloc(&e->d_srec, 2 * n_own * sizeof(uint4)));
         HIPCHK(hipMalloc(&e->d_sstate, e->rows));
@@ -1751,6 +1801,7 @@ int gg_topology_export(gg_engine* e, int64_t* row_ptr, int32_t* col, uint64_t ca
 }
 
 static int add_window(gg_engine* e, int64_t a, int64_t b, Window&& w) {
+    if (e->cfg.batch_ticks) return e->fail(GG_EINVAL, "batched gossip has no partition windows");
     if (a >= b) return e->fail(GG_EINVAL, "empty partition window");
     for (const auto& x : e->windows)  // per-edge windows may overlap group windows (and win)
         if (x.edges == w.edges && a < x.to && x.from < b) return e->fail(GG_EINVAL, "overlapping partition windows");

@@ -164,6 +164,12 @@ struct RoundArgs {
     uint32_t push_marked;       // the streamed callbacks of r-1 marked their push receivers and
                                 // wrote pushany: round_prep skips the pushers' out-lists
     uint32_t mark_next;         // this round's callbacks mark their push receivers for r+1
+    uint64_t* pend;             // batched gossip: [rows][nwp] pending values (not yet sent)
+    uint32_t* pend_src;         // batched gossip: [rows] kPendNone, kPendMixed, or the only
+                                // sender's local row | in-edge reciprocal bit << 31
+    uint32_t batch_tick;        // batched gossip: this round ends with a send
+    int32_t* dr;                // batched gossip: first-seen rounds [n_own][dr_w] (GG_TRACK_DELIVERY), or nullptr
+    uint32_t dr_w;
     uint2* nmeta;               // streamed sync rounds: compact_round's node list as (node,
                                 // cand | flg_cur << 8 | sstate << 16), cand cleared; or nullptr
     uint64_t* sat;              // [rows/64] saturation digest (streamed sync rounds, else nullptr):
@@ -2119,6 +2125,163 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
     acc[C_GATHERS] = c_gathers;
     acc[C_NACT] = c_nact;
     acc[C_NACTDEG] = c_nactdeg;
+    acc[C_BYTES] = c_bytes;
+    flush_counters(a, acc, s_red, t_start, K_STREAM);
+}
+
+// ---------------------------------------------------------------------------
+// Batched gossip (gg_config.batch_ticks; new semantics, DESIGN.md §2b — not the
+// parity path): every node, every round. G lanes per node: own set, client
+// broadcasts, the batches its in-neighbours sent last round (their F rows,
+// ascending sender), new values into the pending row; at a send tick the
+// pending row becomes the node's F row (its batch, read by its out-neighbours
+// next round) and one message per out-neighbour is counted, minus one when a
+// single reciprocal neighbour delivered every pending value (the message to it
+// would be empty). F rows are rewritten only when they change (flags: a batch
+// sent two rounds ago in this buffer).
+constexpr uint32_t kPendNone = ~0u, kPendMixed = ~0u - 1;
+template <int G, int WPL>
+__global__ __launch_bounds__(kBlock) void expand_batched(RoundArgs a) {
+    __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
+    const unsigned long long t_start = clock100();
+    const int lg = threadIdx.x % G;
+    const uint32_t off = (uint32_t)lg * WPL;
+    const int gshift = (threadIdx.x & 63) / G * G;
+    const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+    auto group_any = [&](bool x) { return ((__ballot(x) >> gshift) & gmask) != 0; };
+    uint32_t c_new = 0, c_active = 0, c_nact = 0;
+    unsigned long long c_msgs = 0, c_hash = 0, c_bytes = 0, c_gathers = 0;
+    const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
+    const uint64_t first = (uint64_t)blockIdx.x * (kBlock / G) + threadIdx.x / G;
+    // whole groups run the loop together (the group's node, or past the end)
+    const uint64_t bound = (a.n_own + ngroups - 1) / ngroups * ngroups;  // same trip count for every group
+    for (uint64_t i = first; i < bound; i += ngroups) {
+        const bool valid = i < a.n_own;
+        const uint64_t rep = a.own0 + (valid ? i : 0);
+        Row<WPL> S, sp, P;
+        uint32_t src = kPendNone;
+        if (valid) {
+            S = load_row<WPL>(a.base + rep * a.nwp + off);
+            P = load_row<WPL>(a.pend + rep * a.nwp + off);
+            src = a.pend_src[rep];
+        } else {
+#pragma unroll
+            for (int w = 0; w < WPL; ++w) S.w[w] = P.w[w] = 0;
+        }
+        sp = S;
+        // (1) client broadcasts: a new client value goes to every neighbour
+        bool inj_new = false;
+        if (valid && (a.cand[rep] & CA_INJ)) {
+            uint32_t lo = 0, hi = a.n_inj;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (a.inj[2 * mid] < (uint32_t)i) lo = mid + 1;
+                else hi = mid;
+            }
+            for (uint32_t q = lo; q < a.n_inj && a.inj[2 * q] == (uint32_t)i; ++q) {
+                const uint32_t ln = a.inj[2 * q + 1];
+                const uint32_t word = ln >> 6;
+                if (word / WPL == (uint32_t)lg) {
+                    Row<WPL> b;
+#pragma unroll
+                    for (int w = 0; w < WPL; ++w) b.w[w] = 0;
+                    set_lane_bit<WPL>(b, word % WPL, ln & 63);
+#pragma unroll
+                    for (int w = 0; w < WPL; ++w) {
+                        inj_new |= (b.w[w] & ~S.w[w]) != 0;
+                        S.w[w] |= b.w[w];
+                    }
+                }
+            }
+        }
+        if (group_any(inj_new)) src = kPendMixed;
+        // (2) last round's batches, ascending sender
+        const int64_t p0 = valid ? a.in_ptr[i] : 0, p1 = valid ? a.in_ptr[i + 1] : 0;
+        for (int64_t e = p0; e < p1; ++e) {
+            const uint32_t c = a.in_col[e];
+            const Row<WPL> x = load_row<WPL>(a.F_prev + (uint64_t)(c & kColMask) * a.nwp + off);
+            bool got = false;
+#pragma unroll
+            for (int w = 0; w < WPL; ++w) {
+                const uint64_t cw = x.w[w] & ~S.w[w];
+                S.w[w] |= cw;
+                got |= cw != 0;
+            }
+            if (group_any(got)) {
+                const uint32_t u = (c & kColMask) | (c & kRecipBit);
+                src = src == kPendNone ? u : ((src != kPendMixed && (src & kColMask) == (c & kColMask)) ? src : kPendMixed);
+            }
+        }
+        // new state
+        Row<WPL> F;
+        uint32_t T = 0;
+        bool pend_any = false;
+        const uint64_t g = gid_of(a, i);
+#pragma unroll
+        for (int w = 0; w < WPL; ++w) {
+            F.w[w] = S.w[w] & ~sp.w[w];
+            T += __popcll(F.w[w]);
+            if (F.w[w]) c_hash += gg_word_hash(g * a.nw + a.word0 + off + w, F.w[w]);
+            if (a.dr && valid && off + w < a.dr_w / 64) {
+                uint64_t y = F.w[w];
+                while (y) {
+                    const int b = __builtin_ctzll(y);
+                    y &= y - 1;
+                    a.dr[i * a.dr_w + (off + w) * 64 + b] = (int32_t)a.round;
+                }
+            }
+            P.w[w] |= F.w[w];
+            pend_any |= P.w[w] != 0;
+        }
+        const bool any = group_any(T != 0);
+        const bool send = a.batch_tick && group_any(pend_any);
+        if (valid) {
+            if (any) store_row<WPL>(a.base + rep * a.nwp + off, S);
+            const uint8_t fl = a.flg_cur[rep];  // a batch of round r-2 in this F buffer
+            if (send || (fl & FL_ACT)) {
+                Row<WPL> out;
+#pragma unroll
+                for (int w = 0; w < WPL; ++w) out.w[w] = send ? P.w[w] : 0ull;
+                store_row<WPL>(a.F_cur + rep * a.nwp + off, out);
+            }
+            if (send) {
+#pragma unroll
+                for (int w = 0; w < WPL; ++w) P.w[w] = 0;
+            }
+            if (any || send) store_row<WPL>(a.pend + rep * a.nwp + off, P);
+            if (lg == 0) {
+                if (send || fl) a.flg_cur[rep] = send ? FL_ACT : 0;
+                if (a.cand[rep]) a.cand[rep] = 0;
+                unsigned long long msgs = 0;
+                if (send) {
+                    msgs = (unsigned long long)(a.out_ptr[i + 1] - a.out_ptr[i]);
+                    // one reciprocal neighbour delivered every pending value: no message to it
+                    if (src != kPendMixed && src != kPendNone && (src & kRecipBit)) msgs--;
+                }
+                const uint32_t nsrc = a.batch_tick ? kPendNone : src;
+                if (nsrc != a.pend_src[rep]) a.pend_src[rep] = nsrc;
+                c_msgs += msgs;
+                c_active += 1;
+                c_nact += send ? 1u : 0u;
+                c_gathers += (unsigned long long)(p1 - p0);
+                const unsigned long long rowb = 8ull * a.nwp;
+                c_bytes += 16 + 4ull * (p1 - p0) + rowb * (2 + (p1 - p0)) + (any ? rowb : 0) +
+                           ((send || (fl & FL_ACT)) ? rowb : 0) + ((any || send) ? rowb : 0);
+            }
+            c_new += T;
+        }
+    }
+    unsigned long long acc[C_NUM];
+#pragma unroll
+    for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
+    acc[C_NEW] = c_new;
+    acc[C_FWD_SENT] = c_msgs;
+    acc[C_FWD_DELIV] = c_msgs;
+    acc[C_NEXT_ACKS] = c_msgs;
+    acc[C_HASH] = c_hash;
+    acc[C_ACTIVE] = c_active;
+    acc[C_GATHERS] = c_gathers;
+    acc[C_NACT] = c_nact;
     acc[C_BYTES] = c_bytes;
     flush_counters(a, acc, s_red, t_start, K_STREAM);
 }

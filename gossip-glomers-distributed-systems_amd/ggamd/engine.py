@@ -40,6 +40,7 @@ class GGConfig(C.Structure):
         ("rank", C.c_uint32),
         ("world", C.c_uint32),
         ("lane_groups", C.c_uint32),
+        ("batch_ticks", C.c_uint32),
     ]
 
 
@@ -204,11 +205,12 @@ class Engine:
     def __init__(self, n_nodes: int, n_lanes: int, *, seed: int = 0, sync_base: int = 20,
                  sync_jitter: int = 10, enable_sync: bool = True, track_delivery: bool = False,
                  device: int = -1, rank: int = 0, world: int = 1, lane_groups: int = 1,
-                 library: str | None = None):
+                 batch_ticks: int = 0, library: str | None = None):
         self.lib = load_library(library or HIP_LIB)
         self.library = os.path.abspath(library or HIP_LIB)
         cfg = GGConfig(n_nodes, n_lanes, GG_TRACK_DELIVERY if track_delivery else 0, seed,
-                       sync_base, sync_jitter, 1 if enable_sync else 0, device, rank, world, lane_groups)
+                       sync_base, sync_jitter, 1 if enable_sync else 0, device, rank, world, lane_groups,
+                       batch_ticks)
         h = C.c_void_p()
         rc = self.lib.gg_create(C.byref(cfg), C.byref(h))
         if rc != 0:

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 3
+#define GG_ABI_VERSION 4
 
 #define GG_OK 0
 #define GG_EIO (-5)
@@ -84,6 +84,13 @@ typedef struct {
                                    of different groups never exchange anything (a value's propagation
                                    depends on no other value), so lane_groups == world needs no
                                    exchange at all and such an engine runs with gg_step. */
+    uint32_t batch_ticks;       /* 0: the reference's semantics (parity mode). B >= 1: batched gossip,
+                                   new semantics: a node keeps the
+                                   values it learns as pending and, at the end of every round r with
+                                   (r+1) % B == 0, sends ONE `broadcast` message per out-neighbour
+                                   carrying its pending values (none to a neighbour that delivered all
+                                   of them first); fwd_sent/fwd_delivered/acks count messages, not
+                                   values. Single engine, no sync timers, no partition windows. */
 } gg_config;
 
 typedef struct {

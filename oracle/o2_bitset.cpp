@@ -96,6 +96,9 @@ struct gg_engine {
     std::vector<int64_t> sync_next;        // owned
     std::vector<uint32_t> sync_k;
     std::vector<int32_t> dr;               // owned rows * W
+    // batched gossip (cfg.batch_ticks): pending values, and who delivered them
+    std::vector<uint64_t> pend;            // owned rows * nw
+    std::vector<uint32_t> pend_src;        // owned: kNone, kMixed, or the only sender (global id)
     std::vector<Window> windows;
     std::unordered_map<int64_t, uint32_t> lanes;
     std::vector<int64_t> lane_value;
@@ -160,6 +163,8 @@ struct gg_engine {
             sync_next[i] = gg_sync_interval(cfg.seed, lo + i, 0, cfg.sync_base_ticks, cfg.sync_jitter_ticks);
         }
         std::fill(dr.begin(), dr.end(), -1);
+        std::fill(pend.begin(), pend.end(), 0ull);
+        std::fill(pend_src.begin(), pend_src.end(), ~0u);
         lanes.clear();
         lane_value.clear();
         inj.clear();
@@ -169,7 +174,97 @@ struct gg_engine {
         dist_open = false;
     }
     void compute_round(Acc& total);
+    void compute_round_batched(Acc& total);
 };
+
+// Batched gossip (gg_config.batch_ticks = B >= 1; new semantics, not the
+// reference's): per node v in round r, (1) client broadcasts, (2) the batches
+// sent to v in r-1, ascending sender (a value's first deliverer is its
+// claimer), new values join v's pending set P; at the end of a round with
+// (r+1) % B == 0, v sends P to every out-neighbour w in one message, except to
+// a w that delivered every value of P first (the message would
+// be empty: rebroadcastAllExcept's exclusion, per batch). pend_src tracks that:
+// kNone (P empty), kMixed (several deliverers or a client), or the one sender.
+void gg_engine::compute_round_batched(Acc& a) {
+    constexpr uint32_t kNone = ~0u, kMixed = ~0u - 1;
+    const int64_t r = round;
+    const uint64_t n_own = hi - lo;
+    const uint32_t W = (uint32_t)(nw * 64);
+    std::vector<uint64_t>& sp_all = seen[(r + 1) & 1];
+    std::vector<uint64_t>& sc_all = seen[r & 1];
+    std::vector<uint64_t>& Fp_all = F[(r + 1) & 1];
+    std::vector<uint64_t>& Fc_all = F[r & 1];
+    std::unordered_map<uint32_t, std::vector<uint32_t>> inj_by_node;
+    {
+        auto it = inj.find(r);
+        if (it != inj.end()) {
+            for (const auto& x : it->second) inj_by_node[x.node].push_back(x.lane);
+            inj.erase(it);
+        }
+    }
+    const bool tick = (r + 1) % (int64_t)cfg.batch_ticks == 0;
+    std::vector<uint64_t> S(nw), sp(nw);
+    for (uint64_t i = 0; i < n_own; ++i) {
+        const uint64_t g = lo + i;
+        for (uint64_t j = 0; j < nw; ++j) sp[j] = S[j] = sp_all[i * nw + j];
+        uint32_t& src = pend_src[i];
+        auto ij = inj_by_node.find((uint32_t)g);  // (1) client broadcasts
+        if (ij != inj_by_node.end())
+            for (uint32_t lane : ij->second) {
+                const uint64_t b = 1ull << (lane & 63);
+                if (!(S[lane >> 6] & b)) src = kMixed;  // a client value goes to every neighbour
+                S[lane >> 6] |= b;
+            }
+        for (int64_t e = in_ptr[i]; e < in_ptr[i + 1]; ++e) {  // (2) batches, ascending sender
+            const uint64_t u = in_col[e];
+            const uint64_t* x = &Fp_all[u * nw];
+            bool got = false;
+            for (uint64_t j = 0; j < nw; ++j) {
+                const uint64_t c = x[j] & ~S[j];
+                S[j] |= c;
+                got |= c != 0;
+            }
+            if (got) src = src == kNone ? (uint32_t)u : (src == (uint32_t)u ? src : kMixed);
+        }
+        uint64_t* sc = &sc_all[i * nw];
+        uint64_t* fc = &Fc_all[i * nw];
+        uint64_t* P = &pend[i * nw];
+        bool pend_any = false;
+        for (uint64_t j = 0; j < nw; ++j) {
+            sc[j] = S[j];
+            const uint64_t f = S[j] & ~sp[j];
+            a.new_bits += popc(f);
+            if (f) a.hash += gg_word_hash(g * nw_g + w0 + j, f);
+            if (f && !dr.empty()) {
+                uint64_t y = f;
+                while (y) {
+                    int b = __builtin_ctzll(y);
+                    y &= y - 1;
+                    dr[i * W + j * 64 + b] = (int32_t)r;
+                }
+            }
+            P[j] |= f;
+            pend_any |= P[j] != 0;
+            fc[j] = 0;
+        }
+        if (tick) {
+            if (pend_any) {
+                uint64_t msgs = (uint64_t)(out_ptr[i + 1] - out_ptr[i]);
+                if (src != kMixed && src != kNone &&
+                    std::binary_search(out_col.begin() + out_ptr[i], out_col.begin() + out_ptr[i + 1], src))
+                    msgs--;  // that neighbour delivered every pending value: no message to it
+                a.fwd_sent += msgs;
+                a.fwd_deliv += msgs;
+                a.next_acks += msgs;
+                for (uint64_t j = 0; j < nw; ++j) {
+                    fc[j] = P[j];
+                    P[j] = 0;
+                }
+            }
+            src = kNone;
+        }
+    }
+}
 
 void gg_engine::compute_round(Acc& total) {
     const int64_t r = round;
@@ -356,6 +451,7 @@ int gg_create(const gg_config* cfg, gg_engine** out) {
     if (cfg->world == 0 || cfg->rank >= cfg->world) return GG_EINVAL;
     const uint32_t L = cfg->lane_groups ? cfg->lane_groups : 1u;
     if (cfg->world % L || L > cfg->n_lanes / 64) return GG_EINVAL;
+    if (cfg->batch_ticks && (cfg->enable_sync || cfg->world != 1)) return GG_EINVAL;  // batched: single, no sync
     auto* e = new gg_engine();
     e->cfg = *cfg;
     e->V = cfg->n_nodes;
@@ -464,6 +560,8 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     e->sync_k.assign(n_own, 0);
     if (e->cfg.flags & GG_TRACK_DELIVERY) e->dr.assign(n_own * e->nw * 64, -1);
     else e->dr.clear();
+    e->pend.assign(e->cfg.batch_ticks ? n_own * e->nw : 0, 0ull);
+    e->pend_src.assign(e->cfg.batch_ticks ? n_own : 0, ~0u);
     e->have_topo = true;
     e->reset_state();
     return GG_OK;
@@ -471,6 +569,7 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
 
 static int add_window(gg_engine* e, int64_t a, int64_t b, Window&& w) {
     if (!e) return GG_EINVAL;
+    if (e->cfg.batch_ticks) return e->fail(GG_EINVAL, "batched gossip has no partition windows");
     if (a >= b) return e->fail(GG_EINVAL, "empty partition window");
     for (const auto& x : e->windows)  // per-edge windows may overlap group windows (and win)
         if (x.edges == w.edges && a < x.to && x.from < b) return e->fail(GG_EINVAL, "overlapping partition windows");
@@ -582,7 +681,8 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
     if (e->P != 1) return e->fail(GG_EINVAL, "vertex-sharded engine: use gg_dist_round_begin/end");
     for (uint32_t k = 0; k < n; ++k) {
         Acc a;
-        e->compute_round(a);
+        if (e->cfg.batch_ticks) e->compute_round_batched(a);
+        else e->compute_round(a);
         gg_round_stats s;
         fill_stats(e, a, &s);
         if (out) out[k] = s;

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol(lib, cpu_lib):
     missing = [n for n in _declared(os.path.join(REPO, "include", "gossip.h")) if not hasattr(dll, n)]
     assert not missing, missing
     dll.gg_abi_version.restype = C.c_int
-    assert dll.gg_abi_version() == 3
+    assert dll.gg_abi_version() == 4
 
 
 def test_host_builders_export_every_declared_symbol():
