@@ -360,3 +360,26 @@ def test_device_partition_equals_single(hip_lib, world, mode):
             owned_all.append(owned)
         assert np.array_equal(np.sort(np.concatenate(owned_all)), np.arange(sc.topo.n_nodes)), k
         single.close()
+
+
+def test_device_partition_with_lane_groups(hip_lib):
+    """2 lane groups x 2 device-built vertex parts (world 4): counters summed
+    over all ranks equal one engine; sets OR-ed and delivery rounds max-ed
+    over a node's owners equal its own."""
+    scs = [sc for sc in _gen_scenarios() if sc.W // 64 >= 2]
+    res = _run(hip_lib, scs, 4, lane_groups=2, env={"GG_XCHG_MODE": "exact"}, generate=True)
+    for k, sc in enumerate(scs):
+        single = make_engine(hip_lib, sc, device=0)
+        s1 = single.step(sc.rounds)
+        V = sc.topo.n_nodes
+        bits = np.zeros((V, sc.W // 64), np.uint64)
+        dr = np.full((V, sc.W), -1, np.int32)
+        for rank in range(4):
+            stats, owned, b, d = res[rank][k]
+            assert not diff_stats(s1, stats), (k, rank, diff_stats(s1, stats)[:10])
+            o = owned.astype(np.int64)
+            bits[o] |= b
+            dr[o] = np.maximum(dr[o], d)
+        assert np.array_equal(bits, single.read_bits()), k
+        assert np.array_equal(dr, single.delivery_rounds()), k
+        single.close()
