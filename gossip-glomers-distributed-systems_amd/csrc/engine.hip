@@ -211,6 +211,7 @@ struct gg_engine {
     uint32_t* d_nodes = nullptr;     // [n_own] candidate-node list (sparse lean rounds)
     uint32_t* d_act = nullptr;       // [4] ring: nodes that became active per round
     unsigned long long* d_act_deg = nullptr;  // [4] ring: their out-degree sums
+    unsigned long long* d_tot = nullptr;      // [4] ring: new bits of the owned nodes in rounds <= r
     uint64_t* d_abits = nullptr;     // [rows/64] ACT bits of the previous round (flags-first rounds)
     bool ff_ok = false;              // flags-first gathers allowed
     // hubs (see expand_kernels.hpp): in-edge chunks of high in-degree nodes,
@@ -325,6 +326,7 @@ void gg_engine::free_topology() {
     dfree(d_nodes);
     dfree(d_act);
     dfree(d_act_deg);
+    dfree(d_tot);
     dfree(d_abits);
     for (auto& p : d_fired) dfree(p);
     dfree(d_sync_next);
@@ -406,6 +408,7 @@ int reset_device_state(gg_engine* e) {
     seg(e->d_tile_cand, e->tile_bytes, 0);
     seg(e->d_act, 16, 0);
     seg(e->d_act_deg, 32, 0);
+    seg(e->d_tot, 32, 0);
     if (e->d_sat) {
         seg(e->d_sat, e->rows / 8, 0);
         seg(e->d_sat_new, e->rows / 8, 0);
@@ -742,6 +745,9 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     }
     a.inj = d_inj;
     a.n_inj = n_inj;
+    static const bool no_full = getenv("GG_ALL_FULL") && atoi(getenv("GG_ALL_FULL")) == 0;  // A/B
+    a.tot = no_full ? nullptr : e->d_tot;
+    a.full_new = (unsigned long long)e->n_own * lanes_through(e, r - 1);
     a.counters = d_ctr;
     a.n_own = e->n_own;
     a.own0 = 0;
@@ -773,6 +779,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             hipLaunchKernelGGL(gg::mark_injections, dim3((n_inj + 255) / 256), dim3(256), 0, e->stream, a);
             HIPCHK(hipGetLastError());
         }
+        a.tot = nullptr;  // no round_prep here to start each round's slot
         a.dr = e->d_dr;  // first-seen rounds are written by the kernel (F rows hold batches here)
         a.dr_w = (uint32_t)(e->nw * 64);
         if (a.n_own) launch_batched(a, e->stream);
@@ -996,7 +1003,7 @@ int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& o
     for (size_t t = 0; t < 2 * total; ++t) h = gg_mix64(h ^ e->h_inj[t]);
     for (size_t k = 0; k <= m; ++k) h = gg_mix64(h ^ off[k]);
     key.inj_hash = h;
-    if (e->d_sat) {
+    {  // the digest's usat and the all-full test's full_new follow the lanes injected so far
         uint64_t u = gg_mix64(~0ull);
         for (int64_t q = r0 - 1; q < r0 + (int64_t)m; ++q) u = gg_mix64(u ^ lanes_through(e, q));
         key.u_hash = u;
@@ -1301,6 +1308,7 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     HIPCHK(hipMalloc(&e->d_nodes, std::max<uint64_t>(1, n_own) * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->d_act, 4 * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->d_act_deg, 4 * 8));
+    HIPCHK(hipMalloc(&e->d_tot, 4 * 8));
     // flags-first gathers (ff_round): rows of >= 64 B (the request-rate-bound
     // regime) and a mean in-degree >= 4; GG_FLAGS_FIRST=0/1 overrides
     {

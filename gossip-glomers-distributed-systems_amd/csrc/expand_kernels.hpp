@@ -139,6 +139,9 @@ struct RoundArgs {
     unsigned long long* act_deg;  // [4] ring: their out-degree sum (edges carrying F rows next round)
     uint64_t* abits;            // [rows/64] bit u: sender u is ACT in round r-1 (pack_act_bits; flags-first)
     int32_t ff_ok;              // flags-first gathers allowed (engine choice: W/64 >= 8, mean degree >= 4)
+    unsigned long long* tot;    // [4] ring: new bits of the owned nodes in rounds <= r (slot r&3), or nullptr
+    unsigned long long full_new;  // n_own x lanes injected in rounds <= r-1: tot of r-1 equal to it means
+                                  // every owned set holds every injected lane (sets hold injected lanes only)
     // hubs (lean rounds): owned nodes with in-degree > hub_deg skip expand_stream
     // and take hub_chunks + hub_finish; senders with out-degree > hub_deg are
     // marked by hub_mark instead of round_prep (0: no hubs)
@@ -288,6 +291,13 @@ __device__ __forceinline__ bool ff_round(const RoundArgs& a) {
            2.0 * (double)a.act_deg[(a.round - 1) & 3] < (double)a.n_edges;
 }
 
+// Every owned node already holds every lane injected so far and the round
+// injects nothing: no set can change (e.g. the quiescence round that ends an
+// episode), so a lean round gathers nothing; only stale F rows are cleared.
+__device__ __forceinline__ bool all_full(const RoundArgs& a) {
+    return a.tot && a.n_inj == 0 && a.tot[(a.round - 1) & 3] == a.full_new;
+}
+
 // Original node id of local row i (hashes, sync timers, partition groups).
 __device__ __forceinline__ uint64_t gid_of(const RoundArgs& a, uint64_t i) {
     return a.gid ? (uint64_t)a.gid[i] : a.lo + i;
@@ -435,6 +445,7 @@ __device__ __forceinline__ void flush_counters(const RoundArgs& a, unsigned long
         if (s) atomicAdd(&a.counters[(blockIdx.x % kSlots) * kCounters + idx], s);
         if (threadIdx.x == C_NACT && s) atomicAdd(&a.act[a.round & 3], (uint32_t)s);
         if (threadIdx.x == C_NACTDEG && s && a.act_deg) atomicAdd(&a.act_deg[a.round & 3], s);
+        if (threadIdx.x == C_NEW && s && a.tot) atomicAdd(&a.tot[a.round & 3], s);
     }
     if (threadIdx.x == 0) stamp(a, kind, t_start);
 }
@@ -453,6 +464,7 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
         a.act[(a.round + 1) & 3] = 0;  // next round's act slot
         if (a.act_deg) a.act_deg[(a.round + 1) & 3] = 0;
         a.n_work[0] = a.n_work[1] = 0;  // compact_round runs after this kernel
+        if (a.tot) a.tot[a.round & 3] = a.round > 0 ? a.tot[(a.round - 1) & 3] : 0ull;  // expand kernels add
     }
     if (a.sat) {  // last round's digest bits in (readers of this round see rounds < r only)
         const uint64_t nw = (a.n_own + 63) / 64;
@@ -1243,6 +1255,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         return;
     }
     const bool ff = !MASKW && ff_round(a);  // flags-first gathers (block-uniform)
+    const bool full = !MASKW && all_full(a);  // nothing can arrive: no gathers, no own rows
     constexpr uint32_t kAllD = (1u << D) - 1u;
     // per-lane counts that fit 32 bits stay 32-bit (register budget)
     uint32_t c_new = 0, c_active = 0, c_gathers = 0, c_nact = 0, c_nactdeg = 0;
@@ -1277,6 +1290,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             m.deg = (uint32_t)(a.in_ptr[n + 1] - m.p0);
             m.ca = a.cand[a.own0 + n];      // CA_INJ: client broadcasts this round
             m.fl = a.flg_cur[a.own0 + n];   // flags of round r-2 (ACT: stale F row)
+            if (full) m.deg = 0;
             if (a.hub_deg && m.deg > a.hub_deg) {  // a hub: hub_chunks/hub_finish take it
                 m.node |= kHubBit;
                 m.deg = 0;
@@ -1310,7 +1324,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         const uint64_t rep = a.own0 + i;
         // (a) DMA node i's own row and its first D sender rows (masked rounds:
         // and the words of the window bitmaps covering its first D in-edges)
-        if (!hub) dma16((const void*)(a.base + rep * a.nwp + off), my + D * 1024);
+        if (!hub && !full) dma16((const void*)(a.base + rep * a.nwp + off), my + D * 1024);
         uint64_t mw[3][2];
         if constexpr (MASKW) {
 #pragma unroll
@@ -1334,10 +1348,13 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         const uint32_t n3 = node_of(k + 3 * stride);
         vm_drain();
         if (!hub) {
-        const ulonglong2 o = *reinterpret_cast<const ulonglong2*>(my + D * 1024 + lane16);
         Row<WPL> sp, S;
-        sp.w[0] = o.x;  // lean rounds precede every sync timer: no LAG
-        sp.w[1] = o.y;
+        sp.w[0] = sp.w[1] = 0;
+        if (!full) {
+            const ulonglong2 o = *reinterpret_cast<const ulonglong2*>(my + D * 1024 + lane16);
+            sp.w[0] = o.x;  // lean rounds precede every sync timer: no LAG
+            sp.w[1] = o.y;
+        }
         S = sp;
         if (m0.ca & CA_INJ) {  // (1) client broadcasts of this round
             uint32_t lo = 0, hi = a.n_inj;
@@ -1416,6 +1433,9 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             uint32_t cb[D];
 #pragma unroll
             for (int b = 0; b < D; ++b) cb[b] = e + b < p1 ? a.in_col[e + b] : 0u;
+            // one wait for the columns: the compiler cannot see the DMAs below, so
+            // without it each DMA would get a vmcnt(0) of its own (serialising them)
+            vm_drain();
             // flags-first: only the active senders' rows (bits looked up first)
             const uint32_t am = ff ? active_senders<G, D>(a.abits, cb, (uint32_t)(p1 - e), lg, gbase) : kAllD;
 #pragma unroll
@@ -1486,7 +1506,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             if constexpr (!MASKW) c_nactdeg += any ? (uint32_t)deg : 0u;  // masked rounds: no flags-first next
             // row_ptr + cand + flag bytes + col (+ a sender bit, flags-first), own row + gathered
             // sender rows, F / base / flag writes
-            c_bytes += (dense ? 0 : 4) + 8 + 2 + 4 * nin + (ff ? (nin + 7) / 8 : 0) + rowb +
+            c_bytes += (dense ? 0 : 4) + 8 + 2 + 4 * nin + (ff ? (nin + 7) / 8 : 0) + (full ? 0 : rowb) +
                        ((any || zm) ? rowb : 0) + (any ? rowb + 1 : 0);
         }
         }  // !hub
@@ -1553,6 +1573,7 @@ void expand_stream1(RoundArgs a) {
     uint32_t c_new = 0, c_active = 0, c_gathers = 0, c_nact = 0;
     unsigned long long c_fwd = 0, c_hash = 0, c_bytes = 0, c_nactdeg = 0;
     const uint32_t stride = gridDim.x * kBlock;
+    const bool full = all_full(a);  // nothing can arrive: no gathers, no own rows
 
     struct Meta {
         int64_t p0;
@@ -1571,6 +1592,7 @@ void expand_stream1(RoundArgs a) {
             m.deg = (uint32_t)(a.in_ptr[n + 1] - m.p0);
             m.ca = a.cand[a.own0 + n];
             m.fl = a.flg_cur[a.own0 + n];
+            if (full) m.deg = 0;
             if (a.hub_deg && m.deg > a.hub_deg) {
                 m.node |= kHubBit;
                 m.deg = 0;
@@ -1600,7 +1622,7 @@ void expand_stream1(RoundArgs a) {
         const uint64_t rep = a.own0 + i;
         // (a) own row and the first D sender rows
         uint64_t sp = 0, src[D];
-        if (!hub) sp = a.base[rep];
+        if (!hub && !full) sp = a.base[rep];
 #pragma unroll
         for (int b = 0; b < D; ++b) src[b] = ((uint32_t)b < m0.deg) ? a.F_prev[c0[b] & kColMask] : 0ull;
         // (b) prefetch the next items' columns, row pointers and list entry
@@ -1663,7 +1685,8 @@ void expand_stream1(RoundArgs a) {
             c_active += 1;
             c_nact += any ? 1 : 0;
             c_nactdeg += any ? deg : 0;
-            c_bytes += (dense ? 0 : 4) + 8 + 2 + 4ull * nin + 8ull * (1 + nin) + ((any || zm) ? 8 : 0) + (any ? 9 : 0);
+            c_bytes += (dense ? 0 : 4) + 8 + 2 + 4ull * nin + 8ull * ((full ? 0 : 1) + nin) + ((any || zm) ? 8 : 0) +
+                       (any ? 9 : 0);
         }
         m0 = m1;
         m1 = m2;
