@@ -57,13 +57,20 @@ namespace gg {
 #endif
 
 // Sender rows a lane keeps in flight (LDS slots) in expand_stream, and its occupancy.
+// 4: the lean kernel fits 95 VGPRs (5 waves/SIMD) and the masked one 123 without
+// spills (6: 103 / 128 + 28 B scratch); A/B at 2M nodes: C3 7.88 -> 6.97 ms per
+// episode, C2 equal (its internal nodes take a second batch of one row)
 #ifndef GG_STREAM_ROWS
-#define GG_STREAM_ROWS 6
+#define GG_STREAM_ROWS 4
 #endif
 #ifndef GG_STREAM_WAVES_PER_EU
 #define GG_STREAM_WAVES_PER_EU 4
 #endif
 constexpr int kStreamRows = GG_STREAM_ROWS;
+// Sender rows a lane of expand_stream1 (W = 64) keeps in flight.
+#ifndef GG_STREAM1_ROWS
+#define GG_STREAM1_ROWS 8
+#endif
 
 // Sender (flag, row) pairs a lane keeps in flight in dense lean rounds.
 #ifndef GG_SPEC_BATCH
@@ -261,6 +268,12 @@ __device__ __forceinline__ void store_row(uint64_t* p, const Row<WPL>& r) {
 #pragma unroll
         for (int k = 0; k < WPL; ++k) p[k] = r.w[k];
     }
+}
+
+// 16-byte non-temporal store of a lane's two words
+__device__ __forceinline__ void store_row_nt(uint64_t* p, const Row<2>& r) {
+    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store((u64x2){r.w[0], r.w[1]}, reinterpret_cast<u64x2*>(p));
 }
 
 __device__ __forceinline__ bool bit_at(const uint64_t* bm, uint64_t row) {
@@ -1484,8 +1497,11 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         }
         const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
         const bool zm = (m0.fl & FL_ACT) != 0;  // F row of round r-2 in this buffer
-        if (any || zm) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
-        if (any) store_row<WPL>(a.base + rep * a.nwp + off, S);
+        // rows written this round are read next round from HBM anyway (F by
+        // other nodes' gathers, base by this node): streamed past the caches,
+        // they leave L2 to the gathers (C2 -2.5%, C3 -1.4% kernel time)
+        if (any || zm) store_row_nt(a.F_cur + rep * a.nwp + off, F);
+        if (any) store_row_nt(a.base + rep * a.nwp + off, S);
         if (lg == 0) {
             if (any || m0.fl) a.flg_cur[rep] = any ? FL_ACT : 0;
             if (m0.ca) a.cand[rep] = 0;
@@ -1557,7 +1573,7 @@ void expand_stream_masked(RoundArgs a) {
 // as expand_stream.
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GG_STREAM_WAVES_PER_EU)))
 void expand_stream1(RoundArgs a) {
-    constexpr int D = 8;  // sender rows in flight per lane
+    constexpr int D = GG_STREAM1_ROWS;  // sender rows in flight per lane
     __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
     const unsigned long long t_start = clock100();
     if (!a.stream_ok) {
