@@ -1,0 +1,87 @@
+"""BASELINE.json's two largest configs at their full size, in the GPU suite
+(graphs built in HBM by the on-device generators, gossip_gen.h).
+
+* C5, 2^30 nodes (grid + one long link per node, W = 64): the grid spans
+  every node, so each message must reach all V nodes (P1), and before any
+  sync timer fires every node forwards each value to all neighbours but its
+  claimer, so forwards = K (nnz - (V - 1)) (KAT-3 / P2); every delivered
+  broadcast is acked one round later. Checked round by round to quiescence.
+* C4, 10^8 nodes (R-MAT, W = 4096): the single engine against the two
+  lane-group ranks of a 2-GPU strong-scaling job run one after the other on
+  this GPU (gg_config.lane_groups: 2048 lanes each, another kernel
+  instantiation over another row width): every round's counters and delivery
+  hash, summed over the ranks, equal the single engine's.
+The reference has no full-size fixtures; these are size-independent
+properties of broadcast.go's algorithm, the CPU oracle O2 is
+pinned against it at 4K nodes (tests/test_golden.py).
+"""
+import pytest
+
+from ggamd.engine import COUNT_FIELDS, Engine
+from ggamd.workload import BASE_SEED, inject, injection_arrays, uniform_injections
+
+pytestmark = pytest.mark.gpu
+
+M64 = (1 << 64) - 1
+
+
+def _to_quiescence(e, inj, cap=60):
+    inject(e, inj)
+    out = []
+    while True:
+        s = e.step(1)[0]
+        out.append(s)
+        if (s["new_bits"] == 0 and len(out) > 1) or len(out) >= cap:
+            return out
+
+
+def test_c5_full_size_properties(hip_lib):
+    side, K = 32768, 64
+    V = side * side
+    seed = BASE_SEED + 5
+    e = Engine(V, K, seed=seed, enable_sync=True, library=hip_lib)
+    try:
+        nnz = e.generate("grid_links", side, seed=seed)
+        st = _to_quiescence(e, injection_arrays(uniform_injections(V, K, seed)))
+    finally:
+        e.close()
+    assert st[-1]["new_bits"] == 0, "no quiescence within 60 rounds"
+    assert all(s["syncs_fired"] == 0 for s in st), "a sync timer fired before quiescence"
+    assert sum(s["new_bits"] for s in st) == V * K  # P1: every message reached every node
+    assert sum(s["fwd_sent"] for s in st) == K * (nnz - (V - 1))  # KAT-3 / P2
+    for a, b in zip(st, st[1:]):
+        assert b["acks"] == a["fwd_delivered"] + a["push_delivered"]
+    print(f"C5 2^30: {len(st) - 1} rounds to full delivery, {nnz} adjacency entries")
+
+
+def test_c4_full_size_lane_groups_equal_single(hip_lib):
+    V, K = 100_000_000, 4096
+    seed = BASE_SEED + 4
+    gen = dict(kind="rmat", n=V, k=16, seed=seed, a=0.57, b=0.19, c=0.19)
+    inj = injection_arrays(uniform_injections(V, K, seed))
+    e = Engine(V, K, seed=seed, enable_sync=True, library=hip_lib)
+    try:
+        e.generate(**gen)
+        want = _to_quiescence(e, inj)
+    finally:
+        e.close()
+    assert want[-1]["new_bits"] == 0
+    R = len(want)
+    got = None
+    for rank in range(2):
+        e = Engine(V, K, seed=seed, enable_sync=True, library=hip_lib, rank=rank, world=2, lane_groups=2)
+        try:
+            e.generate(**gen)
+            inject(e, inj)
+            st = e.step(R)
+        finally:
+            e.close()
+        if got is None:
+            got = [dict(s) for s in st]
+        else:
+            for g, s in zip(got, st):
+                for f in COUNT_FIELDS:
+                    g[f] = (g[f] + s[f]) & M64
+    for g, w in zip(got, want):
+        for f in COUNT_FIELDS:
+            assert g[f] == (w[f] & M64), f"round {w['round']} {f}: lane groups {g[f]} != single {w[f]}"
