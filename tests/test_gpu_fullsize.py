@@ -6,6 +6,9 @@
   sync timer fires every node forwards each value to all neighbours but its
   claimer, so forwards = K (nnz - (V - 1)) (KAT-3 / P2); every delivered
   broadcast is acked one round later. Checked round by round to quiescence.
+* C3, 10^7 nodes (random 8-regular, a seeded bisection in rounds [2, 12),
+  healed by the sync timers): connected, so after the heal every message
+  reaches all V nodes (P1) and the run quiesces.
 * C4, 10^8 nodes (R-MAT, W = 4096): the single engine against the two
   lane-group ranks of a 2-GPU strong-scaling job run one after the other on
   this GPU (gg_config.lane_groups: 2048 lanes each, another kernel
@@ -52,6 +55,24 @@ def test_c5_full_size_properties(hip_lib):
     for a, b in zip(st, st[1:]):
         assert b["acks"] == a["fwd_delivered"] + a["push_delivered"]
     print(f"C5 2^30: {len(st) - 1} rounds to full delivery, {nnz} adjacency entries")
+
+
+def test_c3_full_size_heals(hip_lib):
+    V, K = 10_000_000, 1024
+    seed = BASE_SEED + 3
+    e = Engine(V, K, seed=seed, enable_sync=True, library=hip_lib)
+    try:
+        e.generate("random_regular", V, k=8, seed=seed)
+        e.partition_seeded(2, 12, seed ^ 0x5EED)
+        inject(e, injection_arrays(uniform_injections(V, K, seed)))
+        st = e.step(48)  # the halves go quiet inside the window; the timers (round >= 20) heal it
+    finally:
+        e.close()
+    assert sum(s["dropped"] for s in st) > 0  # the window cut messages
+    assert sum(s["new_bits"] for s in st) == V * K  # P1 after the heal
+    last = max(s["round"] for s in st if s["new_bits"])
+    assert last >= 20  # the heal needed the sync timers
+    print(f"C3 10^7: {last} rounds to full delivery")
 
 
 def test_c4_full_size_lane_groups_equal_single(hip_lib):
