@@ -212,6 +212,9 @@ struct gg_engine {
     uint32_t* d_act = nullptr;       // [4] ring: nodes that became active per round
     unsigned long long* d_act_deg = nullptr;  // [4] ring: their out-degree sums
     unsigned long long* d_tot = nullptr;      // [4] ring: new bits of the owned nodes in rounds <= r
+    uint32_t* d_act_s = nullptr;              // [4][64] the three rings' per-round increments, spread
+    unsigned long long* d_act_deg_s = nullptr;
+    unsigned long long* d_tot_s = nullptr;
     uint64_t* d_abits = nullptr;     // [rows/64] ACT bits of the previous round (flags-first rounds)
     bool ff_ok = false;              // flags-first gathers allowed
     // hubs (see expand_kernels.hpp): in-edge chunks of high in-degree nodes,
@@ -327,6 +330,9 @@ void gg_engine::free_topology() {
     dfree(d_act);
     dfree(d_act_deg);
     dfree(d_tot);
+    dfree(d_act_s);
+    dfree(d_act_deg_s);
+    dfree(d_tot_s);
     dfree(d_abits);
     for (auto& p : d_fired) dfree(p);
     dfree(d_sync_next);
@@ -409,6 +415,9 @@ int reset_device_state(gg_engine* e) {
     seg(e->d_act, 16, 0);
     seg(e->d_act_deg, 32, 0);
     seg(e->d_tot, 32, 0);
+    seg(e->d_act_s, 4 * gg::kSlots * 4, 0);
+    seg(e->d_act_deg_s, 4 * gg::kSlots * 8, 0);
+    seg(e->d_tot_s, 4 * gg::kSlots * 8, 0);
     if (e->d_sat) {
         seg(e->d_sat, e->rows / 8, 0);
         seg(e->d_sat_new, e->rows / 8, 0);
@@ -697,6 +706,9 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.nodes = e->d_nodes;
     a.act = e->d_act;
     a.act_deg = e->d_act_deg;
+    a.act_s = e->d_act_s;
+    a.act_deg_s = e->d_act_deg_s;
+    a.tot_s = e->d_tot_s;
     a.abits = e->d_abits;
     a.ff_ok = e->ff_ok ? 1 : 0;
     a.tile_nodes = (uint32_t)e->tile_nodes;
@@ -793,6 +805,9 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     }
     a.stream_ok = ((!syncw && (!maskw || (e->symmetric && e->n_hubs == 0 && e->nwp >= 2))) || sync_stream) ? 1 : 0;
 
+    // the rings of round r-1 from their spread slots (every kernel of this round reads them)
+    hipLaunchKernelGGL(gg::fold_ring, dim3(1), dim3(gg::kSlots), 0, e->stream, a);
+    HIPCHK(hipGetLastError());
     if (a.n_own) {
         {
             // grid-stride over the nodes; a capped grid keeps the launch cheap in
@@ -1309,6 +1324,9 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     HIPCHK(hipMalloc(&e->d_act, 4 * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->d_act_deg, 4 * 8));
     HIPCHK(hipMalloc(&e->d_tot, 4 * 8));
+    HIPCHK(hipMalloc(&e->d_act_s, 4 * gg::kSlots * 4));
+    HIPCHK(hipMalloc(&e->d_act_deg_s, 4 * gg::kSlots * 8));
+    HIPCHK(hipMalloc(&e->d_tot_s, 4 * gg::kSlots * 8));
     // flags-first gathers (ff_round): rows of >= 64 B (the request-rate-bound
     // regime) and a mean in-degree >= 4; GG_FLAGS_FIRST=0/1 overrides
     {
@@ -2150,7 +2168,7 @@ int gg_dist_round_end(gg_engine* e, gg_round_stats* out) {
         ua.base = e->d_base;
         ua.flg_cur = e->d_flg[r & 1];
         ua.stamp = e->d_stamp;
-        ua.act_cur = e->d_act + (r & 3);
+        ua.act_cur = e->d_act_s + (r & 3) * gg::kSlots;
         ua.in = e->d_xrecv;
         ua.seg_off = e->d_xroff;
         ua.gfirst = e->d_gfirst;

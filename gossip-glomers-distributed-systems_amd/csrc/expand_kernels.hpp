@@ -142,8 +142,15 @@ struct RoundArgs {
     struct TileWork* work;      // live tiles of a sparse round (compact_round; expand_round)
     uint32_t* n_work;           // [2]: live tiles, candidate nodes
     uint32_t* nodes;            // candidate nodes of a sparse lean round (compact_round; expand_stream)
-    uint32_t* act;              // [4] ring: nodes that became active in round r (slot r&3)
+    uint32_t* act;              // [4] ring: nodes that became active in round r (slot r&3), summed by fold_ring
     unsigned long long* act_deg;  // [4] ring: their out-degree sum (edges carrying F rows next round)
+    // the same three rings spread over kSlots addresses per round ([4][kSlots]): the
+    // kernels of round r add into slot r&3 (block % kSlots), fold_ring sums them at the
+    // start of round r+1 — one same-address atomic per block on a single word was a
+    // serial tail at the end of every launch
+    uint32_t* act_s;
+    unsigned long long* act_deg_s;
+    unsigned long long* tot_s;
     uint64_t* abits;            // [rows/64] bit u: sender u is ACT in round r-1 (pack_act_bits; flags-first)
     int32_t ff_ok;              // flags-first gathers allowed (engine choice: W/64 >= 8, mean degree >= 4)
     unsigned long long* tot;    // [4] ring: new bits of the owned nodes in rounds <= r (slot r&3), or nullptr
@@ -456,11 +463,40 @@ __device__ __forceinline__ void flush_counters(const RoundArgs& a, unsigned long
         for (int w = 0; w < kBlock / 64; ++w) s += s_red[w][threadIdx.x];
         const int idx = threadIdx.x == C_BYTES ? kBytes0 + kind : (int)threadIdx.x;
         if (s) atomicAdd(&a.counters[(blockIdx.x % kSlots) * kCounters + idx], s);
-        if (threadIdx.x == C_NACT && s) atomicAdd(&a.act[a.round & 3], (uint32_t)s);
-        if (threadIdx.x == C_NACTDEG && s && a.act_deg) atomicAdd(&a.act_deg[a.round & 3], s);
-        if (threadIdx.x == C_NEW && s && a.tot) atomicAdd(&a.tot[a.round & 3], s);
+        const int sl = (int)(a.round & 3) * kSlots + (int)(blockIdx.x % kSlots);
+        if (threadIdx.x == C_NACT && s) atomicAdd(&a.act_s[sl], (uint32_t)s);
+        if (threadIdx.x == C_NACTDEG && s && a.act_deg) atomicAdd(&a.act_deg_s[sl], s);
+        if (threadIdx.x == C_NEW && s && a.tot) atomicAdd(&a.tot_s[sl], s);
     }
     if (threadIdx.x == 0) stamp(a, kind, t_start);
+}
+
+// ---------------------------------------------------------------------------
+// fold_ring: first launch of round r (one wave): the act / act_deg / tot rings of
+// round r-1 from their kSlots spread slots, and round r's spread slots cleared
+// for this round's kernels. tot is cumulative: tot[r-1] = tot[r-2] + new bits of r-1.
+__global__ __launch_bounds__(kSlots) void fold_ring(RoundArgs a) {
+    static_assert(kSlots == 64, "one lane per slot");
+    const int t = threadIdx.x;
+    const int64_t r = a.round;
+    const int p = (int)((r - 1) & 3), c = (int)(r & 3);
+    unsigned long long x = 0, d = 0, n = 0;
+    if (r > 0) {
+        x = a.act_s[p * kSlots + t];
+        d = a.act_deg_s[p * kSlots + t];
+        n = a.tot_s[p * kSlots + t];
+    }
+    x = wave_sum(x);
+    d = wave_sum(d);
+    n = wave_sum(n);
+    a.act_s[c * kSlots + t] = 0;
+    a.act_deg_s[c * kSlots + t] = 0;
+    a.tot_s[c * kSlots + t] = 0;
+    if (t == 0 && r > 0) {
+        a.act[p] = (uint32_t)x;
+        a.act_deg[p] = d;
+        a.tot[p] = (r > 1 ? a.tot[(r - 2) & 3] : 0ull) + n;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -474,10 +510,7 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
     const unsigned long long t_start = clock100();
     const bool dense = dense_round(a);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        a.act[(a.round + 1) & 3] = 0;  // next round's act slot
-        if (a.act_deg) a.act_deg[(a.round + 1) & 3] = 0;
         a.n_work[0] = a.n_work[1] = 0;  // compact_round runs after this kernel
-        if (a.tot) a.tot[a.round & 3] = a.round > 0 ? a.tot[(a.round - 1) & 3] : 0ull;  // expand kernels add
     }
     if (a.sat) {  // last round's digest bits in (readers of this round see rounds < r only)
         const uint64_t nw = (a.n_own + 63) / 64;
@@ -709,7 +742,10 @@ __global__ void mark_injections(RoundArgs a) {
 // One atomic per block reserves the block's slots: same-address atomics are
 // serialised in L2, so blocks cover 8 KB of candidate bytes each. Order is
 // irrelevant: nodes/tiles are independent within a round and the counters are sums.
-constexpr int kCompactQ = 4;
+#ifndef GG_COMPACT_Q
+#define GG_COMPACT_Q 4
+#endif
+constexpr int kCompactQ = GG_COMPACT_Q;
 __global__ __launch_bounds__(kBlock) void compact_round(RoundArgs a) {
     __shared__ uint32_t s_cnt[kBlock / 64];
     __shared__ uint32_t s_base;
@@ -2894,7 +2930,7 @@ struct UnpackArgs {
     uint64_t* base;
     uint8_t* flg_cur;
     uint32_t* stamp;             // [n_ghost] last round a ghost's F row arrived
-    uint32_t* act_cur;           // act ring slot of round r
+    uint32_t* act_cur;           // spread act slots of round r ([kSlots])
     const uint8_t* in;
     const uint64_t* seg_off;     // [parts + 1] capacity offset of each source's segment
     const uint32_t* gfirst;      // [parts + 1] first ghost index from each source part
@@ -2957,7 +2993,7 @@ __global__ __launch_bounds__(kBlock) void unpack_ghosts(UnpackArgs x) {
         }
     }
     const unsigned long long s = wave_sum(nact);
-    if ((threadIdx.x & 63) == 0 && s) atomicAdd(x.act_cur, (uint32_t)s);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(x.act_cur + (blockIdx.x % kSlots), (uint32_t)s);
 }
 
 // Ghosts whose F row of round r-2 sits in this round's buffer and that sent no
