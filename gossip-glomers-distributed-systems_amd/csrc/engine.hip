@@ -805,9 +805,6 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     }
     a.stream_ok = ((!syncw && (!maskw || (e->symmetric && e->n_hubs == 0 && e->nwp >= 2))) || sync_stream) ? 1 : 0;
 
-    // the rings of round r-1 from their spread slots (every kernel of this round reads them)
-    hipLaunchKernelGGL(gg::fold_ring, dim3(1), dim3(gg::kSlots), 0, e->stream, a);
-    HIPCHK(hipGetLastError());
     if (a.n_own) {
         {
             // grid-stride over the nodes; a capped grid keeps the launch cheap in

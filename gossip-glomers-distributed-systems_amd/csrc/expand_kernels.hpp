@@ -142,12 +142,12 @@ struct RoundArgs {
     struct TileWork* work;      // live tiles of a sparse round (compact_round; expand_round)
     uint32_t* n_work;           // [2]: live tiles, candidate nodes
     uint32_t* nodes;            // candidate nodes of a sparse lean round (compact_round; expand_stream)
-    uint32_t* act;              // [4] ring: nodes that became active in round r (slot r&3), summed by fold_ring
+    uint32_t* act;              // [4] ring: nodes that became active in round r (slot r&3), summed by round_prep
     unsigned long long* act_deg;  // [4] ring: their out-degree sum (edges carrying F rows next round)
     // the same three rings spread over kSlots addresses per round ([4][kSlots]): the
-    // kernels of round r add into slot r&3 (block % kSlots), fold_ring sums them at the
-    // start of round r+1 — one same-address atomic per block on a single word was a
-    // serial tail at the end of every launch
+    // kernels of round r add into slot r&3 (block % kSlots), round_prep of round r+1
+    // sums them — one same-address atomic per block on a single word was a serial
+    // tail at the end of every launch
     uint32_t* act_s;
     unsigned long long* act_deg_s;
     unsigned long long* tot_s;
@@ -472,34 +472,6 @@ __device__ __forceinline__ void flush_counters(const RoundArgs& a, unsigned long
 }
 
 // ---------------------------------------------------------------------------
-// fold_ring: first launch of round r (one wave): the act / act_deg / tot rings of
-// round r-1 from their kSlots spread slots, and round r's spread slots cleared
-// for this round's kernels. tot is cumulative: tot[r-1] = tot[r-2] + new bits of r-1.
-__global__ __launch_bounds__(kSlots) void fold_ring(RoundArgs a) {
-    static_assert(kSlots == 64, "one lane per slot");
-    const int t = threadIdx.x;
-    const int64_t r = a.round;
-    const int p = (int)((r - 1) & 3), c = (int)(r & 3);
-    unsigned long long x = 0, d = 0, n = 0;
-    if (r > 0) {
-        x = a.act_s[p * kSlots + t];
-        d = a.act_deg_s[p * kSlots + t];
-        n = a.tot_s[p * kSlots + t];
-    }
-    x = wave_sum(x);
-    d = wave_sum(d);
-    n = wave_sum(n);
-    a.act_s[c * kSlots + t] = 0;
-    a.act_deg_s[c * kSlots + t] = 0;
-    a.tot_s[c * kSlots + t] = 0;
-    if (t == 0 && r > 0) {
-        a.act[p] = (uint32_t)x;
-        a.act_deg[p] = d;
-        a.tot[p] = (r > 1 ? a.tot[(r - 2) & 3] : 0ull) + n;
-    }
-}
-
-// ---------------------------------------------------------------------------
 // round_prep: one thread per owned node (64 consecutive nodes per wave, so a
 // wave owns whole words of the fired bitmap). In dense rounds the per-node
 // flag/stale-row work moves into expand_stream and no candidates are marked,
@@ -508,9 +480,27 @@ template <bool SYNCW, bool MASKW>
 __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
     __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
     const unsigned long long t_start = clock100();
-    const bool dense = dense_round(a);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        a.n_work[0] = a.n_work[1] = 0;  // compact_round runs after this kernel
+    // Round r-1's rings from their spread slots (one slot per lane, summed per wave):
+    // this kernel decides dense/sparse from its own sum, block 0 publishes the sums
+    // for the round's later launches and clears round r's slots (nothing in this
+    // kernel adds to them).
+    const int lane = threadIdx.x & 63;
+    const int pr = (int)((a.round - 1) & 3), cr = (int)(a.round & 3);
+    const unsigned long long act_prev = wave_sum((unsigned long long)a.act_s[pr * kSlots + lane]);
+    const bool dense = a.stream_ok &&
+                       2.0 * (double)act_prev * (double)a.n_edges >= (double)a.n_own * (double)a.n_own;
+    if (blockIdx.x == 0 && threadIdx.x < kSlots) {
+        const unsigned long long d = wave_sum(a.act_deg_s[pr * kSlots + lane]);
+        const unsigned long long n = wave_sum(a.tot_s[pr * kSlots + lane]);
+        a.act_s[cr * kSlots + lane] = 0;
+        a.act_deg_s[cr * kSlots + lane] = 0;
+        a.tot_s[cr * kSlots + lane] = 0;
+        if (lane == 0) {
+            a.act[pr] = (uint32_t)act_prev;
+            a.act_deg[pr] = d;
+            if (a.tot) a.tot[pr] = (a.round > 0 ? a.tot[(a.round - 2) & 3] : 0ull) + n;
+            a.n_work[0] = a.n_work[1] = 0;  // compact_round runs after this kernel
+        }
     }
     if (a.sat) {  // last round's digest bits in (readers of this round see rounds < r only)
         const uint64_t nw = (a.n_own + 63) / 64;
