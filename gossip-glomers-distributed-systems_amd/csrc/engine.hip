@@ -2086,7 +2086,9 @@ static int dist_begin(gg_engine* e, gg_exchange* x, bool host_sizes) {
     }
     const size_t slot = (size_t)gg::kSlots * gg::kCounters;
     unsigned long long* ctr = e->d_counters + e->dist_k * slot;
-    HIPCHK(hipMemsetAsync(ctr, 0, slot * 8, e->stream));
+    // the counter slots of a whole batch of rounds are cleared once, when it starts
+    // (fold_pending has read the last one): one call instead of one per round
+    if (e->dist_k == 0) HIPCHK(hipMemsetAsync(e->d_counters, 0, kMaxBatch * slot * 8, e->stream));
     if ((rc = enqueue_round(e, d_inj, (uint32_t)total, ctr))) return rc;
     const uint32_t P = e->P;
     if (e->dist_round_of.size() < kMaxBatch) e->dist_round_of.resize(kMaxBatch);
