@@ -400,8 +400,16 @@ int reset_device_state(gg_engine* e) {
     // (a stale row is cleared in the round it expires), e.g. after an episode
     // run to quiescence. Single engine only: ghost rows follow remote rounds.
     // After exactly one quiet round r only the buffers of round r-1 (parity
-    // dirty_parity = (r+1) & 1, recorded by gg_reset) can hold non-zero rows.
-    if (!(e->P == 1 && e->quiet >= 2)) {
+    // dirty_parity = (r+1) & 1, recorded by gg_reset) can hold non-zero rows,
+    // and only where their flag byte is set: those rows and the flags are
+    // cleared (a sparse last delivery round: 1 MB read instead of C2's 134 MB
+    // F buffer written; batched engines keep whole-buffer clears).
+    if (e->P == 1 && e->quiet == 1 && !e->d_pend && e->nwp >= 2 && e->nwp <= 128 && !(e->nwp & (e->nwp - 1))) {
+        ra.sparse_F = e->d_F[e->dirty_parity];
+        ra.sparse_flg = e->d_flg[e->dirty_parity];
+        ra.sparse_rows = e->rows;
+        ra.nwp = (uint32_t)e->nwp;
+    } else if (!(e->P == 1 && e->quiet >= 2)) {
         for (int b = 0; b < 2; ++b) {
             if (e->P == 1 && e->quiet == 1 && b != e->dirty_parity) continue;
             seg(e->d_F[b], rowbytes, 0);  // F rows are zero unless ACT

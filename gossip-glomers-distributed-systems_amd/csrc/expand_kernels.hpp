@@ -2701,6 +2701,12 @@ struct ResetArgs {
     const uint32_t* gid;
     uint64_t seed;
     uint32_t sync_base, sync_jitter;
+    // an F buffer whose rows are zero where their flag byte is: only the flagged
+    // rows and the flags are cleared (or nullptr)
+    uint64_t* sparse_F;
+    uint8_t* sparse_flg;  // [sparse_rows] flag bytes
+    uint64_t sparse_rows;
+    uint32_t nwp;         // even, <= 128
 };
 
 __global__ __launch_bounds__(kBlock) void reset_state(ResetArgs ra) {
@@ -2720,6 +2726,22 @@ __global__ __launch_bounds__(kBlock) void reset_state(ResetArgs ra) {
             for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(v, p + k * kBlock);  // chunk < 4 * kBlock
         }
         for (uint64_t w = pieces * kPiece + t0; w < s.n; w += stride) s.p[w] = s.val;
+    }
+    if (ra.sparse_F) {
+        // one lane per 16-byte piece of a row, the rows of a wave whole (nwp / 2
+        // divides 64, and so the stride): every lane of the wave has read the
+        // row's flag byte before the piece-0 lane clears it
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        const uint32_t pieces = ra.nwp / 2;
+        uint8_t* flg = reinterpret_cast<uint8_t*>(ra.sparse_flg);
+        const uint64_t n = ra.sparse_rows * pieces;
+        for (uint64_t t = t0; t < n; t += stride) {
+            const uint64_t row = t / pieces;
+            const uint32_t pc = (uint32_t)(t % pieces);
+            if (!flg[row]) continue;
+            __builtin_nontemporal_store((u64x2){0ull, 0ull}, reinterpret_cast<u64x2*>(ra.sparse_F + row * ra.nwp) + pc);
+            if (pc == 0) flg[row] = 0;
+        }
     }
     for (uint64_t t = t0; t < ra.n_own + ra.n_ghost; t += stride) {
         const uint64_t i = t < ra.n_own ? t : ra.ghost0 + (t - ra.n_own);

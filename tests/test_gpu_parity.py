@@ -200,6 +200,32 @@ def test_reset_after_quiet_rounds(hip_lib, cpu_lib, shift, extra_quiet):
     assert np.array_equal(c.read_bits(), g.read_bits())
 
 
+@pytest.mark.parametrize("shift", [0, 1])
+def test_reset_after_quiet_sync_round(hip_lib, cpu_lib, shift):
+    """As above with the sync timers running when the episode goes quiet (the
+    bench's case: the last delivery rounds are sync rounds, whose F rows and
+    flags include LAG rows): gg_reset clears only the flagged rows of the dirty
+    buffer; the next episode must equal a fresh oracle run."""
+    topo = T.tree(4096, 4)
+    inj = [(n, v, 16 + shift) for n, v, _ in uniform_injections(4096, 256, 94)]
+    g = make_engine(hip_lib, Scenario(topo, 256, 60, inj, seed=95, enable_sync=True))
+    r, st = 0, []
+    while True:
+        r += 1
+        st.append(g.step(1)[0])
+        if st[-1]["new_bits"] == 0 and r > 18 + shift:
+            break
+    assert any(s["syncs_fired"] for s in st), "no timer fired before the quiet round"
+    g.reset()
+    c = make_engine(cpu_lib, Scenario(topo, 256, 40, [], seed=95, enable_sync=True))
+    for n, v, _ in uniform_injections(4096, 200, 96):
+        g.broadcast(n, v, 0)
+        c.broadcast(n, v, 0)
+    d = diff_stats(c.step(40), g.step(40))
+    assert not d, d[:5]
+    assert np.array_equal(c.read_bits(), g.read_bits())
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_degree_order_vs_o2(hip_lib, cpu_lib, monkeypatch, seed):
     """GG_ORDER=degree: local rows by descending in-degree (the default on
