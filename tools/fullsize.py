@@ -22,6 +22,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -110,7 +111,21 @@ def main():
     exp_fwd = int((comp_deg[lab[srcs]] - (comp_size[lab[srcs]] - 1)).sum())
     probe = [int(srcs[0]), int(srcs[len(srcs) // 2])]
     probe_lane = [eng.lane_of(list(first.keys())[0]), eng.lane_of(list(first.keys())[len(srcs) // 2])]
-    dist = [T.bfs(topo, s) for s in probe]
+    # a heartbeat while the serial BFS probes run (minutes at 2^30 nodes): a
+    # GPU-box run that prints nothing for 3 minutes is taken to be hung
+    done = threading.Event()
+
+    def beat():
+        while not done.wait(30):
+            log(f"  host facts: BFS probes running ({time.time() - t2:.0f}s)")
+
+    hb = threading.Thread(target=beat, daemon=True)
+    hb.start()
+    try:
+        dist = [T.bfs(topo, s) for s in probe]
+    finally:
+        done.set()
+        hb.join()
     log(f"host facts in {time.time() - t2:.1f}s: components {len(np.unique(lab))}, expected deliveries "
         f"{exp_deliv}, probe sources {probe}")
     S = min(args.sample, V)
