@@ -374,7 +374,13 @@ def cpu_baseline(cfg, topo, inj, V, K, seed, R):
     from ggamd.engine import Engine
     from ggamd.workload import BASE_SEED, inject, uniform_injections
     host_cpus, affinity = cpu_counts()
-    threads = min(16, affinity)  # the box's CPU share for one GPU
+    # the CPU share this process is given: the runtime's declared thread budget
+    # (OMP_NUM_THREADS: the GPU box's per-GPU share of its host cores), else every
+    # core this process may run on
+    share = os.environ.get("OMP_NUM_THREADS")
+    threads = max(1, min(int(share), affinity)) if share and share.isdigit() else affinity
+    basis = "OMP_NUM_THREADS (the declared per-GPU CPU share)" if share and share.isdigit() else \
+        "sched_getaffinity (every core this process may use)"
 
     def o2_episodes(topo_, inj_, V_, K_, seed_, thr, budget_s, rounds=None):
         os.environ["GG_CPU_THREADS"] = str(thr)
@@ -420,7 +426,7 @@ def cpu_baseline(cfg, topo, inj, V, K, seed, R):
     return {"value": v_all, "unit": "deliveries/s", "cores": threads, "kind": "port",
             "sample": f"O2 bitset oracle (oracle/o2_bitset.cpp, -O3, AVX-512 host) on {threads} threads: "
                       f"{sample_all}",
-            "host_cpus": host_cpus, "affinity_cpus": affinity,
+            "host_cpus": host_cpus, "affinity_cpus": affinity, "cores_basis": basis,
             "single_thread": {"value": v_one, "unit": "deliveries/s", "cores": 1, "sample": sample_one},
             "o1_per_message": o1}
 

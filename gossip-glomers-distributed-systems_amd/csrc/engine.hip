@@ -40,6 +40,19 @@ namespace {
 constexpr uint32_t kMaxBatch = 256;  // rounds per counter readback
 constexpr int kMaxBlocks = 2048;
 
+// Test hooks: environment variables the test suite sets to force a code path
+// that the engine would otherwise choose by size (every forced path is
+// bit-exact; only the kernels that run change): GG_HUB_DEG, GG_HUB_CHUNK,
+// GG_SYNC_TILES, GG_SYNC_DIGEST, GG_ORDER, GG_XCHG_MODE, GG_PREP_BLOCKS.
+const char* test_knob(const char* name) { return getenv(name); }
+// A/B switches of past measurements (GG_ALL_FULL, GG_NO_GRAPH, GG_SYNC_ALLPUSH,
+// GG_FLAGS_FIRST, GG_XCHG_EXACT_BYTES): read only in a -DGG_AB_KNOBS build.
+#ifdef GG_AB_KNOBS
+const char* ab_knob(const char* name) { return getenv(name); }
+#else
+const char* ab_knob(const char*) { return nullptr; }
+#endif
+
 struct Window {
     int64_t from, to;
     bool seeded;
@@ -189,6 +202,7 @@ struct gg_engine {
     bool xexact = false;                       // any exact direction
     std::vector<uint64_t> xsend_bytes, xrecv_bytes, xsend_off, xrecv_off;  // [world]
     uint32_t dist_k = 0;                       // pending rounds (counter slots in use)
+    uint32_t ctr_dirty = kMaxBatch;            // counter slots [0, ctr_dirty) may be non-zero
     std::vector<int64_t> dist_round_of;        // round of each pending slot
     std::vector<uint64_t> dist_sent;           // payload bytes sent in each pending slot
     std::vector<gg_round_stats> dist_done;     // folded, not yet flushed
@@ -766,7 +780,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     }
     a.inj = d_inj;
     a.n_inj = n_inj;
-    static const bool no_full = getenv("GG_ALL_FULL") && atoi(getenv("GG_ALL_FULL")) == 0;  // A/B
+    static const bool no_full = ab_knob("GG_ALL_FULL") && atoi(ab_knob("GG_ALL_FULL")) == 0;  // A/B
     a.tot = no_full ? nullptr : e->d_tot;
     a.full_new = (unsigned long long)e->n_own * lanes_through(e, r - 1);
     a.counters = d_ctr;
@@ -819,7 +833,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             // grid-stride over the nodes; a capped grid keeps the launch cheap in
             // dense lean rounds, where it is a no-op (C2 A/B: 1024 blocks 1.99 ms/episode,
             // 4096 2.02, 256 2.10; GG_PREP_BLOCKS overrides)
-            static const uint64_t prep_cap = getenv("GG_PREP_BLOCKS") ? (uint64_t)atoi(getenv("GG_PREP_BLOCKS")) : 1024;
+            static const uint64_t prep_cap = test_knob("GG_PREP_BLOCKS") ? (uint64_t)atoi(test_knob("GG_PREP_BLOCKS")) : 1024;
             if (e->d_sat && r == base + 2) {  // the digest's first bits (sat_scan)
                 const uint64_t thr = a.n_own * (e->nwp / 2);
                 hipLaunchKernelGGL(gg::sat_scan, dim3((unsigned)((thr + gg::kBlock - 1) / gg::kBlock)), dim3(gg::kBlock),
@@ -998,7 +1012,7 @@ size_t pack_injections(gg_engine* e, int64_t r0, uint32_t n, std::vector<size_t>
 // saved. GG_NO_GRAPH=1 disables it.
 template <class F>
 int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& off, size_t total, F&& enqueue) {
-    static const bool no_graph = getenv("GG_NO_GRAPH") != nullptr;
+    static const bool no_graph = ab_knob("GG_NO_GRAPH") != nullptr;
     uint64_t h = gg_mix64(total);
     for (size_t t = 0; t < 2 * total; ++t) h = gg_mix64(h ^ e->h_inj[t]);
     // the same pairs as the last upload (every episode of a benchmark loop): d_inj
@@ -1158,7 +1172,7 @@ void choose_partition(uint64_t V, const int64_t* row_ptr, const int32_t* col, co
 // random relabelling. Claim order is unaffected (in-lists stay ascending by
 // original id). Empty: keep the native order.
 std::vector<uint32_t> degree_order(uint64_t V, const int64_t* tin) {
-    const char* o = getenv("GG_ORDER");
+    const char* o = test_knob("GG_ORDER");
     if (o && !strcmp(o, "native")) return {};
     uint64_t maxd = 0;
     for (uint64_t v = 0; v < V; ++v) maxd = std::max<uint64_t>(maxd, (uint64_t)(tin[v + 1] - tin[v]));
@@ -1189,6 +1203,9 @@ int gg_create(const gg_config* cfg, gg_engine** out) {
     if (cfg->world == 0 || cfg->rank >= cfg->world) return GG_EINVAL;
     const uint32_t L = cfg->lane_groups ? cfg->lane_groups : 1u;
     if (cfg->world % L || L > cfg->n_lanes / 64) return GG_EINVAL;
+    // the exchange kernels keep one LDS slot per source part (unpack_ghosts) and
+    // one lane per destination part (finish_pack, a 64-thread block)
+    if (cfg->world / L > 63) return GG_EINVAL;
     if (cfg->batch_ticks && (cfg->enable_sync || cfg->world != 1)) return GG_EINVAL;  // batched: single, no sync
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GG_EIO;
@@ -1229,7 +1246,7 @@ const char* gg_last_error(const gg_engine* e) { return e ? e->err.c_str() : "nul
 
 // In-/out-degree above which a node takes the hub path (GG_HUB_DEG overrides).
 static uint32_t hub_threshold() {
-    if (const char* h = getenv("GG_HUB_DEG")) return (uint32_t)std::max(1, atoi(h));
+    if (const char* h = test_knob("GG_HUB_DEG")) return (uint32_t)std::max(1, atoi(h));
     return 512;
 }
 
@@ -1245,7 +1262,7 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     {
         e->hub_deg = hub_threshold();
         uint64_t per = 128ull * (gg::kBlock / lanes_per_node((uint32_t)e->nwp));  // senders per chunk
-        if (const char* h = getenv("GG_HUB_CHUNK")) per = (uint64_t)std::max(1, atoi(h));
+        if (const char* h = test_knob("GG_HUB_CHUNK")) per = (uint64_t)std::max(1, atoi(h));
         std::vector<uint32_t> hubs, hub_c0;
         std::vector<gg::HubChunk> hch, mch;
         for (uint64_t i = 0; iptr && i < n_own; ++i) {
@@ -1280,7 +1297,7 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
         }
     }
     // streamed sync rounds need no in-hubs and two words per lane
-    e->sync_tiles = getenv("GG_SYNC_TILES") && atoi(getenv("GG_SYNC_TILES")) != 0;
+    e->sync_tiles = test_knob("GG_SYNC_TILES") && atoi(test_knob("GG_SYNC_TILES")) != 0;
     dfree(e->d_srec);
     dfree(e->d_pushb);
     dfree(e->d_rev);
@@ -1302,7 +1319,7 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
         HIPCHK(hipMalloc(&e->d_ibits, e->rows / 8));
         HIPCHK(hipMalloc(&e->d_nmeta, n_own * sizeof(uint2)));
         // saturation digest (GG_SYNC_DIGEST=0 turns it off, for A/B)
-        if (!(getenv("GG_SYNC_DIGEST") && atoi(getenv("GG_SYNC_DIGEST")) == 0)) {
+        if (!(test_knob("GG_SYNC_DIGEST") && atoi(test_knob("GG_SYNC_DIGEST")) == 0)) {
             HIPCHK(hipMalloc(&e->d_sat, e->rows / 8));
             HIPCHK(hipMalloc(&e->d_sat_new, e->rows / 8));
         }
@@ -1317,7 +1334,7 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     // non-empty pushes per out-edge, written by each sync callback (SyncBroadcast
     // sends nothing for an empty difference): receivers of empty pushes are not
     // candidates (GG_SYNC_ALLPUSH=1 keeps every push edge, for A/B)
-    if (e->cfg.enable_sync && e->n_out_edges && !(getenv("GG_SYNC_ALLPUSH") && atoi(getenv("GG_SYNC_ALLPUSH"))))
+    if (e->cfg.enable_sync && e->n_out_edges && !(ab_knob("GG_SYNC_ALLPUSH") && atoi(ab_knob("GG_SYNC_ALLPUSH"))))
         HIPCHK(hipMalloc(&e->d_pushb, e->n_out_edges));
     if (!e->d_pushb) dfree(e->d_rev);
     if (e->d_pushb && e->d_srec) HIPCHK(hipMalloc(&e->d_pushany, e->rows));
@@ -1340,7 +1357,7 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     // flags-first gathers (ff_round): rows of >= 64 B (the request-rate-bound
     // regime) and a mean in-degree >= 4; GG_FLAGS_FIRST=0/1 overrides
     {
-        const char* f = getenv("GG_FLAGS_FIRST");
+        const char* f = ab_knob("GG_FLAGS_FIRST");
         e->ff_ok = f ? atoi(f) != 0 : (e->nwp >= 8 && e->n_in_edges >= 4 * std::max<uint64_t>(1, n_own));
         if (e->ff_ok) HIPCHK(hipMalloc(&e->d_abits, e->rows / 8));
     }
@@ -1411,9 +1428,9 @@ static int setup_exchange(gg_engine* e) {
     // a direction whose static capacity exceeds GG_XCHG_EXACT_BYTES (default
     // 4 MiB) sends its exact size first and then only the used bytes (one host
     // wait per round); GG_XCHG_MODE=exact|static forces every direction
-    const char* mode = getenv("GG_XCHG_MODE");
+    const char* mode = test_knob("GG_XCHG_MODE");
     uint64_t lim = 4ull << 20;
-    if (const char* l = getenv("GG_XCHG_EXACT_BYTES")) lim = strtoull(l, nullptr, 10);
+    if (const char* l = ab_knob("GG_XCHG_EXACT_BYTES")) lim = strtoull(l, nullptr, 10);
     e->xexact_s.assign(Wd, 0);
     e->xexact_r.assign(Wd, 0);
     e->xexact = false;
@@ -1765,7 +1782,7 @@ int gg_topology_generate(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_ou
         return e->fail(rc, err);
     }
     {  // degree_order's rule, on the device: power-law graphs get rows by descending degree
-        const char* o = getenv("GG_ORDER");
+        const char* o = test_knob("GG_ORDER");
         const double mean = (double)g.nnz / (double)std::max<uint64_t>(1, e->V);
         const bool want = o && !strcmp(o, "degree") ? true
                           : o && !strcmp(o, "native") ? false
@@ -2008,6 +2025,7 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
             return GG_OK;
         };
         rc = run_batch(e, r0, m, off, total, enqueue_batch);
+        e->ctr_dirty = std::max(e->ctr_dirty, m);
         e->round = save_round + m;
         if (rc) return rc;
         HIPCHK(hipStreamSynchronize(e->stream));
@@ -2094,9 +2112,14 @@ static int dist_begin(gg_engine* e, gg_exchange* x, bool host_sizes) {
     }
     const size_t slot = (size_t)gg::kSlots * gg::kCounters;
     unsigned long long* ctr = e->d_counters + e->dist_k * slot;
-    // the counter slots of a whole batch of rounds are cleared once, when it starts
-    // (fold_pending has read the last one): one call instead of one per round
-    if (e->dist_k == 0) HIPCHK(hipMemsetAsync(e->d_counters, 0, kMaxBatch * slot * 8, e->stream));
+    // the counter slots of a batch of rounds are cleared once, when it starts
+    // (fold_pending has read the last one), and only as far as they were used:
+    // a caller that folds every round (gg_dist_round_end with out) clears one slot
+    if (e->dist_k == 0 && e->ctr_dirty) {
+        HIPCHK(hipMemsetAsync(e->d_counters, 0, e->ctr_dirty * slot * 8, e->stream));
+        e->ctr_dirty = 0;
+    }
+    e->ctr_dirty = std::max(e->ctr_dirty, e->dist_k + 1);
     if ((rc = enqueue_round(e, d_inj, (uint32_t)total, ctr))) return rc;
     const uint32_t P = e->P;
     if (e->dist_round_of.size() < kMaxBatch) e->dist_round_of.resize(kMaxBatch);

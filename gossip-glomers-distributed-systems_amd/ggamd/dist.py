@@ -120,11 +120,14 @@ class ShardedRunner:
         st = torch.tensor(ss, dtype=torch.int64, device=size_dev)
         rt = torch.empty_like(st)
         if self.nccl and ext is not None:
+            # torch orders the collective only with the current stream (ext): the
+            # read of its result must be issued on ext as well, not on the default stream
             with torch.cuda.stream(ext):
                 dist.all_to_all_single(rt, st, group=self.group)
+                rs = rt.cpu().tolist()
         else:
             dist.all_to_all_single(rt, st, group=self.group)
-        rs = rt.cpu().tolist()
+            rs = rt.cpu().tolist()
         for i in range(W):
             x.recv_bytes[i] = rs[i]
         if not any(ss) and not any(rs):

@@ -20,7 +20,19 @@
 //   tick {"rounds": k}         front-end extension: run k 100 ms rounds
 //                               (lockstep mode, --tick-ms 0)
 // Any other type: "No handler for <msg>" on stderr and exit status 1, as the
-// pinned maelstrom library does. With --tick-ms T > 0 the process runs one
+// pinned maelstrom library does. A handler that fails (e.g. the engine refuses a
+// broadcast) answers with a Maelstrom error body {"code":13,"text":...} and the
+// process keeps serving, as the library does when a handler returns an error.
+//
+// Values are unbounded, as the reference's map (`broadcast.go:14,73`): each
+// engine holds --lanes values, and when every lane of the newest engine is in
+// use a further engine over the same topology takes the new values. Values
+// never interact (each one's propagation depends on no other value), so a read
+// is the union of the node's sets over the engines — exactly one engine with
+// every value. An older engine whose values can no longer change (symmetric
+// topology, a round without deliveries, no client broadcast queued for it:
+// every node then holds every value of its component) stops stepping until a
+// client re-broadcasts one of its values. With --tick-ms T > 0 the process runs one
 // round every T ms of wall time between input lines (Maelstrom --latency 100
 // is one round per 100 ms).
 //
@@ -39,6 +51,7 @@
 #include <cstring>
 #include <iostream>
 #include <map>
+#include <unordered_map>
 #include <memory>
 #include <string>
 #include <utility>
@@ -255,7 +268,7 @@ class Front {
 public:
     Front(const Options& o, Api& api) : opt_(o), api_(api) {}
     ~Front() {
-        if (eng_) api_.destroy(eng_);
+        for (auto& x : engines_) api_.destroy(x.e);
     }
 
     // one input line; returns false to stop (exit status in *status)
@@ -290,7 +303,7 @@ public:
         if (t == "topology") {
             const Json* top = body->get("topology");
             if (!top || top->kind != Json::OBJ) return fail("topology without a map", status);
-            if (!eng_ && !build(*top, status)) return false;
+            if (engines_.empty() && !build(*top, status)) return false;
             return reply(d, s, msg_id, "topology_ok", "", status);
         }
         if (t == "broadcast") {
@@ -298,10 +311,11 @@ public:
             if (!m || m->kind != Json::NUM || !m->integral) return fail("broadcast without an integer message", status);
             const int64_t v = node_index(d);
             if (v < 0) return fail("broadcast to a non-node " + d, status);
-            if (!eng_ && !build(Json{}, status)) return false;  // no topology yet: no neighbours
+            if (!engines_.empty() && v >= V_) return error_reply(d, s, msg_id, "broadcast to an unknown node " + d);
+            if (engines_.empty() && !build(Json{}, status)) return false;  // no topology yet: no neighbours
             if (s.empty() || s[0] != 'n') {  // from a client: the engine schedules it for this round
-                const int rc = api_.broadcast(eng_, (uint32_t)v, m->inum, api_.current_round(eng_));
-                if (rc) return fail(std::string("gg_broadcast: ") + api_.last_error(eng_), status);
+                std::string why;
+                if (!client_broadcast((uint32_t)v, m->inum, why)) return error_reply(d, s, msg_id, why);
                 pending_[(uint32_t)v].push_back(m->inum);
             }
             return reply(d, s, msg_id, "broadcast_ok", "", status);
@@ -309,22 +323,23 @@ public:
         if (t == "read") {
             const int64_t v = node_index(d);
             if (v < 0) return fail("read at a non-node " + d, status);
-            if (!eng_ && !build(Json{}, status)) return false;
-            std::vector<int64_t> vals(64);
-            uint64_t n = 0;
-            int rc = api_.read(eng_, (uint32_t)v, vals.data(), vals.size(), &n);
-            if (rc == 0 && n > vals.size()) {
-                vals.resize(n);
-                rc = api_.read(eng_, (uint32_t)v, vals.data(), vals.size(), &n);
+            if (engines_.empty() && !build(Json{}, status)) return false;
+            std::vector<int64_t> vals;
+            for (auto& x : engines_) {  // the union over the engines (disjoint value sets)
+                std::vector<int64_t> part(64);
+                uint64_t n = 0;
+                int rc = api_.read(x.e, (uint32_t)v, part.data(), part.size(), &n);
+                if (rc == 0 && n > part.size()) {
+                    part.resize(n);
+                    rc = api_.read(x.e, (uint32_t)v, part.data(), part.size(), &n);
+                }
+                if (rc) return error_reply(d, s, msg_id, std::string("gg_read: ") + api_.last_error(x.e));
+                vals.insert(vals.end(), part.begin(), part.begin() + (std::ptrdiff_t)n);
             }
-            if (rc) return fail(std::string("gg_read: ") + api_.last_error(eng_), status);
-            vals.resize(n);
             auto it = pending_.find((uint32_t)v);  // client broadcasts not yet run through a round
-            if (it != pending_.end()) {
-                vals.insert(vals.end(), it->second.begin(), it->second.end());
-                std::sort(vals.begin(), vals.end());
-                vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
-            }
+            if (it != pending_.end()) vals.insert(vals.end(), it->second.begin(), it->second.end());
+            std::sort(vals.begin(), vals.end());
+            vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
             // ReadResponse.Messages starts as a nil slice (broadcast.go:125): an
             // empty read marshals as null, not []
             std::string extra = ",\"messages\":";
@@ -348,14 +363,98 @@ public:
     }
 
     bool run_rounds(uint32_t n, int* status) {
-        if (!eng_ || !n) return true;
-        const int rc = api_.step(eng_, n, nullptr);
-        if (rc) return fail(std::string("gg_step: ") + api_.last_error(eng_), status);
+        if (engines_.empty() || !n) return true;
+        std::vector<gg_round_stats> st(n);
+        for (size_t k = 0; k < engines_.size(); ++k) {
+            Slot& x = engines_[k];
+            if (x.frozen) continue;
+            const int rc = api_.step(x.e, n, st.data());
+            if (rc) return fail(std::string("gg_step: ") + api_.last_error(x.e), status);
+            // an older engine (no new values) on a symmetric topology whose last round
+            // delivered nothing and that has no queued broadcast is final
+            x.queued = false;
+            x.frozen = sym_ && k + 1 < engines_.size() && st[n - 1].new_bits == 0;
+        }
         pending_.clear();
         return true;
     }
 
+    size_t engine_count() const { return engines_.size(); }
+
 private:
+    struct Slot {
+        gg_engine* e = nullptr;
+        bool frozen = false;
+        bool queued = false;  // a client broadcast waits for the next round
+    };
+
+    // the engine that holds `value` (a new value: the newest engine, or a new one
+    // when its lanes are all in use), scheduled for this round
+    bool client_broadcast(uint32_t node, int64_t value, std::string& why) {
+        auto it = owner_.find(value);
+        size_t k = it != owner_.end() ? it->second : engines_.size() - 1;
+        int rc = api_.broadcast(engines_[k].e, node, value, api_.current_round(engines_[k].e));
+        if (rc == GG_ENOSPC && it == owner_.end()) {
+            if (!add_engine(why)) return false;
+            k = engines_.size() - 1;
+            engines_[k - 1].frozen = false;  // it may freeze at its next quiet round
+            rc = api_.broadcast(engines_[k].e, node, value, api_.current_round(engines_[k].e));
+        }
+        if (rc) {
+            why = std::string("gg_broadcast: ") + api_.last_error(engines_[k].e);
+            return false;
+        }
+        owner_[value] = k;
+        engines_[k].frozen = false;
+        engines_[k].queued = true;
+        return true;
+    }
+
+    // a further engine over the same topology, at the same round
+    bool add_engine(std::string& why) {
+        gg_config c{};
+        c.n_nodes = (uint64_t)V_;
+        c.n_lanes = opt_.lanes;
+        c.seed = opt_.seed;
+        c.sync_base_ticks = 20;
+        c.sync_jitter_ticks = 10;
+        c.enable_sync = opt_.sync ? 1 : 0;
+        c.device = opt_.device;
+        c.world = 1;
+        gg_engine* e = nullptr;
+        int rc = api_.create(&c, &e);
+        if (rc) {
+            why = "gg_create failed: " + std::to_string(rc);
+            return false;
+        }
+        rc = api_.topology(e, rp_.data(), col_.empty() ? nullptr : col_.data(), col_.size());
+        // catch up with the current round: no values yet, so only the timers run
+        const int64_t r = engines_.empty() ? 0 : api_.current_round(engines_.front().e);
+        if (rc == 0 && r > 0) rc = api_.step(e, (uint32_t)r, nullptr);
+        if (rc) {
+            why = std::string("gg_topology/gg_step: ") + api_.last_error(e);
+            api_.destroy(e);
+            return false;
+        }
+        engines_.push_back({e, false, false});
+        return true;
+    }
+
+    // Maelstrom error reply (code 13 = crash: the handler failed; the node keeps serving)
+    bool error_reply(const std::string& from, const std::string& to, int64_t in_reply_to, const std::string& text) {
+        std::string o = "{\"src\":";
+        quote(o, from);
+        o += ",\"dest\":";
+        quote(o, to);
+        o += ",\"body\":{\"code\":13,\"in_reply_to\":" + std::to_string(in_reply_to) + ",\"text\":";
+        quote(o, text);
+        o += ",\"type\":\"error\"}}\n";
+        fwrite(o.data(), 1, o.size(), stdout);
+        fflush(stdout);
+        fprintf(stderr, "%s\n", text.c_str());
+        return true;
+    }
+
     bool fail(const std::string& what, int* status) {
         fprintf(stderr, "%s\n", what.c_str());
         *status = 1;
@@ -404,34 +503,36 @@ private:
                 }
             }
         }
-        std::vector<int64_t> rp((size_t)V + 1, 0);
-        std::vector<int32_t> col;
+        rp_.assign((size_t)V + 1, 0);
+        col_.clear();
         for (int64_t v = 0; v < V; ++v) {
             auto& r = rows[(size_t)v];
             std::sort(r.begin(), r.end());
             r.erase(std::unique(r.begin(), r.end()), r.end());
-            col.insert(col.end(), r.begin(), r.end());
-            rp[(size_t)v + 1] = (int64_t)col.size();
+            col_.insert(col_.end(), r.begin(), r.end());
+            rp_[(size_t)v + 1] = (int64_t)col_.size();
         }
-        gg_config c{};
-        c.n_nodes = (uint64_t)V;
-        c.n_lanes = opt_.lanes;
-        c.seed = opt_.seed;
-        c.sync_base_ticks = 20;
-        c.sync_jitter_ticks = 10;
-        c.enable_sync = opt_.sync ? 1 : 0;
-        c.device = opt_.device;
-        c.world = 1;
-        int rc = api_.create(&c, &eng_);
-        if (rc) return fail("gg_create failed: " + std::to_string(rc), status);
-        rc = api_.topology(eng_, rp.data(), col.empty() ? nullptr : col.data(), col.size());
-        if (rc) return fail(std::string("gg_topology: ") + api_.last_error(eng_), status);
+        sym_ = true;  // u lists w iff w lists u (an older engine may then freeze)
+        for (int64_t u = 0; u < V && sym_; ++u)
+            for (int32_t w : rows[(size_t)u])
+                if (!std::binary_search(rows[(size_t)w].begin(), rows[(size_t)w].end(), (int32_t)u)) {
+                    sym_ = false;
+                    break;
+                }
+        V_ = V;
+        std::string why;
+        if (!add_engine(why)) return fail(why, status);
         return true;
     }
 
     Options opt_;
     Api& api_;
-    gg_engine* eng_ = nullptr;
+    std::vector<Slot> engines_;
+    std::unordered_map<int64_t, size_t> owner_;  // value -> engine
+    std::vector<int64_t> rp_;
+    std::vector<int32_t> col_;
+    bool sym_ = true;
+    int64_t V_ = 0;
     int64_t n_nodes_ = 0;
     std::map<uint32_t, std::vector<int64_t>> pending_;
 };

@@ -199,6 +199,7 @@ class O1Network:
         self._seq += 1
         msg = Msg(src, dest, body, kind, self._seq)
         if kind == "client":  # replies to clients: not inter-node traffic
+            self.last_client_reply = body
             return
         if kind == "fwd":
             c.fwd_sent += 1
@@ -348,6 +349,13 @@ class O1Network:
 
     def read(self, v: int) -> list[int]:
         return sorted(self.nodes[v].received)
+
+    def client_read(self, v: int, msg_id: int = 1) -> dict:
+        """A client `read` of node v through HandleRead (broadcast.go:124-132):
+        the reply body as the handler builds it (messages None = JSON null)."""
+        self.last_client_reply = None
+        self.handle_read(self.nodes[v], Msg(-1, v, {"type": "read", "msg_id": msg_id}, "client"))
+        return self.last_client_reply
 
     def bits(self, v: int) -> list[int]:
         nw = self.W // 64

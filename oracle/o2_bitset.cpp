@@ -451,6 +451,7 @@ int gg_create(const gg_config* cfg, gg_engine** out) {
     if (cfg->world == 0 || cfg->rank >= cfg->world) return GG_EINVAL;
     const uint32_t L = cfg->lane_groups ? cfg->lane_groups : 1u;
     if (cfg->world % L || L > cfg->n_lanes / 64) return GG_EINVAL;
+    if (cfg->world / L > 63) return GG_EINVAL;  // the HIP engine's exchange limit (same ABI)
     if (cfg->batch_ticks && (cfg->enable_sync || cfg->world != 1)) return GG_EINVAL;  // batched: single, no sync
     auto* e = new gg_engine();
     e->cfg = *cfg;

@@ -9,7 +9,9 @@
 * C3, 10^7 nodes (random 8-regular, a seeded bisection in rounds [2, 12),
   healed by the sync timers): connected, so after the heal every message
   reaches all V nodes (P1) and the run quiesces.
-* C4, 10^8 nodes (R-MAT, W = 4096): the single engine against the two
+* C4, 10^8 nodes (R-MAT, W = 4096): P1 and KAT-3 against the graph's
+  connected components (computed on the GPU from the exported graph); and the
+  single engine against the two
   lane-group ranks of a 2-GPU strong-scaling job run one after the other on
   this GPU (gg_config.lane_groups: 2048 lanes each, another kernel
   instantiation over another row width): every round's counters and delivery
@@ -75,18 +77,70 @@ def test_c3_full_size_heals(hip_lib):
     print(f"C3 10^7: {last} rounds to full delivery")
 
 
+def _components(row_ptr, col, device="cuda"):
+    """Connected components of a symmetric CSR on the GPU (torch): min-label
+    propagation over every adjacency entry with pointer jumping, to a fixed
+    point. Returns (label per node, component size per label, degree sum per
+    label) as CPU tensors."""
+    import torch
+    dev = torch.device(device)
+    V = row_ptr.size - 1
+    rp = torch.from_numpy(row_ptr).to(dev)
+    deg = rp[1:] - rp[:-1]
+    cols = torch.from_numpy(col).to(dev)  # int32
+    lab = torch.arange(V, dtype=torch.int64, device=dev)
+    chunk = 1 << 28
+    E = int(col.size)
+    while True:
+        old = lab.clone()
+        for e0 in range(0, E, chunk):
+            e1 = min(E, e0 + chunk)
+            pos = torch.arange(e0, e1, device=dev)
+            rows = torch.searchsorted(rp, pos, right=True) - 1  # row of each entry
+            del pos
+            lab.scatter_reduce_(0, rows, lab[cols[e0:e1].long()], reduce="amin")
+            del rows
+        for _ in range(4):  # pointer jumping
+            lab = lab[lab]
+        if torch.equal(lab, old):
+            break
+    size = torch.bincount(lab, minlength=V)
+    vol = torch.bincount(lab, weights=deg.double(), minlength=V)
+    out = lab.cpu(), size.cpu(), vol.cpu()
+    del lab, size, vol, cols, rp, deg
+    torch.cuda.empty_cache()
+    return out
+
+
 def test_c4_full_size_lane_groups_equal_single(hip_lib):
+    """Also, on the single engine: P1 (every message reaches exactly its
+    source's connected component) and KAT-3 (no timer fires before
+    quiescence, so forwards = Σ_m [vol(comp) - (|comp| - 1)]), with the
+    components computed from the exported graph."""
     V, K = 100_000_000, 4096
     seed = BASE_SEED + 4
     gen = dict(kind="rmat", n=V, k=16, seed=seed, a=0.57, b=0.19, c=0.19)
-    inj = injection_arrays(uniform_injections(V, K, seed))
+    inj_l = uniform_injections(V, K, seed)
+    inj = injection_arrays(inj_l)
     e = Engine(V, K, seed=seed, enable_sync=True, library=hip_lib)
     try:
         e.generate(**gen)
         want = _to_quiescence(e, inj)
+        topo = e.export_topology()
     finally:
         e.close()
     assert want[-1]["new_bits"] == 0
+    assert all(s["syncs_fired"] == 0 for s in want), "a sync timer fired before quiescence"
+    lab, size, vol = _components(topo.row_ptr, topo.col)
+    del topo
+    src = [n for n, _, _ in inj_l]
+    comp = lab[src]
+    p1 = int(size[comp].sum())
+    kat3 = int(round(float(vol[comp].sum()))) - p1 + K
+    assert sum(s["new_bits"] for s in want) == p1, "P1: deliveries != sum of source component sizes"
+    assert sum(s["fwd_sent"] for s in want) == kat3, "KAT-3: forwards != sum of vol(comp) - (|comp| - 1)"
+    for a, b in zip(want, want[1:]):
+        assert b["acks"] == a["fwd_delivered"] + a["push_delivered"]
     R = len(want)
     got = None
     for rank in range(2):

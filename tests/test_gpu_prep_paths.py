@@ -1,0 +1,65 @@
+"""round_prep's grid-capped paths against the CPU oracle, round by round.
+
+round_prep strides over the owned nodes with a capped grid (1024 blocks).
+When the cap would need more than four passes, sparse lean rounds take four
+nodes per thread from one 32-bit load of each flag array (the "quad" path,
+DESIGN.md §7c); at the default cap only graphs above 2^20 nodes take it. The
+cap is read once per process, so the case runs in a child process with
+GG_PREP_BLOCKS=1 (a one-block grid): every graph above 1024 nodes then takes
+the quad path in its sparse rounds, and the sync rounds take the one-node
+path with many passes. Counters (including seen_hash), node sets and delivery
+rounds must equal O2 in every round.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import json, sys
+sys.path[:0] = [%(tests)r, %(pkg)r, %(repo)r]
+import numpy as np
+from ggamd import topology as T
+from ggamd.workload import uniform_injections
+from helpers import Scenario, diff_stats, make_engine
+scs = [
+    Scenario(T.tree(5000, 4), 128, 24, uniform_injections(5000, 100, 3), seed=4, enable_sync=False),
+    Scenario(T.random_regular(6000, 8, seed=5), 64, 16, uniform_injections(6000, 64, 6), seed=7,
+             enable_sync=False),
+    Scenario(T.grid_links(70, seed=8), 256, 30, uniform_injections(4900, 200, 9), seed=10,
+             enable_sync=False),
+    Scenario(T.tree(4100, 4), 1024, 40, uniform_injections(4100, 700, 11), seed=12, sync_base=9,
+             sync_jitter=4),
+]
+bad = []
+for k, sc in enumerate(scs):
+    g = make_engine(%(hip)r, sc, device=0)
+    c = make_engine(%(cpu)r, sc)
+    for r in range(sc.rounds):  # round by round: a late candidate mark would show here
+        d = diff_stats(g.step(1), c.step(1))
+        if d:
+            bad.append((k, d[:5]))
+            break
+        if r %% 4 == 3 and not np.array_equal(g.read_bits(), c.read_bits()):
+            bad.append((k, "sets differ at round %%d" %% r))
+            break
+    if not np.array_equal(g.delivery_rounds(), c.delivery_rounds()):
+        bad.append((k, "delivery rounds differ"))
+    g.close(); c.close()
+print(json.dumps(bad))
+"""
+
+
+def test_prep_quad_path_equals_oracle(hip_lib, cpu_lib):
+    code = CHILD % {"tests": os.path.join(REPO, "tests"), "pkg": os.path.join(REPO, "gossip-glomers-distributed-systems_amd"),
+                    "repo": REPO, "hip": hip_lib, "cpu": cpu_lib}
+    env = dict(os.environ, GG_PREP_BLOCKS="1")
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert json.loads(p.stdout.strip().splitlines()[-1]) == []

@@ -20,7 +20,7 @@ import time
 import pytest
 
 from ggamd import topology as T
-from ggamd.engine import Engine
+from ggamd.engine import Engine, Topology
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(REPO, "gossip-glomers-distributed-systems_amd", "maelstrom-broadcast-hip")
@@ -96,12 +96,12 @@ def test_missing_engine_fails_loudly():
     assert rc == 1 and "cannot load the engine" in err and not out
 
 
-def _workload(seed, V, rounds):
+def _workload(seed, V, rounds, per_round=4):
     rnd = random.Random(seed)
     ev = []  # (round, kind, node, value)
     val = 0
     for r in range(rounds):
-        for _ in range(rnd.randrange(0, 4)):
+        for _ in range(rnd.randrange(0, per_round)):
             if rnd.random() < 0.5:
                 ev.append((r, "broadcast", rnd.randrange(V), val))
                 val += 1
@@ -110,12 +110,14 @@ def _workload(seed, V, rounds):
     return ev
 
 
-def _equivalence(engine_args, ref_lib, device=None):
-    topo = T.random_regular(60, 4, seed=5)
-    V, rounds = topo.n_nodes, 40
-    ev = _workload(11, V, rounds)
+def _equivalence(engine_args, ref_lib, device=None, lanes=128, rounds=40, per_round=4, topo=None):
+    topo = topo or T.random_regular(60, 4, seed=5)
+    V = topo.n_nodes
+    ev = _workload(11, V, rounds, per_round)
     lines, mid = cluster(topo), 100
-    ref = Engine(V, 128, seed=0x6A09E667F3BCC909, sync_base=20, sync_jitter=10, enable_sync=True,
+    n_values = sum(1 for e in ev if e[1] == "broadcast")
+    W = max(128, (n_values + 63) // 64 * 64)
+    ref = Engine(V, W, seed=0x6A09E667F3BCC909, sync_base=20, sync_jitter=10, enable_sync=True,
                  library=ref_lib)
     ref.topology(topo)
     want = []
@@ -135,10 +137,11 @@ def _equivalence(engine_args, ref_lib, device=None):
         lines.append(msg("c0", "n0", {"type": "tick"}))
         ref.step(1)
         pending = {}
-    rc, out, err = run(lines, *engine_args, "--tick-ms", "0", "--lanes", "128")
+    rc, out, err = run(lines, *engine_args, "--tick-ms", "0", "--lanes", str(lanes))
     assert rc == 0, err
     got = [o["body"]["messages"] for o in out if o["body"]["type"] == "read_ok"]
     assert got == want
+    return n_values
 
 
 def test_reads_equal_engine_reads_cpu():
@@ -146,11 +149,42 @@ def test_reads_equal_engine_reads_cpu():
     _equivalence(["--engine", CPU_LIB], CPU_LIB)
 
 
+@pytest.mark.parametrize("directed", [False, True])
+def test_values_beyond_lane_capacity(directed):
+    """More distinct values than --lanes (the reference's map is unbounded,
+    broadcast.go:14,73): further engines take the new values, older quiet
+    engines freeze (symmetric topology), and every read equals one engine with
+    enough lanes for all values. Directed rows never freeze (sync can still
+    deliver along one-way links)."""
+    _need()
+    topo = None
+    if directed:
+        rnd = random.Random(3)
+        topo = Topology.from_rows([sorted(rnd.sample([u for u in range(50) if u != v], 3)) for v in range(50)])
+    n = _equivalence(["--engine", CPU_LIB], CPU_LIB, lanes=64, rounds=80, per_round=12, topo=topo)
+    assert n > 2 * 64  # at least three engines
+
+
+def test_handler_error_is_an_rpc_error():
+    """A broadcast the engine refuses (a node beyond the topology) gets a
+    Maelstrom error reply (code 13) and the node keeps serving."""
+    _need()
+    lines = cluster(T.tree(5, 4)) + [msg("c1", "n9", {"type": "broadcast", "msg_id": 3, "message": 7}),
+                                     msg("c1", "n1", {"type": "read", "msg_id": 4})]
+    rc, out, err = run(lines, "--engine", CPU_LIB, "--tick-ms", "0", "--lanes", "64")
+    assert rc == 0, err
+    assert out[10]["body"]["type"] == "error" and out[10]["body"]["code"] == 13
+    assert out[10]["body"]["in_reply_to"] == 3
+    assert out[11]["body"] == {"type": "read_ok", "in_reply_to": 4, "messages": None}
+
+
 @pytest.mark.gpu
 def test_reads_equal_oracle_reads_on_gpu():
-    """The default engine (libgossip_hip.so next to the binary) against O2."""
+    """The default engine (libgossip_hip.so next to the binary) against O2,
+    within one engine's lanes and beyond them."""
     _need()
     _equivalence([], CPU_LIB)
+    _equivalence([], CPU_LIB, lanes=64, rounds=80, per_round=12)
 
 
 def test_wall_clock_rounds():

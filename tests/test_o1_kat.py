@@ -113,6 +113,12 @@ def test_kat5_partition_blocks_cross_traffic_until_heal():
 
 
 def test_read_of_empty_node_is_null():
+    """HandleRead's ReadResponse.Messages starts as a nil slice
+    (broadcast.go:125): an empty read replies `"messages": null`."""
     o = O1Network(2, 64, enable_sync=False)
     o.topology([[1], [0]])
     assert o.read(0) == []
+    assert o.client_read(0, msg_id=5) == {"type": "read_ok", "messages": None, "in_reply_to": 5}
+    o.broadcast(1, 9, 0)
+    o.step(2)
+    assert o.client_read(0)["messages"] == [9]
