@@ -14,17 +14,20 @@ all ranks / the max-over-ranks wall time.
   grouped RCCL send/recv on its stream.
 --config C4 (configs[3], the 100M-node config the >= 6x scaling target is
   quoted on): R-MAT (.57,.19,.19,.05), edge factor 16, 10^8 nodes, K = 4096
-  messages in round 0. Strong scaling: the graph is fixed and the ranks split
-  the 4096 message lanes (gg_config.lane_groups = N): every GPU holds the whole
-  CSR (13 GB of its 288 GB) and 4096/N lanes of every node, so a round needs no
-  exchange at all; the per-round counters are summed with one all_reduce after
-  the timed episodes.
+  messages in round 0. Strong scaling over a 2-D grid of ranks, N = L x P
+  (--parts P, default 1): P vertex parts (each rank builds only its node range
+  of the graph on its GPU, with ghost copies of the adjacent remote nodes, and
+  exchanges one filtered ghost payload per round with the other parts of its
+  lane group over RCCL) times L = N / P lane groups (each a slice of the 4096
+  message lanes; lane groups never exchange anything). P = 1: every GPU holds
+  the whole CSR and 4096/N lanes, no exchange at all. The per-round counters
+  are summed with one all_reduce after the timed episodes.
 
 N > 1: after the timed region rank 0 runs one episode of a single unsharded
 engine over the whole graph on its own GPU and every round's global counters
 must equal it, else the run exits with status 1.
 
-Usage: python bench.py [--config C2|C4] [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+Usage: python bench.py [--config C2|C4] [--parts P] [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
 For N > 1 launch under torch.distributed.run (one process per GPU).
 """
 from __future__ import annotations
@@ -92,7 +95,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--nodes", type=int, help="C2: nodes per GPU (2^20); C4: nodes (10^8)")
     ap.add_argument("--lanes", type=int, help="C2: 1024; C4: 4096")
+    ap.add_argument("--parts", type=int, default=1, help="C4: vertex parts P (world = lane groups x P)")
+    ap.add_argument("--halves", type=int, default=1, choices=[1, 2],
+                    help="C4 with --parts > 1: 2 = two engines per GPU over the two halves of its lanes, "
+                         "one half's exchange overlapping the other half's kernels (ggamd.dist.HalvesRunner)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fresh-sets", type=int, default=4,
+                    help="N = 1: after the timed region, episodes rotating this many distinct seeded injection "
+                         "sets (every step re-captures its launch graph and uploads its injections; 0: skip)")
     ap.add_argument("--no-check", action="store_true", help="skip the N > 1 single-engine check")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 "
                     "(nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
@@ -146,6 +156,7 @@ def main():
         E = int(topo.nnz)
         eng = Engine(V, K, seed=seed, enable_sync=True, device=local, rank=rank, world=world)
         eng.topology(topo)
+        engs = [eng]
         if world > 1:
             from ggamd.dist import ShardedRunner
             runner = ShardedRunner(eng, device)
@@ -159,11 +170,35 @@ def main():
         seed = BASE_SEED + 4
         topo = None
         gen = dict(kind="rmat", n=V, k=16, seed=seed, a=0.57, b=0.19, c=0.19)
-        eng = Engine(V, K, seed=seed, enable_sync=True, device=local, rank=rank, world=world,
-                     lane_groups=world)
-        E = eng.generate(**gen)  # the whole graph in this GPU's HBM (gossip_gen.h)
-        parallelism = f"message lanes x{world} (every GPU: whole graph, {K // world} lanes)" \
-            if world > 1 else "single GPU"
+        P = args.parts
+        if world % P:
+            raise SystemExit(f"--parts {P} does not divide the world size {world}")
+        L = world // P
+        if args.halves == 2 and P > 1:
+            from ggamd.dist import HalvesRunner
+            g, q = divmod(rank, P)
+            engs = [Engine(V, K, seed=seed, enable_sync=True, device=local, rank=(2 * g + h) * P + q,
+                           world=2 * world, lane_groups=2 * L) for h in range(2)]
+            E = engs[0].generate(**gen)
+            engs[1].generate(**gen)
+            eng = engs[0]
+            runner = HalvesRunner(engs, device)
+        else:
+            eng = Engine(V, K, seed=seed, enable_sync=True, device=local, rank=rank, world=world,
+                         lane_groups=L)
+            E = eng.generate(**gen)  # this rank's rows of the graph, built in its GPU's HBM (gossip_gen.h)
+            engs = [eng]
+            if P > 1:
+                from ggamd.dist import ShardedRunner
+                runner = ShardedRunner(eng, device, transport=None if args.backend == "nccl" else "engine")
+        if world == 1:
+            parallelism = "single GPU"
+        elif P == 1:
+            parallelism = f"message lanes x{world} (every GPU: whole graph, {K // world} lanes)"
+        else:
+            parallelism = (f"{L} lane groups x {P} vertex parts (each GPU: 1/{P} of the nodes + ghosts, "
+                           f"{K // L} lanes" + (", as two engines of half the lanes each, exchange of one "
+                                                "overlapping the other's kernels)" if len(engs) == 2 else ")"))
         scaling = "strong"
         workload = (f"C4: R-MAT (.57,.19,.19,.05) edge factor 16, symmetrized, {V} nodes, {K} messages "
                     "broadcast in round 0 at seeded uniform nodes, sync on, no partitions; graph built "
@@ -180,13 +215,14 @@ def main():
         return runner.step(n, reduce=False)
 
     # warmup 0: the quiescence round R from per-round global counts
-    eng.reset()
-    inject(eng, inj_arr)
+    for e in engs:
+        e.reset()
+        inject(e, inj_arr)
     R = 0
     while True:
-        st = runner.step(1)[0] if runner else eng.step(1)[0]
+        st = runner.step(1, reduce=False)[0] if runner else eng.step(1)[0]
         nb = st["new_bits"]
-        if world > 1 and runner is None:  # lane groups: sum over the ranks
+        if world > 1:  # sum over the ranks
             nb = allreduce_i64([nb])[0]
         R += 1
         if nb == 0 and R > 1:
@@ -197,12 +233,24 @@ def main():
     event_ms = []
 
     def episode():
-        eng.reset()
-        inject(eng, inj_arr)
+        for e in engs:
+            e.reset()
+            inject(e, inj_arr)
         st = run_rounds(R)
         if runner is None:
             event_ms.append(eng.step_device_ms())
         return st
+
+    def quiescence_rounds(arrs):  # single engine: rounds to the round after the last delivery
+        eng.reset()
+        inject(eng, arrs)
+        n = 0
+        while True:
+            n += 1
+            if eng.step(1)[0]["new_bits"] == 0 and n > 1:
+                return n
+            if n > 400:
+                raise RuntimeError("no quiescence within 400 rounds")
 
     for _ in range(max(0, args.warmup - 1)):
         episode()
@@ -216,6 +264,30 @@ def main():
     barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+
+    # fresh episodes (N = 1): every step broadcasts a different seeded value set, so
+    # the launch graph is captured and instantiated again and the injections are
+    # uploaded again, as in a workload whose clients keep sending new values
+    fresh = None
+    if world == 1 and args.fresh_sets > 0:
+        sets = [injection_arrays(uniform_injections(V, K, seed + 7919 * (i + 1))) for i in range(args.fresh_sets)]
+        rounds_of = [quiescence_rounds(a) for a in sets]
+        n_fresh = max(args.fresh_sets, min(args.steps, 2 * args.fresh_sets))
+        torch.cuda.synchronize()
+        f0 = time.perf_counter()
+        fdl = 0
+        for k in range(n_fresh):
+            i = k % args.fresh_sets
+            eng.reset()
+            inject(eng, sets[i])
+            st = eng.step(rounds_of[i], raw=True)
+            fdl += sum(st[j].new_bits for j in range(rounds_of[i]))
+        torch.cuda.synchronize()
+        fdt = time.perf_counter() - f0
+        fresh = {"sets": args.fresh_sets, "steps": n_fresh, "rounds_per_set": rounds_of,
+                 "ms_per_step": fdt / n_fresh * 1e3, "deliveries_per_s": fdl / fdt,
+                 "note": "each step re-captures and instantiates its hipGraph and uploads its injections "
+                         "(the timed `value` replays one cached graph with resident injections)"}
     if runner is None:
         local_stats = [[stats_dict(a[i]) for i in range(R)] for a in local_stats]
     if world > 1:
@@ -232,12 +304,15 @@ def main():
     dinfo = None
     if runner is not None:
         dinfo = eng.dist_info()
-        owned = eng.dist_owned().astype(np.int64)
-        n_own = int(owned.size)
-        E_own = int((topo.row_ptr[owned + 1] - topo.row_ptr[owned]).sum())
+        n_own = dinfo["owned"]
+        if topo is not None:
+            owned = eng.dist_owned().astype(np.int64)
+            E_own = int((topo.row_ptr[owned + 1] - topo.row_ptr[owned]).sum())
+        else:
+            E_own = E  # generate() returned this rank's adjacency entries
     else:
         n_own, E_own = V, E
-    nwp = next_pow2(K // 64 // (world if cfg == "C4" else 1))
+    nwp = next_pow2(K // 64 // (world // args.parts * len(engs) if cfg == "C4" else 1))
     rounds_local = [s for ep in local_stats for s in ep]
     kinds = {}
     for kind, name in KERNELS.items():
@@ -261,7 +336,8 @@ def main():
     if world > 1 and not args.no_check:
         bad = 0
         if rank == 0:
-            eng.close()  # free this rank's shard before building the whole graph
+            for e in engs:
+                e.close()  # free this rank's shard before building the whole graph
             ref = Engine(V, K, seed=seed, enable_sync=True, device=local)
             if gen is None:
                 ref.topology(topo)
@@ -307,11 +383,14 @@ def main():
                 "exchange": (runner.transport if runner is not None else
                              ("none: lane groups never exchange; one all_reduce of the counters "
                               "after the timed episodes" if world > 1 else None)),
+                "lane_groups": world // args.parts if cfg == "C4" else 1,
+                "vertex_parts": args.parts if cfg == "C4" else world,
                 "exchange_bytes_per_round_rank0": xbytes,
                 "shard": dinfo,
                 "hbm_bytes_rank0": hbm_bytes,
                 "setup_s_rank0": setup_s,
                 "check": check,
+                "fresh_injections": fresh,
             },
             "roofline": {
                 "bound": "hbm",

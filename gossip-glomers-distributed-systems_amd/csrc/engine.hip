@@ -284,7 +284,9 @@ struct gg_engine {
     BatchKey graph_key;
     bool graph_broken = false;
 
-    ncclComm_t comm = nullptr;  // engine-owned RCCL communicator (gg_dist_comm_init)
+    ncclComm_t comm = nullptr;  // engine-owned RCCL communicator over the lane group's parts
+    gg_transport xport{};       // or the caller's transport (gg_dist_transport_init)
+    bool have_xport = false;
 
     int fail(int code, const std::string& m) {
         err = m;
@@ -2344,50 +2346,114 @@ int gg_dist_comm_id(uint8_t* id_out) {
 int gg_dist_comm_init(gg_engine* e, const uint8_t* id_in) {
     if (!e || !id_in) return GG_EINVAL;
     if (e->world < 2) return e->fail(GG_EINVAL, "not a sharded engine (world == 1)");
-    if (e->comm) return e->fail(GG_EINVAL, "communicator already set");
+    if (e->comm || e->have_xport) return e->fail(GG_EINVAL, "exchange transport already set");
+    if (e->P < 2) return e->fail(GG_EINVAL, "no vertex parts (lane_groups == world): nothing to exchange");
     const RcclApi& r = rccl();
     if (!r.ok) return e->fail(GG_EIO, r.why);
     HIPCHK(hipSetDevice(e->device));
     ncclUniqueId id;
     std::memcpy(&id, id_in, sizeof(id));
     ncclComm_t c = nullptr;
-    NCCLCHK(r.init_rank(&c, (int)e->world, id, (int)e->rank));
+    // one communicator per lane group: its P parts, rank = part (lane groups never
+    // exchange anything, and a process may hold engines of several lane groups)
+    NCCLCHK(r.init_rank(&c, (int)e->P, id, (int)e->part));
     e->comm = c;
     return GG_OK;
 }
 
+int gg_dist_transport_init(gg_engine* e, const gg_transport* t) {
+    if (!e || !t || !t->group_start || !t->send || !t->recv || !t->group_end) return GG_EINVAL;
+    if (e->world < 2) return e->fail(GG_EINVAL, "not a sharded engine (world == 1)");
+    if (e->comm || e->have_xport) return e->fail(GG_EINVAL, "exchange transport already set");
+    e->xport = *t;
+    e->have_xport = true;
+    return GG_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// One group of point-to-point transfers of gg_dist_step, enqueued on the engine
+// stream over RCCL or the caller's transport; peers are part indices of the
+// engine's lane group. The group is closed even after a failed call.
+struct XGroup {
+    gg_engine* e;
+    int rc = GG_OK;
+    std::string what;
+    explicit XGroup(gg_engine* eng) : e(eng) {
+        if (e->comm) {
+            const ncclResult_t x = rccl().group_start();
+            if (x != ncclSuccess) fail(std::string("ncclGroupStart: ") + rccl().errstr(x));
+        } else if (e->xport.group_start(e->xport.user)) {
+            fail("transport group_start failed");
+        }
+    }
+    void fail(const std::string& m) {
+        if (rc == GG_OK) {
+            rc = GG_EIO;
+            what = m;
+        }
+    }
+    void send(const void* p, uint64_t n, uint32_t q) {
+        if (rc) return;
+        if (e->comm) {
+            const ncclResult_t x = rccl().send(p, n, ncclUint8, (int)q, e->comm, e->stream);
+            if (x != ncclSuccess) fail(std::string("ncclSend: ") + rccl().errstr(x));
+        } else if (e->xport.send(e->xport.user, p, n, q, (void*)e->stream)) {
+            fail("transport send failed");
+        }
+    }
+    void recv(void* p, uint64_t n, uint32_t q) {
+        if (rc) return;
+        if (e->comm) {
+            const ncclResult_t x = rccl().recv(p, n, ncclUint8, (int)q, e->comm, e->stream);
+            if (x != ncclSuccess) fail(std::string("ncclRecv: ") + rccl().errstr(x));
+        } else if (e->xport.recv(e->xport.user, p, n, q, (void*)e->stream)) {
+            fail("transport recv failed");
+        }
+    }
+    int close() {
+        if (e->comm) {
+            const ncclResult_t x = rccl().group_end();
+            if (x != ncclSuccess) fail(std::string("ncclGroupEnd: ") + rccl().errstr(x));
+        } else if (e->xport.group_end(e->xport.user)) {
+            fail("transport group_end failed");
+        }
+        return rc ? e->fail(rc, what) : GG_OK;
+    }
+};
+}  // namespace
+
+extern "C" {
+
 int gg_dist_step(gg_engine* e, uint32_t n_rounds) {
     if (!e) return GG_EINVAL;
-    if (!e->comm) return e->fail(GG_EINVAL, "no communicator (gg_dist_comm_init)");
-    const RcclApi& r = rccl();
     const uint32_t P = e->P;
+    if (P > 1 && !e->comm && !e->have_xport)
+        return e->fail(GG_EINVAL, "no communicator (gg_dist_comm_init or gg_dist_transport_init)");
     auto peer = [&](uint32_t q) {  // shares edges with part q (capacities are non-zero both ways)
         return q != e->part && e->xsoff.size() > q + 1 && e->xsoff[q + 1] > e->xsoff[q];
     };
+    std::vector<uint64_t> sb(P, 0), rb(P, 0);
     for (uint32_t k = 0; k < n_rounds; ++k) {
         gg_exchange x{};
         int rc = dist_begin(e, &x, false);
         if (rc) return rc;
         if (P > 1) {
-            std::vector<uint64_t> sb(P, 0), rb(P, 0);
             for (uint32_t q = 0; q < P; ++q) {
                 sb[q] = e->xsoff[q + 1] - e->xsoff[q];
                 rb[q] = e->xroff[q + 1] - e->xroff[q];
             }
             if (e->xexact) {
-                // exact directions: this round's segment size first (8 bytes), then one wait
-                NCCLCHK(r.group_start());
-                ncclResult_t first = ncclSuccess;
-                for (uint32_t q = 0; q < P && first == ncclSuccess; ++q) {
+                // exact directions: this round's segment sizes first (8 bytes each way),
+                // then one host wait for them (the payload counts are host arguments)
+                XGroup g(e);
+                for (uint32_t q = 0; q < P; ++q) {
                     if (q == e->part) continue;
-                    if (e->xexact_s[q])
-                        first = r.send(e->d_segbytes + q, 1, ncclUint64, (int)e->peer_rank(q), e->comm, e->stream);
-                    if (first == ncclSuccess && e->xexact_r[q])
-                        first = r.recv(e->d_segbytes + P + q, 1, ncclUint64, (int)e->peer_rank(q), e->comm, e->stream);
+                    if (e->xexact_s[q]) g.send(e->d_segbytes + q, 8, q);
+                    if (e->xexact_r[q]) g.recv(e->d_segbytes + P + q, 8, q);
                 }
-                const ncclResult_t ge = r.group_end();
-                NCCLCHK(first);
-                NCCLCHK(ge);
+                if ((rc = g.close())) return rc;
                 HIPCHK(hipMemcpyAsync(e->h_segbytes, e->d_segbytes, 2 * P * 8, hipMemcpyDeviceToHost, e->stream));
                 HIPCHK(hipStreamSynchronize(e->stream));
                 for (uint32_t q = 0; q < P; ++q) {
@@ -2397,18 +2463,13 @@ int gg_dist_step(gg_engine* e, uint32_t n_rounds) {
                         return e->fail(GG_EIO, "exchange segment larger than its capacity");
                 }
             }
-            NCCLCHK(r.group_start());
-            ncclResult_t first = ncclSuccess;  // the group is always closed, even after a failed call
-            for (uint32_t q = 0; q < P && first == ncclSuccess; ++q) {
+            XGroup g(e);
+            for (uint32_t q = 0; q < P; ++q) {
                 if (!peer(q)) continue;  // own part / no shared edges: nothing either way
-                const int pr_q = (int)e->peer_rank(q);
-                if (sb[q]) first = r.send(e->d_xsend + e->xsoff[q], sb[q], ncclUint8, pr_q, e->comm, e->stream);
-                if (first == ncclSuccess && rb[q])
-                    first = r.recv(e->d_xrecv + e->xroff[q], rb[q], ncclUint8, pr_q, e->comm, e->stream);
+                if (sb[q]) g.send(e->d_xsend + e->xsoff[q], sb[q], q);
+                if (rb[q]) g.recv(e->d_xrecv + e->xroff[q], rb[q], q);
             }
-            const ncclResult_t ge = r.group_end();
-            NCCLCHK(first);
-            NCCLCHK(ge);
+            if ((rc = g.close())) return rc;
         }
         if ((rc = gg_dist_round_end(e, nullptr))) return rc;
     }

@@ -14,16 +14,22 @@ network delivery of every forward/push/read/read_ok crossing a shard boundary
     gg_dist_round_end     -> unpack kernel into this rank's ghost rows
 
 On GPUs the backend is "nccl" (= RCCL over xGMI on ROCm). By default `step`
-hands the exchange to the engine: rank 0 makes an RCCL unique id, torch
-broadcasts it, every engine opens its own communicator (gg_dist_comm_init) and
-gg_dist_step(n) runs n rounds with grouped ncclSend/ncclRecv of the non-empty
-segments on the engine stream, with no Python and no cross-stream event hop per
-round. GG_DIST_TRANSPORT=torch (or transport="torch") keeps the per-round
+hands the exchange to the engine: part 0 of every lane group makes an RCCL
+unique id, torch hands the ids round, every engine opens a communicator over
+its lane group's parts (gg_dist_comm_init) and gg_dist_step(n) runs n rounds
+with grouped ncclSend/ncclRecv of the non-empty segments on the engine stream,
+with no Python and no cross-stream event hop per round. With "gloo"
+transport="engine" runs the same gg_dist_step sequencing (size handshake,
+peers, offsets) over `HostTransport`, gg_transport callbacks that move each
+group through host memory with torch.distributed point-to-point ops: the test
+harness for the engine's own exchange on ranks that share one GPU.
+
+GG_DIST_TRANSPORT=torch (or transport="torch") keeps the per-round
 all_to_all_single through torch instead, enqueued on the engine's own HIP stream
-(torch.cuda.ExternalStream). Either way a multi-round step runs without host
-synchronisation and the per-round counters are collected once at the end
-(gg_dist_flush) and summed over ranks with one all_reduce. With "gloo" (CPU tests, or several ranks sharing one GPU in the GPU
-tests) the payloads are staged through host memory.
+(torch.cuda.ExternalStream); with "gloo" (CPU tests, or several ranks sharing
+one GPU in the GPU tests) that path stages the payloads through host memory.
+Either way the per-round counters are collected once at the end (gg_dist_flush)
+and summed over ranks with one all_reduce.
 """
 from __future__ import annotations
 
@@ -54,6 +60,68 @@ def _view(ptr: int, nbytes: int, on_device: bool, device: torch.device) -> torch
     return torch.from_numpy(arr)
 
 
+class HostTransport:
+    """gg_transport over torch.distributed (gloo), staged through host memory.
+
+    The engine calls group_start, send/recv per peer part, group_end at the
+    points where it would issue its RCCL group; group_end synchronises the
+    engine stream, copies the send buffers out, runs the point-to-point ops
+    with the peers' global ranks, and writes the receive buffers back before
+    returning (gossip.h: stream semantics of a host-staged transport)."""
+
+    def __init__(self, eng: Engine, device: torch.device, group=None, rank_of: list[int] | None = None):
+        from .engine import XPORT_START, XPORT_XFER, GGTransport
+        self.device, self.group = device, group
+        P = eng.parts
+        lgrp = eng.rank // P
+        glob = (lambda r: r) if group is None else (lambda r: dist.get_global_rank(group, r))
+        # the process rank of each part of this engine's lane group (default: one engine per process)
+        self._rank_of = rank_of or [glob(lgrp * P + q) for q in range(P)]
+        self.ops = []
+        self.error = None
+        self.groups = 0
+        self._cbs = (XPORT_START(self._start), XPORT_XFER(self._send), XPORT_XFER(self._recv), XPORT_START(self._end))
+        self.struct = GGTransport(None, *self._cbs)
+        eng.dist_transport_init(self.struct)
+
+    def _start(self, _user):
+        self.ops = []
+        return 0
+
+    def _send(self, _user, buf, nbytes, part, stream):
+        self.ops.append(("send", buf, nbytes, part, stream))
+        return 0
+
+    def _recv(self, _user, buf, nbytes, part, stream):
+        self.ops.append(("recv", buf, nbytes, part, stream))
+        return 0
+
+    def _end(self, _user):
+        try:
+            self.groups += 1
+            if not self.ops:
+                return 0
+            torch.cuda.ExternalStream(self.ops[0][4], device=self.device).synchronize()
+            p2p, back = [], []
+            for kind, buf, n, part, _ in self.ops:
+                dv = _view(buf, n, True, self.device)
+                if kind == "send":
+                    p2p.append(dist.P2POp(dist.isend, dv.cpu(), self._rank_of[part], self.group))
+                else:
+                    hb = torch.empty(n, dtype=torch.uint8)
+                    p2p.append(dist.P2POp(dist.irecv, hb, self._rank_of[part], self.group))
+                    back.append((dv, hb))
+            for w in dist.batch_isend_irecv(p2p):
+                w.wait()
+            for dv, hb in back:
+                dv.copy_(hb)
+            torch.cuda.synchronize(self.device)
+            return 0
+        except BaseException as exc:  # noqa: BLE001  (reported by the engine as GG_EIO)
+            self.error = exc
+            return 1
+
+
 class ShardedRunner:
     def __init__(self, eng: Engine, device: torch.device, group=None, transport: str | None = None):
         self.eng = eng
@@ -68,24 +136,40 @@ class ShardedRunner:
         want = transport or os.environ.get("GG_DIST_TRANSPORT", "engine")
         if want not in ("engine", "torch"):
             raise ValueError(f"transport {want!r}: 'engine' or 'torch'")
-        self.engine_comm = self.nccl and want == "engine" and self._init_engine_comm()
-        self.transport = "engine RCCL send/recv" if self.engine_comm else (
-            "torch all_to_all_single" if self.nccl else "gloo via host")
+        self.host_xport = None
+        if self.nccl:
+            self.engine_comm = want == "engine" and self._init_engine_comm()
+        else:  # gloo: the engine's own sequencing only when asked (transport="engine")
+            self.engine_comm = transport == "engine" and eng.parts > 1
+            if self.engine_comm:
+                self.host_xport = HostTransport(eng, device, group)
+        if eng.parts == 1 and self.nccl:
+            self.engine_comm = True  # lane groups only: nothing to exchange, gg_dist_step runs the rounds
+        if self.engine_comm:
+            self.transport = "none (lane groups only)" if eng.parts == 1 else (
+                "engine RCCL send/recv" if self.nccl else "engine sequencing, gloo host transport")
+        else:
+            self.transport = "torch all_to_all_single" if self.nccl else "gloo via host"
 
     def _init_engine_comm(self) -> bool:
-        """Open the engine's own RCCL communicator if every rank can (agreed by
-        an all_reduce first, so no rank waits in a collective init alone)."""
+        """Open the engine's own RCCL communicator (over its lane group's parts)
+        if every rank can (agreed by an all_reduce first, so no rank waits in a
+        collective init alone). Part 0 of each lane group makes the group's id;
+        one all_gather hands every rank its group's id."""
+        if self.eng.parts == 1:
+            return False
         ok, why = self.eng.dist_comm_available()
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
         if int(flag.item()) == 0:
             return False
+        P = self.eng.parts
         uid = torch.zeros(128, dtype=torch.uint8, device=self.device)
-        if self.rank == 0:
+        if self.rank % P == 0:
             uid.copy_(torch.frombuffer(bytearray(self.eng.dist_comm_id()), dtype=torch.uint8))
-        src = 0 if self.group is None else dist.get_global_rank(self.group, 0)
-        dist.broadcast(uid, src=src, group=self.group)
-        self.eng.dist_comm_init(uid.cpu().numpy().tobytes())
+        ids = [torch.empty_like(uid) for _ in range(self.world)]
+        dist.all_gather(ids, uid, group=self.group)
+        self.eng.dist_comm_init(ids[self.rank // P * P].cpu().numpy().tobytes())
         return True
 
     def _view(self, ptr, nbytes, on_dev):
@@ -110,6 +194,11 @@ class ShardedRunner:
         round), then the segments move point-to-point into the
         receivers' fixed segment offsets."""
         x = self.eng.dist_round_begin()
+        self.exchange(x)
+        return self.eng.dist_round_end(wait=wait)
+
+    def exchange(self, x) -> None:
+        """The exchange of a begun round (gg_dist_round_begin's gg_exchange)."""
         W = self.world
         on_dev = bool(x.on_device)
         ss = [int(x.send_bytes[i]) for i in range(W)]
@@ -131,7 +220,7 @@ class ShardedRunner:
         for i in range(W):
             x.recv_bytes[i] = rs[i]
         if not any(ss) and not any(rs):
-            return self.eng.dist_round_end(wait=wait)
+            return
         send = self._view(x.send, x.send_total, on_dev)
         recv = self._view(x.recv, x.recv_total, on_dev)
         stage = on_dev and not self.nccl  # gloo with device buffers (ranks sharing one GPU): via host
@@ -161,11 +250,15 @@ class ShardedRunner:
                     recv.copy_(recv_b)
             else:
                 recv.copy_(recv_b)
-        return self.eng.dist_round_end(wait=wait)
 
     def step(self, n_rounds: int, reduce: bool = True) -> list[dict]:
         if self.engine_comm:
-            self.eng.dist_step(n_rounds)
+            try:
+                self.eng.dist_step(n_rounds)
+            except Exception:
+                if self.host_xport is not None and self.host_xport.error is not None:
+                    raise self.host_xport.error
+                raise
         else:
             for _ in range(n_rounds):
                 self.round(wait=False)
@@ -194,3 +287,75 @@ class ShardedRunner:
                 d[f] = int(tot[k, j]) & M64
             out.append(d)
         return out
+
+
+def _sum_rounds(a: list[dict], b: list[dict]) -> list[dict]:
+    """Per-round counters of two engines over disjoint lanes, summed (seen_hash mod 2^64)."""
+    out = []
+    for x, y in zip(a, b):
+        d = dict(x)
+        for f in COUNT_FIELDS:
+            d[f] = (x[f] + y[f]) & M64
+        d["kernel_ms"] = max(x["kernel_ms"], y["kernel_ms"])
+        d["sent_bytes"] = x["sent_bytes"] + y["sent_bytes"]
+        out.append(d)
+    return out
+
+
+class HalvesRunner:
+    """Two engines per GPU, each half of this process's message lanes, so one
+    half's exchange overlaps the other half's kernels.
+
+    Process p = g * P + q of a job with L lane groups x P vertex parts holds
+    engines (2g, q) and (2g + 1, q) of a 2L x P engine grid (gg_config
+    lane_groups = 2L, world = 2N): the same vertex range, lanes split in two.
+    Lane groups never interact, so the job's results are those of the L x P
+    job. Each engine has its own HIP stream and its own exchange (an RCCL
+    communicator over its lane group's P parts, or HostTransport over gloo), and
+    a round is enqueued half by half: while half A's payload moves, half B's
+    kernels run, and the reverse for A's next round. On a graph where every
+    node has remote neighbours (R-MAT, random long links) this is the overlap
+    that interior-first ordering cannot give: there are no interior nodes."""
+
+    def __init__(self, engines: list[Engine], device: torch.device, group=None):
+        assert len(engines) == 2
+        self.engs = engines
+        self.device, self.group = device, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        P = engines[0].parts
+        self.P = P
+        g, q = divmod(self.rank, P)
+        for h, e in enumerate(engines):
+            assert e.world == 2 * self.world and e.rank == (2 * g + h) * P + q and e.parts == P
+        self.nccl = dist.get_backend(group) == "nccl"
+        glob = (lambda r: r) if group is None else (lambda r: dist.get_global_rank(group, r))
+        self.xports = []
+        if P == 1:
+            self.transport = "none (lane groups only)"
+        elif self.nccl:
+            ok = all(e.dist_comm_available()[0] for e in engines)
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+            if int(flag.item()) == 0:
+                raise RuntimeError("RCCL entry points unavailable on some rank")
+            uid = torch.zeros(2, 128, dtype=torch.uint8, device=device)
+            if q == 0:
+                for h, e in enumerate(engines):
+                    uid[h].copy_(torch.frombuffer(bytearray(e.dist_comm_id()), dtype=torch.uint8))
+            ids = [torch.empty_like(uid) for _ in range(self.world)]
+            dist.all_gather(ids, uid, group=group)
+            for h, e in enumerate(engines):
+                e.dist_comm_init(ids[g * P][h].cpu().numpy().tobytes())
+            self.transport = "engine RCCL send/recv, two lane halves per GPU"
+        else:
+            for e in engines:
+                self.xports.append(HostTransport(e, device, group, rank_of=[glob(g * P + x) for x in range(P)]))
+            self.transport = "engine sequencing, gloo host transport, two lane halves per GPU"
+
+    def step(self, n_rounds: int, reduce: bool = True) -> list[dict]:
+        for _ in range(n_rounds):
+            for e in self.engs:  # half A's round, then half B's: B's kernels run during A's exchange
+                e.dist_step(1)
+        local = _sum_rounds(self.engs[0].dist_flush(), self.engs[1].dist_flush())
+        return ShardedRunner.reduce(self, local) if reduce else local

@@ -87,6 +87,20 @@ class GGExchange(C.Structure):
     ]
 
 
+XPORT_START = C.CFUNCTYPE(C.c_int, C.c_void_p)
+XPORT_XFER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p)
+
+
+class GGTransport(C.Structure):  # include/gossip.h gg_transport
+    _fields_ = [
+        ("user", C.c_void_p),
+        ("group_start", XPORT_START),
+        ("send", XPORT_XFER),
+        ("recv", XPORT_XFER),
+        ("group_end", XPORT_START),
+    ]
+
+
 class GGGenSpec(C.Structure):  # include/gossip_gen.h
     _fields_ = [
         ("kind", C.c_uint32),
@@ -114,7 +128,7 @@ GG_SYMBOLS = [
     "gg_current_round", "gg_step_device_ms", "gg_read", "gg_read_bits", "gg_delivery_rounds", "gg_reset",
     "gg_read_bits_nodes", "gg_delivery_rounds_nodes",
     "gg_dist_round_begin", "gg_dist_round_end", "gg_dist_flush", "gg_dist_owned", "gg_dist_info",
-    "gg_dist_comm_available", "gg_dist_comm_id", "gg_dist_comm_init", "gg_dist_step",
+    "gg_dist_comm_available", "gg_dist_comm_id", "gg_dist_comm_init", "gg_dist_transport_init", "gg_dist_step",
 ]
 
 _LIBS: dict[str, C.CDLL] = {}
@@ -159,6 +173,7 @@ def load_library(path: str) -> C.CDLL:
     lib.gg_dist_comm_id.argtypes = [C.c_void_p]
     lib.gg_dist_comm_init.argtypes = [C.c_void_p, C.c_void_p]
     lib.gg_dist_step.argtypes = [C.c_void_p, C.c_uint32]
+    lib.gg_dist_transport_init.argtypes = [C.c_void_p, P(GGTransport)]
     lib.gg_delivery_rounds_nodes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
     if hasattr(lib, "gg_topology_generate"):
         lib.gg_topology_generate.argtypes = [C.c_void_p, P(GGGenSpec), P(C.c_uint64)]
@@ -390,6 +405,12 @@ class Engine:
         assert len(uid) == 128
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         self._ok(self.lib.gg_dist_comm_init(self.h, buf))
+
+    def dist_transport_init(self, t: "GGTransport") -> None:
+        """The engine-driven exchange over the caller's transport (callbacks kept
+        alive by the caller for the engine's lifetime)."""
+        self._xport = t
+        self._ok(self.lib.gg_dist_transport_init(self.h, C.byref(t)))
 
     def dist_step(self, n_rounds: int) -> None:
         """n sharded rounds with the engine's own RCCL exchange; counters pending (dist_flush)."""

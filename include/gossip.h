@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 4
+#define GG_ABI_VERSION 5
 
 #define GG_OK 0
 #define GG_EIO (-5)
@@ -220,18 +220,40 @@ int gg_dist_info(const gg_engine* e, uint64_t* n_own, uint64_t* n_ghost, uint64_
 int gg_dist_owned(const gg_engine* e, uint32_t* nodes, uint64_t cap, uint64_t* n_out);
 
 /* Engine-owned exchange over RCCL (GPU engines): the rounds run without a caller
- * collective. Every rank of the sharded job passes the same 128-byte id (rank 0
- * makes it with gg_dist_comm_id and the caller broadcasts it); gg_dist_comm_init
- * is collective (all ranks call it together). gg_dist_step(n) then enqueues n
- * rounds, each gg_dist_round_begin + grouped ncclSend/ncclRecv of the non-empty
- * segments on the engine stream + gg_dist_round_end(NULL); counters stay pending
- * for gg_dist_flush. Replaces the per-round all_to_all_single the caller would
- * issue (the network delivery of every cross-shard message, broadcast.go:55,99,106,120).
+ * collective. The communicator spans the P vertex parts of the engine's lane group
+ * (lane groups never exchange anything, so a process may hold engines of several
+ * lane groups on one GPU, each with its own communicator): every rank of the lane
+ * group passes the same 128-byte id (its part 0 makes it with gg_dist_comm_id and
+ * the caller hands it round) and gg_dist_comm_init is collective over the group.
+ * gg_dist_step(n) then enqueues n rounds, each gg_dist_round_begin + grouped
+ * ncclSend/ncclRecv of the non-empty segments on the engine stream +
+ * gg_dist_round_end(NULL); counters stay pending for gg_dist_flush. Replaces the
+ * per-round all_to_all_single the caller would issue (the network delivery of every
+ * cross-shard message, broadcast.go:55,99,106,120). Directions in exact-size mode
+ * (GG_XCHG_MODE, or capacity > 4 MiB) first exchange their 8-byte sizes, and the
+ * host waits for them once per round (payload counts are host arguments).
  * gg_dist_comm_available: 0 if the RCCL entry points resolve in this process
  * (why = reason otherwise); the CPU oracle library has no RCCL and returns GG_EIO. */
 int gg_dist_comm_available(char* why, uint64_t cap);
 int gg_dist_comm_id(uint8_t* id_out /* 128 bytes */);
 int gg_dist_comm_init(gg_engine* e, const uint8_t* id /* 128 bytes */);
+/* The same exchange over the caller's transport instead of RCCL (e.g. a test
+ * harness over another backend). gg_dist_step calls group_start, then send/recv of
+ * device buffers to/from part indices of the lane group, then group_end, exactly
+ * where it would issue the RCCL group. Stream semantics as in RCCL: the operations
+ * act in `stream` order (a transport that stages through the host synchronises the
+ * stream before reading and has written the receive buffers when group_end
+ * returns). Callbacks return 0 on success. */
+typedef struct {
+    void* user;
+    int (*group_start)(void* user);
+    int (*send)(void* user, const void* buf, uint64_t bytes, uint32_t part, void* stream);
+    int (*recv)(void* user, void* buf, uint64_t bytes, uint32_t part, void* stream);
+    int (*group_end)(void* user);
+} gg_transport;
+int gg_dist_transport_init(gg_engine* e, const gg_transport* t);
+/* n sharded rounds with the engine's exchange (RCCL or the transport; none needed
+ * when the engine has no other vertex part). */
 int gg_dist_step(gg_engine* e, uint32_t n_rounds);
 
 /* gg_read_bits / gg_delivery_rounds for a list of owned nodes (any engine). */

@@ -30,7 +30,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, lib, scenarios, q, lane_groups=1, env=None, generate=False):
+def _worker(rank, world, port, lib, scenarios, q, lane_groups=1, env=None, generate=False, transport=None):
     import torch
     import torch.distributed as dist
 
@@ -42,9 +42,13 @@ def _worker(rank, world, port, lib, scenarios, q, lane_groups=1, env=None, gener
         dev = torch.device("cuda", 0)
         for sc in scenarios:
             e = make_engine(lib, sc, rank=rank, world=world, device=0, lane_groups=lane_groups, generate=generate)
-            r = ShardedRunner(e, dev)
+            r = ShardedRunner(e, dev, transport=transport)
+            if transport == "engine" and e.parts > 1:  # gg_dist_step's own sequencing, over gloo
+                assert r.host_xport is not None, r.transport
             half = sc.rounds // 2
             stats = r.step(half) + r.step(sc.rounds - half)  # two flushes
+            if r.host_xport is not None:
+                assert r.host_xport.groups >= sc.rounds, r.host_xport.groups  # one group per round at least
             owned = e.dist_owned()
             out.append((stats, owned, e.read_bits_nodes(owned), e.delivery_rounds_nodes(owned)))
             e.close()
@@ -56,17 +60,18 @@ def _worker(rank, world, port, lib, scenarios, q, lane_groups=1, env=None, gener
         dist.destroy_process_group()
 
 
-def _run(lib, scenarios, world, lane_groups=1, env=None, generate=False):
+def _run(lib, scenarios, world, lane_groups=1, env=None, generate=False, transport=None, timeout=150):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, lib, scenarios, q, lane_groups, env, generate))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, lib, scenarios, q, lane_groups, env, generate,
+                                               transport))
              for r in range(world)]
     for p in procs:
         p.start()
     res = {}
     for _ in range(world):
-        r, got = q.get(timeout=150)
+        r, got = q.get(timeout=timeout)
         assert not isinstance(got, str), got
         res[r] = got
     for p in procs:
@@ -383,3 +388,158 @@ def test_device_partition_with_lane_groups(hip_lib):
         assert np.array_equal(bits, single.read_bits()), k
         assert np.array_equal(dr, single.delivery_rounds()), k
         single.close()
+
+
+@pytest.mark.parametrize("world,mode", [(2, "exact"), (3, "exact"), (3, "static")])
+def test_engine_exchange_sequencing_equals_single(hip_lib, world, mode):
+    """gg_dist_step's own sequencing — the exact-size handshake, the peer
+    choice, the segment offsets, one host wait per round — run through
+    gg_transport callbacks over gloo (ggamd.dist.HostTransport) instead of
+    RCCL, which refuses two ranks on one device: bit-exact against one engine,
+    host-built and device-built partitions."""
+    scs = _scenarios()[:5]
+    res = _run(hip_lib, scs, world, env={"GG_XCHG_MODE": mode}, transport="engine")
+    gen = _gen_scenarios()
+    res_g = _run(hip_lib, gen, world, env={"GG_XCHG_MODE": mode, "GG_HUB_DEG": "40"}, generate=True,
+                 transport="engine")
+    old = os.environ.get("GG_HUB_DEG")
+    for sc_list, rr, hub in ((scs, res, None), (gen, res_g, "40")):
+        if hub:
+            os.environ["GG_HUB_DEG"] = hub
+        try:
+            for k, sc in enumerate(sc_list):
+                single = make_engine(hip_lib, sc, device=0)
+                s1 = single.step(sc.rounds)
+                for rank in range(world):
+                    stats, owned, bits, dr = rr[rank][k]
+                    d = diff_stats(s1, stats)
+                    assert not d, (k, rank, d[:10])
+                    assert np.array_equal(bits, single.read_bits_nodes(owned)), (k, rank)
+                    assert np.array_equal(dr, single.delivery_rounds_nodes(owned)), (k, rank)
+                single.close()
+        finally:
+            if old is None:
+                os.environ.pop("GG_HUB_DEG", None)
+            else:
+                os.environ["GG_HUB_DEG"] = old
+
+
+def _world8_scenarios():
+    """BASELINE's 8-GPU shapes at a size one GPU's eight ranks run in seconds:
+    C4 (R-MAT, edge factor 16, hubs on the hub path with GG_HUB_DEG=24) and C5
+    (grid + one long link per node, W = 64), each with the sync timers firing
+    during propagation so sets cross the cut as well as F rows."""
+    from ggamd import topology as T
+    from ggamd.workload import uniform_injections
+    return [
+        Scenario(T.rmat(8192, 16, seed=51), 256, 26, uniform_injections(8192, 256, 52), seed=53, sync_base=6,
+                 sync_jitter=3, gen=dict(kind="rmat", n=8192, k=16, seed=51, a=0.57, b=0.19, c=0.19)),
+        Scenario(T.grid_links(96, seed=54), 64, 40, uniform_injections(96 * 96, 64, 55), seed=56, sync_base=9,
+                 sync_jitter=4, gen=dict(kind="grid_links", n=96, seed=54)),
+    ]
+
+
+def _check_against_oracle(cpu_lib, scs, res, world, lane_groups=1):
+    """Summed counters of every round, every node's set and delivery rounds
+    (OR / max over a node's lane-group owners) against O2 directly."""
+    for k, sc in enumerate(scs):
+        ref = make_engine(cpu_lib, sc)
+        want = ref.step(sc.rounds)
+        V = sc.topo.n_nodes
+        bits = np.zeros((V, sc.W // 64), np.uint64)
+        dr = np.full((V, sc.W), -1, np.int32)
+        seen = np.zeros(V, np.int64)
+        for rank in range(world):
+            stats, owned, b, d = res[rank][k]
+            assert not diff_stats(want, stats), (k, rank, diff_stats(want, stats)[:10])
+            o = owned.astype(np.int64)
+            bits[o] |= b
+            dr[o] = np.maximum(dr[o], d)
+            seen[o] += 1
+        assert np.all(seen == lane_groups), k  # every node owned once per lane group
+        assert np.array_equal(bits, ref.read_bits()), k
+        assert np.array_equal(dr, ref.delivery_rounds()), k
+        ref.close()
+
+
+@pytest.mark.parametrize("build", ["host_csr", "device"])
+@pytest.mark.parametrize("transport", ["torch", "engine"])
+def test_world8_equals_oracle(hip_lib, cpu_lib, build, transport):
+    """World 8 (BASELINE's GPU count) as 8 ranks on this GPU, vertex-range
+    sharded 8 ways, against the CPU oracle O2: the C4 and C5 shapes, host-CSR
+    partitions (gg_topology: locality order) and device-built ones
+    (gg_topology_generate: native ranges), over the Python all-to-all-v
+    sequencing and over the engine's own gg_dist_step sequencing."""
+    scs = _world8_scenarios()
+    res = _run(hip_lib, scs, 8, env={"GG_HUB_DEG": "24", "GG_XCHG_MODE": "exact"},
+               generate=(build == "device"), transport=transport, timeout=240)
+    _check_against_oracle(cpu_lib, scs, res, 8)
+
+
+def test_world8_lane_groups_by_parts_equals_oracle(hip_lib, cpu_lib):
+    """2 lane groups x 4 vertex parts (world 8), device-built partitions, the
+    engine's exchange sequencing, against O2."""
+    scs = [sc for sc in _world8_scenarios() if sc.W >= 128]
+    res = _run(hip_lib, scs, 8, lane_groups=2, env={"GG_HUB_DEG": "24"}, generate=True, transport="engine",
+               timeout=240)
+    _check_against_oracle(cpu_lib, scs, res, 8, lane_groups=2)
+
+
+def _halves_worker(rank, world, port, lib, scenarios, q, parts, env):
+    import torch
+    import torch.distributed as dist
+
+    from ggamd.dist import HalvesRunner
+    os.environ.update(env or {})
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        out = []
+        dev = torch.device("cuda", 0)
+        g, part = divmod(rank, parts)
+        L = world // parts
+        for sc in scenarios:
+            engs = [make_engine(lib, sc, rank=(2 * g + h) * parts + part, world=2 * world, device=0,
+                                lane_groups=2 * L, generate=True) for h in range(2)]
+            r = HalvesRunner(engs, dev)
+            half = sc.rounds // 2
+            stats = r.step(half) + r.step(sc.rounds - half)  # summed over ranks
+            owned = engs[0].dist_owned()
+            assert np.array_equal(owned, engs[1].dist_owned())
+            bits = engs[0].read_bits_nodes(owned) | engs[1].read_bits_nodes(owned)
+            dr = np.maximum(engs[0].delivery_rounds_nodes(owned), engs[1].delivery_rounds_nodes(owned))
+            out.append((stats, owned, bits, dr))
+            for e in engs:
+                e.close()
+        q.put((rank, out))
+    except BaseException as exc:
+        q.put((rank, f"rank {rank} failed: {exc!r}"))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,parts", [(2, 2), (4, 4), (4, 2)])
+def test_lane_halves_equal_oracle(hip_lib, cpu_lib, world, parts):
+    """ggamd.dist.HalvesRunner: two engines per process over the two halves of
+    its lanes, device-built vertex parts, the engines' own exchange over gloo,
+    half A's round then half B's: per-rank counters (summed over ranks) and
+    every node's set and delivery rounds equal O2."""
+    scs = [sc for sc in _world8_scenarios() if sc.W >= 256]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_halves_worker, args=(r, world, port, hip_lib, scs, q, parts,
+                                                      {"GG_HUB_DEG": "24", "GG_XCHG_MODE": "exact"}))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, got = q.get(timeout=240)
+        assert not isinstance(got, str), got
+        res[r] = got
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res = [res[r] for r in range(world)]
+    _check_against_oracle(cpu_lib, scs, res, world, lane_groups=world // parts)

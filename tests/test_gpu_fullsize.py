@@ -20,6 +20,7 @@ The reference has no full-size fixtures; these are size-independent
 properties of broadcast.go's algorithm, the CPU oracle O2 is
 pinned against it at 4K nodes (tests/test_golden.py).
 """
+import numpy as np
 import pytest
 
 from ggamd.engine import COUNT_FIELDS, Engine
@@ -77,37 +78,43 @@ def test_c3_full_size_heals(hip_lib):
     print(f"C3 10^7: {last} rounds to full delivery")
 
 
-def _components(row_ptr, col, device="cuda"):
+def _components(row_ptr, col, device="cuda", chunk=1 << 29):
     """Connected components of a symmetric CSR on the GPU (torch): min-label
-    propagation over every adjacency entry with pointer jumping, to a fixed
-    point. Returns (label per node, component size per label, degree sum per
-    label) as CPU tensors."""
+    propagation over every adjacency entry (rows and columns resident as int64
+    chunks) with pointer jumping, to a fixed point. Returns (label per node,
+    component size per label, degree sum per label) as CPU tensors."""
+    import time
+
     import torch
     dev = torch.device(device)
+    t0 = time.time()
     V = row_ptr.size - 1
-    rp = torch.from_numpy(row_ptr).to(dev)
-    deg = rp[1:] - rp[:-1]
-    cols = torch.from_numpy(col).to(dev)  # int32
-    lab = torch.arange(V, dtype=torch.int64, device=dev)
-    chunk = 1 << 28
+    deg = torch.from_numpy(row_ptr[1:] - row_ptr[:-1]).to(dev)
     E = int(col.size)
+    chunks = []  # (rows, cols) int64 on the device
+    for e0 in range(0, E, chunk):
+        e1 = min(E, e0 + chunk)
+        v0 = int(np.searchsorted(row_ptr, e0, side="right")) - 1
+        v1 = int(np.searchsorted(row_ptr, e1 - 1, side="right"))
+        rp = torch.from_numpy(np.clip(row_ptr[v0:v1 + 1], e0, e1) - e0).to(dev)
+        rows = torch.repeat_interleave(torch.arange(v0, v1, device=dev), rp[1:] - rp[:-1])
+        chunks.append((rows, torch.from_numpy(col[e0:e1]).to(dev).long()))
+    lab = torch.arange(V, dtype=torch.int64, device=dev)
+    it = 0
     while True:
         old = lab.clone()
-        for e0 in range(0, E, chunk):
-            e1 = min(E, e0 + chunk)
-            pos = torch.arange(e0, e1, device=dev)
-            rows = torch.searchsorted(rp, pos, right=True) - 1  # row of each entry
-            del pos
-            lab.scatter_reduce_(0, rows, lab[cols[e0:e1].long()], reduce="amin")
-            del rows
-        for _ in range(4):  # pointer jumping
+        for rows, cols in chunks:
+            lab.scatter_reduce_(0, rows, lab[cols], reduce="amin")
+        for _ in range(8):  # pointer jumping
             lab = lab[lab]
+        it += 1
+        print(f"components: pass {it}, {time.time() - t0:.1f} s", flush=True)
         if torch.equal(lab, old):
             break
     size = torch.bincount(lab, minlength=V)
     vol = torch.bincount(lab, weights=deg.double(), minlength=V)
     out = lab.cpu(), size.cpu(), vol.cpu()
-    del lab, size, vol, cols, rp, deg
+    del lab, size, vol, chunks, deg
     torch.cuda.empty_cache()
     return out
 
@@ -126,6 +133,7 @@ def test_c4_full_size_lane_groups_equal_single(hip_lib):
     try:
         e.generate(**gen)
         want = _to_quiescence(e, inj)
+        print("C4: episode done, exporting the graph", flush=True)
         topo = e.export_topology()
     finally:
         e.close()
