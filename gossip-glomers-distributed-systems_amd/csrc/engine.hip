@@ -1697,6 +1697,8 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
 // its ghosts, send lists and ghost -> owned lists on the device
 // (gg_gen::shard_csr): no rank holds the whole graph, in HBM or in host
 // memory (host memory: the rank's ghost ids and per-part offsets only).
+static int install_shard(gg_engine* e, gg_gen::Csr g, const std::vector<uint64_t>& plo, uint64_t* nnz_out);
+
 static int generate_sharded(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_out) {
     const uint64_t V = e->V;
     const uint32_t P = e->P;
@@ -1708,6 +1710,17 @@ static int generate_sharded(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz
     std::string err;
     int rc = gg_gen::build_csr_rows(*spec, e->stream, 0u, lo, hi, &g, &err);
     if (rc) return e->fail(rc, err);
+    return install_shard(e, g, plo, nnz_out);
+}
+
+// A rank's own rows [plo[part], plo[part+1]) of a symmetric graph (g: row_ptr
+// from 0, global column ids, on the device; the engine takes both arrays) ->
+// its ghosts, send lists and ghost -> owned lists on the device
+// (gg_gen::shard_csr), then the engine's per-node state.
+static int install_shard(gg_engine* e, gg_gen::Csr g, const std::vector<uint64_t>& plo, uint64_t* nnz_out) {
+    const uint64_t lo = plo[e->part], hi = plo[e->part + 1];
+    std::string err;
+    int rc = 0;
     const uint64_t n_own = hi - lo;
     const uint64_t ghost0 = (n_own + 63) / 64 * 64;
     gg_gen::Shard sh;
@@ -1813,6 +1826,61 @@ int gg_topology_generate(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_ou
         HIPCHK(hipMemcpy(iptr.data(), g.row_ptr, (e->V + 1) * 8, hipMemcpyDeviceToHost));
     }
     return finish_topology(e, iptr.empty() ? nullptr : iptr.data(), nullptr);
+}
+
+// HandleTopology on a vertex-sharded engine from this rank's own rows only
+// (broadcast.go:40-45: each node keeps its own row; here each rank its range):
+// uploaded as they are, then the same device path as a generated shard.
+int gg_topology_part(gg_engine* e, const uint64_t* part_lo, const int64_t* row_ptr, const int32_t* col,
+                     uint64_t nnz) {
+    if (!e || !part_lo || !row_ptr || (nnz && !col)) return GG_EINVAL;
+    if (e->P < 2) return e->fail(GG_EINVAL, "gg_topology_part: not a vertex-sharded engine (use gg_topology)");
+    const uint32_t P = e->P;
+    std::vector<uint64_t> plo(part_lo, part_lo + P + 1);
+    if (plo[0] != 0 || plo[P] != e->V) return e->fail(GG_EINVAL, "gg_topology_part: part_lo must run from 0 to n_nodes");
+    for (uint32_t q = 0; q < P; ++q)
+        if (plo[q + 1] < plo[q]) return e->fail(GG_EINVAL, "gg_topology_part: part_lo not ascending");
+    const uint64_t lo = plo[e->part], hi = plo[e->part + 1], n = hi - lo;
+    if (n == 0) return e->fail(GG_EINVAL, "gg_topology_part: empty part");
+    if (row_ptr[0] != 0 || (uint64_t)row_ptr[n] != nnz) return e->fail(GG_EINVAL, "row_ptr[0]/row_ptr[n] mismatch");
+    {
+        std::atomic<int> bad{0};  // 1 monotone, 2 range, 3 order, 4 self-asymmetric
+        host_parallel(n, [&](uint64_t a, uint64_t b) {
+            for (uint64_t i = a; i < b && !bad.load(std::memory_order_relaxed); ++i) {
+                if (row_ptr[i + 1] < row_ptr[i]) { bad = 1; return; }
+                for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; ++k) {
+                    if (col[k] < 0 || (uint64_t)col[k] >= e->V) { bad = 2; return; }
+                    if (k > row_ptr[i] && col[k] <= col[k - 1]) { bad = 3; return; }
+                    // links inside the part must be listed both ways (the rest is the caller's promise)
+                    const uint64_t w = (uint64_t)col[k];
+                    if (w >= lo && w < hi &&
+                        !std::binary_search(col + row_ptr[w - lo], col + row_ptr[w - lo + 1], (int32_t)(lo + i))) {
+                        bad = 4;
+                        return;
+                    }
+                }
+            }
+        });
+        if (bad == 1) return e->fail(GG_EINVAL, "row_ptr not monotone");
+        if (bad == 2) return e->fail(GG_EINVAL, "neighbour id out of range");
+        if (bad == 3) return e->fail(GG_EINVAL, "neighbour list not ascending/unique");
+        if (bad == 4) return e->fail(GG_EINVAL, "gg_topology_part: the topology must be symmetric");
+    }
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->free_topology();
+    e->have_topo = false;
+    e->host_rp.clear();
+    e->windows.erase(std::remove_if(e->windows.begin(), e->windows.end(), [](const Window& w) { return w.edges; }),
+                     e->windows.end());
+    gg_gen::Csr g{};
+    g.V = n;
+    g.nnz = nnz;
+    HIPCHK(hipMalloc(&g.row_ptr, (n + 1) * 8));
+    HIPCHK(hipMalloc(&g.col, std::max<uint64_t>(1, nnz) * 4));
+    HIPCHK(hipMemcpy(g.row_ptr, row_ptr, (n + 1) * 8, hipMemcpyHostToDevice));
+    if (nnz) HIPCHK(hipMemcpy(g.col, col, nnz * 4, hipMemcpyHostToDevice));
+    return install_shard(e, g, plo, nullptr);
 }
 
 int gg_topology_export(gg_engine* e, int64_t* row_ptr, int32_t* col, uint64_t cap, uint64_t* nnz_out) {

@@ -237,7 +237,8 @@ __global__ void degree_max(const int64_t* rp, uint64_t V, unsigned long long* ou
 // Grids are capped and every kernel strides: a dispatch's grid size in
 // work-items is a 32-bit field, so 2^32 or more threads (6.4e9 keys at C5)
 // cannot be launched one per item.
-unsigned grid_of(uint64_t n) { return (unsigned)std::min<uint64_t>((n + kBlk - 1) / kBlk, 1u << 16); }
+// grid-stride kernels: at least one block (an empty input still launches validly)
+unsigned grid_of(uint64_t n) { return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + kBlk - 1) / kBlk, 1u << 16)); }
 
 // host/topology.cpp:100-106 (the permutation is part of the graph's definition)
 std::vector<uint32_t> permutation(uint64_t V, uint64_t seed) {

@@ -130,6 +130,19 @@ int gg_abi_version(void);
  * Directed lists are allowed; symmetric ones take a faster path. */
 int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64_t nnz);
 
+/* Vertex-sharded engines (world / lane_groups = P > 1): HandleTopology from this
+ * rank's own node range only (broadcast.go:40-45 keeps each node's own row; here
+ * each rank keeps its range and no rank ever holds another's rows). Every rank of
+ * a lane group passes the same part boundaries part_lo[0..P] (0 = part_lo[0] <=
+ * ... <= part_lo[P] = n_nodes; part p owns nodes [part_lo[p], part_lo[p+1])) and
+ * only its own rows: row_ptr[0..n] from 0 (n = its node count), col = global node
+ * ids, ascending and unique per row. The topology must be symmetric (u lists v
+ * iff v lists u), as Maelstrom's are: links inside the part are checked, links to
+ * other parts are the caller's promise. Ghosts and send lists are built on the
+ * device. Per-edge windows (gg_set_partition) need gg_topology's whole graph. */
+int gg_topology_part(gg_engine* e, const uint64_t* part_lo, const int64_t* row_ptr, const int32_t* col,
+                     uint64_t nnz);
+
 /* Partition windows [round_from, round_to): a message sent in such a round
  * between nodes of different groups is dropped. Windows must not overlap.
  * Seeded: group(v) = bisection bit from (seed, epoch_seed, v). */

@@ -820,6 +820,9 @@ int gg_dist_comm_available(char* why, uint64_t cap) {
 int gg_dist_comm_id(uint8_t*) { return GG_EIO; }
 int gg_dist_comm_init(gg_engine* e, const uint8_t*) { return e ? e->fail(GG_EIO, "CPU oracle: no RCCL") : GG_EINVAL; }
 int gg_dist_step(gg_engine* e, uint32_t) { return e ? e->fail(GG_EIO, "CPU oracle: no RCCL") : GG_EINVAL; }
+int gg_topology_part(gg_engine* e, const uint64_t*, const int64_t*, const int32_t*, uint64_t) {
+    return e ? e->fail(GG_ENOSYS, "CPU oracle: sharded engines take the whole graph (gg_topology)") : GG_EINVAL;
+}
 int gg_dist_transport_init(gg_engine* e, const gg_transport*) {
     return e ? e->fail(GG_EIO, "CPU oracle: the engine-driven exchange is the HIP engine's") : GG_EINVAL;
 }

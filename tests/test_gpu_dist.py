@@ -543,3 +543,103 @@ def test_lane_halves_equal_oracle(hip_lib, cpu_lib, world, parts):
         assert p.exitcode == 0
     res = [res[r] for r in range(world)]
     _check_against_oracle(cpu_lib, scs, res, world, lane_groups=world // parts)
+
+
+def _part_worker(rank, world, port, lib, scenarios, bounds, q, transport):
+    import torch
+    import torch.distributed as dist
+
+    from ggamd.dist import ShardedRunner
+    from ggamd.engine import Engine
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        out = []
+        dev = torch.device("cuda", 0)
+        for sc, plo in zip(scenarios, bounds):
+            t = sc.topo
+            lo, hi = int(plo[rank]), int(plo[rank + 1])
+            rp = t.row_ptr[lo:hi + 1] - t.row_ptr[lo]  # this rank's rows only
+            col = t.col[t.row_ptr[lo]:t.row_ptr[hi]]
+            e = Engine(t.n_nodes, sc.W, seed=sc.seed, sync_base=sc.sync_base, sync_jitter=sc.sync_jitter,
+                       enable_sync=sc.enable_sync, track_delivery=True, device=0, rank=rank, world=world,
+                       library=lib)
+            e.topology_part(plo, rp, col)
+            for w in sc.windows:
+                e.partition_seeded(w[1], w[2], w[3])
+            for n, v, r in sc.injections:
+                e.broadcast(int(n), int(v), int(r))
+            r = ShardedRunner(e, dev, transport=transport)
+            stats = r.step(sc.rounds)
+            owned = e.dist_owned()
+            assert np.array_equal(owned, np.arange(lo, hi))
+            out.append((stats, owned, e.read_bits_nodes(owned), e.delivery_rounds_nodes(owned)))
+            e.close()
+        q.put((rank, out))
+    except BaseException as exc:
+        q.put((rank, f"rank {rank} failed: {exc!r}"))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,transport", [(2, "torch"), (3, "engine")])
+def test_topology_part_equals_single(hip_lib, world, transport):
+    """gg_topology_part: every rank is handed only its own rows (uneven,
+    caller-chosen ranges; global column ids) and builds ghosts and send lists
+    on the device; no rank sees another's rows. Equal to one engine given the
+    whole graph: counters, owned sets and delivery rounds."""
+    from ggamd import topology as T
+    from ggamd.workload import uniform_injections
+    rnd = random.Random(61)
+    scs = [Scenario(T.grid_links(40, seed=62), 128, 40, uniform_injections(1600, 100, 63), seed=64, sync_base=7,
+                    sync_jitter=3, windows=[("seeded", 3, 8, 9)]),
+           Scenario(T.rmat(3000, 8, seed=65), 256, 30, uniform_injections(3000, 200, 66), seed=67, sync_base=9,
+                    sync_jitter=4),
+           Scenario(T.tree(2500, 4), 64, 30, uniform_injections(2500, 64, 68), seed=69, sync_base=8, sync_jitter=2)]
+    bounds = []
+    for sc in scs:
+        V = sc.topo.n_nodes
+        cuts = sorted(rnd.sample(range(1, V), world - 1))
+        bounds.append(np.array([0] + cuts + [V], np.uint64))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_part_worker, args=(r, world, port, hip_lib, scs, bounds, q, transport))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, got = q.get(timeout=150)
+        assert not isinstance(got, str), got
+        res[r] = got
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for k, sc in enumerate(scs):
+        single = make_engine(hip_lib, sc, device=0)
+        s1 = single.step(sc.rounds)
+        for rank in range(world):
+            stats, owned, bits, dr = res[rank][k]
+            d = diff_stats(s1, stats)
+            assert not d, (k, rank, d[:10])
+            assert np.array_equal(bits, single.read_bits_nodes(owned)), (k, rank)
+            assert np.array_equal(dr, single.delivery_rounds_nodes(owned)), (k, rank)
+        single.close()
+
+
+def test_topology_part_refusals(hip_lib):
+    """gg_topology_part refuses a non-sharded engine, bad part boundaries, and
+    a part whose own links are not listed both ways."""
+    from ggamd.engine import Engine, GGError
+    e1 = Engine(8, 64, device=0, library=hip_lib)
+    with pytest.raises(GGError, match="not a vertex-sharded"):
+        e1.topology_part([0, 8], [0, 0], [])
+    e1.close()
+    e = Engine(8, 64, device=0, rank=0, world=2, library=hip_lib)
+    with pytest.raises(GGError, match="from 0 to n_nodes"):
+        e.topology_part([0, 4, 7], [0] * 5, [])
+    with pytest.raises(GGError, match="symmetric"):  # 0 -> 1 listed, 1 -> 0 missing
+        e.topology_part([0, 4, 8], [0, 1, 1, 1, 1], [1])
+    e.topology_part([0, 4, 8], [0, 1, 2, 2, 2], [1, 0])
+    e.close()

@@ -111,12 +111,15 @@ def _components(row_ptr, col, device="cuda", chunk=1 << 29):
         print(f"components: pass {it}, {time.time() - t0:.1f} s", flush=True)
         if torch.equal(lab, old):
             break
-    size = torch.bincount(lab, minlength=V)
-    vol = torch.bincount(lab, weights=deg.double(), minlength=V)
-    out = lab.cpu(), size.cpu(), vol.cpu()
-    del lab, size, vol, chunks, deg
+    lab = lab.cpu().numpy()
+    del chunks, deg
     torch.cuda.empty_cache()
-    return out
+    # per-label sums on the host: the giant component's label would take every
+    # device atomic of a bincount on one address
+    size = np.bincount(lab, minlength=V)
+    vol = np.bincount(lab, weights=(row_ptr[1:] - row_ptr[:-1]).astype(np.float64), minlength=V)
+    print(f"components: {int((size > 0).sum())} labels, {time.time() - t0:.1f} s", flush=True)
+    return lab, size, vol
 
 
 def test_c4_full_size_lane_groups_equal_single(hip_lib):
@@ -142,7 +145,7 @@ def test_c4_full_size_lane_groups_equal_single(hip_lib):
     lab, size, vol = _components(topo.row_ptr, topo.col)
     del topo
     src = [n for n, _, _ in inj_l]
-    comp = lab[src]
+    comp = lab[np.asarray(src, np.int64)]
     p1 = int(size[comp].sum())
     kat3 = int(round(float(vol[comp].sum()))) - p1 + K
     assert sum(s["new_bits"] for s in want) == p1, "P1: deliveries != sum of source component sizes"

@@ -70,6 +70,7 @@ def _worker(rank, world, port, args, q):
                 nnz = eng.generate(**gen)
                 torch.cuda.synchronize()
                 hbm = f0 - torch.cuda.mem_get_info(0)[0]
+                print(f"rank {rank}: {hbm / 2**30:.2f} GiB, {eng.dist_info()}", flush=True)
             dist.barrier()
         info = eng.dist_info()
         runner = ShardedRunner(eng, dev, transport="torch")
@@ -89,6 +90,9 @@ def _worker(rank, world, port, args, q):
             rounds.append(st)
             nb = torch.tensor([st["new_bits"]], dtype=torch.int64)
             dist.all_reduce(nb)
+            if rank == 0:
+                print(f"round {len(rounds) - 1}: new {int(nb)}, rank 0: {st['kernel_ms']:.2f} ms, "
+                      f"sent {st['sent_bytes']} B, received {recv} B", flush=True)
             if (int(nb) == 0 and len(rounds) > 1) or len(rounds) >= args.max_rounds:
                 break
         q.put((rank, {"rounds": rounds, "info": info, "hbm": hbm, "nnz_rank": nnz,

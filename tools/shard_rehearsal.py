@@ -5,7 +5,9 @@ generated graph on the device (gg_topology_generate -> gg_gen::shard_csr), run
 one episode, and rank 0 then runs the same episode on one unsharded engine and
 compares every round's counters (summed over ranks; seen_hash fingerprints
 every node's set). Reports per rank: topology setup seconds, peak host RSS,
-owned / ghost rows, and the episode time.
+owned / ghost rows, HBM bytes (free-memory delta of its setup; the ranks set
+up one at a time), payload bytes sent per round, and the episode time; and the
+single engine's HBM bytes (BASELINE configs[4]: "HBM footprint per GPU").
 
 Usage: python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \\
          --master-addr 127.0.0.1 --master-port P tools/shard_rehearsal.py [--side 8192] [--json out.json]
@@ -49,9 +51,15 @@ def main():
     # the reference run first (rank 0): its round count bounds the sharded episode
     R = args.rounds
     want = None
+    hbm1 = 0
     if rank == 0:
+        torch.cuda.synchronize()
+        f0 = torch.cuda.mem_get_info(0)[0]
         e1 = Engine(V, K, seed=seed, enable_sync=True, device=0)
         e1.generate(**gen)
+        torch.cuda.synchronize()
+        hbm1 = f0 - torch.cuda.mem_get_info(0)[0]
+        print(f"single engine: {hbm1 / 2**30:.1f} GiB", flush=True)
         for n, v, r in inj:
             e1.broadcast(int(n), int(v), int(r))
         if not R:
@@ -70,10 +78,19 @@ def main():
     dist.broadcast(t, 0)
     R = int(t.item())
     rss0 = rss_mb()
-    t0 = time.perf_counter()
-    e = Engine(V, K, seed=seed, enable_sync=True, device=0, rank=rank, world=world)
-    e.generate(**gen)
-    setup_s = time.perf_counter() - t0
+    e, setup_s, hbm = None, 0.0, 0
+    for k in range(world):  # one rank at a time: a clean free-memory delta per rank
+        if k == rank:
+            torch.cuda.synchronize()
+            f0 = torch.cuda.mem_get_info(0)[0]
+            t0 = time.perf_counter()
+            e = Engine(V, K, seed=seed, enable_sync=True, device=0, rank=rank, world=world)
+            e.generate(**gen)
+            torch.cuda.synchronize()
+            setup_s = time.perf_counter() - t0
+            hbm = f0 - torch.cuda.mem_get_info(0)[0]
+            print(f"rank {rank}: set up in {setup_s:.1f} s, {hbm / 2**30:.2f} GiB", flush=True)
+        dist.barrier()
     info = e.dist_info()
     n_own, n_ghost, n_send = info["owned"], info["ghosts"], info["sent_per_round"]
     for n, v, r in inj:
@@ -81,19 +98,23 @@ def main():
     runner = ShardedRunner(e, torch.device("cuda", 0))
     dist.barrier()
     t1 = time.perf_counter()
-    got = []
+    got, sent = [], []
     for r in range(R):
-        got += runner.step(1)
-        if rank == 0 and r % 4 == 0:
-            print(f"round {r}: new {got[-1]['new_bits']}", flush=True)
+        local = runner.step(1, reduce=False)
+        sent.append(local[0]["sent_bytes"])
+        got += runner.reduce(local)
+        if rank == 0:
+            print(f"round {r}: new {got[-1]['new_bits']}, rank 0 sent {sent[-1]} B", flush=True)
     episode_s = time.perf_counter() - t1
     me = {"rank": rank, "owned": n_own, "ghosts": n_ghost, "send_entries": n_send, "setup_s": setup_s,
-          "peak_rss_MB": rss_mb(), "rss_before_setup_MB": rss0, "episode_s": episode_s}
+          "hbm_bytes": hbm, "peak_rss_MB": rss_mb(), "rss_before_setup_MB": rss0, "episode_s": episode_s,
+          "payload_bytes_per_round": sent, "payload_bytes_max_round": max(sent) if sent else 0}
     allr = [None] * world
     dist.all_gather_object(allr, me)
     if rank == 0:
         diffs = [f"round {a['round']} {f}" for a, b in zip(got, want) for f in COUNT_FIELDS if a[f] != b[f]]
-        out = {"nodes": V, "lanes": K, "ranks": world, "rounds": R, "per_rank": allr,
+        out = {"nodes": V, "lanes": K, "ranks": world, "rounds": R, "single_engine_hbm_bytes": hbm1,
+               "per_rank": allr,
                "counters_equal_single": not diffs, "first_diffs": diffs[:5],
                "deliveries": sum(s["new_bits"] for s in got), "transport": "gloo (host-staged, one GPU)"}
         print(json.dumps(out), flush=True)
