@@ -255,6 +255,8 @@ struct gg_engine {
     std::vector<uint64_t> u_bits;    // those lanes (nw words)
     bool sync_tiles = false;         // GG_SYNC_TILES=1: sync rounds on the tile path (A/B)
     uint64_t* d_hscratch = nullptr;
+    uint32_t* d_hflag = nullptr;     // [hub chunks] streamed sync rounds with hubs
+    uint8_t* d_hlive = nullptr;      // [hubs] streamed sync rounds with hubs
     uint64_t tile_nodes = 0, tile_bytes = 0;
     uint64_t n_in_edges = 0;
     uint64_t* d_fired[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -340,6 +342,8 @@ void gg_engine::free_topology() {
     dfree(d_pend);
     dfree(d_pend_src);
     dfree(d_hscratch);
+    dfree(d_hflag);
+    dfree(d_hlive);
     n_hubs = n_hchunks = n_mchunks = 0;
     dfree(d_work);
     dfree(d_n_work);
@@ -409,7 +413,8 @@ int reset_device_state(gg_engine* e) {
     // bytes: rows is a multiple of 64) and starts the sync timers
     gg::ResetArgs ra{};
     auto seg = [&](void* p, uint64_t bytes, uint64_t val) {
-        ra.seg[ra.n_seg++] = {reinterpret_cast<uint64_t*>(p), bytes / 8, val};
+        if (ra.n_seg < gg::kResetSegs) ra.seg[ra.n_seg++] = {reinterpret_cast<uint64_t*>(p), bytes / 8, val};
+        else e->err = "internal: reset segment table full";  // caught below
     };
     seg(e->d_base, rowbytes, 0);
     // F rows and flags are already all zero after two rounds without new bits
@@ -447,6 +452,7 @@ int reset_device_state(gg_engine* e) {
         seg(e->d_sat, e->rows / 8, 0);
         seg(e->d_sat_new, e->rows / 8, 0);
     }
+    if (e->d_hlive) seg(e->d_hlive, (e->n_hubs + 7) / 8 * 8, 0);
     if (e->d_pend) {
         seg(e->d_pend, e->rows * e->nwp * 8, 0);
         seg(e->d_pend_src, e->rows * 4, ~0ull);
@@ -465,6 +471,7 @@ int reset_device_state(gg_engine* e) {
     ra.seed = e->cfg.seed;
     ra.sync_base = e->cfg.sync_base_ticks;
     ra.sync_jitter = e->cfg.sync_jitter_ticks;
+    if (e->err == "internal: reset segment table full") return GG_EIO;
     const uint64_t blocks = std::min<uint64_t>(std::max<uint64_t>(1, rowbytes / 16384), 4096);
     hipLaunchKernelGGL(gg::reset_state, dim3((unsigned)blocks), dim3(gg::kBlock), 0, e->stream, ra);
     HIPCHK(hipGetLastError());
@@ -582,6 +589,31 @@ void launch_hubs_t(const gg::RoundArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((gg::hub_finish<G, WPL>), dim3(bh), dim3(gg::kBlock), 0, s, a);
 }
 
+// Streamed sync rounds with hubs (symmetric topologies): hub_sync_chunks,
+// hub_sync_finish, hub_sync_push (expand_kernels.hpp), after expand_stream_sync.
+template <int G, int WPL = 2>
+void launch_hub_sync_t(const gg::RoundArgs& a, hipStream_t s) {
+    const unsigned bc = (unsigned)std::min<uint64_t>(a.n_hchunks, 8192);
+    const unsigned bh = (unsigned)std::min<uint64_t>(a.n_hubs, 8192);
+    hipLaunchKernelGGL((gg::hub_sync_chunks<G, WPL>), dim3(bc), dim3(gg::kBlock), 0, s, a);
+    hipLaunchKernelGGL((gg::hub_sync_finish<G, WPL>), dim3(bh), dim3(gg::kBlock), 0, s, a);
+    hipLaunchKernelGGL((gg::hub_sync_push<G, WPL>), dim3(bc), dim3(gg::kBlock), 0, s, a);
+}
+
+void launch_hub_sync(const gg::RoundArgs& a, hipStream_t s) {
+    switch (a.nwp) {
+        case 1: launch_hub_sync_t<1, 1>(a, s); break;
+        case 2: launch_hub_sync_t<1>(a, s); break;
+        case 4: launch_hub_sync_t<2>(a, s); break;
+        case 8: launch_hub_sync_t<4>(a, s); break;
+        case 16: launch_hub_sync_t<8>(a, s); break;
+        case 32: launch_hub_sync_t<16>(a, s); break;
+        case 64: launch_hub_sync_t<32>(a, s); break;
+        case 128: launch_hub_sync_t<64>(a, s); break;
+        default: break;
+    }
+}
+
 void launch_hubs(const gg::RoundArgs& a, hipStream_t s) {
     switch (a.nwp) {
         case 1: launch_hubs_t<1, 1>(a, s); break;
@@ -624,14 +656,14 @@ void launch_stream(const gg::RoundArgs& a, bool maskw, hipStream_t s) {
     }
 }
 
-template <int G>
+template <int G, int WPL = 2>
 void launch_stream_sync_t(const gg::RoundArgs& a, hipStream_t s) {
     static int resident = 0;
     if (!resident) {
         int dev = 0, cus = 0, per_cu = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gg::expand_stream_sync<G>, gg::kBlock, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gg::expand_stream_sync<G, WPL>, gg::kBlock, 0);
         resident = std::max(1, cus) * std::max(1, per_cu);
     }
     const uint64_t rb = std::min<uint64_t>((a.n_own + gg::kBlock - 1) / gg::kBlock, 4096);
@@ -639,11 +671,12 @@ void launch_stream_sync_t(const gg::RoundArgs& a, hipStream_t s) {
     const uint64_t ngb = gg::kBlock / G;
     uint64_t blocks = (a.n_own + ngb - 1) / ngb;
     blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)resident));
-    hipLaunchKernelGGL((gg::expand_stream_sync<G>), dim3((unsigned)blocks), dim3(gg::kBlock), 0, s, a);
+    hipLaunchKernelGGL((gg::expand_stream_sync<G, WPL>), dim3((unsigned)blocks), dim3(gg::kBlock), 0, s, a);
 }
 
 void launch_stream_sync(const gg::RoundArgs& a, hipStream_t s) {
     switch (a.nwp) {
+        case 1: launch_stream_sync_t<1, 1>(a, s); break;  // W = 64: one word per node, one lane
         case 2: launch_stream_sync_t<1>(a, s); break;
         case 4: launch_stream_sync_t<2>(a, s); break;
         case 8: launch_stream_sync_t<4>(a, s); break;
@@ -752,6 +785,8 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.hub_c0 = e->d_hub_c0;
     a.n_hubs = e->n_hubs;
     a.hscratch = e->d_hscratch;
+    a.hflag = e->d_hflag;
+    a.hlive = e->d_hlive;
     a.mchunks = e->d_mchunks;
     a.srec = e->d_srec;
     a.pushb = e->d_pushb;
@@ -805,7 +840,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     const bool syncw = e->cfg.enable_sync && r >= base + 2;
     // streaming rounds: no sync event reaches the expand; partition windows only
     // on symmetric graphs without hubs at W >= 128 (expand_stream<.., MASKW>)
-    // streamed sync rounds (sync_records + expand_stream_sync): no masks, no in-hubs, nwp >= 2
+    // streamed sync rounds (sync_records + expand_stream_sync [+ hub_sync_*]): no masks
     const bool sync_stream = syncw && !maskw && e->d_srec != nullptr;
     a.nmeta = sync_stream ? e->d_nmeta : nullptr;
     if (e->cfg.batch_ticks) {  // batched gossip: one kernel over every node
@@ -837,7 +872,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             // 4096 2.02, 256 2.10; GG_PREP_BLOCKS overrides)
             static const uint64_t prep_cap = test_knob("GG_PREP_BLOCKS") ? (uint64_t)atoi(test_knob("GG_PREP_BLOCKS")) : 1024;
             if (e->d_sat && r == base + 2) {  // the digest's first bits (sat_scan)
-                const uint64_t thr = a.n_own * (e->nwp / 2);
+                const uint64_t thr = a.n_own * std::max<uint64_t>(1, e->nwp / 2);
                 hipLaunchKernelGGL(gg::sat_scan, dim3((unsigned)((thr + gg::kBlock - 1) / gg::kBlock)), dim3(gg::kBlock),
                                    0, e->stream, e->d_base, a.n_own, (uint32_t)e->nwp, lanes_through(e, r - 1), e->d_sat);
                 HIPCHK(hipGetLastError());
@@ -875,6 +910,10 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         }
         if (sync_stream) {
             launch_stream_sync(a, e->stream);
+            if (e->n_hubs) {
+                HIPCHK(hipGetLastError());
+                launch_hub_sync(a, e->stream);
+            }
         } else if (a.stream_ok) {  // lean rounds: all nodes (dense) or the candidate list (sparse)
             if (e->ff_ok && !maskw) {  // the sender bitmap of a flags-first round (the kernel decides)
                 const uint64_t blocks = std::min<uint64_t>((e->rows + gg::kBlock - 1) / gg::kBlock, 4096);
@@ -1291,14 +1330,21 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
             HIPCHK(hipMemcpy(e->d_hub_c0, hub_c0.data(), hub_c0.size() * 4, hipMemcpyHostToDevice));
             HIPCHK(hipMalloc(&e->d_hchunks, hch.size() * sizeof(gg::HubChunk)));
             HIPCHK(hipMemcpy(e->d_hchunks, hch.data(), hch.size() * sizeof(gg::HubChunk), hipMemcpyHostToDevice));
-            HIPCHK(hipMalloc(&e->d_hscratch, hch.size() * 2 * e->nwp * 8));
+            // streamed sync rounds (symmetric, sync on): a third row per chunk (hub_sync_*)
+            const bool hsync = e->cfg.enable_sync && e->symmetric;
+            HIPCHK(hipMalloc(&e->d_hscratch, hch.size() * (hsync ? 3 : 2) * e->nwp * 8));
+            if (hsync) {
+                HIPCHK(hipMalloc(&e->d_hflag, hch.size() * 4));
+                HIPCHK(hipMalloc(&e->d_hlive, (hubs.size() + 7) / 8 * 8));
+            }
         }
         if (e->n_mchunks) {
             HIPCHK(hipMalloc(&e->d_mchunks, mch.size() * sizeof(gg::HubChunk)));
             HIPCHK(hipMemcpy(e->d_mchunks, mch.data(), mch.size() * sizeof(gg::HubChunk), hipMemcpyHostToDevice));
         }
     }
-    // streamed sync rounds need no in-hubs and two words per lane
+    // streamed sync rounds: any row width (W = 64: one word per node, one lane);
+    // hubs on symmetric topologies only (hub_sync_*: a hub's in-list is its out-list)
     e->sync_tiles = test_knob("GG_SYNC_TILES") && atoi(test_knob("GG_SYNC_TILES")) != 0;
     dfree(e->d_srec);
     dfree(e->d_pushb);
@@ -1315,7 +1361,7 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
         HIPCHK(hipMalloc(&e->d_pend, e->rows * e->nwp * 8));
         HIPCHK(hipMalloc(&e->d_pend_src, e->rows * 4));
     }
-    if (e->cfg.enable_sync && e->n_hubs == 0 && e->nwp >= 2 && !e->sync_tiles && n_own) {
+    if (e->cfg.enable_sync && (e->n_hubs == 0 || e->symmetric) && !e->sync_tiles && n_own) {
         HIPCHK(hipMalloc(&e->d_srec, 2 * n_own * sizeof(uint4)));
         HIPCHK(hipMalloc(&e->d_sstate, e->rows));
         HIPCHK(hipMalloc(&e->d_ibits, e->rows / 8));

@@ -165,7 +165,12 @@ struct RoundArgs {
     const uint32_t* hubs;            // [n_hubs] hub local rows
     const uint32_t* hub_c0;          // [n_hubs+1] first chunk of each hub
     uint64_t n_hubs;
-    uint64_t* hscratch;              // [n_hchunks][2][nwp] (union, first-claimer-recip) per chunk
+    uint64_t* hscratch;              // [n_hchunks][2][nwp] (union, first-claimer-recip) per chunk;
+                                     // streamed sync engines: [n_hchunks][3][nwp], the third row the
+                                     // chunk's callback prefix (hub_sync_*)
+    uint32_t* hflag;                 // [n_hchunks] streamed sync rounds: HF_* of the chunk this round
+    uint8_t* hlive;                  // [n_hubs] streamed sync rounds: the hub is processed this round
+                                     // (its candidate byte, | CA_NODE; written by sync_records)
     const struct HubChunk* mchunks;  // out-edge chunks of high out-degree senders
     uint64_t n_mchunks;
     uint4* srec;                // [2 n_own] sync records (streamed sync rounds), or nullptr
@@ -394,6 +399,13 @@ __device__ __forceinline__ void sat_mark(const RoundArgs& a, const Row<WPL>& S, 
 // 64/cpn consecutive nodes, one word's worth of bits, and ORs them in at once.
 __global__ __launch_bounds__(kBlock) void sat_scan(const uint64_t* base, uint64_t n_own, uint32_t nwp, uint32_t usat,
                                                    uint64_t* sat) {
+    if (nwp == 1) {  // W = 64: one word per node, one node per lane, a wave = one digest word
+        const uint64_t node = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+        const bool full = node < n_own && (uint32_t)__popcll(base[node]) == usat;
+        const unsigned long long m = __ballot(full);
+        if ((threadIdx.x & 63) == 0 && m) atomicOr(sat + (node >> 6), m);
+        return;
+    }
     const uint32_t cpn = nwp / 2;
     const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     const uint64_t node = t / cpn;
@@ -666,11 +678,15 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                 }
                 // reads v sent in r-1 arrive now; each answered by a read_ok (:131)
                 if (fm1) {
-                    for (int64_t e = o0; e < o1; ++e) {
-                        const uint64_t w = a.out_col[e] & kColMask;
-                        if (masked<MASKW>(a, 2, rep, w, e)) continue;
-                        c_read_oks++;
-                        if (masked<MASKW>(a, 3, w, rep, e)) c_dropped++;
+                    if constexpr (MASKW) {
+                        for (int64_t e = o0; e < o1; ++e) {
+                            const uint64_t w = a.out_col[e] & kColMask;
+                            if (masked<MASKW>(a, 2, rep, w, e)) continue;
+                            c_read_oks++;
+                            if (masked<MASKW>(a, 3, w, rep, e)) c_dropped++;
+                        }
+                    } else {  // no window: every read arrives and is answered (a hub's list is long)
+                        c_read_oks += (unsigned long long)(o1 - o0);
                     }
                 }
                 // (5) the sync timer (main.go:42-51): read RPC to every neighbour (:119-121)
@@ -1829,8 +1845,21 @@ constexpr uint32_t SR_CB = 1u << 27;           // sync callback (fired in r-2)
 constexpr uint32_t SR_LAG = 1u << 28;          // base lacks F_prev
 constexpr uint32_t SR_STALE = 1u << 29;        // F row of round r-2 in this round's F buffer
 constexpr uint32_t SR_INJ = 1u << 30;          // client broadcasts this round
+constexpr uint32_t SR_HUB = 1u << 31;          // in-degree above hub_deg: hub_sync_chunks / hub_sync_finish /
+                                               // hub_sync_push take the node (its cand byte is left set)
 // second word: .x/.y out_ptr[i] (callback), .z peers' LAG mask (first 32 peers),
 // .w bits 0-2: recorded sender j pushes, bits 3-5: recorded sender j is LAG
+
+// Index of hub node i in the ascending hub list.
+__device__ __forceinline__ uint32_t hub_index(const RoundArgs& a, uint32_t i) {
+    uint32_t lo = 0, hi = (uint32_t)a.n_hubs;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.hubs[mid] < i) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
 
 __global__ __launch_bounds__(kBlock) void sync_records(RoundArgs a) {
     __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
@@ -1860,6 +1889,14 @@ __global__ __launch_bounds__(kBlock) void sync_records(RoundArgs a) {
         }
         const uint64_t rep = a.own0 + i;
         const int64_t p0 = a.in_ptr[i], p1 = a.in_ptr[i + 1];
+        if (a.hub_deg && p1 - p0 > (int64_t)a.hub_deg) {
+            // a hub: the hub_sync kernels take it (its candidate byte moves to hlive;
+            // the byte itself may be marked for the next round meanwhile)
+            a.hlive[hub_index(a, i)] = (uint8_t)(ca | CA_NODE);
+            a.srec[2 * (uint64_t)i] = make_uint4(SR_HUB, 0, 0, 0);
+            c_bytes += 16 + 16 + 1;
+            continue;
+        }
         const int64_t o0 = sym ? p0 : a.out_ptr[i], o1 = sym ? p1 : a.out_ptr[i + 1];
         const uint64_t dout = (uint64_t)(o1 - o0);
         const bool cbk = (st & SE_FM2) != 0;
@@ -1970,9 +2007,8 @@ __global__ __launch_bounds__(kBlock) void sync_records(RoundArgs a) {
     flush_counters(a, acc, s_red, t_start, K_PREP);
 }
 
-template <int G>
+template <int G, int WPL>
 __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
-    constexpr int WPL = 2;
     constexpr int kCb = 4;  // callback peers / in-list senders per batch
     __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
     const unsigned long long t_start = clock100();
@@ -1992,8 +2028,13 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
     };
     auto zero = []() {
         Row<WPL> z;
-        z.w[0] = z.w[1] = 0;
+#pragma unroll
+        for (int w = 0; w < WPL; ++w) z.w[w] = 0;
         return z;
+    };
+    auto or_in = [](Row<WPL>& d, const Row<WPL>& x) {
+#pragma unroll
+        for (int w = 0; w < WPL; ++w) d.w[w] |= x.w[w];
     };
     auto row_at = [&](const uint64_t* arr, uint64_t u) { return load_row<WPL>(arr + u * a.nwp + off); };
 
@@ -2008,6 +2049,18 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
         const uint64_t i = n0;
         const uint64_t rep = a.own0 + i;
         const uint32_t x = r0.x;
+        if (x & SR_HUB) {  // the hub_sync kernels take it
+            const uint32_t n2 = node_of(k + 2 * stride);
+            r0 = make_uint4(0, 0, 0, 0);
+            q0 = r0;
+            if (n1 < a.n_own) {
+                r0 = a.srec[2 * (uint64_t)n1];
+                q0 = a.srec[2 * (uint64_t)n1 + 1];
+            }
+            n0 = n1;
+            n1 = n2;
+            continue;
+        }
         const bool lag = (x & SR_LAG) != 0, slow = (x & SR_SLOW) != 0, cbk = (x & SR_CB) != 0;
         const bool quiet = (x & SR_QUIET) != 0, satv = (x & SR_SATV) != 0;
         const uint32_t nc = slow ? 0u : (x >> SR_NC) & 3u;
@@ -2056,8 +2109,7 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
             continue;
         }
 
-        sp.w[0] |= of.w[0];
-        sp.w[1] |= of.w[1];
+        or_in(sp, of);
         Row<WPL> S = sp;
         if (x & SR_INJ) {  // (1) client broadcasts of this round
             uint32_t lo = 0, hi = a.n_inj;
@@ -2075,18 +2127,21 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
         // (2) node broadcasts and pushes, ascending sender: first deliverer claims
         unsigned long long cl_recip = 0;
         auto claim = [&](const Row<WPL>& src, uint32_t c) {
-            const uint64_t w0 = src.w[0] & ~S.w[0], w1 = src.w[1] & ~S.w[1];
-            S.w[0] |= w0;
-            S.w[1] |= w1;
-            if (c & kRecipBit) cl_recip += __popcll(w0) + __popcll(w1);
+            unsigned long long n = 0;
+#pragma unroll
+            for (int w = 0; w < WPL; ++w) {
+                const uint64_t cw = src.w[w] & ~S.w[w];
+                S.w[w] |= cw;
+                n += __popcll(cw);
+            }
+            if (c & kRecipBit) cl_recip += n;
         };
         unsigned long long nrows = 1 + (lag ? 1 : 0), nextra = 32;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             if ((uint32_t)j < nc) {
                 Row<WPL> r = fr[j];
-                r.w[0] |= br[j].w[0];
-                r.w[1] |= br[j].w[1];
+                or_in(r, br[j]);
                 claim(r, cs[j]);
                 const bool push = (sb >> j) & 1u, slag = (sb >> (3 + j)) & 1u;
                 nrows += (push ? 1 : 0) + ((!push || slag) ? 1 : 0);
@@ -2114,8 +2169,7 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
                     const bool push = f[b] & SE_FM3, con = f[b] & (FL_ACT | SE_FM3), slag = f[b] & FL_LAG;
                     const Row<WPL> fb = (con && (!push || slag)) ? row_at(a.F_prev, u) : zero();
                     r[b] = push ? row_at(a.base, u) : zero();
-                    r[b].w[0] |= fb.w[0];
-                    r[b].w[1] |= fb.w[1];
+                    or_in(r[b], fb);
                     nrows += (push ? 1 : 0) + ((con && (!push || slag)) ? 1 : 0);
                     c_gathers += (lg == 0 && con) ? 1u : 0u;
                 }
@@ -2140,8 +2194,7 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
                     const bool slag = e >= 32 || ((lagm >> e) & 1u);
                     R[b] = (e < dout && !same[b]) ? row_at(a.base, pw[b]) : zero();
                     const Row<WPL> f = (e < dout && !same[b] && slag) ? row_at(a.F_prev, pw[b]) : zero();
-                    R[b].w[0] |= f.w[0];
-                    R[b].w[1] |= f.w[1];
+                    or_in(R[b], f);
                     nrows += (e < dout && !same[b]) ? (slag ? 2 : 1) : 0;
                 }
                 // columns of the next batch, in flight with these rows
@@ -2658,6 +2711,349 @@ __global__ __launch_bounds__(kBlock) void hub_finish(RoundArgs a) {
     flush_counters(a, acc, s_red, t_start, K_STREAM);
 }
 
+// ---------------------------------------------------------------------------
+// Streamed sync rounds on graphs with hubs (symmetric topologies: a hub's
+// out-list is its in-list, so one chunk list serves both directions). A hub
+// takes three launches instead of one node group walking its whole list:
+//   hub_sync_chunks  one block per edge chunk of a live hub: the chunk's senders
+//                    under expand_stream_sync's rules (an ACT sender contributes
+//                    its F row; a pusher — fired in r-3, pushb says it sent this
+//                    hub something — its set base | (LAG ? F)), reduced in sender
+//                    order to (union, first-claimer-reciprocal); whether a sender
+//                    is a callback of this round (it reads the hub's set: keep);
+//                    and, when the hub is a callback itself (fired in r-2), the OR
+//                    of the chunk's peers' sets (their read_ok payloads).
+//   hub_sync_finish  one block per live hub: its chunks combined in order with
+//                    its own set and client broadcasts (the claims); a callback
+//                    hub turns the chunk ORs into each chunk's exclusive prefix
+//                    (its running set before the chunk's first peer,
+//                    broadcast.go:110-114) and takes every peer's set; the node is
+//                    written as expand_stream_sync writes it.
+//   hub_sync_push    one block per chunk of a live callback hub: an ordered
+//                    prefix OR over the chunk's peers gives each peer's push
+//                    S_{i-1} & ~R_i (broadcast.go:104-108): push counts, pushb,
+//                    the receivers' candidate bytes for the next round.
+// Liveness: hlive (sync_records' copy of the hub's candidate byte, cleared by
+// hub_sync_finish); hflag carries it from the chunks to the push launch.
+constexpr uint32_t HF_KEEP = 1, HF_LIVE = 2, HF_CB = 4;
+
+template <int G, int WPL>
+__global__ __launch_bounds__(kBlock) void hub_sync_chunks(RoundArgs a) {
+    constexpr int NGB = kBlock / G;
+    constexpr int D = 4;  // senders in flight per lane
+    __shared__ uint64_t s_or[NGB * G * WPL], s_rc[NGB * G * WPL];
+    __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
+    __shared__ uint32_t s_keep;
+    const unsigned long long t_start = clock100();
+    const int j = threadIdx.x / G, lg = threadIdx.x % G;
+    const uint64_t off = (uint64_t)lg * WPL;
+    unsigned long long c_bytes = 0, c_gathers = 0;
+    for (uint64_t c = blockIdx.x; c < a.n_hchunks; c += gridDim.x) {
+        const HubChunk hc = a.hchunks[c];
+        const uint64_t rep = a.own0 + hc.node;
+        if (!a.hlive[hub_index(a, hc.node)]) {  // block-uniform
+            if (threadIdx.x == 0) a.hflag[c] = 0;
+            continue;
+        }
+        const bool cbk = bit_at(a.fired_m2, rep);
+        if (threadIdx.x == 0) s_keep = 0;
+        __syncthreads();
+        const uint32_t per = (hc.n + NGB - 1) / NGB;
+        const int64_t e0 = hc.e0 + (int64_t)j * per;
+        const int64_t e1 = min(hc.e0 + (int64_t)hc.n, e0 + (int64_t)per);
+        Row<WPL> O, R, Q, Z;
+#pragma unroll
+        for (int w = 0; w < WPL; ++w) O.w[w] = R.w[w] = Q.w[w] = Z.w[w] = 0;
+        bool keep = false;
+        for (int64_t e = e0; e < e1; e += D) {
+            uint32_t cb[D];
+            uint8_t f[D];
+#pragma unroll
+            for (int b = 0; b < D; ++b) cb[b] = e + b < e1 ? a.in_col[e + b] : 0u;
+#pragma unroll
+            for (int b = 0; b < D; ++b) keep |= e + b < e1 && bit_at(a.fired_m2, cb[b] & kColMask);
+#pragma unroll
+            for (int b = 0; b < D; ++b)
+                f[b] = (e + b < e1 && bit_at(a.ibits, cb[b] & kColMask)) ? a.sstate[cb[b] & kColMask] : (uint8_t)0;
+#pragma unroll
+            for (int b = 0; b < D; ++b) {  // a push from an owned sender that sent nothing is no push
+                if ((f[b] & SE_FM3) && a.rev && (cb[b] & kColMask) < a.n_own && !a.pushb[a.rev[e + b]])
+                    f[b] &= (uint8_t)~SE_FM3;
+            }
+            Row<WPL> r[D], fb[D], sb[D];
+#pragma unroll
+            for (int b = 0; b < D; ++b) {
+                const uint64_t u = cb[b] & kColMask;
+                const bool push = f[b] & SE_FM3, con = f[b] & (FL_ACT | SE_FM3), slag = f[b] & FL_LAG;
+                const bool needf = (con && (!push || slag)) || (cbk && slag && e + b < e1);
+                const bool needb = push || (cbk && e + b < e1);
+#pragma unroll
+                for (int w = 0; w < WPL; ++w) fb[b].w[w] = sb[b].w[w] = 0;
+                if (needf) fb[b] = load_row<WPL>(a.F_prev + u * a.nwp + off);
+                if (needb) sb[b] = load_row<WPL>(a.base + u * a.nwp + off);
+                if (lg == 0) c_bytes += 8ull * a.nwp * ((needf ? 1 : 0) + (needb ? 1 : 0));
+#pragma unroll
+                for (int w = 0; w < WPL; ++w) r[b].w[w] = (con && (!push || slag) ? fb[b].w[w] : 0) | (push ? sb[b].w[w] : 0);
+                c_gathers += (lg == 0 && con) ? 1u : 0u;
+            }
+#pragma unroll
+            for (int b = 0; b < D; ++b) {
+                if (f[b] & (FL_ACT | SE_FM3)) {
+#pragma unroll
+                    for (int w = 0; w < WPL; ++w) {
+                        const uint64_t cw = r[b].w[w] & ~O.w[w];
+                        O.w[w] |= cw;
+                        if (cb[b] & kRecipBit) R.w[w] |= cw;
+                    }
+                }
+                if (cbk && e + b < e1) {  // the peer's read_ok payload: its whole set
+#pragma unroll
+                    for (int w = 0; w < WPL; ++w) Q.w[w] |= sb[b].w[w] | ((f[b] & FL_LAG) ? fb[b].w[w] : 0);
+                }
+            }
+        }
+        if (lg == 0 && e1 > e0) c_bytes += (unsigned long long)(e1 - e0) * 6;
+        if (keep) atomicOr(&s_keep, 1u);
+        hub_block_reduce<G, WPL>(O, R, s_or, s_rc);
+        if (j == 0) {
+            uint64_t* dst = a.hscratch + c * 3 * a.nwp;
+            store_row<WPL>(dst + off, O);
+            store_row<WPL>(dst + a.nwp + off, R);
+        }
+        __syncthreads();  // LDS reuse
+        if (cbk) {
+            hub_block_reduce<G, WPL>(Q, Z, s_or, s_rc);  // an OR: the order does not matter
+            if (j == 0) store_row<WPL>(a.hscratch + c * 3 * a.nwp + 2 * a.nwp + off, Q);
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            a.hflag[c] = (s_keep ? HF_KEEP : 0u) | HF_LIVE | (cbk ? HF_CB : 0u);
+            c_bytes += 16 + 16ull * a.nwp + (cbk ? 8ull * a.nwp : 0);
+        }
+    }
+    unsigned long long acc[C_NUM];
+#pragma unroll
+    for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
+    acc[C_GATHERS] = c_gathers;
+    acc[C_BYTES] = c_bytes;
+    flush_counters(a, acc, s_red, t_start, K_STREAM);
+}
+
+template <int G, int WPL>
+__global__ __launch_bounds__(kBlock) void hub_sync_finish(RoundArgs a) {
+    constexpr int NGB = kBlock / G;
+    __shared__ uint64_t s_or[NGB * G * WPL], s_rc[NGB * G * WPL];
+    __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
+    __shared__ uint32_t s_keep;
+    const unsigned long long t_start = clock100();
+    const int j = threadIdx.x / G, lg = threadIdx.x % G;
+    const uint64_t off = (uint64_t)lg * WPL;
+    const int gshift = (threadIdx.x & 63) / G * G;
+    const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+    unsigned long long c_new = 0, c_fwd = 0, c_hash = 0, c_active = 0, c_nact = 0, c_bytes = 0, c_nactdeg = 0;
+    for (uint64_t h = blockIdx.x; h < a.n_hubs; h += gridDim.x) {
+        const uint32_t i = a.hubs[h];
+        const uint64_t rep = a.own0 + i;
+        const uint8_t ca = a.hlive[h];
+        if (!ca) continue;  // block-uniform
+        if (threadIdx.x == 0) s_keep = 0;
+        __syncthreads();
+        const uint32_t c0 = a.hub_c0[h], c1 = a.hub_c0[h + 1];
+        const uint32_t per = (c1 - c0 + NGB - 1) / NGB;
+        const uint32_t q0 = c0 + j * per, q1 = min(c1, q0 + per);
+        Row<WPL> O, R;
+#pragma unroll
+        for (int w = 0; w < WPL; ++w) O.w[w] = R.w[w] = 0;
+        bool keep = false;
+        for (uint32_t q = q0; q < q1; ++q) {
+            const uint64_t* src = a.hscratch + (uint64_t)q * 3 * a.nwp;
+            hub_combine<WPL>(O, R, load_row<WPL>(src + off), load_row<WPL>(src + a.nwp + off));
+            keep |= (a.hflag[q] & HF_KEEP) != 0;
+        }
+        if (keep) atomicOr(&s_keep, 1u);
+        hub_block_reduce<G, WPL>(O, R, s_or, s_rc);
+        if (j == 0) {
+            const uint8_t st = a.sstate[rep], fo = a.flg_cur[rep];
+            const bool lag = (st & FL_LAG) != 0, cbk = (st & SE_FM2) != 0;
+            const bool keep_all = s_keep || (st & SE_FM3);  // read by a callback, or pushed by this node
+            Row<WPL> sp = load_row<WPL>(a.base + rep * a.nwp + off);
+            if (lag) {
+                const Row<WPL> of = load_row<WPL>(a.F_prev + rep * a.nwp + off);
+#pragma unroll
+                for (int w = 0; w < WPL; ++w) sp.w[w] |= of.w[w];
+            }
+            Row<WPL> S = sp;
+            if (ca & CA_INJ) {  // (1) client broadcasts of this round
+                uint32_t lo = 0, hi = a.n_inj;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (a.inj[2 * mid] < i) lo = mid + 1;
+                    else hi = mid;
+                }
+                for (uint32_t k = lo; k < a.n_inj && a.inj[2 * k] == i; ++k) {
+                    const uint32_t lane = a.inj[2 * k + 1];
+                    const uint32_t word = lane >> 6;
+                    if (word / WPL == (uint32_t)lg) set_lane_bit<WPL>(S, word % WPL, lane & 63);
+                }
+            }
+            // (2) node broadcasts and pushes: every new bit's first deliverer claims it
+            unsigned long long cl_recip = 0, cb_new = 0;
+#pragma unroll
+            for (int w = 0; w < WPL; ++w) {
+                const uint64_t claim = O.w[w] & ~S.w[w];
+                cl_recip += __popcll(claim & R.w[w]);
+                S.w[w] |= claim;
+            }
+            // (3) its callback: each chunk's exclusive prefix, then every peer's set
+            if (cbk) {
+                Row<WPL> P = S;
+                for (uint32_t q = c0; q < c1; ++q) {
+                    uint64_t* qr = a.hscratch + (uint64_t)q * 3 * a.nwp + 2 * a.nwp + off;
+                    const Row<WPL> Qc = load_row<WPL>(qr);
+                    store_row<WPL>(qr, P);
+#pragma unroll
+                    for (int w = 0; w < WPL; ++w) P.w[w] |= Qc.w[w];
+                }
+#pragma unroll
+                for (int w = 0; w < WPL; ++w) {
+                    cb_new += __popcll(P.w[w] & ~S.w[w]);
+                    S.w[w] = P.w[w];
+                }
+                if (lg == 0 && a.pushany) a.pushany[rep] = 0;  // hub_sync_push sets it where a push had content
+            }
+            Row<WPL> F;
+            unsigned long long T = 0;
+            const uint64_t g = gid_of(a, i);
+#pragma unroll
+            for (int w = 0; w < WPL; ++w) {
+                F.w[w] = S.w[w] & ~sp.w[w];
+                T += __popcll(F.w[w]);
+                if (F.w[w]) {
+                    const uint64_t idx = g * a.nw + a.word0 + off + w;
+                    c_hash += gg_word_hash(idx, F.w[w]);
+                }
+            }
+            const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
+            const bool zm = (fo & FL_ACT) != 0;
+            if (any || zm) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
+            if (keep_all) {
+                if (lag) store_row<WPL>(a.base + rep * a.nwp + off, sp);
+            } else if (any || lag) {
+                store_row<WPL>(a.base + rep * a.nwp + off, S);
+            }
+            if (any && a.sat_new) sat_mark<G, WPL>(a, S, rep, lg);
+            const uint64_t dout = (uint64_t)(a.in_ptr[i + 1] - a.in_ptr[i]);
+            c_new += T;
+            c_fwd += dout * T - cl_recip - cb_new;
+            if (lg == 0) {
+                if (any || zm) a.flg_cur[rep] = any ? (uint8_t)(FL_ACT | (keep_all ? FL_LAG : 0)) : (uint8_t)0;
+                a.hlive[h] = 0;
+                c_active += 1;
+                c_nact += any ? 1 : 0;
+                c_nactdeg += any ? dout : 0;
+                c_bytes += 16 + 3 + (uint64_t)(c1 - c0) * (4 + 16ull * a.nwp + (cbk ? 16ull * a.nwp : 0)) +
+                           8ull * a.nwp * (1 + (lag ? 1 : 0) + ((any || zm) ? 1 : 0) + ((keep_all ? lag : any || lag) ? 1 : 0));
+            }
+        }
+        __syncthreads();  // LDS reuse
+    }
+    unsigned long long acc[C_NUM];
+#pragma unroll
+    for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
+    acc[C_NEW] = c_new;
+    acc[C_FWD_SENT] = c_fwd;
+    acc[C_FWD_DELIV] = c_fwd;
+    acc[C_HASH] = c_hash;
+    acc[C_NEXT_ACKS] = c_fwd;
+    acc[C_ACTIVE] = c_active;
+    acc[C_NACT] = c_nact;
+    acc[C_NACTDEG] = c_nactdeg;
+    acc[C_BYTES] = c_bytes;
+    flush_counters(a, acc, s_red, t_start, K_STREAM);
+}
+
+template <int G, int WPL>
+__global__ __launch_bounds__(kBlock) void hub_sync_push(RoundArgs a) {
+    constexpr int NGB = kBlock / G;
+    __shared__ uint64_t s_q[NGB * G * WPL];
+    __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
+    __shared__ uint32_t s_any;
+    const unsigned long long t_start = clock100();
+    const int j = threadIdx.x / G, lg = threadIdx.x % G;
+    const uint64_t off = (uint64_t)lg * WPL;
+    const int gshift = (threadIdx.x & 63) / G * G;
+    const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+    unsigned long long c_push = 0, c_bytes = 0;
+    for (uint64_t c = blockIdx.x; c < a.n_hchunks; c += gridDim.x) {
+        const uint32_t fl = a.hflag[c];
+        if ((fl & (HF_LIVE | HF_CB)) != (HF_LIVE | HF_CB)) continue;  // block-uniform
+        const HubChunk hc = a.hchunks[c];
+        if (threadIdx.x == 0) s_any = 0;
+        const uint32_t per = (hc.n + NGB - 1) / NGB;
+        const int64_t e0 = hc.e0 + (int64_t)j * per;
+        const int64_t e1 = min(hc.e0 + (int64_t)hc.n, e0 + (int64_t)per);
+        auto peer_set = [&](int64_t e, uint32_t& w) {
+            w = a.in_col[e] & kColMask;
+            Row<WPL> r = load_row<WPL>(a.base + (uint64_t)w * a.nwp + off);
+            if (bit_at(a.ibits, w) && (a.sstate[w] & FL_LAG)) {
+                const Row<WPL> f = load_row<WPL>(a.F_prev + (uint64_t)w * a.nwp + off);
+#pragma unroll
+                for (int q = 0; q < WPL; ++q) r.w[q] |= f.w[q];
+            }
+            return r;
+        };
+        // the OR of each node group's slice, then every slice's exclusive prefix in order
+        Row<WPL> X;
+#pragma unroll
+        for (int q = 0; q < WPL; ++q) X.w[q] = 0;
+        for (int64_t e = e0; e < e1; ++e) {
+            uint32_t w;
+            const Row<WPL> r = peer_set(e, w);
+#pragma unroll
+            for (int q = 0; q < WPL; ++q) X.w[q] |= r.w[q];
+        }
+#pragma unroll
+        for (int q = 0; q < WPL; ++q) s_q[j * G * WPL + lg * WPL + q] = X.w[q];
+        __syncthreads();
+        Row<WPL> P = load_row<WPL>(a.hscratch + c * 3 * a.nwp + 2 * a.nwp + off);  // S before the chunk
+        for (int jj = 0; jj < j; ++jj) {
+#pragma unroll
+            for (int q = 0; q < WPL; ++q) P.w[q] |= s_q[jj * G * WPL + lg * WPL + q];
+        }
+        bool pushed = false;
+        for (int64_t e = e0; e < e1; ++e) {
+            uint32_t w;
+            const Row<WPL> r = peer_set(e, w);
+            unsigned long long pp = 0;
+#pragma unroll
+            for (int q = 0; q < WPL; ++q) {
+                pp += __popcll(P.w[q] & ~r.w[q]);
+                P.w[q] |= r.w[q];
+            }
+            c_push += pp;
+            const bool nz = ((__ballot(pp != 0) >> gshift) & gmask) != 0;
+            if (lg == 0) {
+                if (a.pushb) a.pushb[e] = nz ? 1 : 0;
+                pushed |= nz;
+                if (nz && a.mark_next && w < a.n_own) a.cand[a.own0 + w] = CA_NODE;
+            }
+        }
+        if (lg == 0 && e1 > e0) c_bytes += (uint64_t)(e1 - e0) * (8 + 2 * 8ull * a.nwp + 1);
+        if (pushed) atomicOr(&s_any, 1u);
+        __syncthreads();
+        if (threadIdx.x == 0 && s_any && a.pushany) a.pushany[a.own0 + hc.node] = 1;
+        __syncthreads();  // LDS reuse
+    }
+    unsigned long long acc[C_NUM];
+#pragma unroll
+    for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
+    acc[C_PUSH] = c_push;
+    acc[C_PUSH_DELIV] = c_push;
+    acc[C_NEXT_ACKS] = c_push;
+    acc[C_BYTES] = c_bytes;
+    flush_counters(a, acc, s_red, t_start, K_STREAM);
+}
+
 // Senders with out-degree > hub_deg that were active (or pushed) last round
 // mark their owned receivers; one block per out-edge chunk (sparse rounds).
 __global__ __launch_bounds__(kBlock) void hub_mark(RoundArgs a) {
@@ -2729,7 +3125,7 @@ __global__ void fold_slots(const unsigned long long* ctr, unsigned long long* ou
 
 // Episode reset: fill up to kResetSegs arrays (8-byte words) and start the
 // sync timers, in one launch.
-constexpr int kResetSegs = 24;
+constexpr int kResetSegs = 32;
 struct ResetSeg {
     uint64_t* p;
     uint64_t n;    // 8-byte words

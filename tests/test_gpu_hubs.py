@@ -83,3 +83,31 @@ def test_masked_streaming_rounds(hip_lib, cpu_lib, monkeypatch, W):
         sc.windows = [("seeded", 2, 6, rnd.randrange(1 << 30)), ("seeded", 6, 9, rnd.randrange(1 << 30)),
                       ("groups", 12, 20, np.array([rnd.randrange(3) for _ in range(sc.topo.n_nodes)], np.uint8))]
         _compare(sc, hip_lib, cpu_lib)
+
+
+@pytest.mark.parametrize("W,deg,chunk", [(256, 16, 7), (64, 24, 5), (4096, 40, 1000), (1024, 8, 3)])
+def test_rmat_hubs_sync_rounds(hip_lib, cpu_lib, monkeypatch, W, deg, chunk):
+    """Sync rounds on a power-law graph with hubs (streamed: hub_sync_chunks /
+    hub_sync_finish / hub_sync_push beside sync_records + expand_stream_sync):
+    hubs receive pushes, answer reads, run callbacks over many chunks (the
+    exclusive prefix across chunks), late client broadcasts reach them, and
+    every round equals O2; the tile kernel never runs in those rounds."""
+    monkeypatch.setenv("GG_HUB_DEG", str(deg))
+    monkeypatch.setenv("GG_HUB_CHUNK", str(chunk))
+    monkeypatch.setenv("GG_SYNC_TILES", "0")
+    topo = T.rmat(4096, 16, seed=47)
+    assert int(np.diff(topo.row_ptr).max()) > 4 * deg
+    K = min(W, 200)
+    inj = uniform_injections(4096, K // 2, 48) + [(n, K // 2 + v, 9 + v % 7) for n, v, _ in
+                                                   uniform_injections(4096, K - K // 2, 49)]
+    sc = Scenario(topo, W, 36, inj, seed=50, sync_base=3, sync_jitter=2)
+    g = make_engine(hip_lib, sc, device=0)
+    c = make_engine(cpu_lib, sc)
+    gs = g.step(sc.rounds)
+    d = diff_stats(gs, c.step(sc.rounds))
+    assert not d, d[:10]
+    assert np.array_equal(g.read_bits(), c.read_bits())
+    assert np.array_equal(g.delivery_rounds(), c.delivery_rounds())
+    sync = [s for s in gs if s["round"] >= sc.sync_base + 2]
+    assert sum(s["pushes"] for s in sync) > 0 and sum(s["syncs_fired"] for s in gs) > 0
+    assert all(s["expand_bytes"] == 0 for s in sync), [s["expand_bytes"] for s in sync]

@@ -1,6 +1,6 @@
 """GPU parity of the streamed sync rounds (sync_records + expand_stream_sync):
 rounds after the sync timers start, without partition windows, on graphs
-without in-hubs at W >= 128. Every case runs on the default (streamed) path and
+without in-hubs, at every row width (W = 64: one word per node, one lane). Every case runs on the default (streamed) path and
 on the tile path (GG_SYNC_TILES=1) and must equal the CPU oracle O2 bit for bit
 (counters of every round, node sets, delivery rounds). The cases push the
 record format to its edges: sparse and dense rounds, more than three
@@ -26,7 +26,7 @@ def _compare(sc, hip_lib, cpu_lib, path):
     d = diff_stats(gs, c.step(sc.rounds))
     assert not d, d[:10]
     sync = [s for s in gs if s["round"] >= sc.sync_base + 2]
-    if path == "stream" and sc.W >= 128:  # the tile kernel never runs in sync rounds
+    if path == "stream":  # the tile kernel never runs in sync rounds
         assert sync and all(s["expand_bytes"] == 0 for s in sync)
         assert sum(s["stream_bytes"] for s in sync) > 0
     elif path == "tiles":
@@ -41,7 +41,7 @@ def path(request, monkeypatch):
     return request.param
 
 
-@pytest.mark.parametrize("W", [128, 1024, 4096])
+@pytest.mark.parametrize("W", [64, 128, 1024, 4096])
 @pytest.mark.parametrize("directed_p", [0.0, 0.3])
 def test_random_sync_rounds(hip_lib, cpu_lib, path, W, directed_p):
     rnd = random.Random(W * 7 + int(directed_p * 10))
@@ -131,3 +131,14 @@ def test_digest_lane_groups(hip_lib, cpu_lib, monkeypatch):
         for a, b in zip(tot, ref):
             for f in COUNT_FIELDS:
                 assert a[f] == b[f], (L, a["round"], f, a[f], b[f])
+
+
+@pytest.mark.parametrize("jitter", [0, 5])
+def test_w64_grid_links_sync(hip_lib, cpu_lib, path, jitter):
+    """C5's shape (grid + one long link per node, W = 64) run into the sync
+    phase, with late broadcasts and synchronous timers: the W = 64 streamed
+    sync kernel against O2."""
+    topo = T.grid_links(64, seed=96)
+    inj = uniform_injections(4096, 40, 97) + [(n, 40 + v, 26 + v % 5) for n, v, _ in uniform_injections(4096, 24, 98)]
+    sc = Scenario(topo, 64, 50, inj, seed=99, sync_base=8, sync_jitter=jitter)
+    _compare(sc, hip_lib, cpu_lib, path)
