@@ -51,6 +51,16 @@ struct Shard {
 };
 int shard_csr(Csr* g, uint64_t lo, uint64_t hi, const std::vector<uint64_t>& plo, uint64_t ghost0, uint32_t col_or,
               hipStream_t st, Shard* out, std::string* err);
+// A shard's local rows in locality order (the single engine's degree_reorder
+// rule): owned rows by descending degree, ghost rows by descending count of
+// owned receivers (the rows the shard's gathers hit most come first), ties by
+// the old row. Renumbers g's columns, sh's gid (device and host), send_idx and
+// ghost -> owned lists (re-indexed by the new ghost rows). Returns, on the
+// device, grow[old ghost index] = new ghost index (the exchange still delivers
+// ghosts in the sender's order, ascending id) and, on the host, own_row[old
+// owned row] = new owned row.
+int shard_reorder(Csr* g, Shard* sh, uint64_t ghost0, uint32_t col_or, hipStream_t st, uint32_t** grow_out,
+                  std::vector<uint32_t>* own_row, std::string* err);
 
 }  // namespace gg_gen
 

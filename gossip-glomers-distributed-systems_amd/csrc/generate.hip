@@ -709,6 +709,171 @@ __global__ void fill_gid(uint64_t rows, uint64_t lo, uint64_t n_own, uint64_t gh
                  : (r >= ghost0 && r < ghost0 + n_ghost) ? ghosts[r - ghost0] : ~0u;
 }
 
+// ---- shard_reorder ----------------------------------------------------------
+// keys of n items: (0xffffffff - count) << 32 | item, count = ptr[i+1] - ptr[i]
+__global__ void count_keys(const int64_t* ptr, uint64_t n, uint64_t* keys) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        keys[i] = ((uint64_t)(0xffffffffu - (uint32_t)(ptr[i + 1] - ptr[i])) << 32) | i;
+}
+
+// sorted keys -> order[new] = old, inverse perm[old] = new, new counts (for the scan)
+__global__ void perm_from_keys(const uint64_t* keys, const int64_t* ptr, uint64_t n, uint32_t* order, uint32_t* perm,
+                               int64_t* ncnt) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t old = (uint32_t)(keys[i] & 0xffffffffu);
+        order[i] = old;
+        perm[old] = (uint32_t)i;
+        ncnt[i] = ptr[old + 1] - ptr[old];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) ncnt[n] = 0;
+}
+
+// a local row under the new numbering (owned: perm, ghosts: gperm; | the recip bit kept)
+__device__ __forceinline__ uint32_t renum(uint32_t c, uint64_t n_own, uint64_t ghost0, const uint32_t* perm,
+                                          const uint32_t* gperm) {
+    const uint32_t r = c & 0x7fffffffu, hi = c & 0x80000000u;
+    if (r < n_own) return perm[r] | hi;
+    if (r >= ghost0) return (uint32_t)(ghost0 + gperm[r - ghost0]) | hi;
+    return c;
+}
+
+// entry j of the reordered list arrays: its new row (binary search in nptr),
+// that row's old row, the same entry of the old list, renumbered
+__global__ void copy_lists(const int64_t* ptr, const uint32_t* vals, const int64_t* nptr, const uint32_t* order,
+                           uint64_t n, uint64_t nnz, int renumber, uint64_t n_own, uint64_t ghost0,
+                           const uint32_t* perm, const uint32_t* gperm, const uint32_t* vals2, uint32_t* nvals,
+                           uint32_t* nvals2) {
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nnz; j += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t lo = 0, hi = n - 1;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi + 1) >> 1;
+            if ((uint64_t)nptr[mid] <= j) lo = mid;
+            else hi = mid - 1;
+        }
+        const uint64_t src = (uint64_t)ptr[order[lo]] + (j - (uint64_t)nptr[lo]);
+        const uint32_t v = vals[src];
+        nvals[j] = renumber ? renum(v, n_own, ghost0, perm, gperm) : v;
+        if (nvals2) nvals2[j] = vals2[src];
+    }
+}
+
+__global__ void renum_array(uint32_t* a, uint64_t n, uint64_t n_own, uint64_t ghost0, const uint32_t* perm,
+                            const uint32_t* gperm) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        a[i] = renum(a[i], n_own, ghost0, perm, gperm);
+}
+
+__global__ void permute_gid(const uint32_t* gid, uint64_t rows, uint64_t n_own, uint64_t ghost0, uint64_t n_ghost,
+                            const uint32_t* order, const uint32_t* gorder, uint32_t* ngid) {
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (uint64_t)gridDim.x * blockDim.x) {
+        if (r < n_own) ngid[r] = gid[order[r]];
+        else if (r >= ghost0 && r < ghost0 + n_ghost) ngid[r] = gid[ghost0 + gorder[r - ghost0]];
+        else ngid[r] = gid[r];
+    }
+}
+
+}  // namespace
+
+namespace {
+// order/perm of n items by descending count (ptr differences), and the new ptr
+int order_by_count(const int64_t* ptr, uint64_t n, hipStream_t st, Scoped& mem, uint32_t** order, uint32_t** perm,
+                   int64_t** nptr, std::string* err) {
+    uint64_t* keys = nullptr;
+    uint64_t* alt = nullptr;
+    int64_t* ncnt = nullptr;
+    GCHK(mem.alloc(&keys, std::max<uint64_t>(1, n) * 8));
+    GCHK(mem.alloc(&alt, std::max<uint64_t>(1, n) * 8));
+    GCHK(mem.alloc(order, std::max<uint64_t>(1, n) * 4));
+    GCHK(mem.alloc(perm, std::max<uint64_t>(1, n) * 4));
+    GCHK(mem.alloc(&ncnt, (n + 1) * 8));
+    GCHK(mem.alloc(nptr, (n + 1) * 8));
+    hipLaunchKernelGGL(count_keys, dim3(grid_of(n)), dim3(kBlk), 0, st, ptr, n, keys);
+    GCHK(hipGetLastError());
+    size_t tb = 0;
+    void* tmp = nullptr;
+    if (n) {
+        rocprim::double_buffer<uint64_t> db(keys, alt);
+        GCHK(rocprim::radix_sort_keys(nullptr, tb, db, (size_t)n, 0, 64, st));
+        GCHK(mem.alloc(&tmp, tb));
+        GCHK(rocprim::radix_sort_keys(tmp, tb, db, (size_t)n, 0, 64, st));
+        if (db.current() != keys) std::swap(keys, alt);
+        mem.release(tmp);
+    }
+    hipLaunchKernelGGL(perm_from_keys, dim3(grid_of(n)), dim3(kBlk), 0, st, keys, ptr, n, *order, *perm, ncnt);
+    GCHK(hipGetLastError());
+    tb = 0;
+    GCHK(rocprim::exclusive_scan(nullptr, tb, ncnt, *nptr, (int64_t)0, n + 1, rocprim::plus<int64_t>(), st));
+    GCHK(mem.alloc(&tmp, tb));
+    GCHK(rocprim::exclusive_scan(tmp, tb, ncnt, *nptr, (int64_t)0, n + 1, rocprim::plus<int64_t>(), st));
+    mem.release(tmp);
+    mem.release(keys);
+    mem.release(alt);
+    mem.release(ncnt);
+    return 0;
+}
+}  // namespace
+
+int shard_reorder(Csr* g, Shard* sh, uint64_t ghost0, uint32_t col_or, hipStream_t st, uint32_t** grow_out,
+                  std::vector<uint32_t>* own_row, std::string* err) {
+    (void)col_or;
+    const uint64_t n = g->V, m = g->nnz, ng = sh->n_ghost, nc = sh->n_cut;
+    const uint64_t rows = std::max<uint64_t>(64, (ghost0 + ng + 63) / 64 * 64);
+    Scoped mem;
+    uint32_t *order = nullptr, *perm = nullptr, *gorder = nullptr, *gperm = nullptr;
+    int64_t *nrp = nullptr, *ngp = nullptr;
+    if (int r = order_by_count(g->row_ptr, n, st, mem, &order, &perm, &nrp, err)) return r;
+    if (int r = order_by_count(sh->gout_ptr, ng, st, mem, &gorder, &gperm, &ngp, err)) return r;
+    uint32_t *ncol = nullptr, *ngcol = nullptr, *ngsidx = nullptr, *ngid = nullptr;
+    GCHK(mem.alloc(&ncol, std::max<uint64_t>(1, m) * 4));
+    GCHK(mem.alloc(&ngcol, std::max<uint64_t>(1, nc) * 4));
+    GCHK(mem.alloc(&ngsidx, std::max<uint64_t>(1, nc) * 4));
+    GCHK(mem.alloc(&ngid, rows * 4));
+    if (m) {
+        hipLaunchKernelGGL(copy_lists, dim3(grid_of(m)), dim3(kBlk), 0, st, g->row_ptr, g->col, nrp, order, n, m, 1,
+                           n, ghost0, perm, gperm, (const uint32_t*)nullptr, ncol, (uint32_t*)nullptr);
+        GCHK(hipGetLastError());
+    }
+    if (nc) {  // ghost -> owned lists by new ghost row: receivers renumbered, send entries kept
+        hipLaunchKernelGGL(copy_lists, dim3(grid_of(nc)), dim3(kBlk), 0, st, sh->gout_ptr, sh->gout_col, ngp, gorder,
+                           ng, nc, 1, n, ghost0, perm, gperm, sh->gout_sidx, ngcol, ngsidx);
+        GCHK(hipGetLastError());
+    }
+    if (sh->n_send) {  // send entries keep their positions (the receiver's ghost order); rows renumbered
+        hipLaunchKernelGGL(renum_array, dim3(grid_of(sh->n_send)), dim3(kBlk), 0, st, sh->send_idx, sh->n_send, n,
+                           ghost0, perm, gperm);
+        GCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(permute_gid, dim3(grid_of(rows)), dim3(kBlk), 0, st, sh->gid, rows, n, ghost0, ng, order,
+                       gorder, ngid);
+    GCHK(hipGetLastError());
+    own_row->resize(n);
+    if (n) GCHK(hipMemcpyAsync(own_row->data(), perm, n * 4, hipMemcpyDeviceToHost, st));
+    GCHK(hipStreamSynchronize(st));
+    (void)hipFree(g->row_ptr);
+    (void)hipFree(g->col);
+    (void)hipFree(sh->gout_ptr);
+    (void)hipFree(sh->gout_col);
+    (void)hipFree(sh->gout_sidx);
+    (void)hipFree(sh->gid);
+    g->row_ptr = nrp;
+    g->col = ncol;
+    sh->gout_ptr = ngp;
+    sh->gout_col = ngcol;
+    sh->gout_sidx = ngsidx;
+    sh->gid = ngid;
+    mem.keep(nrp);
+    mem.keep(ncol);
+    mem.keep(ngp);
+    mem.keep(ngcol);
+    mem.keep(ngsidx);
+    mem.keep(ngid);
+    mem.keep(gperm);
+    *grow_out = gperm;
+    return 0;
+}
+
+namespace {
+
 template <class K>
 int sort_unique(K* keys, uint64_t n, int bits, hipStream_t st, uint64_t* n_unique, std::string* err) {
     Scoped mem;

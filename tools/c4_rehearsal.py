@@ -134,7 +134,15 @@ def main():
     ap.add_argument("--link-gbs", type=float, default=64.0,
                     help="xGMI bandwidth per link and direction used in the projection (GB/s)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--single-only", type=int, default=0,
+                    help="run only the single engine for this many rounds and print its per-round times")
     args = ap.parse_args()
+    if args.single_only:
+        st, nnz, hbm = _single(args, args.single_only)
+        print(json.dumps({"nodes": args.nodes, "lanes": args.lanes, "order": os.environ.get("GG_ORDER", "auto"),
+                          "nnz": nnz, "hbm_bytes": hbm, "round_ms": [s["kernel_ms"] for s in st],
+                          "new_bits": [s["new_bits"] for s in st]}))
+        return
     import torch.multiprocessing as mp
     world = args.parts * args.lane_groups
     ctx = mp.get_context("spawn")
