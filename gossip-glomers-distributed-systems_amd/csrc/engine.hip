@@ -43,7 +43,8 @@ constexpr int kMaxBlocks = 2048;
 // Test hooks: environment variables the test suite sets to force a code path
 // that the engine would otherwise choose by size (every forced path is
 // bit-exact; only the kernels that run change): GG_HUB_DEG, GG_HUB_CHUNK,
-// GG_SYNC_TILES, GG_SYNC_DIGEST, GG_ORDER, GG_XCHG_MODE, GG_PREP_BLOCKS.
+// GG_SYNC_TILES, GG_SYNC_DIGEST, GG_ORDER, GG_XCHG_MODE, GG_PREP_BLOCKS,
+// GG_SHARD_NATIVE (device-built shards keep native row order).
 const char* test_knob(const char* name) { return getenv(name); }
 // A/B switches of past measurements (GG_ALL_FULL, GG_NO_GRAPH, GG_SYNC_ALLPUSH,
 // GG_FLAGS_FIRST, GG_XCHG_EXACT_BYTES): read only in a -DGG_AB_KNOBS build.
@@ -167,7 +168,10 @@ struct gg_engine {
     std::vector<uint32_t> gid;     // [rows] original id of each local row (~0u: padding)
     std::vector<uint32_t> loc_of;  // [V] local row of an owned node, ~0u otherwise (sharded)
     bool range_mode = false;       // device-partitioned shard: owned nodes [range_lo, range_hi)
-    uint64_t range_lo = 0, range_hi = 0;  // are rows 0.. (no loc_of)
+    uint64_t range_lo = 0, range_hi = 0;  // are rows 0.. (no loc_of), or own_row[node - range_lo]
+    std::vector<uint32_t> own_row; // [n_own] range shard in locality order: row of node range_lo + i
+    uint32_t* d_grow = nullptr;    // [n_ghost] range shard in locality order: ghost row of the g-th ghost
+                                   // in exchange order (ascending id)
     bool have_topo = false, symmetric = true;
     std::vector<int64_t> host_rp;  // vertex-sharded: the caller's row offsets (gg_set_partition)
     uint32_t* d_gid = nullptr;     // sharded only (single engine: row == id)
@@ -360,6 +364,8 @@ void gg_engine::free_topology() {
     dfree(d_sync_k);
     dfree(d_dr);
     dfree(d_gid);
+    dfree(d_grow);
+    own_row.clear();
     dfree(d_send_idx);
     dfree(d_gout_ptr);
     dfree(d_gout_col);
@@ -1014,7 +1020,10 @@ int ensure_inj(gg_engine* e, size_t pairs) {
 // Local row of an owned node, ~0u if another engine owns it.
 uint32_t local_row(const gg_engine* e, uint64_t node) {
     if (node >= e->V) return ~0u;
-    if (e->range_mode) return node >= e->range_lo && node < e->range_hi ? (uint32_t)(node - e->range_lo) : ~0u;
+    if (e->range_mode) {
+        if (node < e->range_lo || node >= e->range_hi) return ~0u;
+        return e->own_row.empty() ? (uint32_t)(node - e->range_lo) : e->own_row[node - e->range_lo];
+    }
     if (e->loc_of.empty()) return (uint32_t)node;
     return e->loc_of[node];
 }
@@ -1776,6 +1785,14 @@ static int install_shard(gg_engine* e, gg_gen::Csr g, const std::vector<uint64_t
         (void)hipFree(g.col);
         return e->fail(rc, err);
     }
+    // rows in locality order (the single engine's degree order): hot rows together
+    std::vector<uint32_t> own_row;
+    uint32_t* d_grow = nullptr;
+    g.V = n_own;
+    if (!test_knob("GG_SHARD_NATIVE")) {
+        rc = gg_gen::shard_reorder(&g, &sh, ghost0, gg::kRecipBit, e->stream, &d_grow, &own_row, &err);
+        if (rc) return e->fail(rc, err);
+    }
     e->range_mode = true;
     e->range_lo = lo;
     e->range_hi = hi;
@@ -1787,9 +1804,15 @@ static int install_shard(gg_engine* e, gg_gen::Csr g, const std::vector<uint64_t
     e->rows = std::max<uint64_t>(64, (ghost0 + sh.n_ghost + 63) / 64 * 64);
     if (e->rows > 0x7fffffffull) return e->fail(GG_EINVAL, "local rows exceed 2^31");
     e->gid.assign(e->rows, ~0u);
-    for (uint64_t i = 0; i < n_own; ++i) e->gid[i] = (uint32_t)(lo + i);
-    for (uint64_t k = 0; k < sh.n_ghost; ++k) e->gid[ghost0 + k] = sh.ghosts_host[k];
+    if (own_row.empty()) {
+        for (uint64_t i = 0; i < n_own; ++i) e->gid[i] = (uint32_t)(lo + i);
+        for (uint64_t k = 0; k < sh.n_ghost; ++k) e->gid[ghost0 + k] = sh.ghosts_host[k];
+    } else {  // the reordered rows' ids
+        HIPCHK(hipMemcpy(e->gid.data(), sh.gid, e->rows * 4, hipMemcpyDeviceToHost));
+    }
     std::vector<uint32_t>().swap(sh.ghosts_host);
+    e->own_row.swap(own_row);
+    e->d_grow = d_grow;
     e->d_gid = sh.gid;
     e->d_in_ptr = g.row_ptr;
     e->d_in_col = g.col;
@@ -2320,6 +2343,7 @@ int gg_dist_round_end(gg_engine* e, gg_round_stats* out) {
         ua.base = e->d_base;
         ua.flg_cur = e->d_flg[r & 1];
         ua.stamp = e->d_stamp;
+        ua.grow = e->d_grow;
         ua.act_cur = e->d_act_s + (r & 3) * gg::kSlots;
         ua.in = e->d_xrecv;
         ua.seg_off = e->d_xroff;

@@ -3380,7 +3380,8 @@ struct UnpackArgs {
     uint64_t* F_cur;
     uint64_t* base;
     uint8_t* flg_cur;
-    uint32_t* stamp;             // [n_ghost] last round a ghost's F row arrived
+    uint32_t* stamp;             // [n_ghost] last round a ghost's F row arrived (by ghost row)
+    const uint32_t* grow;        // [n_ghost] ghost row of the g-th ghost in exchange order, or nullptr (same)
     uint32_t* act_cur;           // spread act slots of round r ([kSlots])
     const uint8_t* in;
     const uint64_t* seg_off;     // [parts + 1] capacity offset of each source's segment
@@ -3425,7 +3426,8 @@ __global__ __launch_bounds__(kBlock) void unpack_ghosts(UnpackArgs x) {
         const uint8_t* ent = x.in + x.seg_off[p] + 16 + (uint64_t)(j - s_pref[lo]) * x.stride;
         const uint32_t hd = *reinterpret_cast<const uint32_t*>(ent);
         const bool set = (hd & XK_SET) != 0;
-        const uint64_t g = x.gfirst[p] + (hd & ~XK_SET);
+        const uint64_t g0 = x.gfirst[p] + (hd & ~XK_SET);
+        const uint64_t g = x.grow ? x.grow[g0] : g0;  // locality-ordered shards: the ghost's row
         const uint64_t row = x.ghost0 + g;
         if (ch == 0) {
             if (x.nwp == 1) {
