@@ -48,24 +48,45 @@ METRIC = "(node,msg) deliveries/sec at 1/2/4/8 GPUs; % of HBM roofline; msgs/op"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 KERNELS = {"prep": "round_prep", "expand": "expand_round", "stream": "expand_stream"}
-TRAFFIC_JSON = os.path.join(REPO, "profiles", "traffic.json")
+# the kernels stamping each kind: a kind's "launch" is one round, so its
+# counter traffic per launch is the sum over these kernels' dispatches per round
+KIND_KERNELS = {
+    "prep": ["round_prep", "compact_round", "mark_injections", "hub_mark", "sync_records"],
+    "expand": ["expand_round", "expand_round_lean"],
+    "stream": ["expand_stream", "expand_stream_masked", "expand_stream1", "expand_stream_sync", "hub_chunks",
+               "hub_finish", "hub_sync_chunks", "hub_sync_finish", "hub_sync_push", "expand_batched"],
+}
+TRAFFIC_JSON = {"C2": os.path.join(REPO, "profiles", "traffic.json"),  # committed PMC passes per config
+                "C4": os.path.join(REPO, "profiles", "traffic_C4.json")}
 CPU_LIB = os.path.join(REPO, "oracle", "_build", "libgossip_cpu.so")
 
 
-def pmc_traffic(kernel: str, config: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (tools/traffic.py: FETCH_SIZE and WRITE_SIZE in separate passes over this
-    same bench command, FETCH_SIZE doubled for gfx950). None if not profiled."""
+def pmc_traffic(kind: str, config: str):
+    """HBM bytes per round of a kernel kind from the committed rocprofv3 PMC
+    passes (tools/traffic.py: FETCH_SIZE and WRITE_SIZE in separate passes over
+    this same bench command, FETCH_SIZE doubled for gfx950): the sum over the
+    kind's kernels of bytes x dispatches, per dispatch of its main kernel (one
+    per round). None if not profiled."""
+    path = TRAFFIC_JSON.get(config)
     try:
-        d = json.load(open(TRAFFIC_JSON))
-    except (OSError, ValueError):
+        d = json.load(open(path))
+    except (OSError, ValueError, TypeError):
         return None, None
     if d.get("config", "C2") != config:
         return None, None
+    base = lambda name: name.split("(")[0].split("<")[0].split("::")[-1]  # noqa: E731
+    ents = {}
     for name, ent in d.get("kernels", {}).items():
-        if name.split("(")[0].split("<")[0].split("::")[-1] == kernel:
-            return ent["traffic_bytes_per_dispatch"], f'{os.path.relpath(TRAFFIC_JSON, REPO)} ({d.get("source", "")})'
-    return None, None
+        b = base(name)
+        if b in KIND_KERNELS[kind]:
+            e = ents.setdefault(b, [0.0, 0])
+            e[0] += ent["traffic_bytes_per_dispatch"] * ent["dispatches"]
+            e[1] += ent["dispatches"]
+    main = KERNELS[kind]
+    if main not in ents or not ents[main][1]:
+        return None, None
+    per_round = sum(v[0] for v in ents.values()) / ents[main][1]
+    return per_round, f'{os.path.relpath(path, REPO)} ({d.get("source", "")}; kernels {sorted(ents)})'
 
 
 def dense_bytes_per_round(V: int, E: int, nwp: int) -> int:
@@ -324,7 +345,7 @@ def main():
     dom = max(kinds, key=lambda k: kinds[k]["total_ms"])
     D = kinds[dom]
     achieved = D["GBps"]
-    traffic, traffic_src = pmc_traffic(D["kernel"], cfg)
+    traffic, traffic_src = pmc_traffic(dom, cfg)
     round_ms = sum(s["kernel_ms"] for s in rounds_local)
     round_bytes = sum(s["prep_bytes"] + s["expand_bytes"] + s["stream_bytes"] for s in rounds_local)
     xbytes = None
@@ -395,6 +416,8 @@ def main():
             "roofline": {
                 "bound": "hbm",
                 "kernel": D["kernel"],
+                "kind": dom,
+                "kind_kernels": "every kernel stamping this kind per round: " + ", ".join(KIND_KERNELS[dom]),
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -1382,9 +1382,9 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
         }
         if (e->n_in_edges) {  // receivers look up whether an owned pusher sent them anything
             HIPCHK(hipMalloc(&e->d_rev, e->n_in_edges * 4));
-            const unsigned blocks = (unsigned)std::min<uint64_t>((n_own + 255) / 256, 4096);
+            const unsigned blocks = (unsigned)std::min<uint64_t>((e->n_in_edges / 8 + 255) / 256 + 1, 16384);
             hipLaunchKernelGGL(gg::build_rev, dim3(blocks), dim3(256), 0, e->stream, e->d_in_ptr, e->d_in_col,
-                               e->d_out_ptr, e->d_out_col, e->d_gid, n_own, e->d_rev);
+                               e->d_out_ptr, e->d_out_col, e->d_gid, n_own, e->n_in_edges, e->d_rev);
             HIPCHK(hipGetLastError());
         }
     }

@@ -2451,21 +2451,37 @@ __global__ __launch_bounds__(kBlock) void expand_batched(RoundArgs a) {
 // owned senders (streamed sync rounds read pushb through it); ~0u for ghosts.
 // Out-lists ascend by node id (gid), so a binary search by id.
 __global__ void build_rev(const int64_t* in_ptr, const uint32_t* in_col, const int64_t* out_ptr,
-                          const uint32_t* out_col, const uint32_t* gid, uint64_t n_own, uint32_t* rev) {
-    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n_own; v += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t gv = gid ? gid[v] : v;
-        for (int64_t k = in_ptr[v]; k < in_ptr[v + 1]; ++k) {
+                          const uint32_t* out_col, const uint32_t* gid, uint64_t n_own, uint64_t n_edges,
+                          uint32_t* rev) {
+    // edge-parallel (a hub's in-list is no single thread's serial walk): each
+    // thread takes a slice of consecutive in-edges, finds the slice's first row
+    // by binary search in in_ptr, and for each edge v <- u binary-searches v in
+    // u's out-list (ascending by original id)
+    constexpr uint64_t kSlice = 8;
+    const uint64_t slices = (n_edges + kSlice - 1) / kSlice;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < slices; s += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k0 = s * kSlice, k1 = k0 + kSlice < n_edges ? k0 + kSlice : n_edges;
+        uint64_t lo = 0, hi = n_own - 1;  // largest v with in_ptr[v] <= k0
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi + 1) >> 1;
+            if ((uint64_t)in_ptr[mid] <= k0) lo = mid;
+            else hi = mid - 1;
+        }
+        uint64_t v = lo;
+        for (uint64_t k = k0; k < k1; ++k) {
+            while ((uint64_t)in_ptr[v + 1] <= k) ++v;  // empty rows in between
+            const uint64_t gv = gid ? gid[v] : v;
             const uint32_t u = in_col[k] & kColMask;
             uint32_t r = ~0u;
             if (u < n_own) {
-                int64_t lo = out_ptr[u], hi = out_ptr[u + 1];
-                while (lo < hi) {
-                    const int64_t mid = (lo + hi) >> 1;
+                int64_t a = out_ptr[u], b = out_ptr[u + 1];
+                while (a < b) {
+                    const int64_t mid = (a + b) >> 1;
                     const uint32_t w = out_col[mid] & kColMask;
-                    if ((gid ? (uint64_t)gid[w] : (uint64_t)w) < gv) lo = mid + 1;
-                    else hi = mid;
+                    if ((gid ? (uint64_t)gid[w] : (uint64_t)w) < gv) a = mid + 1;
+                    else b = mid;
                 }
-                r = (uint32_t)lo;
+                r = (uint32_t)a;
             }
             rev[k] = r;
         }

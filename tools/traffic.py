@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """rocprofv3 PMC passes -> profiles/traffic.json (read by bench.py).
 
-Usage: tools/traffic.py <fetch counter_collection.csv> <write counter_collection.csv> <source note> [out]
+Usage: tools/traffic.py <fetch counter_collection.csv> <write counter_collection.csv> <source note> [out] [config]
 
 FETCH_SIZE and WRITE_SIZE come from separate passes of the same command (they
 cannot share a pass on gfx950). Per MI355X_MICROARCH.md (HBM section),
@@ -31,7 +31,8 @@ def main():
         wk = sum(wl) / len(wl) if wl else 0.0
         ker[k] = {"dispatches": len(f[k]), "fetch_kB": fk, "write_kB": wk,
                   "traffic_bytes_per_dispatch": (2.0 * fk + wk) * 1024.0}
-    json.dump({"source": sys.argv[3], "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950)",
+    cfg = sys.argv[5] if len(sys.argv) > 5 else "C2"
+    json.dump({"source": sys.argv[3], "config": cfg, "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950)",
                "kernels": ker}, open(out, "w"), indent=1)
     for k, v in sorted(ker.items(), key=lambda kv: -kv[1]["traffic_bytes_per_dispatch"] * kv[1]["dispatches"]):
         print(f'{v["dispatches"]:5d} {v["traffic_bytes_per_dispatch"] / 1e6:10.2f} MB  {k[:90]}')
