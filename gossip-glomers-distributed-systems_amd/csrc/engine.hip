@@ -252,6 +252,7 @@ struct gg_engine {
     uint64_t* d_sat = nullptr;       // [rows/64] saturation digest (streamed sync rounds)
     uint64_t* d_pend = nullptr;      // batched gossip: [rows][nwp] pending values
     uint32_t* d_pend_src = nullptr;  // batched gossip: [rows] who delivered them
+    uint64_t* d_bset[2] = {nullptr, nullptr};  // batched gossip with sync: sets after odd / even rounds
     uint8_t* d_pushany = nullptr;    // [rows] a streamed callback pushed to some peer
     uint2* d_nmeta = nullptr;        // [n_own] node list with the nodes' bytes (streamed sync rounds)
     uint64_t* d_sat_new = nullptr;   // [rows/64] its bits found in the current round
@@ -345,6 +346,8 @@ void gg_engine::free_topology() {
     dfree(d_nmeta);
     dfree(d_pend);
     dfree(d_pend_src);
+    dfree(d_bset[0]);
+    dfree(d_bset[1]);
     dfree(d_hscratch);
     dfree(d_hflag);
     dfree(d_hlive);
@@ -826,6 +829,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     static const bool no_full = ab_knob("GG_ALL_FULL") && atoi(ab_knob("GG_ALL_FULL")) == 0;  // A/B
     a.tot = no_full ? nullptr : e->d_tot;
     a.full_new = (unsigned long long)e->n_own * lanes_through(e, r - 1);
+    a.lanes_prev = lanes_through(e, r - 1);
     a.counters = d_ctr;
     a.n_own = e->n_own;
     a.own0 = 0;
@@ -853,6 +857,11 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         a.pend = e->d_pend;
         a.pend_src = e->d_pend_src;
         a.batch_tick = (r + 1) % (int64_t)e->cfg.batch_ticks == 0 ? 1u : 0u;
+        if (e->d_bset[0]) {  // sync timers: this round's fired bits are set by the kernel
+            a.bset_prev = e->d_bset[(r + 1) & 1];
+            a.bset_cur = e->d_bset[r & 1];
+            HIPCHK(hipMemsetAsync(a.fired_cur, 0, e->rows / 8, e->stream));
+        }
         if (n_inj) {
             hipLaunchKernelGGL(gg::mark_injections, dim3((n_inj + 255) / 256), dim3(256), 0, e->stream, a);
             HIPCHK(hipGetLastError());
@@ -885,8 +894,9 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             }
             // sync rounds do real work per node: a larger capped grid (each block's
             // counter flush is a few same-address atomics, so not one block per 256 nodes)
+            static const uint64_t sync_cap = ab_knob("GG_SYNC_PREP_BLOCKS") ? (uint64_t)atoi(ab_knob("GG_SYNC_PREP_BLOCKS")) : 4096;
             const uint64_t blocks = std::max<uint64_t>(
-                1, std::min<uint64_t>((a.n_own + gg::kBlock - 1) / gg::kBlock, syncw_prep ? 4096 : prep_cap));
+                1, std::min<uint64_t>((a.n_own + gg::kBlock - 1) / gg::kBlock, syncw_prep ? sync_cap : prep_cap));
             dim3 grid((unsigned)blocks), block(gg::kBlock);
             if (syncw_prep) {
                 if (maskw) hipLaunchKernelGGL((gg::round_prep<true, true>), grid, block, 0, e->stream, a);
@@ -1256,7 +1266,7 @@ int gg_create(const gg_config* cfg, gg_engine** out) {
     // the exchange kernels keep one LDS slot per source part (unpack_ghosts) and
     // one lane per destination part (finish_pack, a 64-thread block)
     if (cfg->world / L > 63) return GG_EINVAL;
-    if (cfg->batch_ticks && (cfg->enable_sync || cfg->world != 1)) return GG_EINVAL;  // batched: single, no sync
+    if (cfg->batch_ticks && cfg->world != 1) return GG_EINVAL;  // batched gossip: one engine
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GG_EIO;
     auto* e = new gg_engine();
@@ -1366,11 +1376,17 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     dfree(e->d_nmeta);
     dfree(e->d_pend);
     dfree(e->d_pend_src);
+    for (int b = 0; b < 2; ++b) dfree(e->d_bset[b]);
     if (e->cfg.batch_ticks) {
         HIPCHK(hipMalloc(&e->d_pend, e->rows * e->nwp * 8));
         HIPCHK(hipMalloc(&e->d_pend_src, e->rows * 4));
+        if (e->cfg.enable_sync)  // every node writes its set of round r into d_bset[r & 1]
+            for (int b = 0; b < 2; ++b) {
+                HIPCHK(hipMalloc(&e->d_bset[b], e->rows * e->nwp * 8));
+                HIPCHK(hipMemset(e->d_bset[b], 0, e->rows * e->nwp * 8));
+            }
     }
-    if (e->cfg.enable_sync && (e->n_hubs == 0 || e->symmetric) && !e->sync_tiles && n_own) {
+    if (e->cfg.enable_sync && !e->cfg.batch_ticks && (e->n_hubs == 0 || e->symmetric) && !e->sync_tiles && n_own) {
         HIPCHK(hipMalloc(&e->d_srec, 2 * n_own * sizeof(uint4)));
         HIPCHK(hipMalloc(&e->d_sstate, e->rows));
         HIPCHK(hipMalloc(&e->d_ibits, e->rows / 8));
@@ -1993,7 +2009,6 @@ int gg_topology_export(gg_engine* e, int64_t* row_ptr, int32_t* col, uint64_t ca
 }
 
 static int add_window(gg_engine* e, int64_t a, int64_t b, Window&& w) {
-    if (e->cfg.batch_ticks) return e->fail(GG_EINVAL, "batched gossip has no partition windows");
     if (a >= b) return e->fail(GG_EINVAL, "empty partition window");
     for (const auto& x : e->windows)  // per-edge windows may overlap group windows (and win)
         if (x.edges == w.edges && a < x.to && x.from < b) return e->fail(GG_EINVAL, "overlapping partition windows");

@@ -156,6 +156,9 @@ struct RoundArgs {
     unsigned long long* tot;    // [4] ring: new bits of the owned nodes in rounds <= r (slot r&3), or nullptr
     unsigned long long full_new;  // n_own x lanes injected in rounds <= r-1: tot of r-1 equal to it means
                                   // every owned set holds every injected lane (sets hold injected lanes only)
+    uint32_t lanes_prev;        // lanes of this engine injected in rounds <= r-1 (0: none yet). A node whose
+                                // set holds that many lanes is saturated: sender rows of r-1 carry only
+                                // those lanes, so it has nothing to gather (expand_stream1)
     // hubs (lean rounds): owned nodes with in-degree > hub_deg skip expand_stream
     // and take hub_chunks + hub_finish; senders with out-degree > hub_deg are
     // marked by hub_mark instead of round_prep (0: no hubs)
@@ -190,6 +193,8 @@ struct RoundArgs {
     uint32_t* pend_src;         // batched gossip: [rows] kPendNone, kPendMixed, or the only
                                 // sender's local row | in-edge reciprocal bit << 31
     uint32_t batch_tick;        // batched gossip: this round ends with a send
+    const uint64_t* bset_prev;  // batched gossip with sync: [rows][nwp] every node's set after r-1
+    uint64_t* bset_cur;         // (read by push receivers and callbacks), and after r (written by all)
     int32_t* dr;                // batched gossip: first-seen rounds [n_own][dr_w] (GG_TRACK_DELIVERY), or nullptr
     uint32_t dr_w;
     uint2* nmeta;               // streamed sync rounds: compact_round's node list as (node,
@@ -1585,8 +1590,14 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         // rows written this round are read next round from HBM anyway (F by
         // other nodes' gathers, base by this node): streamed past the caches,
         // they leave L2 to the gathers (C2 -2.5%, C3 -1.4% kernel time)
-        if (any || zm) store_row_nt(a.F_cur + rep * a.nwp + off, F);
-        if (any) store_row_nt(a.base + rep * a.nwp + off, S);
+        // per lane, only the 16-byte chunks that changed: a chunk without new bits
+        // keeps its base bytes, and its F bytes are already zero unless the node's
+        // F row of round r-2 sits in this buffer (zm: then every chunk is written).
+        // While most nodes learn a few of W values (C2 rounds 10-13: 15-66 % of
+        // the chunks change) this drops most of the row stores of a dense round
+        const bool lane_new = (F.w[0] | F.w[1]) != 0;
+        if (lane_new || zm) store_row_nt(a.F_cur + rep * a.nwp + off, F);
+        if (lane_new) store_row_nt(a.base + rep * a.nwp + off, S);
         if (lg == 0) {
             if (any || m0.fl) a.flg_cur[rep] = any ? FL_ACT : 0;
             if (m0.ca) a.cand[rep] = 0;
@@ -1608,8 +1619,9 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             // row_ptr + cand + flag bytes + col (+ a sender bit, flags-first), own row + gathered
             // sender rows, F / base / flag writes
             c_bytes += (dense ? 0 : 4) + 8 + 2 + 4 * nin + (ff ? (nin + 7) / 8 : 0) + (full ? 0 : rowb) +
-                       ((any || zm) ? rowb : 0) + (any ? rowb + 1 : 0);
+                       (any ? 1 : 0);
         }
+        c_bytes += ((lane_new || zm) ? 16 : 0) + (lane_new ? 16 : 0);  // this lane's F / base chunk stores
         }  // !hub
         m0 = m1;
         m1 = m2;
@@ -1676,8 +1688,14 @@ void expand_stream1(RoundArgs a) {
     const uint32_t stride = gridDim.x * kBlock;
     const bool full = all_full(a);  // nothing can arrive: no gathers, no own rows
 
+    // the own row rides with the row pointers, two items ahead: a saturated node
+    // (its set holds every lane injected through r-1) gathers nothing and reads no
+    // columns. C5's last dense rounds deliver a few bits to few nodes while most
+    // sets are already full (2^26 nodes: 19·10^6 and 44 new bits in rounds 14 and
+    // 15, each a full 3.2 ms pass before)
     struct Meta {
         int64_t p0;
+        uint64_t own;
         uint32_t deg, node;
         uint8_t ca, fl;
     };
@@ -1693,13 +1711,16 @@ void expand_stream1(RoundArgs a) {
             m.deg = (uint32_t)(a.in_ptr[n + 1] - m.p0);
             m.ca = a.cand[a.own0 + n];
             m.fl = a.flg_cur[a.own0 + n];
+            m.own = full ? 0ull : a.base[a.own0 + n];
             if (full) m.deg = 0;
-            if (a.hub_deg && m.deg > a.hub_deg) {
+            if (a.hub_deg && m.deg > a.hub_deg) {  // hub_chunks / hub_finish take it
                 m.node |= kHubBit;
                 m.deg = 0;
             }
+            if (a.lanes_prev && (uint32_t)__popcll(m.own) == a.lanes_prev) m.deg = 0;  // saturated
         } else {
             m.p0 = 0;
+            m.own = 0;
             m.deg = 0;
             m.ca = m.fl = 0;
         }
@@ -1722,8 +1743,8 @@ void expand_stream1(RoundArgs a) {
         const uint64_t i = m0.node & ~kHubBit;
         const uint64_t rep = a.own0 + i;
         // (a) own row and the first D sender rows
-        uint64_t sp = 0, src[D];
-        if (!hub && !full) sp = a.base[rep];
+        const uint64_t sp = m0.own;
+        uint64_t src[D];
 #pragma unroll
         for (int b = 0; b < D; ++b) src[b] = ((uint32_t)b < m0.deg) ? a.F_prev[c0[b] & kColMask] : 0ull;
         // (b) prefetch the next items' columns, row pointers and list entry
@@ -2292,14 +2313,21 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
 
 // ---------------------------------------------------------------------------
 // Batched gossip (gg_config.batch_ticks; new semantics, DESIGN.md §2b — not the
-// parity path): every node, every round. G lanes per node: own set, client
-// broadcasts, the batches its in-neighbours sent last round (their F rows,
-// ascending sender), new values into the pending row; at a send tick the
+// parity path; message-level restatement oracle/o1_batched.py, bitset one
+// O2 compute_round_batched): every node, every round. G lanes per node: own set,
+// client broadcasts, the messages its in-neighbours sent last round and no
+// partition window dropped (their batch = F row, and on a push edge their whole
+// set of r-1: the push carried every value the sender held that this node's
+// read_ok lacked, ascending sender), the read_oks of a sync callback (peers'
+// sets of r-1, ascending) followed by one push per such peer when S & ~R is not
+// empty; new values into the pending row; the sync timer; at a send tick the
 // pending row becomes the node's F row (its batch, read by its out-neighbours
-// next round) and one message per out-neighbour is counted, minus one when a
-// single reciprocal neighbour delivered every pending value (the message to it
-// would be empty). F rows are rewritten only when they change (flags: a batch
-// sent two rounds ago in this buffer).
+// next round) and one message per out-neighbour is counted, except to the one
+// neighbour that delivered every pending value (the message to it would be
+// empty). F rows are rewritten only when they change (flags: a batch sent two
+// rounds ago in this buffer). With sync, sets are also double-buffered
+// (bset_prev / bset_cur): pushes and read_oks carry sets of r-1 while nodes
+// update theirs in place.
 constexpr uint32_t kPendNone = ~0u, kPendMixed = ~0u - 1;
 template <int G, int WPL>
 __global__ __launch_bounds__(kBlock) void expand_batched(RoundArgs a) {
@@ -2310,10 +2338,17 @@ __global__ __launch_bounds__(kBlock) void expand_batched(RoundArgs a) {
     const int gshift = (threadIdx.x & 63) / G * G;
     const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
     auto group_any = [&](bool x) { return ((__ballot(x) >> gshift) & gmask) != 0; };
+    const bool sync = a.enable_sync && a.bset_prev != nullptr;
+    bool win = false;  // some partition window covers r-3 .. r+1
+#pragma unroll
+    for (int k = 0; k < 5; ++k) win |= a.grp[k] != nullptr;
     uint32_t c_new = 0, c_active = 0, c_nact = 0;
-    unsigned long long c_msgs = 0, c_hash = 0, c_bytes = 0, c_gathers = 0;
+    unsigned long long c_msgs = 0, c_deliv = 0, c_hash = 0, c_bytes = 0, c_gathers = 0;
+    unsigned long long c_push = 0, c_push_deliv = 0, c_ackdrop = 0, c_dropped = 0;
+    unsigned long long c_reads = 0, c_read_oks = 0, c_fired = 0;
     const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
     const uint64_t first = (uint64_t)blockIdx.x * (kBlock / G) + threadIdx.x / G;
+    const unsigned long long rowb = 8ull * a.nwp;
     // whole groups run the loop together (the group's node, or past the end)
     const uint64_t bound = (a.n_own + ngroups - 1) / ngroups * ngroups;  // same trip count for every group
     for (uint64_t i = first; i < bound; i += ngroups) {
@@ -2330,6 +2365,9 @@ __global__ __launch_bounds__(kBlock) void expand_batched(RoundArgs a) {
             for (int w = 0; w < WPL; ++w) S.w[w] = P.w[w] = 0;
         }
         sp = S;
+        auto deliver = [&](uint32_t d) {  // d: local row | kRecipBit when d is an out-neighbour
+            src = src == kPendNone ? d : ((src != kPendMixed && (src & kColMask) == (d & kColMask)) ? src : kPendMixed);
+        };
         // (1) client broadcasts: a new client value goes to every neighbour
         bool inj_new = false;
         if (valid && (a.cand[rep] & CA_INJ)) {
@@ -2356,11 +2394,24 @@ __global__ __launch_bounds__(kBlock) void expand_batched(RoundArgs a) {
             }
         }
         if (group_any(inj_new)) src = kPendMixed;
-        // (2) last round's batches, ascending sender
+        // (2) last round's batches and pushes, ascending sender
         const int64_t p0 = valid ? a.in_ptr[i] : 0, p1 = valid ? a.in_ptr[i + 1] : 0;
         for (int64_t e = p0; e < p1; ++e) {
             const uint32_t c = a.in_col[e];
-            const Row<WPL> x = load_row<WPL>(a.F_prev + (uint64_t)(c & kColMask) * a.nwp + off);
+            const uint64_t u = c & kColMask;
+            if (sync && bit_at(a.fired_m1, u) && !masked<true>(a, 2, u, rep, e)) {  // u's read, answered now
+                c_read_oks++;
+                if (masked<true>(a, 3, rep, u, e)) c_dropped++;
+            }
+            if (win && masked<true>(a, 2, u, rep, e)) continue;  // dropped in flight (r-1)
+            const bool push = sync && bit_at(a.fired_m3, u) && !masked<true>(a, 0, u, rep, e) &&
+                              !masked<true>(a, 1, rep, u, e);
+            Row<WPL> x = load_row<WPL>(a.F_prev + u * a.nwp + off);
+            if (push) {
+                const Row<WPL> y = load_row<WPL>(a.bset_prev + u * a.nwp + off);
+#pragma unroll
+                for (int w = 0; w < WPL; ++w) x.w[w] |= y.w[w];
+            }
             bool got = false;
 #pragma unroll
             for (int w = 0; w < WPL; ++w) {
@@ -2368,9 +2419,40 @@ __global__ __launch_bounds__(kBlock) void expand_batched(RoundArgs a) {
                 S.w[w] |= cw;
                 got |= cw != 0;
             }
-            if (group_any(got)) {
-                const uint32_t u = (c & kColMask) | (c & kRecipBit);
-                src = src == kPendNone ? u : ((src != kPendMixed && (src & kColMask) == (c & kColMask)) ? src : kPendMixed);
+            if (group_any(got)) deliver((uint32_t)u | (c & kRecipBit));
+            c_gathers += push ? 2 : 1;
+        }
+        // (3) sync callback (fired in r-2): read_oks of the peers ascending, then one push each
+        const int64_t o0 = valid ? a.out_ptr[i] : 0, o1 = valid ? a.out_ptr[i + 1] : 0;
+        if (sync && valid && bit_at(a.fired_m2, rep)) {
+            for (int pass = 0; pass < 2; ++pass) {
+                for (int64_t e = o0; e < o1; ++e) {
+                    const uint64_t w = a.out_col[e] & kColMask;
+                    if (masked<true>(a, 1, rep, w, e) || masked<true>(a, 2, w, rep, e)) continue;
+                    const Row<WPL> R = load_row<WPL>(a.bset_prev + w * a.nwp + off);
+                    c_gathers++;
+                    if (pass == 0) {
+                        bool got = false;
+#pragma unroll
+                        for (int q = 0; q < WPL; ++q) {
+                            got |= (R.w[q] & ~S.w[q]) != 0;
+                            S.w[q] |= R.w[q];
+                        }
+                        if (group_any(got)) deliver((uint32_t)w | kRecipBit);
+                    } else {
+                        bool any = false;
+#pragma unroll
+                        for (int q = 0; q < WPL; ++q) any |= (S.w[q] & ~R.w[q]) != 0;
+                        if (!group_any(any)) continue;
+                        c_push++;
+                        if (masked<true>(a, 3, rep, w, e)) {
+                            c_dropped++;
+                        } else {
+                            c_push_deliv++;
+                            if (masked<true>(a, 4, w, rep, e)) c_ackdrop++;
+                        }
+                    }
+                }
             }
         }
         // new state
@@ -2398,6 +2480,7 @@ __global__ __launch_bounds__(kBlock) void expand_batched(RoundArgs a) {
         const bool send = a.batch_tick && group_any(pend_any);
         if (valid) {
             if (any) store_row<WPL>(a.base + rep * a.nwp + off, S);
+            if (sync) store_row<WPL>(a.bset_cur + rep * a.nwp + off, S);
             const uint8_t fl = a.flg_cur[rep];  // a batch of round r-2 in this F buffer
             if (send || (fl & FL_ACT)) {
                 Row<WPL> out;
@@ -2413,20 +2496,43 @@ __global__ __launch_bounds__(kBlock) void expand_batched(RoundArgs a) {
             if (lg == 0) {
                 if (send || fl) a.flg_cur[rep] = send ? FL_ACT : 0;
                 if (a.cand[rep]) a.cand[rep] = 0;
-                unsigned long long msgs = 0;
-                if (send) {
-                    msgs = (unsigned long long)(a.out_ptr[i + 1] - a.out_ptr[i]);
-                    // one reciprocal neighbour delivered every pending value: no message to it
-                    if (src != kPendMixed && src != kPendNone && (src & kRecipBit)) msgs--;
+                const uint64_t deg = (uint64_t)(o1 - o0);
+                // (5) the sync timer (main.go:42-51): a read to every neighbour
+                if (sync && (int64_t)a.sync_next[i] == a.round) {
+                    c_fired++;
+                    c_reads += deg;
+                    if (win)
+                        for (int64_t e = o0; e < o1; ++e)
+                            if (masked<true>(a, 3, rep, a.out_col[e] & kColMask, e)) c_dropped++;
+                    atomicOr(a.fired_cur + (rep >> 6), 1ull << (rep & 63));
+                    const uint32_t kk = a.sync_k[i] + 1;
+                    a.sync_k[i] = kk;
+                    a.sync_next[i] = (int32_t)(a.round + gg_sync_interval(a.seed, g, kk, a.sync_base, a.sync_jitter));
+                }
+                // (6) the batch: one message per out-neighbour but the single deliverer
+                const bool single = src != kPendMixed && src != kPendNone;
+                if (send && !win) {
+                    const unsigned long long msgs = deg - ((single && (src & kRecipBit)) ? 1 : 0);
+                    c_msgs += msgs;
+                    c_deliv += msgs;
+                } else if (send) {
+                    for (int64_t e = o0; e < o1; ++e) {
+                        const uint64_t w = a.out_col[e] & kColMask;
+                        if (single && (src & kColMask) == (uint32_t)w) continue;
+                        c_msgs++;
+                        if (masked<true>(a, 3, rep, w, e)) {
+                            c_dropped++;
+                        } else {
+                            c_deliv++;
+                            if (masked<true>(a, 4, w, rep, e)) c_ackdrop++;
+                        }
+                    }
                 }
                 const uint32_t nsrc = a.batch_tick ? kPendNone : src;
                 if (nsrc != a.pend_src[rep]) a.pend_src[rep] = nsrc;
-                c_msgs += msgs;
                 c_active += 1;
                 c_nact += send ? 1u : 0u;
-                c_gathers += (unsigned long long)(p1 - p0);
-                const unsigned long long rowb = 8ull * a.nwp;
-                c_bytes += 16 + 4ull * (p1 - p0) + rowb * (2 + (p1 - p0)) + (any ? rowb : 0) +
+                c_bytes += 16 + 4ull * (p1 - p0) + rowb * 2 + (any ? rowb : 0) + (sync ? rowb : 0) +
                            ((send || (fl & FL_ACT)) ? rowb : 0) + ((any || send) ? rowb : 0);
             }
             c_new += T;
@@ -2435,15 +2541,25 @@ __global__ __launch_bounds__(kBlock) void expand_batched(RoundArgs a) {
     unsigned long long acc[C_NUM];
 #pragma unroll
     for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
+    if (lg != 0) {  // per-message counts were taken once per node group (lane 0) or by every lane
+        c_push = c_push_deliv = c_ackdrop = c_dropped = c_read_oks = 0;
+    }
     acc[C_NEW] = c_new;
     acc[C_FWD_SENT] = c_msgs;
-    acc[C_FWD_DELIV] = c_msgs;
-    acc[C_NEXT_ACKS] = c_msgs;
+    acc[C_FWD_DELIV] = c_deliv;
+    acc[C_PUSH] = c_push;
+    acc[C_PUSH_DELIV] = c_push_deliv;
+    acc[C_NEXT_ACKS] = c_deliv + c_push_deliv;
+    acc[C_NEXT_ACKDROP] = c_ackdrop;
+    acc[C_DROPPED] = c_dropped;
+    acc[C_READS] = c_reads;
+    acc[C_READ_OKS] = c_read_oks;
+    acc[C_FIRED] = c_fired;
     acc[C_HASH] = c_hash;
     acc[C_ACTIVE] = c_active;
-    acc[C_GATHERS] = c_gathers;
+    acc[C_GATHERS] = c_gathers * (lg == 0 ? 1 : 0);
     acc[C_NACT] = c_nact;
-    acc[C_BYTES] = c_bytes;
+    acc[C_BYTES] = c_bytes + (lg == 0 ? c_gathers * rowb : 0);
     flush_counters(a, acc, s_red, t_start, K_STREAM);
 }
 

@@ -90,7 +90,10 @@ typedef struct {
                                    (r+1) % B == 0, sends ONE `broadcast` message per out-neighbour
                                    carrying its pending values (none to a neighbour that delivered all
                                    of them first); fwd_sent/fwd_delivered/acks count messages, not
-                                   values. Single engine, no sync timers, no partition windows. */
+                                   values. Sync timers: the read_ok callback adds what it lacked to
+                                   the pending values and sends each peer one push with everything the
+                                   peer's reply lacked; partition windows drop batches as in parity
+                                   mode. Single engine (world == 1). */
 } gg_config;
 
 typedef struct {

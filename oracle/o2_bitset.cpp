@@ -178,22 +178,32 @@ struct gg_engine {
 };
 
 // Batched gossip (gg_config.batch_ticks = B >= 1; new semantics, not the
-// reference's): per node v in round r, (1) client broadcasts, (2) the batches
-// sent to v in r-1, ascending sender (a value's first deliverer is its
-// claimer), new values join v's pending set P; at the end of a round with
+// reference's; message-level restatement: oracle/o1_batched.py): per node v in
+// round r, (1) client broadcasts, (2) the messages sent to v in r-1 and not
+// dropped, ascending sender: the sender's batch (its F row of r-1) and, on a
+// push edge, its push (its whole set after r-1: the push carried every value it
+// held that v's read_ok of r-2 lacked, and v's set has grown past that reply);
+// a value's first deliverer is its claimer and new values join v's pending set
+// P; (3) if v's timer fired in r-2, the read_oks of its peers, ascending (sent
+// in r-1 with the peer's set after r-1): new values join S and P (deliverer:
+// the peer); then one push per such peer carrying S & ~R if not empty; (5) the
+// timer (reads to every neighbour); (6) at the end of a round with
 // (r+1) % B == 0, v sends P to every out-neighbour w in one message, except to
-// a w that delivered every value of P first (the message would
-// be empty: rebroadcastAllExcept's exclusion, per batch). pend_src tracks that:
-// kNone (P empty), kMixed (several deliverers or a client), or the one sender.
+// a w that delivered every value of P first (rebroadcastAllExcept's exclusion,
+// per batch). pend_src tracks that: kNone (P empty), kMixed (several
+// deliverers or a client), or the one deliverer. Partition windows drop
+// messages as in parity mode; every delivered message is acked.
 void gg_engine::compute_round_batched(Acc& a) {
     constexpr uint32_t kNone = ~0u, kMixed = ~0u - 1;
     const int64_t r = round;
     const uint64_t n_own = hi - lo;
+    const bool sync = cfg.enable_sync != 0;
     const uint32_t W = (uint32_t)(nw * 64);
     std::vector<uint64_t>& sp_all = seen[(r + 1) & 1];
     std::vector<uint64_t>& sc_all = seen[r & 1];
     std::vector<uint64_t>& Fp_all = F[(r + 1) & 1];
     std::vector<uint64_t>& Fc_all = F[r & 1];
+    std::fill(fired[r & 3].begin(), fired[r & 3].end(), 0ull);
     std::unordered_map<uint32_t, std::vector<uint32_t>> inj_by_node;
     {
         auto it = inj.find(r);
@@ -204,10 +214,12 @@ void gg_engine::compute_round_batched(Acc& a) {
     }
     const bool tick = (r + 1) % (int64_t)cfg.batch_ticks == 0;
     std::vector<uint64_t> S(nw), sp(nw);
+    std::vector<uint64_t> firedw;
     for (uint64_t i = 0; i < n_own; ++i) {
         const uint64_t g = lo + i;
         for (uint64_t j = 0; j < nw; ++j) sp[j] = S[j] = sp_all[i * nw + j];
         uint32_t& src = pend_src[i];
+        auto deliver = [&](uint32_t d) { src = src == kNone ? d : (src == d ? src : kMixed); };
         auto ij = inj_by_node.find((uint32_t)g);  // (1) client broadcasts
         if (ij != inj_by_node.end())
             for (uint32_t lane : ij->second) {
@@ -215,16 +227,51 @@ void gg_engine::compute_round_batched(Acc& a) {
                 if (!(S[lane >> 6] & b)) src = kMixed;  // a client value goes to every neighbour
                 S[lane >> 6] |= b;
             }
-        for (int64_t e = in_ptr[i]; e < in_ptr[i + 1]; ++e) {  // (2) batches, ascending sender
+        for (int64_t e = in_ptr[i]; e < in_ptr[i + 1]; ++e) {  // (2) batches and pushes, ascending sender
             const uint64_t u = in_col[e];
+            if (sync && fired_at(r - 1, u) && !masked(r - 1, u, g)) {  // u's read arrives, read_ok sent now
+                a.read_oks++;
+                if (masked(r, g, u)) a.node_dropped++;
+            }
+            if (masked(r - 1, u, g)) continue;  // dropped in flight
+            const bool push = sync && fired_at(r - 3, u) && !masked(r - 3, u, g) && !masked(r - 2, g, u);
             const uint64_t* x = &Fp_all[u * nw];
+            const uint64_t* y = &sp_all[u * nw];
             bool got = false;
             for (uint64_t j = 0; j < nw; ++j) {
-                const uint64_t c = x[j] & ~S[j];
+                const uint64_t c = (x[j] | (push ? y[j] : 0ull)) & ~S[j];
                 S[j] |= c;
                 got |= c != 0;
             }
-            if (got) src = src == kNone ? (uint32_t)u : (src == (uint32_t)u ? src : kMixed);
+            if (got) deliver((uint32_t)u);
+        }
+        if (sync && fired_at(r - 2, g)) {  // (3) read_ok callbacks, ascending peer, then the pushes
+            for (int pass = 0; pass < 2; ++pass)
+                for (int64_t e = out_ptr[i]; e < out_ptr[i + 1]; ++e) {
+                    const uint64_t w = out_col[e];
+                    if (masked(r - 2, g, w) || masked(r - 1, w, g)) continue;
+                    const uint64_t* R = &sp_all[w * nw];
+                    if (pass == 0) {
+                        bool got = false;
+                        for (uint64_t j = 0; j < nw; ++j) {
+                            got |= (R[j] & ~S[j]) != 0;
+                            S[j] |= R[j];
+                        }
+                        if (got) deliver((uint32_t)w);
+                    } else {
+                        bool any = false;
+                        for (uint64_t j = 0; j < nw; ++j) any |= (S[j] & ~R[j]) != 0;
+                        if (!any) continue;
+                        a.pushes++;
+                        if (masked(r, g, w)) {
+                            a.dropped++;
+                        } else {
+                            a.push_deliv++;
+                            a.next_acks++;
+                            if (masked(r + 1, w, g)) a.next_ackdrop++;
+                        }
+                    }
+                }
         }
         uint64_t* sc = &sc_all[i * nw];
         uint64_t* fc = &Fc_all[i * nw];
@@ -247,15 +294,30 @@ void gg_engine::compute_round_batched(Acc& a) {
             pend_any |= P[j] != 0;
             fc[j] = 0;
         }
-        if (tick) {
+        const uint64_t deg = (uint64_t)(out_ptr[i + 1] - out_ptr[i]);
+        if (sync && r == sync_next[i]) {  // (5) sync timer: read RPC to every neighbour
+            a.fired++;
+            a.reads += deg;
+            for (int64_t e = out_ptr[i]; e < out_ptr[i + 1]; ++e)
+                if (masked(r, g, out_col[e])) a.node_dropped++;
+            firedw.push_back(g);
+            sync_k[i]++;
+            sync_next[i] = r + gg_sync_interval(cfg.seed, g, sync_k[i], cfg.sync_base_ticks, cfg.sync_jitter_ticks);
+        }
+        if (tick) {  // (6) the batch
             if (pend_any) {
-                uint64_t msgs = (uint64_t)(out_ptr[i + 1] - out_ptr[i]);
-                if (src != kMixed && src != kNone &&
-                    std::binary_search(out_col.begin() + out_ptr[i], out_col.begin() + out_ptr[i + 1], src))
-                    msgs--;  // that neighbour delivered every pending value: no message to it
-                a.fwd_sent += msgs;
-                a.fwd_deliv += msgs;
-                a.next_acks += msgs;
+                for (int64_t e = out_ptr[i]; e < out_ptr[i + 1]; ++e) {
+                    const uint64_t w = out_col[e];
+                    if (src == (uint32_t)w) continue;  // w delivered every pending value: no message
+                    a.fwd_sent++;
+                    if (masked(r, g, w)) {
+                        a.dropped++;
+                    } else {
+                        a.fwd_deliv++;
+                        a.next_acks++;
+                        if (masked(r + 1, w, g)) a.next_ackdrop++;
+                    }
+                }
                 for (uint64_t j = 0; j < nw; ++j) {
                     fc[j] = P[j];
                     P[j] = 0;
@@ -264,6 +326,9 @@ void gg_engine::compute_round_batched(Acc& a) {
             src = kNone;
         }
     }
+    a.dropped += a.node_dropped;
+    a.node_dropped = 0;
+    for (uint64_t g : firedw) fired[r & 3][g >> 6] |= 1ull << (g & 63);
 }
 
 void gg_engine::compute_round(Acc& total) {
@@ -452,7 +517,7 @@ int gg_create(const gg_config* cfg, gg_engine** out) {
     const uint32_t L = cfg->lane_groups ? cfg->lane_groups : 1u;
     if (cfg->world % L || L > cfg->n_lanes / 64) return GG_EINVAL;
     if (cfg->world / L > 63) return GG_EINVAL;  // the HIP engine's exchange limit (same ABI)
-    if (cfg->batch_ticks && (cfg->enable_sync || cfg->world != 1)) return GG_EINVAL;  // batched: single, no sync
+    if (cfg->batch_ticks && cfg->world != 1) return GG_EINVAL;  // batched gossip: one engine
     auto* e = new gg_engine();
     e->cfg = *cfg;
     e->V = cfg->n_nodes;
@@ -570,7 +635,6 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
 
 static int add_window(gg_engine* e, int64_t a, int64_t b, Window&& w) {
     if (!e) return GG_EINVAL;
-    if (e->cfg.batch_ticks) return e->fail(GG_EINVAL, "batched gossip has no partition windows");
     if (a >= b) return e->fail(GG_EINVAL, "empty partition window");
     for (const auto& x : e->windows)  // per-edge windows may overlap group windows (and win)
         if (x.edges == w.edges && a < x.to && x.from < b) return e->fail(GG_EINVAL, "overlapping partition windows");

@@ -131,14 +131,92 @@ def test_batched_fewer_messages_than_parity(cpu_lib):
 
 def test_batched_config_rules(cpu_lib):
     with pytest.raises(GGError):
-        Engine(10, 64, batch_ticks=2, enable_sync=True, library=cpu_lib)
-    with pytest.raises(GGError):
         Engine(10, 64, batch_ticks=2, enable_sync=False, world=2, library=cpu_lib)
-    e = Engine(10, 64, batch_ticks=2, enable_sync=False, library=cpu_lib)
+    # sync timers and partition windows are part of batched mode
+    e = Engine(10, 64, batch_ticks=2, enable_sync=True, library=cpu_lib)
     from ggamd import topology as T
     e.topology(T.tree(10, 2))
-    with pytest.raises(GGError):
-        e.partition_seeded(1, 3, 5)
+    e.partition_seeded(1, 3, 5)
+
+
+def make_o1b(sc: Scenario, B: int):
+    from oracle.o1_batched import O1Batched
+    from helpers import apply
+    o = O1Batched(sc.topo.n_nodes, sc.W, sc.seed, sc.sync_base, sc.sync_jitter, sc.enable_sync, batch_ticks=B)
+    apply(o, sc)
+    return o
+
+
+def _check_vs_o1b(lib, sc, B, **kw):
+    o = make_o1b(sc, B)
+    e = make_engine(lib, sc, batch_ticks=B, **kw)
+    ref, got = o.step(sc.rounds), e.step(sc.rounds)
+    for k, (a, b) in enumerate(zip(ref, got)):
+        for f, v in a.items():
+            assert b[f] == v, (B, k, f, b[f], v)
+    for v in range(sc.topo.n_nodes):
+        assert e.read(v) == o.read(v), v
+    dr = e.delivery_rounds()
+    for (v, val), r in o.first_seen.items():
+        assert dr[v][e.lane_of(val)] == r
+
+
+@pytest.mark.parametrize("B", [1, 2, 3])
+def test_o1_batched_equals_message_level(B):
+    """O1B (oracle/o1_batched.py, the handlers with batched sends) against the
+    independent per-value restatement above, where both apply: no sync, no windows."""
+    for sc in _scenarios(300 + B):
+        ref, reads, first = batched_reference(sc, B)
+        sc.enable_sync = False
+        o = make_o1b(sc, B)
+        got = o.step(sc.rounds)
+        for k, (a, b) in enumerate(zip(ref, got)):
+            for f, v in a.items():
+                assert b[f] == v, (B, k, f, b[f], v)
+        assert [o.read(v) for v in range(sc.topo.n_nodes)] == reads
+        assert o.first_seen == first
+
+
+def _sync_scenarios(seed, n=8, W=128):
+    """random graphs (directed links included), sync timers from round 1-6,
+    seeded and explicit partition windows; every third one symmetric with
+    per-edge windows (gg_set_partition) over its group windows"""
+    from helpers import symmetric_random_scenario
+    rnd = random.Random(seed)
+    out = []
+    for k in range(n):
+        if k % 3 == 2:
+            sc = symmetric_random_scenario(rnd, max_v=24, W=W, rounds=40)
+        else:
+            sc = random_scenario(rnd, max_v=24, W=W, rounds=40)
+        sc.enable_sync = True
+        sc.injections = [(nd, v, rnd.randrange(0, 12)) for nd, v, _ in sc.injections]
+        out.append(sc)
+    return out
+
+
+@pytest.mark.parametrize("B", [1, 2, 3])
+def test_o2_batched_sync_partitions_equal_o1b(cpu_lib, B):
+    for sc in _sync_scenarios(400 + B):
+        _check_vs_o1b(cpu_lib, sc, B)
+
+
+def test_batched_c1_bisection_loses_nothing(cpu_lib):
+    """C1 (25-node tree4, the reference's Maelstrom setting) with a seeded
+    bisection window, batched at B = 2 with sync on: every value reaches every
+    node (the partition drops batches; the sync pushes repair them), and O2
+    equals O1B message for message."""
+    from ggamd.workload import c1
+    wl, _ = c1(partition=True)
+    sc = Scenario(wl.topo, wl.n_lanes, wl.max_rounds, list(wl.injections), seed=wl.seed,
+                  enable_sync=True, windows=list(wl.windows))
+    _check_vs_o1b(cpu_lib, sc, 2)
+    e = make_engine(cpu_lib, sc, batch_ticks=2)
+    st = e.step(sc.rounds)
+    assert sum(s["dropped"] for s in st) > 0  # the window cut something
+    vals = sorted({v for _, v, _ in sc.injections})
+    for v in range(sc.topo.n_nodes):
+        assert e.read(v) == vals
 
 
 @pytest.mark.gpu
@@ -162,3 +240,35 @@ def test_hip_batched_equals_o2(hip_lib, cpu_lib, W, B):
         assert not d, d[:10]
         assert np.array_equal(g.read_bits(), c.read_bits())
         assert np.array_equal(g.delivery_rounds(), c.delivery_rounds())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W", [64, 128, 512])
+@pytest.mark.parametrize("B", [1, 2, 3])
+def test_hip_batched_sync_partitions_equal_o2(hip_lib, cpu_lib, W, B):
+    """HIP batched rounds with sync timers, pushes, callbacks and partition
+    windows (seeded, explicit groups) against O2 (pinned to O1B above)."""
+    from helpers import diff_stats
+    for sc in _sync_scenarios(500 + W + B, n=6, W=W):
+        g = make_engine(hip_lib, sc, batch_ticks=B, device=0)
+        c = make_engine(cpu_lib, sc, batch_ticks=B)
+        gs, cs = g.step(sc.rounds), c.step(sc.rounds)
+        d = diff_stats(gs, cs)
+        assert not d, d[:10]
+        assert np.array_equal(g.read_bits(), c.read_bits())
+        assert np.array_equal(g.delivery_rounds(), c.delivery_rounds())
+
+
+@pytest.mark.gpu
+def test_hip_batched_c1_bisection_equals_o2(hip_lib, cpu_lib):
+    from helpers import diff_stats
+    from ggamd.workload import c1
+    wl, _ = c1(partition=True)
+    sc = Scenario(wl.topo, wl.n_lanes, wl.max_rounds, list(wl.injections), seed=wl.seed,
+                  enable_sync=True, windows=list(wl.windows))
+    for B in (1, 2, 5):
+        g = make_engine(hip_lib, sc, batch_ticks=B, device=0)
+        c = make_engine(cpu_lib, sc, batch_ticks=B)
+        d = diff_stats(g.step(sc.rounds), c.step(sc.rounds))
+        assert not d, (B, d[:10])
+        assert np.array_equal(g.read_bits(), c.read_bits())

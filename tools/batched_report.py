@@ -23,19 +23,24 @@ ap.add_argument("--json")
 args = ap.parse_args()
 lib = os.path.join(REPO, "oracle", "_build", "libgossip_cpu.so") if args.cpu else None
 dev = -1 if args.cpu else 0
-wl, nreads = c1(partition=False)
 rows = {}
-e = Engine(25, wl.n_lanes, seed=wl.seed, track_delivery=True, library=lib, device=dev)
-wl.apply(e)
-rows["parity (sync on)"] = broadcast_report(e, wl.injections, nreads, e.step(wl.max_rounds))
-for B in [int(x) for x in args.ticks.split(",")]:
-    e = Engine(25, wl.n_lanes, seed=wl.seed, track_delivery=True, library=lib, device=dev, enable_sync=False,
-               batch_ticks=B)
+for part in (False, True):
+    wl, nreads = c1(partition=part)
+    tag = " + bisection [50,100)" if part else ""
+    e = Engine(25, wl.n_lanes, seed=wl.seed, track_delivery=True, library=lib, device=dev)
     wl.apply(e)
-    rows[f"batched B={B} ({B * 100} ms)"] = broadcast_report(e, wl.injections, nreads, e.step(wl.max_rounds))
+    rows[f"parity (sync on){tag}"] = broadcast_report(e, wl.injections, nreads, e.step(wl.max_rounds))
+    # batched without sync loses what a partition drops; with sync the pushes repair it
+    for sync in ((False, True) if part else (False,)):
+        for B in [int(x) for x in args.ticks.split(",")]:
+            e = Engine(25, wl.n_lanes, seed=wl.seed, track_delivery=True, library=lib, device=dev,
+                       enable_sync=sync, batch_ticks=B)
+            wl.apply(e)
+            rows[f"batched B={B} ({B * 100} ms), sync {'on' if sync else 'off'}{tag}"] = broadcast_report(
+                e, wl.injections, nreads, e.step(wl.max_rounds))
 for name, r in rows.items():
     lat = r["stable_latency_ms"]
-    print(f"{name:28s} msgs/op {r['msgs_per_op']:6.2f}  latency median {lat['median']:6.0f} ms  "
+    print(f"{name:58s} msgs/op {r['msgs_per_op']:6.2f}  latency median {lat['median']:6.0f} ms  "
           f"max {lat['max']:6.0f} ms  lost {len(r['lost'])}", flush=True)
 print(json.dumps(rows, indent=1))
 if args.json:
