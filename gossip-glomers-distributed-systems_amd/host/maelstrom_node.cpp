@@ -259,6 +259,7 @@ struct Options {
     uint32_t lanes = 1024;
     uint64_t seed = 0x6A09E667F3BCC909ull;
     bool sync = true;
+    uint32_t batch = 0;  // gg_config.batch_ticks (0: the reference's per-value gossip)
     int device = 0;
     int tick_ms = 100;
     bool log = false;
@@ -371,11 +372,17 @@ public:
             const int rc = api_.step(x.e, n, st.data());
             if (rc) return fail(std::string("gg_step: ") + api_.last_error(x.e), status);
             // an older engine (no new values) on a symmetric topology whose last round
-            // delivered nothing and that has no queued broadcast is final
+            // delivered nothing and that has no queued broadcast is final; batched
+            // (--batch B): B + 1 quiet rounds in a row, so the last batch sent has
+            // been delivered without news and nothing is pending
+            uint32_t run = 0;
+            while (run < n && st[n - 1 - run].new_bits == 0) ++run;
+            x.quiet_run = run == n ? x.quiet_run + n : run;
             x.queued = false;
-            x.frozen = sym_ && k + 1 < engines_.size() && st[n - 1].new_bits == 0;
+            x.frozen = sym_ && k + 1 < engines_.size() && x.quiet_run >= (opt_.batch ? opt_.batch + 1 : 1);
         }
         pending_.clear();
+        round_ += n;
         return true;
     }
 
@@ -386,6 +393,7 @@ private:
         gg_engine* e = nullptr;
         bool frozen = false;
         bool queued = false;  // a client broadcast waits for the next round
+        uint32_t quiet_run = 0;  // rounds in a row without a delivery
     };
 
     // the engine that holds `value` (a new value: the newest engine, or a new one
@@ -393,12 +401,20 @@ private:
     bool client_broadcast(uint32_t node, int64_t value, std::string& why) {
         auto it = owner_.find(value);
         size_t k = it != owner_.end() ? it->second : engines_.size() - 1;
-        int rc = api_.broadcast(engines_[k].e, node, value, api_.current_round(engines_[k].e));
+        // a frozen engine sat out rounds at its fixed point: step it to the
+        // current round first (nothing changes there, but batched gossip's send
+        // ticks and the sync timers follow the round number)
+        const int64_t behind = round_ - api_.current_round(engines_[k].e);
+        if (behind > 0 && api_.step(engines_[k].e, (uint32_t)behind, nullptr)) {
+            why = std::string("gg_step: ") + api_.last_error(engines_[k].e);
+            return false;
+        }
+        int rc = api_.broadcast(engines_[k].e, node, value, round_);
         if (rc == GG_ENOSPC && it == owner_.end()) {
             if (!add_engine(why)) return false;
             k = engines_.size() - 1;
             engines_[k - 1].frozen = false;  // it may freeze at its next quiet round
-            rc = api_.broadcast(engines_[k].e, node, value, api_.current_round(engines_[k].e));
+            rc = api_.broadcast(engines_[k].e, node, value, round_);
         }
         if (rc) {
             why = std::string("gg_broadcast: ") + api_.last_error(engines_[k].e);
@@ -406,6 +422,7 @@ private:
         }
         owner_[value] = k;
         engines_[k].frozen = false;
+        engines_[k].quiet_run = 0;
         engines_[k].queued = true;
         return true;
     }
@@ -419,6 +436,7 @@ private:
         c.sync_base_ticks = 20;
         c.sync_jitter_ticks = 10;
         c.enable_sync = opt_.sync ? 1 : 0;
+        c.batch_ticks = opt_.batch;
         c.device = opt_.device;
         c.world = 1;
         gg_engine* e = nullptr;
@@ -429,8 +447,7 @@ private:
         }
         rc = api_.topology(e, rp_.data(), col_.empty() ? nullptr : col_.data(), col_.size());
         // catch up with the current round: no values yet, so only the timers run
-        const int64_t r = engines_.empty() ? 0 : api_.current_round(engines_.front().e);
-        if (rc == 0 && r > 0) rc = api_.step(e, (uint32_t)r, nullptr);
+        if (rc == 0 && round_ > 0) rc = api_.step(e, (uint32_t)round_, nullptr);
         if (rc) {
             why = std::string("gg_topology/gg_step: ") + api_.last_error(e);
             api_.destroy(e);
@@ -528,6 +545,7 @@ private:
     Options opt_;
     Api& api_;
     std::vector<Slot> engines_;
+    int64_t round_ = 0;  // rounds run so far (frozen engines lag behind it)
     std::unordered_map<int64_t, size_t> owner_;  // value -> engine
     std::vector<int64_t> rp_;
     std::vector<int32_t> col_;
@@ -549,6 +567,7 @@ std::string self_dir() {
 int usage() {
     fprintf(stderr,
             "usage: maelstrom-broadcast-hip [--engine LIB.so] [--lanes W] [--seed S] [--no-sync]\n"
+            "                               [--batch B (batched gossip: one message per neighbour every B ticks)]\n"
             "                               [--device D] [--tick-ms T (0: lockstep, tick messages)] [--log]\n");
     return 2;
 }
@@ -568,6 +587,7 @@ int main(int argc, char** argv) {
         else if (a == "--device" && (v = next())) o.device = atoi(v);
         else if (a == "--tick-ms" && (v = next())) o.tick_ms = atoi(v);
         else if (a == "--no-sync") o.sync = false;
+        else if (a == "--batch" && (v = next())) o.batch = (uint32_t)strtoul(v, nullptr, 10);
         else if (a == "--log") o.log = true;
         else return usage();
     }

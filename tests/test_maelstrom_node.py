@@ -110,7 +110,7 @@ def _workload(seed, V, rounds, per_round=4):
     return ev
 
 
-def _equivalence(engine_args, ref_lib, device=None, lanes=128, rounds=40, per_round=4, topo=None):
+def _equivalence(engine_args, ref_lib, device=None, lanes=128, rounds=40, per_round=4, topo=None, batch=0):
     topo = topo or T.random_regular(60, 4, seed=5)
     V = topo.n_nodes
     ev = _workload(11, V, rounds, per_round)
@@ -118,7 +118,9 @@ def _equivalence(engine_args, ref_lib, device=None, lanes=128, rounds=40, per_ro
     n_values = sum(1 for e in ev if e[1] == "broadcast")
     W = max(128, (n_values + 63) // 64 * 64)
     ref = Engine(V, W, seed=0x6A09E667F3BCC909, sync_base=20, sync_jitter=10, enable_sync=True,
-                 library=ref_lib)
+                 library=ref_lib, batch_ticks=batch)
+    if batch:
+        engine_args = [*engine_args, "--batch", str(batch)]
     ref.topology(topo)
     want = []
     pending = {}
@@ -147,6 +149,16 @@ def _equivalence(engine_args, ref_lib, device=None, lanes=128, rounds=40, per_ro
 def test_reads_equal_engine_reads_cpu():
     _need()
     _equivalence(["--engine", CPU_LIB], CPU_LIB)
+
+
+@pytest.mark.parametrize("batch", [1, 3])
+def test_batched_front_end(batch):
+    """--batch B: the engines run batched gossip; reads equal
+    one batched engine, within one engine's lanes and beyond them (older
+    engines freeze only after B + 1 quiet rounds: nothing pending)."""
+    _need()
+    _equivalence(["--engine", CPU_LIB], CPU_LIB, batch=batch)
+    _equivalence(["--engine", CPU_LIB], CPU_LIB, lanes=64, rounds=80, per_round=12, batch=batch)
 
 
 @pytest.mark.parametrize("directed", [False, True])
