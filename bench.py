@@ -48,13 +48,17 @@ METRIC = "(node,msg) deliveries/sec at 1/2/4/8 GPUs; % of HBM roofline; msgs/op"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 KERNELS = {"prep": "round_prep", "expand": "expand_round", "stream": "expand_stream"}
+# the kernels one round launches exactly one of, per kind (the launch count of a kind)
+MAIN_KERNELS = {"prep": ["round_prep"], "expand": ["expand_round", "expand_round_lean"],
+                "stream": ["expand_stream", "expand_stream_db", "expand_stream_masked", "expand_stream1",
+                           "expand_stream_sync", "expand_batched"]}
 # the kernels stamping each kind: a kind's "launch" is one round, so its
 # counter traffic per launch is the sum over these kernels' dispatches per round
 KIND_KERNELS = {
     "prep": ["round_prep", "compact_round", "mark_injections", "hub_mark", "sync_records"],
     "expand": ["expand_round", "expand_round_lean"],
-    "stream": ["expand_stream", "expand_stream_masked", "expand_stream1", "expand_stream_sync", "hub_chunks",
-               "hub_finish", "hub_sync_chunks", "hub_sync_finish", "hub_sync_push", "expand_batched"],
+    "stream": ["expand_stream", "expand_stream_db", "expand_stream_masked", "expand_stream1", "expand_stream_sync",
+               "hub_chunks", "hub_finish", "hub_sync_chunks", "hub_sync_finish", "hub_sync_push", "expand_batched"],
 }
 TRAFFIC_JSON = {"C2": os.path.join(REPO, "profiles", "traffic.json"),  # committed PMC passes per config
                 "C4": os.path.join(REPO, "profiles", "traffic_C4.json")}
@@ -82,10 +86,10 @@ def pmc_traffic(kind: str, config: str):
             e = ents.setdefault(b, [0.0, 0])
             e[0] += ent["traffic_bytes_per_dispatch"] * ent["dispatches"]
             e[1] += ent["dispatches"]
-    main = KERNELS[kind]
-    if main not in ents or not ents[main][1]:
+    launches = sum(ents[k][1] for k in MAIN_KERNELS[kind] if k in ents)
+    if not launches:
         return None, None
-    per_round = sum(v[0] for v in ents.values()) / ents[main][1]
+    per_round = sum(v[0] for v in ents.values()) / launches
     return per_round, f'{os.path.relpath(path, REPO)} ({d.get("source", "")}; kernels {sorted(ents)})'
 
 
@@ -339,6 +343,8 @@ def main():
     for kind, name in KERNELS.items():
         ms = sum(s[kind + "_ms"] for s in rounds_local)
         by = sum(s[kind + "_bytes"] for s in rounds_local)
+        if kind == "stream":  # one of the two per lean round (double-buffered rounds)
+            name = "expand_stream / expand_stream_db"
         kinds[kind] = {"kernel": name, "launches": len(rounds_local), "total_ms": ms, "bytes": by,
                        "avg_launch_ms": ms / len(rounds_local),
                        "GBps": by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0}

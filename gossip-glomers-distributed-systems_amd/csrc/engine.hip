@@ -102,8 +102,10 @@ struct BatchKey {
     uint64_t u_hash = 0;  // lanes_through of rounds r0-1 .. r0+m-1 (sync digest)
     size_t windows = 0;
     const void* inj_buf = nullptr;
+    int db_state = 0;  // double-buffered rounds active at r0, and the current set buffer
     bool operator==(const BatchKey& o) const {
-        return r0 == o.r0 && m == o.m && inj_hash == o.inj_hash && u_hash == o.u_hash && windows == o.windows && inj_buf == o.inj_buf;
+        return r0 == o.r0 && m == o.m && inj_hash == o.inj_hash && u_hash == o.u_hash && windows == o.windows &&
+               inj_buf == o.inj_buf && db_state == o.db_state;
     }
 };
 
@@ -218,7 +220,16 @@ struct gg_engine {
     uint32_t* d_in_col = nullptr;
     int64_t* d_out_ptr = nullptr;
     uint32_t* d_out_col = nullptr;
-    uint64_t* d_base = nullptr;
+    uint64_t* d_base = nullptr;      // the buffer holding the current sets (d_sets[set_cur])
+    // double-buffered lean rounds (db_ok engines): round r reads the
+    // sets of r-1 from d_sets[(r+1)&1] and writes d_sets[r&1]; F rows are not written
+    // until the first round that needs them (materialize_F), and from then on the
+    // episode updates d_sets[set_cur] in place
+    uint64_t* d_sets[2] = {nullptr, nullptr};  // d_sets[0] is d_base's allocation
+    bool db_ok = false;       // single engine, no hubs, W >= 128, not batched, both buffers fit
+    bool db_active = false;   // every round of this episode so far was double-buffered
+    int set_cur = 0;
+    bool f_dirty = true;      // some F row may be non-zero (reset must clear them)
     uint64_t* d_F[2] = {nullptr, nullptr};
     uint8_t* d_flg[2] = {nullptr, nullptr};
     uint8_t* d_cand = nullptr;       // [rows] candidate bytes
@@ -325,6 +336,9 @@ void gg_engine::free_topology() {
     dfree(d_out_ptr);
     dfree(d_in_ptr);
     dfree(d_in_col);
+    dfree(d_sets[1]);
+    d_sets[0] = d_sets[1] = nullptr;
+    db_ok = false;
     dfree(d_base);
     for (auto& p : d_F) dfree(p);
     for (auto& p : d_flg) dfree(p);
@@ -425,7 +439,11 @@ int reset_device_state(gg_engine* e) {
         if (ra.n_seg < gg::kResetSegs) ra.seg[ra.n_seg++] = {reinterpret_cast<uint64_t*>(p), bytes / 8, val};
         else e->err = "internal: reset segment table full";  // caught below
     };
-    seg(e->d_base, rowbytes, 0);
+    seg(e->d_sets[0], rowbytes, 0);
+    if (e->db_ok) seg(e->d_sets[1], rowbytes, 0);
+    e->set_cur = 0;
+    e->d_base = e->d_sets[0];
+    e->db_active = e->db_ok;
     // F rows and flags are already all zero after two rounds without new bits
     // (a stale row is cleared in the round it expires), e.g. after an episode
     // run to quiescence. Single engine only: ghost rows follow remote rounds.
@@ -434,7 +452,9 @@ int reset_device_state(gg_engine* e) {
     // and only where their flag byte is set: those rows and the flags are
     // cleared (a sparse last delivery round: 1 MB read instead of C2's 134 MB
     // F buffer written; batched engines keep whole-buffer clears).
-    if (e->P == 1 && e->quiet == 1 && !e->d_pend && e->nwp >= 2 && e->nwp <= 128 && !(e->nwp & (e->nwp - 1))) {
+    if (e->db_ok && !e->f_dirty) {  // only double-buffered rounds ran: F rows are all zero
+        for (int b = 0; b < 2; ++b) seg(e->d_flg[b], e->rows, 0);
+    } else if (e->P == 1 && e->quiet == 1 && !e->d_pend && e->nwp >= 2 && e->nwp <= 128 && !(e->nwp & (e->nwp - 1))) {
         ra.sparse_F = e->d_F[e->dirty_parity];
         ra.sparse_flg = e->d_flg[e->dirty_parity];
         ra.sparse_rows = e->rows;
@@ -447,6 +467,7 @@ int reset_device_state(gg_engine* e) {
         }
     }
     e->quiet = 2;
+    e->f_dirty = !e->db_ok || e->P > 1;  // (sharded: the exchange writes the ghosts' F rows)
     for (int b = 0; b < 4; ++b) seg(e->d_fired[b], e->rows / 8, 0);
     seg(e->d_cand, e->rows, 0);
     seg(e->d_zmark, e->rows, 0);
@@ -564,29 +585,27 @@ void launch_expand(const gg::RoundArgs& a, bool syncw, bool maskw, hipStream_t s
 
 // expand_stream grid: one resident wave of blocks (node groups walk their
 // items grid-stride), so no partial second wave of blocks trails the round.
-template <int G, bool MASKW>
+template <int G, bool MASKW, bool DB = false>
 void launch_stream_t(const gg::RoundArgs& a, hipStream_t s) {
     static int resident = 0;
+    auto kern = MASKW ? gg::expand_stream_masked<G, 2> : (DB ? gg::expand_stream_db<G, 2> : gg::expand_stream<G, 2>);
     if (!resident) {
         int dev = 0, cus = 0, per_cu = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (MASKW)
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gg::expand_stream_masked<G, 2>, gg::kBlock, 0);
-        else
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gg::expand_stream<G, 2>, gg::kBlock, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, gg::kBlock, 0);
         resident = std::max(1, cus) * std::max(1, per_cu);
     }
     const uint64_t ngb = gg::kBlock / G;
     uint64_t blocks = (a.n_own + ngb - 1) / ngb;
     blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)resident));
-    if (MASKW) hipLaunchKernelGGL((gg::expand_stream_masked<G, 2>), dim3((unsigned)blocks), dim3(gg::kBlock), 0, s, a);
-    else hipLaunchKernelGGL((gg::expand_stream<G, 2>), dim3((unsigned)blocks), dim3(gg::kBlock), 0, s, a);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(gg::kBlock), 0, s, a);
 }
 
 template <int G>
 void launch_stream_m(const gg::RoundArgs& a, bool maskw, hipStream_t s) {
     if (maskw) launch_stream_t<G, true>(a, s);
+    else if (a.db) launch_stream_t<G, false, true>(a, s);
     else launch_stream_t<G, false>(a, s);
 }
 
@@ -752,10 +771,47 @@ bool sync_stream_at(gg_engine* e, int64_t r) {
     return true;
 }
 
+// Round r is double-buffered: every round of the episode so far
+// was, and r is a lean streaming round — no sync event reaches the expand and no
+// partition window touches r-3..r+1 (so no message has been dropped yet either:
+// the earlier rounds were lean too).
+bool db_round(const gg_engine* e, int64_t r) {
+    if (!e->db_active) return false;
+    if (e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks + 2) return false;
+    for (int k = 0; k < 5; ++k)
+        if (window_at(e, r - 3 + k)) return false;
+    return true;
+}
+
+// Host state after round r: which buffer holds the sets, and whether the
+// episode has left the double-buffered rounds (for good). enqueue_round calls it
+// while it enqueues; gg_step replays it for a batch replayed from its graph.
+void db_advance(gg_engine* e, int64_t r, bool db) {
+    if (db) {
+        e->set_cur = (int)(r & 1);
+    } else {
+        e->db_active = false;
+        e->f_dirty = true;
+    }
+    e->d_base = e->d_sets[e->set_cur];
+}
+
 // Enqueue round e->round (kernels only). inj: device pairs for this round.
 int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned long long* d_ctr) {
     const int64_t r = e->round;
+    const bool db = db_round(e, r);
+    if (e->db_active && !db && r > 0) {
+        // the first round that needs F rows: those of round r-1, from its two set buffers
+        const uint64_t n = e->n_own * e->nwp;
+        const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 8192));
+        hipLaunchKernelGGL(gg::materialize_F, dim3(blocks), dim3(256), 0, e->stream, e->d_sets[(r - 1) & 1],
+                           e->d_sets[r & 1], e->d_flg[(r - 1) & 1], e->d_F[(r - 1) & 1], e->n_own, (uint32_t)e->nwp);
+        HIPCHK(hipGetLastError());
+    }
+    db_advance(e, r, db);
     gg::RoundArgs a{};
+    a.db = db ? 1 : 0;
+    a.base_prev = db ? e->d_sets[(r + 1) & 1] : nullptr;
     a.in_ptr = e->d_in_ptr;
     a.in_col = e->d_in_col;
     a.out_ptr = e->d_out_ptr;
@@ -948,8 +1004,8 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         if (e->d_dr) {
             const uint64_t n = a.n_own * e->nw;
             hipLaunchKernelGGL(gg::track_delivery, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream,
-                               a.F_cur, a.flg_cur, e->d_dr, a.n_own, a.own0, (uint32_t)e->nwp, (uint32_t)e->nw,
-                               (uint32_t)(e->nw * 64), (int32_t)r);
+                               db ? a.base : a.F_cur, a.flg_cur, e->d_dr, a.n_own, a.own0, (uint32_t)e->nwp,
+                               (uint32_t)e->nw, (uint32_t)(e->nw * 64), (int32_t)r, a.base_prev);
             HIPCHK(hipGetLastError());
         }
     }
@@ -1100,6 +1156,7 @@ int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& o
     key.m = m;
     key.windows = e->windows.size();
     key.inj_buf = e->d_inj;
+    key.db_state = (e->db_active ? 2 : 0) | e->set_cur;
     for (size_t k = 0; k <= m; ++k) h = gg_mix64(h ^ off[k]);
     key.inj_hash = h;
     {  // the digest's usat and the all-full test's full_new follow the lanes injected so far
@@ -1435,6 +1492,14 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
         if (e->ff_ok) HIPCHK(hipMalloc(&e->d_abits, e->rows / 8));
     }
     HIPCHK(hipMalloc(&e->d_base, rowbytes));
+    e->d_sets[0] = e->d_base;
+    e->set_cur = 0;
+    // double-buffered lean rounds: single engines without hubs, W >= 128 (the
+    // streaming kernel), not batched, the second set buffer at most 16 GiB
+    e->db_ok = e->n_hubs == 0 && e->n_mchunks == 0 && e->nwp >= 2 && e->nwp <= 128 &&
+               !e->cfg.batch_ticks && rowbytes <= (16ull << 30) && !ab_knob("GG_NO_DB");
+    if (e->db_ok) HIPCHK(hipMalloc(&e->d_sets[1], rowbytes));
+    e->f_dirty = true;
     for (int b = 0; b < 2; ++b) {
         HIPCHK(hipMalloc(&e->d_F[b], rowbytes));
         HIPCHK(hipMalloc(&e->d_flg[b], e->rows));
@@ -2161,7 +2226,13 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
         const size_t total = pack_injections(e, r0, m, off);
         if (total == (size_t)-1) return GG_EIO;
         const int64_t save_round = e->round;
+        const bool save_db = e->db_active, save_fd = e->f_dirty;
+        const int save_set = e->set_cur;
         auto enqueue_batch = [&]() -> int {
+            e->db_active = save_db;  // (a failed capture may have run it once already)
+            e->f_dirty = save_fd;
+            e->set_cur = save_set;
+            e->d_base = e->d_sets[save_set];
             HIPCHK(hipMemsetAsync(e->d_counters, 0, (size_t)m * gg::kSlots * gg::kCounters * 8, e->stream));
             for (uint32_t k = 0; k < m; ++k) {
                 const uint32_t ni = (uint32_t)(off[k + 1] - off[k]);
@@ -2181,6 +2252,11 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
         rc = run_batch(e, r0, m, off, total, enqueue_batch);
         e->ctr_dirty = std::max(e->ctr_dirty, m);
         e->round = save_round + m;
+        // the double-buffer state after the batch (a replayed graph enqueued nothing)
+        e->db_active = save_db;
+        e->f_dirty = save_fd;
+        e->set_cur = save_set;
+        for (uint32_t k = 0; k < m; ++k) db_advance(e, r0 + k, db_round(e, r0 + k));
         if (rc) return rc;
         HIPCHK(hipStreamSynchronize(e->stream));
         for (uint32_t k = 0; k < m; ++k) {
@@ -2296,6 +2372,8 @@ static int dist_begin(gg_engine* e, gg_exchange* x, bool host_sizes) {
             gg::PackArgs pa{};
             pa.F_cur = e->d_F[r & 1];
             pa.base = e->d_base;
+            // a double-buffered round wrote no F rows: the payload's are set(r) & ~set(r-1)
+            pa.set_prev = e->db_active ? e->d_sets[(r + 1) & 1] : nullptr;
             pa.flg_cur = e->d_flg[r & 1];
             pa.fired_m2 = e->d_fired[(r - 2) & 3];
             pa.needmark = e->d_needmark;

@@ -237,6 +237,10 @@ struct RoundArgs {
     int32_t symmetric;          // out-lists == in-lists
     uint64_t n_edges;           // in_col entries of this engine
     uint64_t rows;              // replica rows
+    int32_t db;                 // double-buffered lean round: sets of r-1 in base_prev,
+                                // this round's sets into base (rows of nodes that changed in r or r-1),
+                                // senders' sets gathered instead of F rows, no F rows written
+    const uint64_t* base_prev;
     int32_t stream_ok;          // lean round (no sync events in expand, no masks) with nwp >= 2:
                                 // expand_stream takes it when it is dense (dense_round)
     int64_t round;
@@ -553,7 +557,7 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
             for (uint32_t j = 0; j < (uint32_t)n4; ++j) {
                 const uint8_t f = (uint8_t)(fp >> (8 * j)), fcj = (uint8_t)(fc >> (8 * j));
                 const uint64_t i = 4 * q + j, rep = a.own0 + i;
-                if ((fcj & FL_ACT) || (f & FL_LAG)) a.cand[rep] = CA_NODE;
+                if ((fcj & FL_ACT) || (f & FL_LAG) || (a.db && (f & FL_ACT))) a.cand[rep] = CA_NODE;
                 if (!(f & FL_ACT)) continue;
                 const int64_t o0 = a.out_ptr[i];
                 int64_t o1 = a.out_ptr[i + 1];
@@ -625,7 +629,8 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                 if (a.stream_ok) {
                     // sparse lean round: expand_stream takes the node (it reads and
                     // rewrites the old flag byte itself); no tile flags (node list)
-                    if (cur.fc & FL_ACT) a.cand[rep] = CA_NODE;
+                    // (double-buffered rounds: a node that changed in r-1 also moves its row forward)
+                    if ((cur.fc & FL_ACT) || (a.db && (f & FL_ACT))) a.cand[rep] = CA_NODE;
                     c_bytes += 2;
                 } else {
                     if (cur.fc & FL_ACT) {
@@ -1339,7 +1344,7 @@ __device__ __forceinline__ uint32_t active_senders(const uint64_t* abits, const 
     return m & ((1u << D) - 1u);
 }
 
-template <int G, int WPL, bool MASKW>
+template <int G, int WPL, bool MASKW, bool DB = false>
 __device__ __forceinline__ void stream_body(RoundArgs a) {
     static_assert(WPL == 2, "DMA slots hold 16 bytes per lane");
     constexpr int NGB = kBlock / G;  // node groups per block
@@ -1359,6 +1364,12 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
     }
     const bool ff = !MASKW && ff_round(a);  // flags-first gathers (block-uniform)
     const bool full = !MASKW && all_full(a);  // nothing can arrive: no gathers, no own rows
+    // double-buffered round: own and sender rows are sets of r-1 (base_prev); in a
+    // lean round without a dropped message so far a sender's set holds nothing new
+    // for v beyond its F row (it forwarded every older value to v), so claims are
+    // unchanged, and no F row is written
+    constexpr bool db = DB && !MASKW;  // a kernel of its own: the F-row kernel keeps its registers
+    const uint64_t* const rows_in = db ? a.base_prev : a.F_prev;
     constexpr uint32_t kAllD = (1u << D) - 1u;
     // per-lane counts that fit 32 bits stay 32-bit (register budget)
     uint32_t c_new = 0, c_active = 0, c_gathers = 0, c_nact = 0, c_nactdeg = 0;
@@ -1368,6 +1379,12 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
     const uint32_t off = (uint32_t)lg * WPL;
     const int gshift = (threadIdx.x & 63) / G * G;
     const int gbase = (int)(threadIdx.x & 63) - lg;  // the node group's first lane in the wave
+    // sharded engines: a ghost sender's row is its F row either way (the exchange
+    // ships F rows), so the sender row's buffer is chosen per sender
+    auto sender_row = [&](uint32_t c) -> const uint64_t* {
+        const uint64_t u = c & kColMask;
+        return ((db && u >= a.ghost0 && a.n_ghost) ? a.F_prev : rows_in) + u * a.nwp + off;
+    };
     const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
     uint8_t* const my = &s_slots[(threadIdx.x >> 6) * (D + 1) * 1024];
     const uint32_t lane16 = (threadIdx.x & 63) * 16;
@@ -1392,7 +1409,9 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             m.p0 = a.in_ptr[n];
             m.deg = (uint32_t)(a.in_ptr[n + 1] - m.p0);
             m.ca = a.cand[a.own0 + n];      // CA_INJ: client broadcasts this round
-            m.fl = a.flg_cur[a.own0 + n];   // flags of round r-2 (ACT: stale F row)
+            // flags of round r-2 (ACT: stale F row), or in double-buffered rounds of
+            // r-1 (ACT: the row in this round's set buffer is two rounds old)
+            m.fl = (db ? a.flg_prev : a.flg_cur)[a.own0 + n];
             if (full) m.deg = 0;
             if (a.hub_deg && m.deg > a.hub_deg) {  // a hub: hub_chunks/hub_finish take it
                 m.node |= kHubBit;
@@ -1427,7 +1446,9 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         const uint64_t rep = a.own0 + i;
         // (a) DMA node i's own row and its first D sender rows (masked rounds:
         // and the words of the window bitmaps covering its first D in-edges)
-        if (!hub && !full) dma16((const void*)(a.base + rep * a.nwp + off), my + D * 1024);
+        // (an all-full double-buffered round: every owned set is the same, row 0's)
+        if (!hub && (!full || db))
+            dma16((const void*)((db ? a.base_prev : a.base) + (full ? a.own0 : rep) * a.nwp + off), my + D * 1024);
         uint64_t mw[3][2];
         if constexpr (MASKW) {
 #pragma unroll
@@ -1441,7 +1462,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
 #pragma unroll
         for (int b = 0; b < D; ++b) {
             if ((uint32_t)b < m0.deg && ((am0 >> b) & 1u))
-                dma16((const void*)(a.F_prev + (uint64_t)(c0[b] & kColMask) * a.nwp + off), my + b * 1024);
+                dma16((const void*)sender_row(c0[b]), my + b * 1024);
         }
         // (b) prefetch: columns of item k+stride, row pointers of item k+2*stride,
         // list entry of item k+3*stride
@@ -1453,7 +1474,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         if (!hub) {
         Row<WPL> sp, S;
         sp.w[0] = sp.w[1] = 0;
-        if (!full) {
+        if (!full || db) {
             const ulonglong2 o = *reinterpret_cast<const ulonglong2*>(my + D * 1024 + lane16);
             sp.w[0] = o.x;  // lean rounds precede every sync timer: no LAG
             sp.w[1] = o.y;
@@ -1544,7 +1565,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
 #pragma unroll
             for (int b = 0; b < D; ++b) {
                 if (e + b < p1 && ((am >> b) & 1u))
-                    dma16((const void*)(a.F_prev + (uint64_t)(cb[b] & kColMask) * a.nwp + off), my + b * 1024);
+                    dma16((const void*)sender_row(cb[b]), my + b * 1024);
             }
             uint64_t ew[3][2];
             if constexpr (MASKW) {
@@ -1586,7 +1607,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             }
         }
         const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
-        const bool zm = (m0.fl & FL_ACT) != 0;  // F row of round r-2 in this buffer
+        const bool zm = !db && (m0.fl & FL_ACT) != 0;  // F row of round r-2 in this buffer
         // rows written this round are read next round from HBM anyway (F by
         // other nodes' gathers, base by this node): streamed past the caches,
         // they leave L2 to the gathers (C2 -2.5%, C3 -1.4% kernel time)
@@ -1596,10 +1617,16 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         // While most nodes learn a few of W values (C2 rounds 10-13: 15-66 % of
         // the chunks change) this drops most of the row stores of a dense round
         const bool lane_new = (F.w[0] | F.w[1]) != 0;
-        if (lane_new || zm) store_row_nt(a.F_cur + rep * a.nwp + off, F);
-        if (lane_new) store_row_nt(a.base + rep * a.nwp + off, S);
+        const bool cp = db && (m0.fl & FL_ACT) != 0;  // db: this buffer's row is two rounds old
+        if (db) {
+            if (lane_new || cp) store_row_nt(a.base + rep * a.nwp + off, S);
+        } else {
+            if (lane_new || zm) store_row_nt(a.F_cur + rep * a.nwp + off, F);
+            if (lane_new) store_row_nt(a.base + rep * a.nwp + off, S);
+        }
         if (lg == 0) {
-            if (any || m0.fl) a.flg_cur[rep] = any ? FL_ACT : 0;
+            // (double-buffered: the flag byte of r-2 is not known here, so always)
+            if (any || db || m0.fl) a.flg_cur[rep] = any ? FL_ACT : 0;
             if (m0.ca) a.cand[rep] = 0;
         }
         const unsigned long long deg = a.symmetric ? nin : (unsigned long long)(a.out_ptr[i + 1] - a.out_ptr[i]);
@@ -1618,10 +1645,11 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             if constexpr (!MASKW) c_nactdeg += any ? (uint32_t)deg : 0u;  // masked rounds: no flags-first next
             // row_ptr + cand + flag bytes + col (+ a sender bit, flags-first), own row + gathered
             // sender rows, F / base / flag writes
-            c_bytes += (dense ? 0 : 4) + 8 + 2 + 4 * nin + (ff ? (nin + 7) / 8 : 0) + (full ? 0 : rowb) +
-                       (any ? 1 : 0);
+            c_bytes += (dense ? 0 : 4) + 8 + 2 + (db ? 1 : 0) + 4 * nin + (ff ? (nin + 7) / 8 : 0) +
+                       (full ? 0 : rowb) + (any ? 1 : 0);
         }
-        c_bytes += ((lane_new || zm) ? 16 : 0) + (lane_new ? 16 : 0);  // this lane's F / base chunk stores
+        // this lane's F / base chunk stores
+        c_bytes += db ? ((lane_new || cp) ? 16 : 0) : ((lane_new || zm) ? 16 : 0) + (lane_new ? 16 : 0);
         }  // !hub
         m0 = m1;
         m1 = m2;
@@ -1660,6 +1688,13 @@ template <int G, int WPL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
 void expand_stream_masked(RoundArgs a) {
     stream_body<G, WPL, true>(a);
+}
+
+// Double-buffered lean rounds (RoundArgs::db): sets of r-1 in, sets of r out.
+template <int G, int WPL>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GG_STREAM_WAVES_PER_EU)))
+void expand_stream_db(RoundArgs a) {
+    stream_body<G, WPL, false, true>(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -3227,13 +3262,16 @@ __global__ void gather_rounds(const uint32_t* rows, uint64_t n, const int32_t* d
 }
 
 // First-seen round of every new bit (GG_TRACK_DELIVERY only; observation).
+// F_cur: the new bits of round r, or (prev != nullptr, double-buffered rounds) the sets of r
 __global__ void track_delivery(const uint64_t* F_cur, const uint8_t* flg_cur, int32_t* dr, uint64_t n_own,
-                               uint64_t own0, uint32_t nwp, uint32_t nw, uint32_t W, int32_t round) {
+                               uint64_t own0, uint32_t nwp, uint32_t nw, uint32_t W, int32_t round,
+                               const uint64_t* prev) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_own * nw) return;
     const uint64_t i = t / nw, j = t % nw;
     if (!(flg_cur[own0 + i] & FL_ACT)) return;
     uint64_t x = F_cur[(own0 + i) * nwp + j];
+    if (prev) x &= ~prev[(own0 + i) * nwp + j];
     while (x) {
         const int b = __builtin_ctzll(x);
         x &= x - 1;
@@ -3243,6 +3281,18 @@ __global__ void track_delivery(const uint64_t* F_cur, const uint8_t* flg_cur, in
 
 // Sum a round's 64 counter slots into one (stamps: max, see kStamp0). One block
 // per round, one thread per counter.
+// The F rows of round q, the last double-buffered round, for the F-row rounds
+// that follow it: F = set(q) & ~set(q-1) for the nodes flagged ACT in q (every
+// other F row is still zero: double-buffered rounds write none).
+__global__ void materialize_F(const uint64_t* set_q, const uint64_t* set_qm1, const uint8_t* flg_q, uint64_t* F_q,
+                              uint64_t n_own, uint32_t nwp) {
+    const uint64_t n = n_own * nwp;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+        if (!(flg_q[t / nwp] & FL_ACT)) continue;
+        F_q[t] = set_q[t] & ~set_qm1[t];
+    }
+}
+
 __global__ void fold_slots(const unsigned long long* ctr, unsigned long long* out) {
     const int j = threadIdx.x;
     const unsigned long long* c = ctr + (size_t)blockIdx.x * kSlots * kCounters;
@@ -3380,6 +3430,7 @@ struct XchgTile {
 struct PackArgs {
     const uint64_t* F_cur;
     const uint64_t* base;
+    const uint64_t* set_prev;   // double-buffered round: no F rows, F = base & ~set_prev
     const uint8_t* flg_cur;
     const uint64_t* fired_m2;   // round r-2: owned pushers of round r+1 (SYNC only)
     uint8_t* needmark;          // [n_send] set read by a callback on the peer in r+1 (cleared here)
@@ -3455,7 +3506,9 @@ __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
             if (ch == 0) {  // head (+ the row word when nwp == 1)
                 v.x = hd;
                 v.y = 0;
-                if (x.nwp == 1) v.y = set ? (x.base[u2] | (lag ? x.F_cur[u2] : 0ull)) : x.F_cur[u2];
+                if (x.nwp == 1)
+                    v.y = set ? (x.base[u2] | (lag ? x.F_cur[u2] : 0ull))
+                              : (x.set_prev ? x.base[u2] & ~x.set_prev[u2] : x.F_cur[u2]);
             } else {
                 const uint64_t o = u2 * x.nwp + 2 * (ch - 1);
                 if (set) {
@@ -3465,6 +3518,11 @@ __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
                         v.x |= f.x;
                         v.y |= f.y;
                     }
+                } else if (x.set_prev) {
+                    v = *reinterpret_cast<const ulonglong2*>(x.base + o);
+                    const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(x.set_prev + o);
+                    v.x &= ~q.x;
+                    v.y &= ~q.y;
                 } else {
                     v = *reinterpret_cast<const ulonglong2*>(x.F_cur + o);
                 }
