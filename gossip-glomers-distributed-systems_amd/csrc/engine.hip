@@ -1494,10 +1494,14 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     HIPCHK(hipMalloc(&e->d_base, rowbytes));
     e->d_sets[0] = e->d_base;
     e->set_cur = 0;
-    // double-buffered lean rounds: single engines without hubs, W >= 128 (the
-    // streaming kernel), not batched, the second set buffer at most 16 GiB
-    e->db_ok = e->n_hubs == 0 && e->n_mchunks == 0 && e->nwp >= 2 && e->nwp <= 128 &&
-               !e->cfg.batch_ticks && rowbytes <= (16ull << 30) && !ab_knob("GG_NO_DB");
+    // double-buffered lean rounds: W >= 128 (the streaming kernels), not batched,
+    // and the second set buffer leaves 16 GiB of HBM free
+    {
+        size_t free_b = 0, total_b = 0;
+        (void)hipMemGetInfo(&free_b, &total_b);
+        e->db_ok = e->nwp >= 2 && e->nwp <= 128 && !e->cfg.batch_ticks && free_b > rowbytes * 4 + (16ull << 30) &&
+                   !ab_knob("GG_NO_DB");
+    }
     if (e->db_ok) HIPCHK(hipMalloc(&e->d_sets[1], rowbytes));
     e->f_dirty = true;
     for (int b = 0; b < 2; ++b) {

@@ -2741,7 +2741,10 @@ __global__ __launch_bounds__(kBlock) void hub_chunks(RoundArgs a) {
 #pragma unroll
             for (int b = 0; b < D; ++b) {
                 if (act[b]) {
-                    src[b] = load_row<WPL>(a.F_prev + (uint64_t)(cb[b] & kColMask) * a.nwp + off);
+                    // double-buffered rounds: the sender's set of r-1 (same claims, §3)
+                    const uint64_t u = cb[b] & kColMask;
+                    const uint64_t* rows = (a.db && !(a.n_ghost && u >= a.ghost0)) ? a.base_prev : a.F_prev;
+                    src[b] = load_row<WPL>(rows + u * a.nwp + off);
                     if (lg == 0) c_bytes += 8ull * a.nwp;
                 } else {
 #pragma unroll
@@ -2809,7 +2812,7 @@ __global__ __launch_bounds__(kBlock) void hub_finish(RoundArgs a) {
         hub_block_reduce<G, WPL>(O, R, s_or, s_rc);
         if (j == 0) {
             const uint64_t rep = a.own0 + i;
-            Row<WPL> sp = load_row<WPL>(a.base + rep * a.nwp + off), S = sp;  // lean: no LAG
+            Row<WPL> sp = load_row<WPL>((a.db ? a.base_prev : a.base) + rep * a.nwp + off), S = sp;  // lean: no LAG
             if (ca & CA_INJ) {  // (1) client broadcasts of this round
                 uint32_t lo = 0, hi = a.n_inj;
                 while (lo < hi) {
@@ -2841,16 +2844,26 @@ __global__ __launch_bounds__(kBlock) void hub_finish(RoundArgs a) {
                 }
             }
             const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
-            const uint8_t fl = a.flg_cur[rep];
-            const bool zm = (fl & FL_ACT) != 0;
-            if (any || zm) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
-            if (any) store_row<WPL>(a.base + rep * a.nwp + off, S);
+            const uint8_t fl = a.db ? a.flg_prev[rep] : a.flg_cur[rep];  // (db: r-1, else r-2)
+            const bool zm = !a.db && (fl & FL_ACT) != 0;
+            const bool lane_new = [&] {
+                bool x = false;
+#pragma unroll
+                for (int w = 0; w < WPL; ++w) x |= F.w[w] != 0;
+                return x;
+            }();
+            if (a.db) {  // chunks that changed now, whole row if it changed in r-1 (§3)
+                if (lane_new || (fl & FL_ACT)) store_row<WPL>(a.base + rep * a.nwp + off, S);
+            } else {
+                if (any || zm) store_row<WPL>(a.F_cur + rep * a.nwp + off, F);
+                if (any) store_row<WPL>(a.base + rep * a.nwp + off, S);
+            }
             const uint64_t nin = (uint64_t)(a.in_ptr[i + 1] - a.in_ptr[i]);
             const unsigned long long deg = a.symmetric ? nin : (unsigned long long)(a.out_ptr[i + 1] - a.out_ptr[i]);
             c_new += T;
             c_fwd += deg * T - cl_recip;
             if (lg == 0) {
-                if (any || fl) a.flg_cur[rep] = any ? FL_ACT : 0;
+                if (any || fl || a.db) a.flg_cur[rep] = any ? FL_ACT : 0;
                 if (ca) a.cand[rep] = 0;
                 c_active += 1;
                 c_gathers += nin;
