@@ -44,7 +44,8 @@ constexpr int kMaxBlocks = 2048;
 // that the engine would otherwise choose by size (every forced path is
 // bit-exact; only the kernels that run change): GG_HUB_DEG, GG_HUB_CHUNK,
 // GG_SYNC_TILES, GG_SYNC_DIGEST, GG_ORDER, GG_XCHG_MODE, GG_PREP_BLOCKS,
-// GG_SHARD_NATIVE (device-built shards keep native row order).
+// GG_SHARD_NATIVE (device-built shards keep native row order), GG_NO_DB (no
+// double-buffered lean rounds: the F-row kernels take them).
 const char* test_knob(const char* name) { return getenv(name); }
 // A/B switches of past measurements (GG_ALL_FULL, GG_NO_GRAPH, GG_SYNC_ALLPUSH,
 // GG_FLAGS_FIRST, GG_XCHG_EXACT_BYTES): read only in a -DGG_AB_KNOBS build.
@@ -1500,7 +1501,7 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
         size_t free_b = 0, total_b = 0;
         (void)hipMemGetInfo(&free_b, &total_b);
         e->db_ok = e->nwp >= 2 && e->nwp <= 128 && !e->cfg.batch_ticks && free_b > rowbytes * 4 + (16ull << 30) &&
-                   !ab_knob("GG_NO_DB");
+                   !test_knob("GG_NO_DB");
     }
     if (e->db_ok) HIPCHK(hipMalloc(&e->d_sets[1], rowbytes));
     e->f_dirty = true;

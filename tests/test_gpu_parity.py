@@ -289,3 +289,37 @@ def test_edge_window_c3_shape_vs_o2(hip_lib, cpu_lib):
                   windows=[("seeded", 2, 12, 7), ("edges", 6, 16, bits)])
     st, _ = _compare(sc, hip_lib, cpu_lib)
     assert sum(s["dropped"] for s in st[12:16]) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("no_db", [False, True])
+@pytest.mark.parametrize("seed", range(3))
+def test_lean_rounds_both_kernels_vs_o2(hip_lib, cpu_lib, monkeypatch, seed, no_db):
+    """Lean episodes (no sync, no windows) with client broadcasts spread over
+    rounds, through the double-buffered kernel (senders' sets of
+    r-1, no F rows) and, with GG_NO_DB, through the F-row kernel; then sync
+    rounds after the double-buffered ones (materialize_F hands over), against
+    O2 per round, with sets and delivery rounds."""
+    if no_db:
+        monkeypatch.setenv("GG_NO_DB", "1")
+    rnd = random.Random(900 + seed)
+    for k in range(4):
+        sc = random_scenario(rnd, max_v=300, W=rnd.choice([128, 256, 1024]), rounds=40)
+        sc.windows = []
+        sc.enable_sync = k % 2 == 1
+        sc.sync_base = rnd.randrange(3, 12)
+        sc.injections = [(n, v, rnd.randrange(0, 10)) for n, v, _ in sc.injections]
+        g, c = make_engine(hip_lib, sc), make_engine(cpu_lib, sc)
+        d = diff_stats(g.step(sc.rounds), c.step(sc.rounds))
+        assert not d, (seed, k, d[:10])
+        assert np.array_equal(g.read_bits(), c.read_bits())
+        assert np.array_equal(g.delivery_rounds(), c.delivery_rounds())
+        # a second episode on the same engines (reset after double-buffered rounds)
+        g.reset()
+        c.reset()
+        for n, v, r in sc.injections:
+            g.broadcast(n, v, r)
+            c.broadcast(n, v, r)
+        d = diff_stats(g.step(sc.rounds), c.step(sc.rounds))
+        assert not d, (seed, k, "episode 2", d[:10])
+        assert np.array_equal(g.read_bits(), c.read_bits())
