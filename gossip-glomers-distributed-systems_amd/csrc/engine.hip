@@ -337,10 +337,14 @@ void gg_engine::free_topology() {
     dfree(d_out_ptr);
     dfree(d_in_ptr);
     dfree(d_in_col);
+    // d_base points at one of the two set buffers (d_sets[set_cur]): free the
+    // allocations, not the alias (a double free left a sticky hipErrorInvalidValue)
+    if (!d_sets[0]) d_sets[0] = d_base;
     dfree(d_sets[1]);
-    d_sets[0] = d_sets[1] = nullptr;
+    dfree(d_sets[0]);
+    d_base = nullptr;
+    set_cur = 0;
     db_ok = false;
-    dfree(d_base);
     for (auto& p : d_F) dfree(p);
     for (auto& p : d_flg) dfree(p);
     dfree(d_cand);
@@ -951,7 +955,10 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             }
             // sync rounds do real work per node: a larger capped grid (each block's
             // counter flush is a few same-address atomics, so not one block per 256 nodes)
-            static const uint64_t sync_cap = ab_knob("GG_SYNC_PREP_BLOCKS") ? (uint64_t)atoi(ab_knob("GG_SYNC_PREP_BLOCKS")) : 4096;
+            // (timer rounds: 8+ nodes per thread; C2 at 2^20 nodes, A/B on one box
+            // (profiles/r3/ab_sync_prep.log): 1024 blocks 20 / 19 us per timer round, 4096 26 / 25 us)
+            const uint64_t sync_cap = ab_knob("GG_SYNC_PREP_BLOCKS") ? (uint64_t)atoi(ab_knob("GG_SYNC_PREP_BLOCKS"))
+                                      : std::min<uint64_t>(4096, std::max<uint64_t>(1024, a.n_own / 2048));
             const uint64_t blocks = std::max<uint64_t>(
                 1, std::min<uint64_t>((a.n_own + gg::kBlock - 1) / gg::kBlock, syncw_prep ? sync_cap : prep_cap));
             dim3 grid((unsigned)blocks), block(gg::kBlock);
