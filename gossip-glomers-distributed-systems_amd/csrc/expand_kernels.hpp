@@ -1836,7 +1836,10 @@ void expand_stream1(RoundArgs a) {
             if (any) a.base[rep] = S;
             if (any || m0.fl) a.flg_cur[rep] = any ? FL_ACT : 0;
             if (m0.ca) a.cand[rep] = 0;
-            const unsigned long long deg = a.symmetric ? nin : (unsigned long long)(a.out_ptr[i + 1] - a.out_ptr[i]);
+            // forward recipients: nin is 0 for a saturated node (no gathers), which can
+            // still learn a client broadcast of this round: then the out-list length
+            const unsigned long long deg =
+                T == 0 ? 0ull : ((a.symmetric && nin) ? nin : (unsigned long long)(a.out_ptr[i + 1] - a.out_ptr[i]));
             c_new += T;
             c_fwd += deg * (unsigned long long)T - cl_recip;
             c_active += 1;

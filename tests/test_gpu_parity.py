@@ -323,3 +323,17 @@ def test_lean_rounds_both_kernels_vs_o2(hip_lib, cpu_lib, monkeypatch, seed, no_
         d = diff_stats(g.step(sc.rounds), c.step(sc.rounds))
         assert not d, (seed, k, "episode 2", d[:10])
         assert np.array_equal(g.read_bits(), c.read_bits())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W", [64, 128])
+def test_saturated_node_learns_client_broadcast(hip_lib, cpu_lib, W):
+    """A node whose set already holds every value broadcast so far skips its
+    gathers (expand_stream1, W = 64); a client broadcast of a new value at it
+    must still be forwarded to every neighbour (regression: the forward count
+    used the skipped in-degree)."""
+    for V in (2, 5, 40):
+        topo = T.tree(V, 4)
+        inj = [(0, 11, 0), (V - 1, 12, 0), (0, 13, 9), (V - 1, 14, 9), (V // 2, 15, 12), (0, 11, 14)]
+        sc = Scenario(topo, W, 24, inj, seed=5, enable_sync=False)
+        _compare(sc, hip_lib, cpu_lib)
