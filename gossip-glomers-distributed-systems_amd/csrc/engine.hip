@@ -45,8 +45,7 @@ constexpr int kMaxBlocks = 2048;
 // bit-exact; only the kernels that run change): GG_HUB_DEG, GG_HUB_CHUNK,
 // GG_SYNC_TILES, GG_SYNC_DIGEST, GG_ORDER, GG_XCHG_MODE, GG_PREP_BLOCKS,
 // GG_SHARD_NATIVE (device-built shards keep native row order), GG_NO_DB (no
-// double-buffered lean rounds: the F-row kernels take them), GG_NO_PULL (no
-// prep_pull: round_prep + compact_round in every round).
+// double-buffered lean rounds: the F-row kernels take them).
 const char* test_knob(const char* name) { return getenv(name); }
 // A/B switches of past measurements (GG_ALL_FULL, GG_NO_GRAPH, GG_SYNC_ALLPUSH,
 // GG_FLAGS_FIRST, GG_XCHG_EXACT_BYTES): read only in a -DGG_AB_KNOBS build.
@@ -232,8 +231,6 @@ struct gg_engine {
     bool db_active = false;   // every round of this episode so far was double-buffered
     int set_cur = 0;
     bool f_dirty = true;      // some F row may be non-zero (reset must clear them)
-    bool pull_ok = false;     // prep_pull for lean rounds before the timers (unsharded, <= 4 in-edges
-                              // per node, no hubs, not batched)
     uint64_t* d_F[2] = {nullptr, nullptr};
     uint8_t* d_flg[2] = {nullptr, nullptr};
     uint8_t* d_cand = nullptr;       // [rows] candidate bytes
@@ -478,7 +475,6 @@ int reset_device_state(gg_engine* e) {
     e->f_dirty = !e->db_ok || e->P > 1;  // (sharded: the exchange writes the ghosts' F rows)
     for (int b = 0; b < 4; ++b) seg(e->d_fired[b], e->rows / 8, 0);
     seg(e->d_cand, e->rows, 0);
-    seg(e->d_n_work, 16, 0);
     seg(e->d_zmark, e->rows, 0);
     seg(e->d_tile_cand, e->tile_bytes, 0);
     seg(e->d_act, 16, 0);
@@ -944,20 +940,8 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         a.push_marked = (sync_stream && sync_stream_at(e, r - 1)) ? 1u : 0u;
     }
     a.stream_ok = ((!syncw && (!maskw || (e->symmetric && e->n_hubs == 0 && e->nwp >= 2))) || sync_stream) ? 1 : 0;
-    // lean rounds before the timers on sparse unsharded graphs: prep_pull (one
-    // launch: ring sums, candidates pulled from the in-lists, the node list)
-    const bool pull = e->pull_ok && a.stream_ok && !maskw && !syncw_prep && !sync_stream;
-    a.n_list = e->d_n_work + (pull ? 2 + (r & 1) : 1);
 
-    if (a.n_own && pull) {
-        if (n_inj) {  // first: prep_pull reads the candidate bytes
-            hipLaunchKernelGGL(gg::mark_injections, dim3((n_inj + 255) / 256), dim3(256), 0, e->stream, a);
-            HIPCHK(hipGetLastError());
-        }
-        hipLaunchKernelGGL(gg::prep_pull, dim3((unsigned)((a.n_own + gg::kBlock - 1) / gg::kBlock)), dim3(gg::kBlock),
-                           0, e->stream, a);
-        HIPCHK(hipGetLastError());
-    } else if (a.n_own) {
+    if (a.n_own) {
         {
             // grid-stride over the nodes; a capped grid keeps the launch cheap in
             // dense lean rounds, where it is a no-op (C2 A/B: 1024 blocks 1.99 ms/episode,
@@ -1004,8 +988,6 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
                                dim3(gg::kBlock), 0, e->stream, a);
             HIPCHK(hipGetLastError());
         }
-    }
-    if (a.n_own) {
         if (sync_stream) {
             launch_stream_sync(a, e->stream);
             if (e->n_hubs) {
@@ -1502,7 +1484,7 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     HIPCHK(hipMalloc(&e->d_zmark, e->rows));
     HIPCHK(hipMalloc(&e->d_tile_cand, e->tile_bytes));
     HIPCHK(hipMalloc(&e->d_work, std::max<uint64_t>(1, ntiles) * sizeof(gg::TileWork)));
-    HIPCHK(hipMalloc(&e->d_n_work, 4 * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&e->d_n_work, 2 * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->d_nodes, std::max<uint64_t>(1, n_own) * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->d_act, 4 * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->d_act_deg, 4 * 8));
@@ -1529,8 +1511,6 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
                    !test_knob("GG_NO_DB");
     }
     if (e->db_ok) HIPCHK(hipMalloc(&e->d_sets[1], rowbytes));
-    e->pull_ok = e->P == 1 && e->n_hubs == 0 && e->n_mchunks == 0 && !e->cfg.batch_ticks &&
-                 e->n_in_edges <= 4 * std::max<uint64_t>(1, n_own) && !test_knob("GG_NO_PULL");
     e->f_dirty = true;
     for (int b = 0; b < 2; ++b) {
         HIPCHK(hipMalloc(&e->d_F[b], rowbytes));

@@ -140,9 +140,7 @@ struct RoundArgs {
     uint8_t* zmark;             // [rows] F row of this parity is stale (node active 2 rounds ago)
     uint8_t* tile_cand;         // [n_tiles rounded to 8] tile has a candidate (sparse rounds)
     struct TileWork* work;      // live tiles of a sparse round (compact_round; expand_round)
-    uint32_t* n_work;           // [4]: live tiles, candidate nodes (compact_round); candidate nodes of
-                                // prep_pull rounds by parity ([2 + (r & 1)])
-    uint32_t* n_list;           // the candidate-node count of this round's list: n_work + 1 or + 2 + (r & 1)
+    uint32_t* n_work;           // [2]: live tiles, candidate nodes
     uint32_t* nodes;            // candidate nodes of a sparse lean round (compact_round; expand_stream)
     uint32_t* act;              // [4] ring: nodes that became active in round r (slot r&3), summed by round_prep
     unsigned long long* act_deg;  // [4] ring: their out-degree sum (edges carrying F rows next round)
@@ -899,88 +897,6 @@ __global__ __launch_bounds__(kBlock) void compact_round(RoundArgs a) {
     if (threadIdx.x == 0) stamp(a, K_PREP, t_start);
 }
 
-// Sparse lean rounds of unsharded engines on sparse graphs (in-edges <= 4 per
-// node; no hubs, no timers yet, no window): one launch instead of round_prep's
-// push marking + compact_round. Each node decides itself whether it is a
-// candidate — a client broadcast (mark_injections ran first), an in-neighbour
-// that was active in r-1 (its in-list, until the first), its own F row of r-2
-// still in this round's buffer (F-row rounds) or its set changed in r-1
-// (double-buffered rounds) — and each block appends its candidates, ascending,
-// with one atomic. The list count lives in a parity slot that the round before
-// zeroed, so no launch has to clear it in between. Dense rounds only publish the
-// rings (round_prep's part) and exit.
-__global__ __launch_bounds__(kBlock) void prep_pull(RoundArgs a) {
-    __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
-    __shared__ uint32_t s_cnt[kBlock / 64];
-    __shared__ uint32_t s_base;
-    const unsigned long long t_start = clock100();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int pr = (int)((a.round - 1) & 3), cr = (int)(a.round & 3);
-    const unsigned long long act_prev = wave_sum((unsigned long long)a.act_s[pr * kSlots + lane]);
-    const bool dense = a.stream_ok &&
-                       2.0 * (double)act_prev * (double)a.n_edges >= (double)a.n_own * (double)a.n_own;
-    if (blockIdx.x == 0 && threadIdx.x < kSlots) {  // round r-1's rings (as round_prep)
-        const unsigned long long d = wave_sum(a.act_deg_s[pr * kSlots + lane]);
-        const unsigned long long n = wave_sum(a.tot_s[pr * kSlots + lane]);
-        a.act_s[cr * kSlots + lane] = 0;
-        a.act_deg_s[cr * kSlots + lane] = 0;
-        a.tot_s[cr * kSlots + lane] = 0;
-        if (lane == 0) {
-            a.act[pr] = (uint32_t)act_prev;
-            a.act_deg[pr] = d;
-            if (a.tot) a.tot[pr] = (a.round > 0 ? a.tot[(a.round - 2) & 3] : 0ull) + n;
-            a.n_work[2 + ((a.round + 1) & 1)] = 0;  // the next round's list count
-        }
-    }
-    if (a.sat) {  // last round's digest bits in (readers of this round see rounds < r only)
-        const uint64_t nw = (a.n_own + 63) / 64;
-        for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < nw; t += (uint64_t)gridDim.x * kBlock) {
-            const uint64_t w = (a.own0 >> 6) + t;
-            a.sat[w] = a.sat_reset ? 0ull : (a.sat[w] | a.sat_new[w]);
-            a.sat_new[w] = 0;
-        }
-    }
-    if (dense) {
-        noop_exit(a, K_PREP, t_start);
-        return;
-    }
-    unsigned long long c_bytes = 0;
-    const uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    bool c = false;
-    if (v < a.n_own) {
-        const uint64_t rep = a.own0 + v;
-        c = a.cand[rep] != 0 || (a.flg_cur[rep] & FL_ACT) || (a.db && (a.flg_prev[rep] & FL_ACT));
-        c_bytes += 3;
-        if (!c) {
-            const int64_t e0 = a.in_ptr[v], e1 = a.in_ptr[v + 1];
-            c_bytes += 16;
-            for (int64_t e = e0; e < e1 && !c; ++e) {
-                c = (a.flg_prev[a.in_col[e] & kColMask] & FL_ACT) != 0;
-                c_bytes += 5;
-            }
-        }
-    }
-    const unsigned long long m = __ballot(c);
-    if (lane == 0) s_cnt[wave] = (uint32_t)__popcll(m);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t tot = 0;
-        for (int w = 0; w < kBlock / 64; ++w) {
-            const uint32_t x = s_cnt[w];
-            s_cnt[w] = tot;
-            tot += x;
-        }
-        s_base = tot ? atomicAdd(a.n_list, tot) : 0u;
-    }
-    __syncthreads();
-    if (c) a.nodes[s_base + s_cnt[wave] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)v;
-    unsigned long long acc[C_NUM];
-#pragma unroll
-    for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
-    acc[C_BYTES] = c_bytes;
-    flush_counters(a, acc, s_red, t_start, K_PREP);
-}
-
 // ---------------------------------------------------------------------------
 // expand_round. G lanes per node, WPL words per lane; SYNCW: sync events
 // possible in r-3..r (timers fire from r >= sync_base); MASKW: some partition
@@ -1441,7 +1357,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         return;
     }
     const bool dense = dense_round(a);
-    const uint32_t n_items = dense ? (uint32_t)a.n_own : *a.n_list;
+    const uint32_t n_items = dense ? (uint32_t)a.n_own : a.n_work[1];
     if ((uint64_t)blockIdx.x * NGB >= n_items) {  // sparse round: no item reaches this block
         noop_exit(a, K_STREAM, t_start);
         return;
@@ -1797,7 +1713,7 @@ void expand_stream1(RoundArgs a) {
         return;
     }
     const bool dense = dense_round(a);
-    const uint32_t n_items = dense ? (uint32_t)a.n_own : *a.n_list;
+    const uint32_t n_items = dense ? (uint32_t)a.n_own : a.n_work[1];
     if ((uint64_t)blockIdx.x * kBlock >= n_items) {  // sparse round: no item reaches this block
         noop_exit(a, K_STREAM, t_start);
         return;

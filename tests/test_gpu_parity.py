@@ -292,17 +292,16 @@ def test_edge_window_c3_shape_vs_o2(hip_lib, cpu_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", [None, "GG_NO_DB", "GG_NO_PULL"])
+@pytest.mark.parametrize("no_db", [False, True])
 @pytest.mark.parametrize("seed", range(3))
-def test_lean_rounds_both_kernels_vs_o2(hip_lib, cpu_lib, monkeypatch, seed, knob):
+def test_lean_rounds_both_kernels_vs_o2(hip_lib, cpu_lib, monkeypatch, seed, no_db):
     """Lean episodes (no sync, no windows) with client broadcasts spread over
     rounds, through the double-buffered kernel (senders' sets of
-    r-1, no F rows) and, with GG_NO_DB, through the F-row kernel; candidates by
-    prep_pull and, with GG_NO_PULL, by round_prep + compact_round; then sync
+    r-1, no F rows) and, with GG_NO_DB, through the F-row kernel; then sync
     rounds after the double-buffered ones (materialize_F hands over), against
     O2 per round, with sets and delivery rounds."""
-    if knob:  # the F-row kernel, or round_prep + compact_round instead of prep_pull
-        monkeypatch.setenv(knob, "1")
+    if no_db:
+        monkeypatch.setenv("GG_NO_DB", "1")
     rnd = random.Random(900 + seed)
     for k in range(4):
         sc = random_scenario(rnd, max_v=300, W=rnd.choice([128, 256, 1024]), rounds=40)
