@@ -231,6 +231,7 @@ struct gg_engine {
     bool db_active = false;   // every round of this episode so far was double-buffered
     int set_cur = 0;
     bool f_dirty = true;      // some F row may be non-zero (reset must clear them)
+    bool db_decided = false;  // ensure_db ran since the topology was installed
     uint64_t* d_F[2] = {nullptr, nullptr};
     uint8_t* d_flg[2] = {nullptr, nullptr};
     uint8_t* d_cand = nullptr;       // [rows] candidate bytes
@@ -774,6 +775,28 @@ bool sync_stream_at(gg_engine* e, int64_t r) {
     for (int k = 0; k < 5; ++k)
         if (window_at(e, r - 3 + k)) return false;
     return true;
+}
+
+// Double-buffered lean rounds need a second set buffer: W >= 128 (the streaming
+// kernels), not batched, and 16 GiB of HBM left free after it and the F rows.
+// Decided at the first step after an install (round 0, so the episode starts in
+// double-buffered rounds), not at the install itself: the device generator's
+// scratch (C4 at 10^8 nodes: tens of GiB) is only freed afterwards.
+int ensure_db(gg_engine* e) {
+    if (e->db_decided) return GG_OK;
+    e->db_decided = true;
+    const size_t rowbytes = e->rows * e->nwp * 8;
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    const bool ok = e->round == 0 && e->nwp >= 2 && e->nwp <= 128 && !e->cfg.batch_ticks &&
+                    free_b > rowbytes + (16ull << 30) && !test_knob("GG_NO_DB");
+    if (!ok) return GG_OK;
+    HIPCHK(hipMalloc(&e->d_sets[1], rowbytes));
+    HIPCHK(hipMemsetAsync(e->d_sets[1], 0, rowbytes, e->stream));
+    e->db_ok = true;
+    e->db_active = true;
+    e->f_dirty = e->P > 1;  // (sharded: the exchange writes the ghosts' F rows)
+    return GG_OK;
 }
 
 // Round r is double-buffered: every round of the episode so far
@@ -1502,15 +1525,10 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     HIPCHK(hipMalloc(&e->d_base, rowbytes));
     e->d_sets[0] = e->d_base;
     e->set_cur = 0;
-    // double-buffered lean rounds: W >= 128 (the streaming kernels), not batched,
-    // and the second set buffer leaves 16 GiB of HBM free
-    {
-        size_t free_b = 0, total_b = 0;
-        (void)hipMemGetInfo(&free_b, &total_b);
-        e->db_ok = e->nwp >= 2 && e->nwp <= 128 && !e->cfg.batch_ticks && free_b > rowbytes * 4 + (16ull << 30) &&
-                   !test_knob("GG_NO_DB");
-    }
-    if (e->db_ok) HIPCHK(hipMalloc(&e->d_sets[1], rowbytes));
+    // double-buffered lean rounds: decided at the first step (ensure_db), when
+    // the generator's scratch is gone
+    e->db_ok = false;
+    e->db_decided = false;
     e->f_dirty = true;
     for (int b = 0; b < 2; ++b) {
         HIPCHK(hipMalloc(&e->d_F[b], rowbytes));
@@ -2224,6 +2242,7 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
     HIPCHK(hipSetDevice(e->device));
     int rc = materialize_windows(e);
     if (rc) return rc;
+    if ((rc = ensure_db(e))) return rc;
     uint32_t done = 0;
     std::vector<size_t> off;
     e->step_event_ms = 0.0;
@@ -2339,6 +2358,7 @@ static int dist_begin(gg_engine* e, gg_exchange* x, bool host_sizes) {
     HIPCHK(hipSetDevice(e->device));
     int rc = materialize_windows(e);
     if (rc) return rc;
+    if ((rc = ensure_db(e))) return rc;
     if (e->dist_k == kMaxBatch && (rc = fold_pending(e))) return rc;
     const int64_t r = e->round;
     std::vector<size_t> off;
