@@ -230,7 +230,6 @@ def main():
                     "in HBM by the on-device generator; one step = one episode to quiescence")
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
-    hbm_bytes = free0 - torch.cuda.mem_get_info(local)[0]
     inj = uniform_injections(V, K, seed)
     inj_arr = injection_arrays(inj)  # converted once, outside the timed loop
 
@@ -254,6 +253,10 @@ def main():
             break
         if R > 400:
             raise RuntimeError("no quiescence within 400 rounds")
+    torch.cuda.synchronize()
+    # after the first episode: the engine's second set buffer (double-buffered
+    # rounds) is allocated at its first step
+    hbm_bytes = free0 - torch.cuda.mem_get_info(local)[0]
 
     event_ms = []
 

@@ -788,7 +788,9 @@ int ensure_db(gg_engine* e) {
     const size_t rowbytes = e->rows * e->nwp * 8;
     size_t free_b = 0, total_b = 0;
     (void)hipMemGetInfo(&free_b, &total_b);
-    const bool ok = e->round == 0 && e->nwp >= 2 && e->nwp <= 128 && !e->cfg.batch_ticks &&
+    // (graphs with hubs are bound by their gathers: C4 at 10^8 nodes ran 1.154 s per
+    // episode either way, profiles/r3/bench_c4_db.json, so they keep their HBM)
+    const bool ok = e->round == 0 && e->nwp >= 2 && e->nwp <= 128 && !e->cfg.batch_ticks && e->n_hubs == 0 &&
                     free_b > rowbytes + (16ull << 30) && !test_knob("GG_NO_DB");
     if (!ok) return GG_OK;
     HIPCHK(hipMalloc(&e->d_sets[1], rowbytes));
