@@ -232,7 +232,6 @@ struct gg_engine {
     int set_cur = 0;
     bool f_dirty = true;      // some F row may be non-zero (reset must clear them)
     bool db_decided = false;  // ensure_db ran since the topology was installed
-    bool sync_alloc = false;  // ensure_sync allocated the streamed-sync buffers
     uint64_t* d_F[2] = {nullptr, nullptr};
     uint8_t* d_flg[2] = {nullptr, nullptr};
     uint8_t* d_cand = nullptr;       // [rows] candidate bytes
@@ -776,44 +775,6 @@ bool sync_stream_at(gg_engine* e, int64_t r) {
     for (int k = 0; k < 5; ++k)
         if (window_at(e, r - 3 + k)) return false;
     return true;
-}
-
-// The streamed-sync buffers (records, sender states, digest, reverse edge index,
-// push bytes), allocated before the first batch that reaches a timer round
-// rather than at the install: an episode that ends before the timers (the C4
-// and C5 benchmarks) never needs them (C5 at 2^30 nodes: 66 GiB).
-int ensure_sync(gg_engine* e, int64_t last_round) {
-    if (e->sync_alloc || !e->cfg.enable_sync || last_round < (int64_t)e->cfg.sync_base_ticks) return GG_OK;
-    e->sync_alloc = true;
-    const uint64_t n_own = e->n_own;
-    if (e->cfg.enable_sync && !e->cfg.batch_ticks && (e->n_hubs == 0 || e->symmetric) && !e->sync_tiles && n_own) {
-        HIPCHK(hipMalloc(&e->d_srec, 2 * n_own * sizeof(uint4)));
-        HIPCHK(hipMalloc(&e->d_sstate, e->rows));
-        HIPCHK(hipMalloc(&e->d_ibits, e->rows / 8));
-        HIPCHK(hipMalloc(&e->d_nmeta, n_own * sizeof(uint2)));
-        // saturation digest (GG_SYNC_DIGEST=0 turns it off, for A/B)
-        if (!(test_knob("GG_SYNC_DIGEST") && atoi(test_knob("GG_SYNC_DIGEST")) == 0)) {
-            HIPCHK(hipMalloc(&e->d_sat, e->rows / 8));
-            HIPCHK(hipMalloc(&e->d_sat_new, e->rows / 8));
-            HIPCHK(hipMemsetAsync(e->d_sat, 0, e->rows / 8, e->stream));
-            HIPCHK(hipMemsetAsync(e->d_sat_new, 0, e->rows / 8, e->stream));
-        }
-        if (e->n_in_edges) {  // receivers look up whether an owned pusher sent them anything
-            HIPCHK(hipMalloc(&e->d_rev, e->n_in_edges * 4));
-            const unsigned blocks = (unsigned)std::min<uint64_t>((e->n_in_edges / 8 + 255) / 256 + 1, 16384);
-            hipLaunchKernelGGL(gg::build_rev, dim3(blocks), dim3(256), 0, e->stream, e->d_in_ptr, e->d_in_col,
-                               e->d_out_ptr, e->d_out_col, e->d_gid, n_own, e->n_in_edges, e->d_rev);
-            HIPCHK(hipGetLastError());
-        }
-    }
-    // non-empty pushes per out-edge, written by each sync callback (SyncBroadcast
-    // sends nothing for an empty difference): receivers of empty pushes are not
-    // candidates (GG_SYNC_ALLPUSH=1 keeps every push edge, for A/B)
-    if (e->cfg.enable_sync && e->n_out_edges && !(ab_knob("GG_SYNC_ALLPUSH") && atoi(ab_knob("GG_SYNC_ALLPUSH"))))
-        HIPCHK(hipMalloc(&e->d_pushb, e->n_out_edges));
-    if (!e->d_pushb) dfree(e->d_rev);
-    if (e->d_pushb && e->d_srec) HIPCHK(hipMalloc(&e->d_pushany, e->rows));
-    return GG_OK;
 }
 
 // Double-buffered lean rounds need a second set buffer: W >= 128 (the streaming
@@ -1515,7 +1476,31 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
                 HIPCHK(hipMemset(e->d_bset[b], 0, e->rows * e->nwp * 8));
             }
     }
-    e->sync_alloc = false;  // the streamed-sync buffers: ensure_sync, before the first timer round
+    if (e->cfg.enable_sync && !e->cfg.batch_ticks && (e->n_hubs == 0 || e->symmetric) && !e->sync_tiles && n_own) {
+        HIPCHK(hipMalloc(&e->d_srec, 2 * n_own * sizeof(uint4)));
+        HIPCHK(hipMalloc(&e->d_sstate, e->rows));
+        HIPCHK(hipMalloc(&e->d_ibits, e->rows / 8));
+        HIPCHK(hipMalloc(&e->d_nmeta, n_own * sizeof(uint2)));
+        // saturation digest (GG_SYNC_DIGEST=0 turns it off, for A/B)
+        if (!(test_knob("GG_SYNC_DIGEST") && atoi(test_knob("GG_SYNC_DIGEST")) == 0)) {
+            HIPCHK(hipMalloc(&e->d_sat, e->rows / 8));
+            HIPCHK(hipMalloc(&e->d_sat_new, e->rows / 8));
+        }
+        if (e->n_in_edges) {  // receivers look up whether an owned pusher sent them anything
+            HIPCHK(hipMalloc(&e->d_rev, e->n_in_edges * 4));
+            const unsigned blocks = (unsigned)std::min<uint64_t>((e->n_in_edges / 8 + 255) / 256 + 1, 16384);
+            hipLaunchKernelGGL(gg::build_rev, dim3(blocks), dim3(256), 0, e->stream, e->d_in_ptr, e->d_in_col,
+                               e->d_out_ptr, e->d_out_col, e->d_gid, n_own, e->n_in_edges, e->d_rev);
+            HIPCHK(hipGetLastError());
+        }
+    }
+    // non-empty pushes per out-edge, written by each sync callback (SyncBroadcast
+    // sends nothing for an empty difference): receivers of empty pushes are not
+    // candidates (GG_SYNC_ALLPUSH=1 keeps every push edge, for A/B)
+    if (e->cfg.enable_sync && e->n_out_edges && !(ab_knob("GG_SYNC_ALLPUSH") && atoi(ab_knob("GG_SYNC_ALLPUSH"))))
+        HIPCHK(hipMalloc(&e->d_pushb, e->n_out_edges));
+    if (!e->d_pushb) dfree(e->d_rev);
+    if (e->d_pushb && e->d_srec) HIPCHK(hipMalloc(&e->d_pushany, e->rows));
     const size_t rowbytes = e->rows * e->nwp * 8;
     e->tile_nodes = gg::kBlock / lanes_per_node((uint32_t)e->nwp);
     const uint64_t ntiles = (n_own + e->tile_nodes - 1) / e->tile_nodes;
@@ -2260,7 +2245,6 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
     int rc = materialize_windows(e);
     if (rc) return rc;
     if ((rc = ensure_db(e))) return rc;
-    if ((rc = ensure_sync(e, e->round + (int64_t)n - 1))) return rc;
     uint32_t done = 0;
     std::vector<size_t> off;
     e->step_event_ms = 0.0;
@@ -2377,7 +2361,6 @@ static int dist_begin(gg_engine* e, gg_exchange* x, bool host_sizes) {
     int rc = materialize_windows(e);
     if (rc) return rc;
     if ((rc = ensure_db(e))) return rc;
-    if ((rc = ensure_sync(e, e->round))) return rc;
     if (e->dist_k == kMaxBatch && (rc = fold_pending(e))) return rc;
     const int64_t r = e->round;
     std::vector<size_t> off;
