@@ -45,10 +45,11 @@ constexpr int kMaxBlocks = 2048;
 // bit-exact; only the kernels that run change): GG_HUB_DEG, GG_HUB_CHUNK,
 // GG_SYNC_TILES, GG_SYNC_DIGEST, GG_ORDER, GG_XCHG_MODE, GG_PREP_BLOCKS,
 // GG_SHARD_NATIVE (device-built shards keep native row order), GG_NO_DB (no
-// double-buffered lean rounds: the F-row kernels take them).
+// double-buffered lean rounds: the F-row kernels take them), GG_COMPACT_ATOMIC /
+// GG_COMPACT_SPLIT (one-launch or split compaction whatever the size).
 const char* test_knob(const char* name) { return getenv(name); }
 // A/B switches of past measurements (GG_ALL_FULL, GG_NO_GRAPH, GG_SYNC_ALLPUSH,
-// GG_FLAGS_FIRST, GG_XCHG_EXACT_BYTES): read only in a -DGG_AB_KNOBS build.
+// GG_FLAGS_FIRST, GG_FF_FRAC16, GG_XCHG_EXACT_BYTES): read only in a -DGG_AB_KNOBS build.
 #ifdef GG_AB_KNOBS
 const char* ab_knob(const char* name) { return getenv(name); }
 #else
@@ -239,6 +240,7 @@ struct gg_engine {
     uint8_t* d_tile_cand = nullptr;  // [tile_bytes]
     gg::TileWork* d_work = nullptr;  // [tiles] live-tile worklist (sparse sync/mask rounds)
     uint32_t* d_n_work = nullptr;    // [2] live tiles, candidate nodes
+    uint32_t* d_bcount = nullptr;    // [compact blocks + 1] split compaction (large graphs)
     uint32_t* d_nodes = nullptr;     // [n_own] candidate-node list (sparse lean rounds)
     uint32_t* d_act = nullptr;       // [4] ring: nodes that became active per round
     unsigned long long* d_act_deg = nullptr;  // [4] ring: their out-degree sums
@@ -248,6 +250,7 @@ struct gg_engine {
     unsigned long long* d_tot_s = nullptr;
     uint64_t* d_abits = nullptr;     // [rows/64] ACT bits of the previous round (flags-first rounds)
     bool ff_ok = false;              // flags-first gathers allowed
+    uint32_t ff_frac16 = 8;          // ... in rounds where < ff_frac16/16 of the in-edges carry data
     // hubs (see expand_kernels.hpp): in-edge chunks of high in-degree nodes,
     // out-edge chunks of high out-degree senders, per-chunk partial rows
     uint32_t hub_deg = 0;
@@ -374,6 +377,7 @@ void gg_engine::free_topology() {
     n_hubs = n_hchunks = n_mchunks = 0;
     dfree(d_work);
     dfree(d_n_work);
+    dfree(d_bcount);
     dfree(d_nodes);
     dfree(d_act);
     dfree(d_act_deg);
@@ -856,6 +860,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.tile_cand = e->d_tile_cand;
     a.work = e->d_work;
     a.n_work = e->d_n_work;
+    a.bcount = e->d_bcount;
     a.nodes = e->d_nodes;
     a.act = e->d_act;
     a.act_deg = e->d_act_deg;
@@ -863,7 +868,10 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.act_deg_s = e->d_act_deg_s;
     a.tot_s = e->d_tot_s;
     a.abits = e->d_abits;
-    a.ff_ok = e->ff_ok ? 1 : 0;
+    a.ff_ok = e->ff_ok ? (int32_t)e->ff_frac16 : 0;
+    // W = 64: a sender's F word is one 8-byte request, so below ~V/256 edges with
+    // data the saved gathers cost less than the bitmap pass over V flag bytes
+    a.ff_min = e->nwp == 1 ? e->n_own / 256 : 0;
     a.tile_nodes = (uint32_t)e->tile_nodes;
     a.symmetric = e->symmetric ? 1 : 0;
     a.n_edges = e->n_in_edges;
@@ -1009,8 +1017,14 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         {
             const uint64_t groups = (a.n_own + 7) / 8;  // >= tile groups
             const uint64_t per_block = (uint64_t)gg::kBlock * gg::kCompactQ;
-            hipLaunchKernelGGL(gg::compact_round, dim3((unsigned)((groups + per_block - 1) / per_block)),
-                               dim3(gg::kBlock), 0, e->stream, a);
+            const uint64_t nb = (groups + per_block - 1) / per_block;
+            if (e->d_bcount) {  // split compaction (large graphs): counts, offsets, list
+                hipLaunchKernelGGL(gg::compact_round<1>, dim3((unsigned)nb), dim3(gg::kBlock), 0, e->stream, a);
+                hipLaunchKernelGGL(gg::compact_scan, dim3(1), dim3(1024), 0, e->stream, a, (uint32_t)nb);
+                hipLaunchKernelGGL(gg::compact_round<2>, dim3((unsigned)nb), dim3(gg::kBlock), 0, e->stream, a);
+            } else {
+                hipLaunchKernelGGL(gg::compact_round<0>, dim3((unsigned)nb), dim3(gg::kBlock), 0, e->stream, a);
+            }
             HIPCHK(hipGetLastError());
         }
         if (sync_stream) {
@@ -1021,7 +1035,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             }
         } else if (a.stream_ok) {  // lean rounds: all nodes (dense) or the candidate list (sparse)
             if (e->ff_ok && !maskw) {  // the sender bitmap of a flags-first round (the kernel decides)
-                const uint64_t blocks = std::min<uint64_t>((e->rows + gg::kBlock - 1) / gg::kBlock, 4096);
+                const uint64_t blocks = std::min<uint64_t>((e->rows / 16 + gg::kBlock - 1) / gg::kBlock, 4096);
                 hipLaunchKernelGGL(gg::pack_act_bits, dim3((unsigned)blocks), dim3(gg::kBlock), 0, e->stream, a);
                 HIPCHK(hipGetLastError());
             }
@@ -1510,6 +1524,12 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     HIPCHK(hipMalloc(&e->d_tile_cand, e->tile_bytes));
     HIPCHK(hipMalloc(&e->d_work, std::max<uint64_t>(1, ntiles) * sizeof(gg::TileWork)));
     HIPCHK(hipMalloc(&e->d_n_work, 2 * sizeof(uint32_t)));
+    {  // split compaction when one atomic per block would serialise (compact_round)
+        const uint64_t per_block = (uint64_t)gg::kBlock * gg::kCompactQ;
+        const uint64_t nb = ((n_own + 7) / 8 + per_block - 1) / per_block;
+        if ((nb > gg::kCompactSplit || test_knob("GG_COMPACT_SPLIT")) && !test_knob("GG_COMPACT_ATOMIC"))
+            HIPCHK(hipMalloc(&e->d_bcount, (nb + 1) * sizeof(uint32_t)));
+    }
     HIPCHK(hipMalloc(&e->d_nodes, std::max<uint64_t>(1, n_own) * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->d_act, 4 * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&e->d_act_deg, 4 * 8));
@@ -1518,10 +1538,15 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     HIPCHK(hipMalloc(&e->d_act_deg_s, 4 * gg::kSlots * 8));
     HIPCHK(hipMalloc(&e->d_tot_s, 4 * gg::kSlots * 8));
     // flags-first gathers (ff_round): rows of >= 64 B (the request-rate-bound
-    // regime) and a mean in-degree >= 4; GG_FLAGS_FIRST=0/1 overrides
+    // regime) or of 8 B (expand_stream1: every gather a random 8-byte request,
+    // the bitmap 1/64 of the F words) and a mean in-degree >= 4;
+    // GG_FLAGS_FIRST=0/1 overrides, GG_FF_FRAC16 sets the threshold (A/B)
     {
         const char* f = ab_knob("GG_FLAGS_FIRST");
-        e->ff_ok = f ? atoi(f) != 0 : (e->nwp >= 8 && e->n_in_edges >= 4 * std::max<uint64_t>(1, n_own));
+        e->ff_ok = f ? atoi(f) != 0
+                     : ((e->nwp >= 8 || e->nwp == 1) && e->n_in_edges >= 4 * std::max<uint64_t>(1, n_own));
+        const char* q = ab_knob("GG_FF_FRAC16");
+        e->ff_frac16 = q ? (uint32_t)std::max(1, atoi(q)) : 8u;
         if (e->ff_ok) HIPCHK(hipMalloc(&e->d_abits, e->rows / 8));
     }
     HIPCHK(hipMalloc(&e->d_base, rowbytes));

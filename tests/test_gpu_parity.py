@@ -337,3 +337,34 @@ def test_saturated_node_learns_client_broadcast(hip_lib, cpu_lib, W):
         inj = [(0, 11, 0), (V - 1, 12, 0), (0, 13, 9), (V - 1, 14, 9), (V // 2, 15, 12), (0, 11, 14)]
         sc = Scenario(topo, W, 24, inj, seed=5, enable_sync=False)
         _compare(sc, hip_lib, cpu_lib)
+
+
+@pytest.mark.parametrize("knobs", ["split", "prep16", "both"])
+def test_large_graph_paths_vs_o2(hip_lib, cpu_lib, monkeypatch, knobs):
+    """Paths the engine takes by size, forced on 4K-10K-node graphs against O2
+    per round: split compaction (GG_COMPACT_SPLIT; by default above 8M nodes:
+    per-block counts, offsets, then the list) and round_prep's sparse scan over
+    16 nodes per thread (GG_PREP_BLOCKS=1: the capped grid covers fewer than a
+    quarter of the nodes, as at 2^26). The C5 shape at W = 64 also takes the
+    flags-first gathers of expand_stream1 in its sparse rounds (checked from the
+    gather counts); the C2 and C4 shapes the double-buffered and hub kernels;
+    lean and with sync timers."""
+    if knobs in ("split", "both"):
+        monkeypatch.setenv("GG_COMPACT_SPLIT", "1")
+    if knobs in ("prep16", "both"):
+        monkeypatch.setenv("GG_PREP_BLOCKS", "1")
+    cases = [
+        (T.grid_links(64, seed=5), 64, False),
+        (T.grid_links(100, seed=6), 64, True),
+        (T.tree(8192, 4), 1024, False),
+        (T.rmat(4096, 16, seed=4), 512, True),
+    ]
+    for k, (topo, W, sync) in enumerate(cases):
+        V = topo.n_nodes
+        inj = [(n, v, (3 * v) % 7) for n, v, _ in uniform_injections(V, W, seed=20 + k)]
+        sc = Scenario(topo, W, 36, inj, seed=13 + k, sync_base=9, enable_sync=sync)
+        sg, _ = _compare(sc, hip_lib, cpu_lib)
+        assert sum(s["new_bits"] for s in sg) > 0
+        if W == 64:  # flags-first: only senders active in r-1 are gathered (>= 4 in-edges per node)
+            assert any(0 < s["work_gathers"] < 2 * s["work_rows"] for s in sg[1:10]), \
+                [(s["work_gathers"], s["work_rows"]) for s in sg[:10]]
