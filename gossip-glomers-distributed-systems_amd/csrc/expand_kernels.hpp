@@ -557,20 +557,45 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
         auto ld16 = [&](const uint8_t* f, uint64_t q) -> ulonglong2 {
             return q < nq ? *reinterpret_cast<const ulonglong2*>(f + a.own0 + 16 * q) : make_ulonglong2(0ull, 0ull);
         };
-        uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-        ulonglong2 fp = ld16(a.flg_prev, q), fc = ld16(a.flg_cur, q);
-        for (; q < nq; q += stride) {
+        // active senders come in clusters (a wave front), so a lane walking the
+        // out-lists of its own up-to-16 active nodes one after another (dependent
+        // row pointer -> column -> mark chains) set the pace; the wave instead lists
+        // its active nodes in LDS and gives each lane one out-list at a time
+        __shared__ uint32_t s_act[kBlock / 64][64 * 16];
+        uint32_t* const L = s_act[threadIdx.x >> 6];
+        const int ln = threadIdx.x & 63;
+        uint64_t qb = (uint64_t)blockIdx.x * kBlock + (threadIdx.x & ~63u);  // wave-uniform loop
+        ulonglong2 fp = ld16(a.flg_prev, qb + ln), fc = ld16(a.flg_cur, qb + ln);
+        for (; qb < nq; qb += stride) {
+            const uint64_t q = qb + ln;
             const ulonglong2 np = ld16(a.flg_prev, q + stride), nc = ld16(a.flg_cur, q + stride);
-            const uint64_t n16 = a.n_own - 16 * q < 16 ? a.n_own - 16 * q : 16;
+            const uint64_t n16 = q >= nq ? 0 : (a.n_own - 16 * q < 16 ? a.n_own - 16 * q : 16);
             c_bytes += 2 * n16;
+            uint32_t actm = 0;
             if (fp.x | fp.y | fc.x | fc.y) {
                 for (uint32_t j = 0; j < (uint32_t)n16; ++j) {
                     const uint64_t wp = j < 8 ? fp.x : fp.y, wc = j < 8 ? fc.x : fc.y;
                     const uint8_t f = (uint8_t)(wp >> (8 * (j & 7))), fcj = (uint8_t)(wc >> (8 * (j & 7)));
-                    if (!(f | fcj)) continue;
-                    const uint64_t i = 16 * q + j, rep = a.own0 + i;
-                    if ((fcj & FL_ACT) || (f & FL_LAG) || (a.db && (f & FL_ACT))) a.cand[rep] = CA_NODE;
-                    if (!(f & FL_ACT)) continue;
+                    if ((fcj & FL_ACT) || (f & FL_LAG) || (a.db && (f & FL_ACT))) a.cand[a.own0 + 16 * q + j] = CA_NODE;
+                    if (f & FL_ACT) actm |= 1u << j;
+                }
+            }
+            const uint32_t cnt = (uint32_t)__popc(actm);
+            uint32_t incl = cnt;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if (ln >= o) incl += y;
+            }
+            const uint32_t total = __shfl(incl, 63, 64);
+            if (total) {
+                uint32_t pos = incl - cnt;
+                for (uint32_t m = actm; m; m &= m - 1) L[pos++] = (uint32_t)(16 * q) + (uint32_t)(__ffs(m) - 1);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (uint32_t k = ln; k < total; k += 64) {
+                    const uint64_t i = L[k];
                     const int64_t o0 = a.out_ptr[i];
                     int64_t o1 = a.out_ptr[i + 1];
                     if (a.hub_deg && o1 - o0 > (int64_t)a.hub_deg) o1 = o0;  // hub_mark does it
@@ -585,6 +610,7 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                             if (w[b] < a.n_own) a.cand[w[b]] = CA_NODE;
                     }
                 }
+                __builtin_amdgcn_wave_barrier();  // the list is rewritten next iteration
             }
             fp = np;
             fc = nc;

@@ -1,8 +1,8 @@
 #!/bin/bash
-# Same-box A/B of flags-first gathers in expand_stream1 (W = 64): C5 at 2^26
+# Same-box A/B of two engine builds on C5 at 2^26
 # nodes, per-round kernel times, alternated:
-#   pre  = libgossip_hip_pre.so (expand_stream1 without flags-first)
-#   cur  = libgossip_hip.so (flags-first below 8/16 of the in-edges carrying data)
+#   pre  = libgossip_hip_pre.so (the previous commit)
+#   cur  = libgossip_hip.so
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 P=gossip-glomers-distributed-systems_amd
