@@ -49,7 +49,7 @@ constexpr int kMaxBlocks = 2048;
 // GG_COMPACT_SPLIT (one-launch or split compaction whatever the size).
 const char* test_knob(const char* name) { return getenv(name); }
 // A/B switches of past measurements (GG_ALL_FULL, GG_NO_GRAPH, GG_SYNC_ALLPUSH,
-// GG_FLAGS_FIRST, GG_FF_FRAC16, GG_XCHG_EXACT_BYTES): read only in a -DGG_AB_KNOBS build.
+// GG_FLAGS_FIRST, GG_FF_FRAC16, GG_PREP_WIDE, GG_XCHG_EXACT_BYTES): read only in a -DGG_AB_KNOBS build.
 #ifdef GG_AB_KNOBS
 const char* ab_knob(const char* name) { return getenv(name); }
 #else
@@ -241,6 +241,7 @@ struct gg_engine {
     gg::TileWork* d_work = nullptr;  // [tiles] live-tile worklist (sparse sync/mask rounds)
     uint32_t* d_n_work = nullptr;    // [2] live tiles, candidate nodes
     uint32_t* d_bcount = nullptr;    // [compact blocks + 1] split compaction (large graphs)
+    uint64_t prep_cap = 1024;        // round_prep's grid cap in rounds without timers (GG_PREP_BLOCKS)
     uint32_t* d_nodes = nullptr;     // [n_own] candidate-node list (sparse lean rounds)
     uint32_t* d_act = nullptr;       // [4] ring: nodes that became active per round
     unsigned long long* d_act_deg = nullptr;  // [4] ring: their out-degree sums
@@ -872,6 +873,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     // W = 64: a sender's F word is one 8-byte request, so below ~V/256 edges with
     // data the saved gathers cost less than the bitmap pass over V flag bytes
     a.ff_min = e->nwp == 1 ? e->n_own / 256 : 0;
+    a.prep_wide = ab_knob("GG_PREP_WIDE") && atoi(ab_knob("GG_PREP_WIDE")) ? 1 : 0;
     a.tile_nodes = (uint32_t)e->tile_nodes;
     a.symmetric = e->symmetric ? 1 : 0;
     a.n_edges = e->n_in_edges;
@@ -979,7 +981,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             // grid-stride over the nodes; a capped grid keeps the launch cheap in
             // dense lean rounds, where it is a no-op (C2 A/B: 1024 blocks 1.99 ms/episode,
             // 4096 2.02, 256 2.10; GG_PREP_BLOCKS overrides)
-            static const uint64_t prep_cap = test_knob("GG_PREP_BLOCKS") ? (uint64_t)atoi(test_knob("GG_PREP_BLOCKS")) : 1024;
+            const uint64_t prep_cap = e->prep_cap;
             if (e->d_sat && r == base + 2) {  // the digest's first bits (sat_scan)
                 const uint64_t thr = a.n_own * std::max<uint64_t>(1, e->nwp / 2);
                 hipLaunchKernelGGL(gg::sat_scan, dim3((unsigned)((thr + gg::kBlock - 1) / gg::kBlock)), dim3(gg::kBlock),
@@ -1524,6 +1526,7 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     HIPCHK(hipMalloc(&e->d_tile_cand, e->tile_bytes));
     HIPCHK(hipMalloc(&e->d_work, std::max<uint64_t>(1, ntiles) * sizeof(gg::TileWork)));
     HIPCHK(hipMalloc(&e->d_n_work, 2 * sizeof(uint32_t)));
+    e->prep_cap = test_knob("GG_PREP_BLOCKS") ? (uint64_t)std::max(1, atoi(test_knob("GG_PREP_BLOCKS"))) : 1024;
     {  // split compaction when one atomic per block would serialise (compact_round)
         const uint64_t per_block = (uint64_t)gg::kBlock * gg::kCompactQ;
         const uint64_t nb = ((n_own + 7) / 8 + per_block - 1) / per_block;

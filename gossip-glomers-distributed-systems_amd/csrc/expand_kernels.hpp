@@ -155,6 +155,7 @@ struct RoundArgs {
     uint64_t* abits;            // [rows/64] bit u: sender u is ACT in round r-1 (pack_act_bits; flags-first)
     int32_t ff_ok;              // flags-first gathers allowed below ff_ok/16 of the in-edges carrying data (0: never)
     uint64_t ff_min;            // ... and from ff_min such edges on (the bitmap pass costs more in smaller rounds)
+    int32_t prep_wide;          // round_prep: the 16-nodes-per-thread sparse scan whatever the size (A/B)
     unsigned long long* tot;    // [4] ring: new bits of the owned nodes in rounds <= r (slot r&3), or nullptr
     unsigned long long full_new;  // n_own x lanes injected in rounds <= r-1: tot of r-1 equal to it means
                                   // every owned set holds every injected lane (sets hold injected lanes only)
@@ -541,7 +542,7 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
     unsigned long long c_reads = 0, c_read_oks = 0, c_dropped = 0, c_fired = 0, c_bytes = 0;
     const uint64_t nwords = (a.n_own + 63) / 64;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    if (!SYNCW && a.stream_ok && !a.n_ghost && (a.n_own + 3) / 4 > stride) {
+    if (!SYNCW && a.stream_ok && !a.n_ghost && (a.prep_wide || (a.n_own + 3) / 4 > stride)) {
         // sparse lean round without timers over more nodes than the capped grid
         // covers in four passes (the loop below, specialised): 16 nodes per
         // thread from one 16-byte load of each flag array (own0 % 64 == 0, rows
