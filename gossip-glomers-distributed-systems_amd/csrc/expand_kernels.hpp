@@ -221,8 +221,10 @@ struct RoundArgs {
                                 // in-edge e are in different groups (masked streaming rounds),
                                 // or the caller's per-edge mask (gg_set_partition windows)
     uint32_t ewin;              // bit k: window k is per-edge (ebits[k] decides, not grp[k])
-    const uint32_t* inj;        // (local node, lane) pairs sorted by node
-    uint32_t n_inj;
+    const uint32_t* inj;        // (local node, lane) pairs sorted by node (inj_tab: of the whole batch)
+    uint32_t n_inj;             // host count (inj_tab == nullptr: the kernels' count)
+    const uint32_t* inj_tab;    // this round's [first pair, end] in inj, in device memory (inj_p / inj_n): a
+                                // captured batch then replays for any injections with the same rounds
     unsigned long long* counters;  // [kSlots][kCounters]
     uint64_t n_own, own0, lo;   // own rows are local rows own0 .. own0+n_own-1 (own0 = 0)
     const uint32_t* gid;        // [rows] original node id of each local row (sharded), or
@@ -251,6 +253,16 @@ struct RoundArgs {
     uint32_t sync_base, sync_jitter;
     int32_t enable_sync;
 };
+
+// This round's client broadcasts: from the batch's device-resident offset table
+// when there is one (the launch sequence does not depend on the pairs), else
+// from the host-set pointer and count.
+__device__ __forceinline__ uint32_t inj_n(const RoundArgs& a) {
+    return a.inj_tab ? a.inj_tab[1] - a.inj_tab[0] : a.n_inj;
+}
+__device__ __forceinline__ const uint32_t* inj_p(const RoundArgs& a) {
+    return a.inj_tab ? a.inj + 2 * (size_t)a.inj_tab[0] : a.inj;
+}
 
 template <int WPL>
 struct Row {
@@ -333,7 +345,7 @@ __device__ __forceinline__ bool ff_round(const RoundArgs& a) {
 // injects nothing: no set can change (e.g. the quiescence round that ends an
 // episode), so a lean round gathers nothing; only stale F rows are cleared.
 __device__ __forceinline__ bool all_full(const RoundArgs& a) {
-    return a.tot && a.n_inj == 0 && a.tot[(a.round - 1) & 3] == a.full_new;
+    return a.tot && inj_n(a) == 0 && a.tot[(a.round - 1) & 3] == a.full_new;
 }
 
 // Original node id of local row i (hashes, sync timers, partition groups).
@@ -828,13 +840,17 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
 }
 
 // Client broadcasts of this round mark their nodes (after round_prep).
+// Grid-stride over a count read on the device (the grid does not depend on it).
 __global__ void mark_injections(RoundArgs a) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= a.n_inj) return;
-    const uint64_t i = a.inj[2 * k];
-    a.cand[a.own0 + i] |= CA_NODE | CA_INJ;  // same value from every thread of a node
-    if (!a.stream_ok) a.tile_cand[i / a.tile_nodes] = 1;  // lean rounds use the node list
+    const uint32_t n = inj_n(a);
+    const uint32_t* p = inj_p(a);
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const uint64_t i = p[2 * k];
+        a.cand[a.own0 + i] |= CA_NODE | CA_INJ;  // same value from every thread of a node
+        if (!a.stream_ok) a.tile_cand[i / a.tile_nodes] = 1;  // lean rounds use the node list
+    }
 }
+constexpr unsigned kMarkInjBlocks = 16;
 
 // Sparse rounds: the candidate nodes -> node list (lean rounds, expand_stream;
 // node-granular, so every node group gets the same share; kCompactQ groups of 8
@@ -1114,14 +1130,14 @@ __device__ __forceinline__ void expand_body(const RoundArgs& a) {
                     nrows += lag ? 2 : 1;
                     // (1) client broadcasts of this round
                     if (has_inj) {
-                        uint32_t lo = 0, hi = a.n_inj;
+                        uint32_t lo = 0, hi = inj_n(a);
                         while (lo < hi) {
                             const uint32_t mid = (lo + hi) >> 1;
-                            if (a.inj[2 * mid] < (uint32_t)i) lo = mid + 1;
+                            if (inj_p(a)[2 * mid] < (uint32_t)i) lo = mid + 1;
                             else hi = mid;
                         }
-                        for (uint32_t k = lo; k < a.n_inj && a.inj[2 * k] == (uint32_t)i; ++k) {
-                            const uint32_t lane = a.inj[2 * k + 1];
+                        for (uint32_t k = lo; k < inj_n(a) && inj_p(a)[2 * k] == (uint32_t)i; ++k) {
+                            const uint32_t lane = inj_p(a)[2 * k + 1];
                             const uint32_t word = lane >> 6;
                             if (word / WPL == (uint32_t)lg) set_lane_bit<WPL>(S, word % WPL, lane & 63);
                         }
@@ -1585,14 +1601,14 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         }
         S = sp;
         if (m0.ca & CA_INJ) {  // (1) client broadcasts of this round
-            uint32_t lo = 0, hi = a.n_inj;
+            uint32_t lo = 0, hi = inj_n(a);
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (a.inj[2 * mid] < (uint32_t)i) lo = mid + 1;
+                if (inj_p(a)[2 * mid] < (uint32_t)i) lo = mid + 1;
                 else hi = mid;
             }
-            for (uint32_t q = lo; q < a.n_inj && a.inj[2 * q] == (uint32_t)i; ++q) {
-                const uint32_t lane = a.inj[2 * q + 1];
+            for (uint32_t q = lo; q < inj_n(a) && inj_p(a)[2 * q] == (uint32_t)i; ++q) {
+                const uint32_t lane = inj_p(a)[2 * q + 1];
                 const uint32_t word = lane >> 6;
                 if (word / WPL == (uint32_t)lg) set_lane_bit<WPL>(S, word % WPL, lane & 63);
             }
@@ -1914,14 +1930,14 @@ void expand_stream1(RoundArgs a) {
         if (!hub) {
             uint64_t S = sp;
             if (m0.ca & CA_INJ) {  // (1) client broadcasts of this round
-                uint32_t lo = 0, hi = a.n_inj;
+                uint32_t lo = 0, hi = inj_n(a);
                 while (lo < hi) {
                     const uint32_t mid = (lo + hi) >> 1;
-                    if (a.inj[2 * mid] < (uint32_t)i) lo = mid + 1;
+                    if (inj_p(a)[2 * mid] < (uint32_t)i) lo = mid + 1;
                     else hi = mid;
                 }
-                for (uint32_t q = lo; q < a.n_inj && a.inj[2 * q] == (uint32_t)i; ++q)
-                    S |= 1ull << (a.inj[2 * q + 1] & 63);
+                for (uint32_t q = lo; q < inj_n(a) && inj_p(a)[2 * q] == (uint32_t)i; ++q)
+                    S |= 1ull << (inj_p(a)[2 * q + 1] & 63);
             }
             // (2) node broadcasts, ascending sender: first deliverer claims
             unsigned long long cl_recip = 0;
@@ -2299,14 +2315,14 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
         or_in(sp, of);
         Row<WPL> S = sp;
         if (x & SR_INJ) {  // (1) client broadcasts of this round
-            uint32_t lo = 0, hi = a.n_inj;
+            uint32_t lo = 0, hi = inj_n(a);
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (a.inj[2 * mid] < (uint32_t)i) lo = mid + 1;
+                if (inj_p(a)[2 * mid] < (uint32_t)i) lo = mid + 1;
                 else hi = mid;
             }
-            for (uint32_t q = lo; q < a.n_inj && a.inj[2 * q] == (uint32_t)i; ++q) {
-                const uint32_t lane = a.inj[2 * q + 1];
+            for (uint32_t q = lo; q < inj_n(a) && inj_p(a)[2 * q] == (uint32_t)i; ++q) {
+                const uint32_t lane = inj_p(a)[2 * q + 1];
                 const uint32_t word = lane >> 6;
                 if (word / WPL == (uint32_t)lg) set_lane_bit<WPL>(S, word % WPL, lane & 63);
             }
@@ -2537,14 +2553,14 @@ __global__ __launch_bounds__(kBlock) void expand_batched(RoundArgs a) {
         // (1) client broadcasts: a new client value goes to every neighbour
         bool inj_new = false;
         if (valid && (a.cand[rep] & CA_INJ)) {
-            uint32_t lo = 0, hi = a.n_inj;
+            uint32_t lo = 0, hi = inj_n(a);
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (a.inj[2 * mid] < (uint32_t)i) lo = mid + 1;
+                if (inj_p(a)[2 * mid] < (uint32_t)i) lo = mid + 1;
                 else hi = mid;
             }
-            for (uint32_t q = lo; q < a.n_inj && a.inj[2 * q] == (uint32_t)i; ++q) {
-                const uint32_t ln = a.inj[2 * q + 1];
+            for (uint32_t q = lo; q < inj_n(a) && inj_p(a)[2 * q] == (uint32_t)i; ++q) {
+                const uint32_t ln = inj_p(a)[2 * q + 1];
                 const uint32_t word = ln >> 6;
                 if (word / WPL == (uint32_t)lg) {
                     Row<WPL> b;
@@ -2953,14 +2969,14 @@ __global__ __launch_bounds__(kBlock) void hub_finish(RoundArgs a) {
             const uint64_t rep = a.own0 + i;
             Row<WPL> sp = load_row<WPL>((a.db ? a.base_prev : a.base) + rep * a.nwp + off), S = sp;  // lean: no LAG
             if (ca & CA_INJ) {  // (1) client broadcasts of this round
-                uint32_t lo = 0, hi = a.n_inj;
+                uint32_t lo = 0, hi = inj_n(a);
                 while (lo < hi) {
                     const uint32_t mid = (lo + hi) >> 1;
-                    if (a.inj[2 * mid] < i) lo = mid + 1;
+                    if (inj_p(a)[2 * mid] < i) lo = mid + 1;
                     else hi = mid;
                 }
-                for (uint32_t k = lo; k < a.n_inj && a.inj[2 * k] == i; ++k) {
-                    const uint32_t lane = a.inj[2 * k + 1];
+                for (uint32_t k = lo; k < inj_n(a) && inj_p(a)[2 * k] == i; ++k) {
+                    const uint32_t lane = inj_p(a)[2 * k + 1];
                     const uint32_t word = lane >> 6;
                     if (word / WPL == (uint32_t)lg) set_lane_bit<WPL>(S, word % WPL, lane & 63);
                 }
@@ -3203,14 +3219,14 @@ __global__ __launch_bounds__(kBlock) void hub_sync_finish(RoundArgs a) {
             }
             Row<WPL> S = sp;
             if (ca & CA_INJ) {  // (1) client broadcasts of this round
-                uint32_t lo = 0, hi = a.n_inj;
+                uint32_t lo = 0, hi = inj_n(a);
                 while (lo < hi) {
                     const uint32_t mid = (lo + hi) >> 1;
-                    if (a.inj[2 * mid] < i) lo = mid + 1;
+                    if (inj_p(a)[2 * mid] < i) lo = mid + 1;
                     else hi = mid;
                 }
-                for (uint32_t k = lo; k < a.n_inj && a.inj[2 * k] == i; ++k) {
-                    const uint32_t lane = a.inj[2 * k + 1];
+                for (uint32_t k = lo; k < inj_n(a) && inj_p(a)[2 * k] == i; ++k) {
+                    const uint32_t lane = inj_p(a)[2 * k + 1];
                     const uint32_t word = lane >> 6;
                     if (word / WPL == (uint32_t)lg) set_lane_bit<WPL>(S, word % WPL, lane & 63);
                 }

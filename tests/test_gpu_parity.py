@@ -368,3 +368,34 @@ def test_large_graph_paths_vs_o2(hip_lib, cpu_lib, monkeypatch, knobs):
         if W == 64:  # flags-first: only senders active in r-1 are gathered (>= 4 in-edges per node)
             assert any(0 < s["work_gathers"] < 2 * s["work_rows"] for s in sg[1:10]), \
                 [(s["work_gathers"], s["work_rows"]) for s in sg[:10]]
+
+
+def test_fresh_injections_replay_vs_o2(hip_lib, cpu_lib):
+    """Episodes with fresh injection sets in the same rounds (same lanes per
+    round) replay the captured launch sequence, which reads the pairs and each
+    round's share from device memory: every episode equals O2, including one
+    whose rounds inject different numbers of pairs and one with a round's
+    pairs moved to another round."""
+    rnd = random.Random(31)
+    base = random_scenario(rnd, max_v=500, W=256, rounds=30)
+    base.windows = []
+    V = base.topo.n_nodes
+    g = make_engine(hip_lib, base)
+    g.step(base.rounds)
+    for ep in range(5):
+        rr = random.Random(100 + ep)
+        if ep < 3:  # same rounds, same count per round, fresh nodes
+            inj = [(rr.randrange(V), v, r) for _, v, r in base.injections]
+        elif ep == 3:  # same rounds, other counts per round
+            inj = [(rr.randrange(V), v, r) for _, v, r in base.injections for _ in range(rr.randrange(1, 3))]
+        else:  # other rounds
+            inj = [(rr.randrange(V), v, (r + 1) % 6) for _, v, r in base.injections]
+        c = make_engine(cpu_lib, base)
+        c.reset()
+        g.reset()
+        for eng in (g, c):
+            for n, v, r in inj:
+                eng.broadcast(n, v, r)
+        d = diff_stats(c.step(base.rounds), g.step(base.rounds))
+        assert not d, (ep, d[:10])
+        assert np.array_equal(g.read_bits(), c.read_bits())
