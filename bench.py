@@ -65,19 +65,22 @@ TRAFFIC_JSON = {"C2": os.path.join(REPO, "profiles", "traffic.json"),  # committ
 CPU_LIB = os.path.join(REPO, "oracle", "_build", "libgossip_cpu.so")
 
 
-def pmc_traffic(kind: str, config: str):
+def pmc_traffic(kind: str, shape: dict):
     """HBM bytes per round of a kernel kind from the committed rocprofv3 PMC
     passes (tools/traffic.py: FETCH_SIZE and WRITE_SIZE in separate passes over
     this same bench command, FETCH_SIZE doubled for gfx950): the sum over the
     kind's kernels of bytes x dispatches, per dispatch of its main kernel (one
-    per round). None if not profiled."""
-    path = TRAFFIC_JSON.get(config)
+    per round). None unless the passes profiled a run of exactly this shape
+    (config, nodes, lanes, world, parts, halves): another run's traffic is not
+    this run's."""
+    path = TRAFFIC_JSON.get(shape["config"])
     try:
         d = json.load(open(path))
     except (OSError, ValueError, TypeError):
         return None, None
-    if d.get("config", "C2") != config:
-        return None, None
+    if d.get("shape") != shape:
+        return None, (f"{os.path.relpath(path, REPO)} profiled {d.get('shape')}, not this run's {shape}: "
+                      "no counter traffic for this shape")
     base = lambda name: name.split("(")[0].split("<")[0].split("::")[-1]  # noqa: E731
     ents = {}
     for name, ent in d.get("kernels", {}).items():
@@ -357,7 +360,9 @@ def main():
     dom = max(kinds, key=lambda k: kinds[k]["total_ms"])
     D = kinds[dom]
     achieved = D["GBps"]
-    traffic, traffic_src = pmc_traffic(dom, cfg)
+    shape = {"config": cfg, "nodes": V // world if cfg == "C2" else V, "lanes": K, "world": world,
+             "parts": args.parts if cfg == "C4" else world, "halves": len(engs)}
+    traffic, traffic_src = pmc_traffic(dom, shape)
     round_ms = sum(s["kernel_ms"] for s in rounds_local)
     round_bytes = sum(s["prep_bytes"] + s["expand_bytes"] + s["stream_bytes"] for s in rounds_local)
     xbytes = None

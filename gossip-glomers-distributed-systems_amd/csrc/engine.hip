@@ -45,7 +45,9 @@ constexpr int kMaxBlocks = 2048;
 // bit-exact; only the kernels that run change): GG_HUB_DEG, GG_HUB_CHUNK,
 // GG_SYNC_TILES, GG_SYNC_DIGEST, GG_ORDER, GG_XCHG_MODE, GG_PREP_BLOCKS,
 // GG_SHARD_NATIVE (device-built shards keep native row order), GG_NO_DB (no
-// double-buffered lean rounds: the F-row kernels take them), GG_COMPACT_ATOMIC /
+// double-buffered lean rounds: the F-row kernels take them), GG_DB (double-buffered
+// lean rounds whatever the free memory), GG_SYNC_EAGER / GG_SYNC_ALLOC_ROUND (the
+// streamed-sync buffers with the topology / from a given round), GG_COMPACT_ATOMIC /
 // GG_COMPACT_SPLIT (one-launch or split compaction whatever the size).
 const char* test_knob(const char* name) { return getenv(name); }
 // A/B switches of past measurements (GG_ALL_FULL, GG_NO_GRAPH, GG_SYNC_ALLPUSH,
@@ -212,6 +214,8 @@ struct gg_engine {
     uint32_t dist_k = 0;                       // pending rounds (counter slots in use)
     uint32_t ctr_dirty = kMaxBatch;            // counter slots [0, ctr_dirty) may be non-zero
     std::vector<int64_t> dist_round_of;        // round of each pending slot
+    std::vector<uint64_t> dist_path;           // its kernel path (GG_PATH_*)
+    uint64_t last_path = 0;                    // path of the round enqueue_round enqueued last
     std::vector<uint64_t> dist_sent;           // payload bytes sent in each pending slot
     std::vector<gg_round_stats> dist_done;     // folded, not yet flushed
     size_t inj_off = 0;                        // pinned injection ring offset (async rounds)
@@ -233,6 +237,7 @@ struct gg_engine {
     int set_cur = 0;
     bool f_dirty = true;      // some F row may be non-zero (reset must clear them)
     bool db_decided = false;  // ensure_db ran since the topology was installed
+    bool sync_alloc = false;  // alloc_sync ran since the topology was installed
     uint64_t* d_F[2] = {nullptr, nullptr};
     uint8_t* d_flg[2] = {nullptr, nullptr};
     uint8_t* d_cand = nullptr;       // [rows] candidate bytes
@@ -734,7 +739,11 @@ void launch_stream_sync(const gg::RoundArgs& a, hipStream_t s) {
 
 // Number of distinct lanes of this engine's word range broadcast in rounds
 // <= r (every engine sees every broadcast: gg_broadcast does not filter by
-// owner), extended round by round while the rounds' lists are still held.
+// owner), extended round by round from the rounds' lists. A round's list is
+// dropped once the round has run (retire_round), which first extends the
+// history through that round: a history extended past a dropped list would
+// miss its lanes (the saturation digest, the all-full test and expand_stream1's
+// saturation skip all compare set sizes with these counts).
 uint32_t lanes_through(gg_engine* e, int64_t r) {
     if (r < 0) return 0;
     if (e->u_bits.size() != e->nw) e->u_bits.assign(e->nw, 0);
@@ -754,6 +763,13 @@ uint32_t lanes_through(gg_engine* e, int64_t r) {
         e->u_hist.push_back(u);
     }
     return e->u_hist[r];
+}
+
+// Round r has run: its client broadcasts are no longer needed, once the lane
+// history covers it.
+void retire_round(gg_engine* e, int64_t r) {
+    (void)lanes_through(e, r);
+    e->inj.erase(r);
 }
 
 template <int G, int WPL>
@@ -787,6 +803,67 @@ bool sync_stream_at(gg_engine* e, int64_t r) {
     return true;
 }
 
+// The streamed-sync buffers (records, sender states and their bitmap, the node
+// list with its bytes, the saturation digest, the reverse edge index, push
+// bytes): no round before the first timer round reads or writes any of them
+// (round_prep, sync_records and the sync expand kernels are the only users, and
+// those run from round sync_base on), so an episode that ends before the timers
+// never needs them — C5 at 2^30 nodes: 66 GiB of the 145. Allocated zeroed at
+// the first call that enqueues a round >= sync_base, which is before the first
+// round whose kernels touch them; from then on they stay for the topology's
+// life (gg_reset keeps them). Every reader of them reads what a kernel of the
+// same or the previous round wrote (pushb/pushany: the callback of r-1; sstate,
+// ibits: round_prep of r; srec, nmeta: the round's own launches; sat: zero or
+// bits of earlier rounds of this episode), so where in the episode the
+// allocation happens cannot change a result.
+int alloc_sync(gg_engine* e) {
+    if (e->sync_alloc) return GG_OK;
+    e->sync_alloc = true;
+    const uint64_t n_own = e->n_own;
+    auto zalloc = [&](auto*& p, size_t bytes) -> int {
+        HIPCHK(hipMalloc(&p, std::max<size_t>(bytes, 8)));
+        HIPCHK(hipMemsetAsync(p, 0, std::max<size_t>(bytes, 8), e->stream));
+        return GG_OK;
+    };
+    int rc = GG_OK;
+    if (e->cfg.enable_sync && !e->cfg.batch_ticks && (e->n_hubs == 0 || e->symmetric) && !e->sync_tiles && n_own) {
+        if ((rc = zalloc(e->d_srec, 2 * n_own * sizeof(uint4)))) return rc;
+        if ((rc = zalloc(e->d_sstate, e->rows))) return rc;
+        if ((rc = zalloc(e->d_ibits, e->rows / 8))) return rc;
+        if ((rc = zalloc(e->d_nmeta, n_own * sizeof(uint2)))) return rc;
+        // saturation digest (GG_SYNC_DIGEST=0 turns it off, for A/B)
+        if (!(test_knob("GG_SYNC_DIGEST") && atoi(test_knob("GG_SYNC_DIGEST")) == 0)) {
+            if ((rc = zalloc(e->d_sat, e->rows / 8))) return rc;
+            if ((rc = zalloc(e->d_sat_new, e->rows / 8))) return rc;
+        }
+        if (e->n_in_edges) {  // receivers look up whether an owned pusher sent them anything
+            HIPCHK(hipMalloc(&e->d_rev, e->n_in_edges * 4));
+            const unsigned blocks = (unsigned)std::min<uint64_t>((e->n_in_edges / 8 + 255) / 256 + 1, 16384);
+            hipLaunchKernelGGL(gg::build_rev, dim3(blocks), dim3(256), 0, e->stream, e->d_in_ptr, e->d_in_col,
+                               e->d_out_ptr, e->d_out_col, e->d_gid, n_own, e->n_in_edges, e->d_rev);
+            HIPCHK(hipGetLastError());
+        }
+    }
+    // non-empty pushes per out-edge, written by each sync callback (SyncBroadcast
+    // sends nothing for an empty difference): receivers of empty pushes are not
+    // candidates (GG_SYNC_ALLPUSH=1 keeps every push edge, for A/B)
+    if (e->cfg.enable_sync && e->n_out_edges && !(ab_knob("GG_SYNC_ALLPUSH") && atoi(ab_knob("GG_SYNC_ALLPUSH"))))
+        if ((rc = zalloc(e->d_pushb, e->n_out_edges))) return rc;
+    if (!e->d_pushb) dfree(e->d_rev);
+    if (e->d_pushb && e->d_srec)
+        if ((rc = zalloc(e->d_pushany, e->rows))) return rc;
+    return GG_OK;
+}
+
+// Before enqueueing rounds up to last_round: the streamed-sync buffers once a
+// timer round is among them (alloc_sync).
+int ensure_sync(gg_engine* e, int64_t last_round) {
+    static const char* at = test_knob("GG_SYNC_ALLOC_ROUND");  // A/B: allocate from this round on
+    const int64_t r0 = at ? (int64_t)atoi(at) : (int64_t)e->cfg.sync_base_ticks;
+    if (e->sync_alloc || !e->cfg.enable_sync || last_round < r0) return GG_OK;
+    return alloc_sync(e);
+}
+
 // Double-buffered lean rounds need a second set buffer: W >= 128 (the streaming
 // kernels), not batched, and 16 GiB of HBM left free after it and the F rows.
 // Decided at the first step after an install (round 0, so the episode starts in
@@ -800,8 +877,12 @@ int ensure_db(gg_engine* e) {
     (void)hipMemGetInfo(&free_b, &total_b);
     // (graphs with hubs are bound by their gathers: C4 at 10^8 nodes ran 1.154 s per
     // episode either way, profiles/r3/bench_c4_db.json, so they keep their HBM)
+    // GG_NO_DB=1 / GG_DB=1 (test hooks): never / whenever the graph allows it,
+    // whatever the free memory (the tests pin both paths; gg_round_stats.path says
+    // which one a round took)
+    const bool force = test_knob("GG_DB") && atoi(test_knob("GG_DB"));
     const bool ok = e->round == 0 && e->nwp >= 2 && e->nwp <= 128 && !e->cfg.batch_ticks && e->n_hubs == 0 &&
-                    free_b > rowbytes + (16ull << 30) && !test_knob("GG_NO_DB");
+                    (force || free_b > rowbytes + (16ull << 30)) && !test_knob("GG_NO_DB");
     if (!ok) return GG_OK;
     HIPCHK(hipMalloc(&e->d_sets[1], rowbytes));
     HIPCHK(hipMemsetAsync(e->d_sets[1], 0, rowbytes, e->stream));
@@ -836,11 +917,28 @@ void db_advance(gg_engine* e, int64_t r, bool db) {
     e->d_base = e->d_sets[e->set_cur];
 }
 
+// Which kernel path round r takes (gg_round_stats.path, diagnostics): the host
+// decides it from the round number, the windows and the buffers, so a replayed
+// batch reports the same bits as the enqueued one. db: db_round(e, r) before
+// db_advance.
+uint64_t path_of(const gg_engine* e, int64_t r, bool db) {
+    if (e->cfg.batch_ticks) return GG_PATH_BATCHED;
+    bool maskw = false;
+    for (int k = 0; k < 5; ++k) maskw |= window_at(e, r - 3 + k) != nullptr;
+    const bool syncw = e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks + 2;
+    uint64_t p = maskw ? GG_PATH_MASKED : 0;
+    if (db) return p | GG_PATH_DB;
+    if (syncw && !maskw && e->d_srec) return p | GG_PATH_SYNC_STREAM;
+    const bool lean = !syncw && (!maskw || (e->symmetric && e->n_hubs == 0 && e->nwp >= 2));
+    return p | (lean ? GG_PATH_STREAM : GG_PATH_TILES);
+}
+
 // Enqueue round e->round (kernels only). inj: device pairs for this round.
 int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned long long* d_ctr,
                   const uint32_t* d_tab = nullptr) {
     const int64_t r = e->round;
     const bool db = db_round(e, r);
+    e->last_path = path_of(e, r, db);
     if (e->db_active && !db && r > 0) {
         // the first round that needs F rows: those of round r-1, from its two set buffers
         const uint64_t n = e->n_own * e->nwp;
@@ -1096,6 +1194,7 @@ void fold_stats(gg_engine* e, const unsigned long long* slots, int64_t round, gg
     s->expand_bytes = c[gg::kBytes0 + gg::K_EXPAND];
     s->stream_bytes = c[gg::kBytes0 + gg::K_STREAM];
     s->sent_bytes = 0;
+    s->path = 0;
     s->round = round;
     s->new_bits = c[gg::C_NEW];
     s->fwd_sent = c[gg::C_FWD_SENT];
@@ -1521,31 +1620,9 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
                 HIPCHK(hipMemset(e->d_bset[b], 0, e->rows * e->nwp * 8));
             }
     }
-    if (e->cfg.enable_sync && !e->cfg.batch_ticks && (e->n_hubs == 0 || e->symmetric) && !e->sync_tiles && n_own) {
-        HIPCHK(hipMalloc(&e->d_srec, 2 * n_own * sizeof(uint4)));
-        HIPCHK(hipMalloc(&e->d_sstate, e->rows));
-        HIPCHK(hipMalloc(&e->d_ibits, e->rows / 8));
-        HIPCHK(hipMalloc(&e->d_nmeta, n_own * sizeof(uint2)));
-        // saturation digest (GG_SYNC_DIGEST=0 turns it off, for A/B)
-        if (!(test_knob("GG_SYNC_DIGEST") && atoi(test_knob("GG_SYNC_DIGEST")) == 0)) {
-            HIPCHK(hipMalloc(&e->d_sat, e->rows / 8));
-            HIPCHK(hipMalloc(&e->d_sat_new, e->rows / 8));
-        }
-        if (e->n_in_edges) {  // receivers look up whether an owned pusher sent them anything
-            HIPCHK(hipMalloc(&e->d_rev, e->n_in_edges * 4));
-            const unsigned blocks = (unsigned)std::min<uint64_t>((e->n_in_edges / 8 + 255) / 256 + 1, 16384);
-            hipLaunchKernelGGL(gg::build_rev, dim3(blocks), dim3(256), 0, e->stream, e->d_in_ptr, e->d_in_col,
-                               e->d_out_ptr, e->d_out_col, e->d_gid, n_own, e->n_in_edges, e->d_rev);
-            HIPCHK(hipGetLastError());
-        }
-    }
-    // non-empty pushes per out-edge, written by each sync callback (SyncBroadcast
-    // sends nothing for an empty difference): receivers of empty pushes are not
-    // candidates (GG_SYNC_ALLPUSH=1 keeps every push edge, for A/B)
-    if (e->cfg.enable_sync && e->n_out_edges && !(ab_knob("GG_SYNC_ALLPUSH") && atoi(ab_knob("GG_SYNC_ALLPUSH"))))
-        HIPCHK(hipMalloc(&e->d_pushb, e->n_out_edges));
-    if (!e->d_pushb) dfree(e->d_rev);
-    if (e->d_pushb && e->d_srec) HIPCHK(hipMalloc(&e->d_pushany, e->rows));
+    // the streamed-sync buffers: before the first round that reaches a timer
+    // (ensure_sync), not here; GG_SYNC_EAGER=1 allocates them with the topology
+    e->sync_alloc = false;
     const size_t rowbytes = e->rows * e->nwp * 8;
     e->tile_nodes = gg::kBlock / lanes_per_node((uint32_t)e->nwp);
     const uint64_t ntiles = (n_own + e->tile_nodes - 1) / e->tile_nodes;
@@ -1611,6 +1688,10 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     e->dist_open = false;
     e->u_hist.clear();
     e->u_bits.clear();
+    if (test_knob("GG_SYNC_EAGER") && atoi(test_knob("GG_SYNC_EAGER"))) {
+        const int rc = alloc_sync(e);
+        if (rc) return rc;
+    }
     return reset_device_state(e);
 }
 
@@ -1955,13 +2036,31 @@ static int install_shard(gg_engine* e, gg_gen::Csr g, const std::vector<uint64_t
         (void)hipFree(g.col);
         return e->fail(rc, err);
     }
-    // rows in locality order (the single engine's degree order): hot rows together
+    // until the engine owns them, every device array of the shard is freed on an
+    // error (gg_topology_part hands its caller's rows in through this path)
     std::vector<uint32_t> own_row;
     uint32_t* d_grow = nullptr;
+    auto drop = [&](int code, const std::string& m) {
+        for (void* p : {(void*)g.row_ptr, (void*)g.col, (void*)sh.send_idx, (void*)sh.gout_ptr, (void*)sh.gout_col,
+                        (void*)sh.gout_sidx, (void*)sh.gid, (void*)d_grow})
+            if (p) (void)hipFree(p);
+        return e->fail(code, m);
+    };
+    // rows in locality order (the single engine's degree order): hot rows together
     g.V = n_own;
     if (!test_knob("GG_SHARD_NATIVE")) {
         rc = gg_gen::shard_reorder(&g, &sh, ghost0, gg::kRecipBit, e->stream, &d_grow, &own_row, &err);
-        if (rc) return e->fail(rc, err);
+        if (rc) return drop(rc, err);
+    }
+    const uint64_t rows = std::max<uint64_t>(64, (ghost0 + sh.n_ghost + 63) / 64 * 64);
+    if (rows > 0x7fffffffull) return drop(GG_EINVAL, "local rows exceed 2^31");
+    e->gid.assign(rows, ~0u);
+    if (own_row.empty()) {
+        for (uint64_t i = 0; i < n_own; ++i) e->gid[i] = (uint32_t)(lo + i);
+        for (uint64_t k = 0; k < sh.n_ghost; ++k) e->gid[ghost0 + k] = sh.ghosts_host[k];
+    } else {  // the reordered rows' ids
+        const hipError_t ce = hipMemcpy(e->gid.data(), sh.gid, rows * 4, hipMemcpyDeviceToHost);
+        if (ce != hipSuccess) return drop(GG_EIO, std::string("hipMemcpy(gid): ") + hipGetErrorString(ce));
     }
     e->range_mode = true;
     e->range_lo = lo;
@@ -1971,15 +2070,7 @@ static int install_shard(gg_engine* e, gg_gen::Csr g, const std::vector<uint64_t
     e->n_own = n_own;
     e->n_ghost = sh.n_ghost;
     e->ghost0 = ghost0;
-    e->rows = std::max<uint64_t>(64, (ghost0 + sh.n_ghost + 63) / 64 * 64);
-    if (e->rows > 0x7fffffffull) return e->fail(GG_EINVAL, "local rows exceed 2^31");
-    e->gid.assign(e->rows, ~0u);
-    if (own_row.empty()) {
-        for (uint64_t i = 0; i < n_own; ++i) e->gid[i] = (uint32_t)(lo + i);
-        for (uint64_t k = 0; k < sh.n_ghost; ++k) e->gid[ghost0 + k] = sh.ghosts_host[k];
-    } else {  // the reordered rows' ids
-        HIPCHK(hipMemcpy(e->gid.data(), sh.gid, e->rows * 4, hipMemcpyDeviceToHost));
-    }
+    e->rows = rows;
     std::vector<uint32_t>().swap(sh.ghosts_host);
     e->own_row.swap(own_row);
     e->d_grow = d_grow;
@@ -2115,10 +2206,15 @@ int gg_topology_part(gg_engine* e, const uint64_t* part_lo, const int64_t* row_p
     gg_gen::Csr g{};
     g.V = n;
     g.nnz = nnz;
-    HIPCHK(hipMalloc(&g.row_ptr, (n + 1) * 8));
-    HIPCHK(hipMalloc(&g.col, std::max<uint64_t>(1, nnz) * 4));
-    HIPCHK(hipMemcpy(g.row_ptr, row_ptr, (n + 1) * 8, hipMemcpyHostToDevice));
-    if (nnz) HIPCHK(hipMemcpy(g.col, col, nnz * 4, hipMemcpyHostToDevice));
+    hipError_t ue = hipMalloc(&g.row_ptr, (n + 1) * 8);
+    if (ue == hipSuccess) ue = hipMalloc(&g.col, std::max<uint64_t>(1, nnz) * 4);
+    if (ue == hipSuccess) ue = hipMemcpy(g.row_ptr, row_ptr, (n + 1) * 8, hipMemcpyHostToDevice);
+    if (ue == hipSuccess && nnz) ue = hipMemcpy(g.col, col, nnz * 4, hipMemcpyHostToDevice);
+    if (ue != hipSuccess) {
+        if (g.row_ptr) (void)hipFree(g.row_ptr);
+        if (g.col) (void)hipFree(g.col);
+        return e->fail(GG_EIO, std::string("gg_topology_part upload: ") + hipGetErrorString(ue));
+    }
     return install_shard(e, g, plo, nullptr);
 }
 
@@ -2302,6 +2398,7 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
     int rc = materialize_windows(e);
     if (rc) return rc;
     if ((rc = ensure_db(e))) return rc;
+    if ((rc = ensure_sync(e, e->round + (int64_t)n - 1))) return rc;
     uint32_t done = 0;
     std::vector<size_t> off;
     e->step_event_ms = 0.0;
@@ -2346,15 +2443,21 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
         e->db_active = save_db;
         e->f_dirty = save_fd;
         e->set_cur = save_set;
-        for (uint32_t k = 0; k < m; ++k) db_advance(e, r0 + k, db_round(e, r0 + k));
+        std::vector<uint64_t> paths(m);
+        for (uint32_t k = 0; k < m; ++k) {
+            const bool dbk = db_round(e, r0 + k);
+            paths[k] = path_of(e, r0 + k, dbk);
+            db_advance(e, r0 + k, dbk);
+        }
         if (rc) return rc;
         HIPCHK(hipStreamSynchronize(e->stream));
         for (uint32_t k = 0; k < m; ++k) {
             gg_round_stats s;
             fold_stats(e, e->h_counters + (size_t)k * gg::kCounters, r0 + k, &s, 1);
+            s.path = paths[k];
             e->quiet = s.new_bits ? 0 : e->quiet + 1;
             if (out) out[done + k] = s;
-            e->inj.erase(r0 + k);
+            retire_round(e, r0 + k);
         }
         done += m;
     }
@@ -2395,6 +2498,7 @@ static int fold_pending(gg_engine* e) {
     for (uint32_t k = 0; k < e->dist_k; ++k) {
         gg_round_stats s;
         fold_stats(e, e->h_counters + (size_t)k * gg::kSlots * gg::kCounters, e->dist_round_of[k], &s);
+        s.path = e->dist_path[k];
         s.sent_bytes = e->d_payload ? e->dist_sent[k] : 0;
         e->dist_done.push_back(s);
     }
@@ -2418,6 +2522,7 @@ static int dist_begin(gg_engine* e, gg_exchange* x, bool host_sizes) {
     int rc = materialize_windows(e);
     if (rc) return rc;
     if ((rc = ensure_db(e))) return rc;
+    if ((rc = ensure_sync(e, e->round))) return rc;
     if (e->dist_k == kMaxBatch && (rc = fold_pending(e))) return rc;
     const int64_t r = e->round;
     std::vector<size_t> off;
@@ -2444,8 +2549,10 @@ static int dist_begin(gg_engine* e, gg_exchange* x, bool host_sizes) {
     if ((rc = enqueue_round(e, d_inj, (uint32_t)total, ctr))) return rc;
     const uint32_t P = e->P;
     if (e->dist_round_of.size() < kMaxBatch) e->dist_round_of.resize(kMaxBatch);
+    if (e->dist_path.size() < kMaxBatch) e->dist_path.resize(kMaxBatch);
     if (e->dist_sent.size() < kMaxBatch) e->dist_sent.resize(kMaxBatch);
     e->dist_round_of[e->dist_k] = r;
+    e->dist_path[e->dist_k] = e->last_path;
     e->xsend_bytes.assign(e->world, 0);
     e->xrecv_bytes.assign(e->world, 0);
     e->xsend_off.assign(e->world, 0);
@@ -2549,7 +2656,7 @@ int gg_dist_round_end(gg_engine* e, gg_round_stats* out) {
         HIPCHK(hipGetLastError());
     }
     e->dist_k++;
-    e->inj.erase(r);
+    retire_round(e, r);
     e->round++;
     e->dist_open = false;
     if (out) {
@@ -2655,13 +2762,26 @@ int gg_dist_comm_available(char* why, uint64_t cap) {
     return r.ok ? GG_OK : GG_EIO;
 }
 
-int gg_dist_comm_id(uint8_t* id_out) {
-    if (!id_out) return GG_EINVAL;
+// The id carries the lane group and part count it was made for in its last 12
+// bytes (RCCL's bootstrap handle — a magic and a socket address — leaves them
+// zero; gg_dist_comm_id checks that), so gg_dist_comm_init can refuse an id of
+// another lane group before ncclCommInitRank, where ranks of two groups with
+// the same part numbers would fail or hang undetectably.
+constexpr size_t kIdTag = 116;
+constexpr uint32_t kIdMagic = 0x474c4747u;  // "GGLG"
+
+int gg_dist_comm_id(const gg_engine* e, uint8_t* id_out) {
+    if (!e || !id_out) return GG_EINVAL;
+    static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
     const RcclApi& r = rccl();
     if (!r.ok) return GG_EIO;
     ncclUniqueId id;
     if (r.get_id(&id) != ncclSuccess) return GG_EIO;
     std::memcpy(id_out, &id, sizeof(id));
+    for (size_t k = kIdTag; k < 128; ++k)
+        if (id_out[k]) return GG_EIO;  // this RCCL uses the bytes the tag would take
+    const uint32_t tag[3] = {kIdMagic, e->lgrp, e->P};
+    std::memcpy(id_out + kIdTag, tag, sizeof(tag));
     return GG_OK;
 }
 
@@ -2670,11 +2790,20 @@ int gg_dist_comm_init(gg_engine* e, const uint8_t* id_in) {
     if (e->world < 2) return e->fail(GG_EINVAL, "not a sharded engine (world == 1)");
     if (e->comm || e->have_xport) return e->fail(GG_EINVAL, "exchange transport already set");
     if (e->P < 2) return e->fail(GG_EINVAL, "no vertex parts (lane_groups == world): nothing to exchange");
+    uint32_t tag[3];
+    std::memcpy(tag, id_in + kIdTag, sizeof(tag));
+    if (tag[0] != kIdMagic) return e->fail(GG_EINVAL, "gg_dist_comm_init: not an id from gg_dist_comm_id");
+    if (tag[1] != e->lgrp || tag[2] != e->P)
+        return e->fail(GG_EINVAL, "gg_dist_comm_init: the id was made for lane group " + std::to_string(tag[1]) +
+                                      " of " + std::to_string(tag[2]) + " parts, this engine is lane group " +
+                                      std::to_string(e->lgrp) + " of " + std::to_string(e->P) +
+                                      " (one id per lane group)");
     const RcclApi& r = rccl();
     if (!r.ok) return e->fail(GG_EIO, r.why);
     HIPCHK(hipSetDevice(e->device));
     ncclUniqueId id;
     std::memcpy(&id, id_in, sizeof(id));
+    std::memset(reinterpret_cast<uint8_t*>(&id) + kIdTag, 0, 128 - kIdTag);  // RCCL's own bytes only
     ncclComm_t c = nullptr;
     // one communicator per lane group: its P parts, rank = part (lane groups never
     // exchange anything, and a process may hold engines of several lane groups)
@@ -2961,6 +3090,35 @@ int gg_reset(gg_engine* e) {
     if (!e->have_topo) return GG_OK;
     HIPCHK(hipSetDevice(e->device));
     return reset_device_state(e);
+}
+
+int gg_device_bytes(const gg_engine* e, uint64_t* total, uint64_t* sync_part) {
+    if (!e) return GG_EINVAL;
+    if (hipSetDevice(e->device) != hipSuccess) return GG_EIO;
+    auto size_of = [](const void* p) -> uint64_t {
+        size_t n = 0;
+        return (p && hipMemPtrGetInfo(const_cast<void*>(p), &n) == hipSuccess) ? (uint64_t)n : 0ull;
+    };
+    const void* sync_ptrs[] = {e->d_srec, e->d_pushb, e->d_rev, e->d_sstate, e->d_ibits,
+                               e->d_sat, e->d_sat_new, e->d_pushany, e->d_nmeta};
+    const void* other[] = {
+        e->d_gid, e->d_grow, e->d_send_idx, e->d_gout_ptr, e->d_gout_col, e->d_xsend, e->d_xrecv, e->d_xsoff,
+        e->d_xroff, e->d_gfirst, e->d_xtiles, e->d_gout_sidx, e->d_needmark, e->d_stamp, e->d_xcnt, e->d_segbytes,
+        e->d_payload, e->d_in_ptr, e->d_in_col, e->d_out_ptr == e->d_in_ptr ? nullptr : e->d_out_ptr,
+        e->d_out_col == e->d_in_col ? nullptr : e->d_out_col, e->d_sets[0] ? e->d_sets[0] : e->d_base,
+        e->d_sets[1], e->d_F[0], e->d_F[1], e->d_flg[0], e->d_flg[1], e->d_cand, e->d_zmark, e->d_tile_cand,
+        e->d_work, e->d_n_work, e->d_bcount, e->d_nodes, e->d_act, e->d_act_deg, e->d_tot, e->d_act_s,
+        e->d_act_deg_s, e->d_tot_s, e->d_abits, e->d_hubs, e->d_hub_c0, e->d_hchunks, e->d_mchunks, e->d_pend,
+        e->d_pend_src, e->d_bset[0], e->d_bset[1], e->d_hscratch, e->d_hflag, e->d_hlive, e->d_fired[0],
+        e->d_fired[1], e->d_fired[2], e->d_fired[3], e->d_sync_next, e->d_sync_k, e->d_dr, e->d_counters,
+        e->d_inj, e->d_injtab};
+    uint64_t s = 0, o = 0;
+    for (const void* p : sync_ptrs) s += size_of(p);
+    for (const void* p : other) o += size_of(p);
+    for (const auto& w : e->windows) o += size_of(w.d_grp) + size_of(w.d_ebits);
+    if (total) *total = s + o;
+    if (sync_part) *sync_part = s;
+    return GG_OK;
 }
 
 }  // extern "C"

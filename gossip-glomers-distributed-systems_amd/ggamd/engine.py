@@ -68,6 +68,7 @@ class GGRoundStats(C.Structure):
         ("expand_bytes", C.c_uint64),
         ("stream_bytes", C.c_uint64),
         ("sent_bytes", C.c_uint64),
+        ("path", C.c_uint64),
     ]
 
 
@@ -118,7 +119,9 @@ GEN_SYMBOLS = ["gg_topology_generate", "gg_topology_export"]  # HIP library only
 
 STAT_FIELDS = [f for f, _ in GGRoundStats._fields_]
 DIAG_FIELDS = ("round", "kernel_ms", "work_rows", "work_gathers", "prep_ms", "expand_ms", "stream_ms",
-               "prep_bytes", "expand_bytes", "stream_bytes", "sent_bytes")
+               "prep_bytes", "expand_bytes", "stream_bytes", "sent_bytes", "path")
+# gg_round_stats.path bits (gossip.h GG_PATH_*)
+PATH_STREAM, PATH_DB, PATH_SYNC_STREAM, PATH_TILES, PATH_MASKED, PATH_BATCHED = 1, 2, 4, 8, 16, 32
 COUNT_FIELDS = [f for f in STAT_FIELDS if f not in DIAG_FIELDS]
 
 GG_SYMBOLS = [
@@ -126,6 +129,7 @@ GG_SYMBOLS = [
     "gg_partition_seeded", "gg_partition_groups", "gg_set_partition", "gg_broadcast", "gg_broadcast_many",
     "gg_lane_of", "gg_step", "gg_topology_part",
     "gg_current_round", "gg_step_device_ms", "gg_read", "gg_read_bits", "gg_delivery_rounds", "gg_reset",
+    "gg_device_bytes",
     "gg_read_bits_nodes", "gg_delivery_rounds_nodes",
     "gg_dist_round_begin", "gg_dist_round_end", "gg_dist_flush", "gg_dist_owned", "gg_dist_info",
     "gg_dist_comm_available", "gg_dist_comm_id", "gg_dist_comm_init", "gg_dist_transport_init", "gg_dist_step",
@@ -164,6 +168,7 @@ def load_library(path: str) -> C.CDLL:
     lib.gg_read_bits.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
     lib.gg_delivery_rounds.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64]
     lib.gg_reset.argtypes = [C.c_void_p]
+    lib.gg_device_bytes.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint64)]
     lib.gg_dist_round_begin.argtypes = [C.c_void_p, P(GGExchange)]
     lib.gg_dist_round_end.argtypes = [C.c_void_p, P(GGRoundStats)]
     lib.gg_dist_flush.argtypes = [C.c_void_p, P(GGRoundStats), C.c_uint64, P(C.c_uint64)]
@@ -171,7 +176,7 @@ def load_library(path: str) -> C.CDLL:
     lib.gg_dist_info.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(C.c_uint64)]
     lib.gg_read_bits_nodes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
     lib.gg_dist_comm_available.argtypes = [C.c_char_p, C.c_uint64]
-    lib.gg_dist_comm_id.argtypes = [C.c_void_p]
+    lib.gg_dist_comm_id.argtypes = [C.c_void_p, C.c_void_p]
     lib.gg_dist_comm_init.argtypes = [C.c_void_p, C.c_void_p]
     lib.gg_dist_step.argtypes = [C.c_void_p, C.c_uint32]
     lib.gg_dist_transport_init.argtypes = [C.c_void_p, P(GGTransport)]
@@ -369,6 +374,13 @@ class Engine:
     def reset(self):
         self._ok(self.lib.gg_reset(self.h))
 
+    def device_bytes(self) -> dict:
+        """Device memory this engine holds: total and the streamed-sync part
+        (allocated at the first round that can reach a sync timer)."""
+        t, s = C.c_uint64(0), C.c_uint64(0)
+        self._ok(self.lib.gg_device_bytes(self.h, C.byref(t), C.byref(s)))
+        return {"total": t.value, "sync": s.value}
+
     # ---- sharded rounds ------------------------------------------------------
 
     def dist_owned(self) -> np.ndarray:
@@ -404,8 +416,10 @@ class Engine:
         return rc == 0, buf.value.decode()
 
     def dist_comm_id(self) -> bytes:
+        """An RCCL id for this engine's lane group (ABI 6: gg_dist_comm_init of an
+        engine in another lane group refuses it)."""
         buf = (C.c_uint8 * 128)()
-        rc = self.lib.gg_dist_comm_id(buf)
+        rc = self.lib.gg_dist_comm_id(self.h, buf)
         if rc:
             raise RuntimeError(f"gg_dist_comm_id failed ({rc})")
         return bytes(buf)

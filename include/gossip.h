@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 5
+#define GG_ABI_VERSION 6
 
 #define GG_OK 0
 #define GG_EIO (-5)
@@ -119,7 +119,16 @@ typedef struct {
     uint64_t expand_bytes;   /*   (DESIGN.md §4), counted by the kernels */
     uint64_t stream_bytes;
     uint64_t sent_bytes;     /*   sharded: payload bytes this engine sent to other ranks */
+    uint64_t path;           /*   GG_PATH_* bits: the kernel path the round took (0 for the CPU oracle) */
 } gg_round_stats;
+
+/* gg_round_stats.path (diagnostics) */
+#define GG_PATH_STREAM 1u       /* lean round, F-row streaming kernels (expand_stream*, hub_*) */
+#define GG_PATH_DB 2u           /* lean round, double-buffered sets (expand_stream_db) */
+#define GG_PATH_SYNC_STREAM 4u  /* streamed sync round (sync_records, expand_stream_sync, hub_sync_*) */
+#define GG_PATH_TILES 8u        /* tile path (expand_round) */
+#define GG_PATH_MASKED 16u      /* a partition window touches rounds r-3..r+1 */
+#define GG_PATH_BATCHED 32u     /* batched gossip (expand_batched) */
 
 /* Inter-node messages of a round = fwd_sent + pushes + acks + reads + read_oks. */
 
@@ -186,6 +195,12 @@ int gg_delivery_rounds(gg_engine* e, uint32_t node_lo, uint32_t node_hi, int32_t
  * topology and partition windows are kept. */
 int gg_reset(gg_engine* e);
 
+/* Device memory the engine holds (bytes of its live allocations; 0 for the CPU
+ * oracle). sync_part: of which the streamed-sync buffers, which exist only once
+ * a round at or after the first possible sync timer (sync_base_ticks) has been
+ * enqueued — an episode that ends before the timers never allocates them. */
+int gg_device_bytes(const gg_engine* e, uint64_t* total, uint64_t* sync_part);
+
 /* ---- sharded mode (cfg.world > 1): one engine per GPU -------------------------
  * Every rank gives gg_topology the whole graph. The engine orders the nodes for
  * locality (its choice, identical on every rank: the native order or a DFS
@@ -251,7 +266,12 @@ int gg_dist_owned(const gg_engine* e, uint32_t* nodes, uint64_t cap, uint64_t* n
  * gg_dist_comm_available: 0 if the RCCL entry points resolve in this process
  * (why = reason otherwise); the CPU oracle library has no RCCL and returns GG_EIO. */
 int gg_dist_comm_available(char* why, uint64_t cap);
-int gg_dist_comm_id(uint8_t* id_out /* 128 bytes */);
+/* ABI 6: the id names the lane group it is for — part 0 of EACH lane group makes
+ * one with its own engine and hands it to the other parts of that group only;
+ * gg_dist_comm_init refuses (GG_EINVAL) an id made for another lane group or part
+ * count, instead of joining a wrong communicator (ABI 5 callers passed one id to
+ * every rank: with lane_groups > 1 that could hang inside RCCL). */
+int gg_dist_comm_id(const gg_engine* e, uint8_t* id_out /* 128 bytes */);
 int gg_dist_comm_init(gg_engine* e, const uint8_t* id /* 128 bytes */);
 /* The same exchange over the caller's transport instead of RCCL (e.g. a test
  * harness over another backend). gg_dist_step calls group_start, then send/recv of

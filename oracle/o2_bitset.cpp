@@ -738,6 +738,7 @@ static void fill_stats(gg_engine* e, const Acc& a, gg_round_stats* s) {
     s->prep_ms = s->expand_ms = s->stream_ms = 0.0;
     s->prep_bytes = s->expand_bytes = s->stream_bytes = 0;
     s->sent_bytes = e->dist_open ? e->xsend_sent : 0;
+    s->path = 0;
 }
 
 int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
@@ -881,7 +882,7 @@ int gg_dist_comm_available(char* why, uint64_t cap) {
     if (why && cap) std::snprintf(why, cap, "%s", "CPU oracle: no RCCL");
     return GG_EIO;
 }
-int gg_dist_comm_id(uint8_t*) { return GG_EIO; }
+int gg_dist_comm_id(const gg_engine*, uint8_t*) { return GG_EIO; }
 int gg_dist_comm_init(gg_engine* e, const uint8_t*) { return e ? e->fail(GG_EIO, "CPU oracle: no RCCL") : GG_EINVAL; }
 int gg_dist_step(gg_engine* e, uint32_t) { return e ? e->fail(GG_EIO, "CPU oracle: no RCCL") : GG_EINVAL; }
 int gg_topology_part(gg_engine* e, const uint64_t*, const int64_t*, const int32_t*, uint64_t) {
@@ -962,6 +963,13 @@ int gg_reset(gg_engine* e) {
     if (!e) return GG_EINVAL;
     if (e->have_topo) e->reset_state();
     e->dist_pending.clear();
+    return GG_OK;
+}
+
+int gg_device_bytes(const gg_engine* e, uint64_t* total, uint64_t* sync_part) {  // no device memory
+    if (!e) return GG_EINVAL;
+    if (total) *total = 0;
+    if (sync_part) *sync_part = 0;
     return GG_OK;
 }
 

@@ -17,7 +17,7 @@ for p in (REPO, PKG):
         sys.path.insert(0, p)
 
 CPU_LIB = os.path.join(REPO, "oracle", "_build", "libgossip_cpu.so")
-HIP_LIB = os.path.join(PKG, "libgossip_hip.so")
+HIP_LIB = os.environ.get("GG_HIP_LIB") or os.path.join(PKG, "libgossip_hip.so")  # GG_HIP_LIB: A/B builds
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
 

@@ -324,8 +324,29 @@ def test_engine_rccl_plumbing():
     e2.topology(Topology.from_rows([sorted({(v + 1) % 64, (v + 63) % 64}) for v in range(64)]))
     with pytest.raises(GGError, match="no communicator"):
         e2.dist_step(1)
+    with pytest.raises(GGError, match="not an id from gg_dist_comm_id"):
+        e2.dist_comm_init(bytes(128))
     e1.close()
     e2.close()
+
+
+def test_comm_id_names_its_lane_group():
+    """ABI 6: an RCCL id made by lane group 0's part 0 is refused by a part of
+    lane group 1 (2 lane groups x 2 parts), before any RCCL call, instead of
+    joining ranks of two groups with equal part numbers in one communicator."""
+    import torch  # noqa: F401
+
+    from ggamd.engine import Engine, GGError, HIP_LIB, Topology
+    ring = Topology.from_rows([sorted({(v + 1) % 64, (v + 63) % 64}) for v in range(64)])
+    engs = [Engine(64, 128, device=0, rank=r, world=4, lane_groups=2, library=HIP_LIB) for r in range(4)]
+    for e in engs:
+        e.topology(ring)
+    uid_g0 = engs[0].dist_comm_id()  # rank 0 = group 0, part 0
+    for r in (2, 3):  # group 1
+        with pytest.raises(GGError, match="lane group 0 of 2 parts"):
+            engs[r].dist_comm_init(uid_g0)
+    for e in engs:
+        e.close()
 
 
 def _gen_scenarios():
@@ -643,3 +664,37 @@ def test_topology_part_refusals(hip_lib):
         e.topology_part([0, 4, 8], [0, 1, 1, 1, 1], [1])
     e.topology_part([0, 4, 8], [0, 1, 2, 2, 2], [1, 0])
     e.close()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("db", ["GG_DB", "GG_NO_DB"])
+def test_sharded_db_paths_equal_oracle(hip_lib, cpu_lib, world, db):
+    """Both lean-round paths of a sharded engine, forced (GG_DB: double-buffered
+    sets — ghost senders' F rows from the exchange, pack_ghosts with set_prev,
+    materialize_F and clear_stale_ghosts at the hand-over to the sync rounds;
+    GG_NO_DB: the F-row kernels), against O2; gg_round_stats.path says which ran."""
+    from ggamd import topology as T
+    from ggamd.engine import PATH_DB
+    from ggamd.workload import uniform_injections
+    scs = [Scenario(T.tree(3000, 4), 256, 34, uniform_injections(3000, 200, 41), seed=42, sync_base=6, sync_jitter=3),
+           Scenario(T.random_regular(2500, 8, seed=43), 128, 30,
+                    [(n, v, v % 4) for n, v, _ in uniform_injections(2500, 120, 44)], seed=45, sync_base=5,
+                    sync_jitter=2),
+           Scenario(T.grid_links(44, seed=46), 512, 36, uniform_injections(44 * 44, 300, 47), seed=48, sync_base=9,
+                    sync_jitter=4, windows=[("seeded", 12, 16, 3)])]
+    res = _run(hip_lib, scs, world, env={db: "1"})
+    for k, sc in enumerate(scs):
+        ref = make_engine(cpu_lib, sc)
+        want = ref.step(sc.rounds)
+        for rank in range(world):
+            stats, owned, bits, dr = res[rank][k]
+            d = diff_stats(want, stats)
+            assert not d, (k, rank, d[:8])
+            assert np.array_equal(bits, ref.read_bits_nodes(owned)), (k, rank)
+            assert np.array_equal(dr, ref.delivery_rounds_nodes(owned)), (k, rank)
+            n_db = sum(1 for s in stats if s["path"] & PATH_DB)
+            if db == "GG_DB":
+                assert n_db >= 4, (k, rank, [s["path"] for s in stats])
+            else:
+                assert n_db == 0, (k, rank)
+        ref.close()
