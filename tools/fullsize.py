@@ -184,6 +184,9 @@ def main():
     st = eng.step(R)
     el = time.perf_counter() - t3
     dl = sum(s["new_bits"] for s in st)
+    torch.cuda.synchronize()
+    footprint_after = free0 - torch.cuda.mem_get_info(0)[0]
+    held = eng.device_bytes()
     kinds = {}
     for k in ("prep", "expand", "stream"):
         ms = sum(s[k + "_ms"] for s in st)
@@ -194,6 +197,8 @@ def main():
            "rounds": R, "rounds_to_full_delivery": last_deliv + 1, "deliveries": dl,
            "episode_s": el, "deliveries_per_s": dl / el, "device_ms": eng.step_device_ms(),
            "hbm_footprint_GiB": footprint / 2**30,
+           "hbm_after_episodes_GiB": footprint_after / 2**30,
+           "engine_device_bytes": held["total"], "engine_sync_buffer_bytes": held["sync"],
            "topology_source": "device generator" if args.device_gen else "host CSR", "engine_ready_s": ready_s, "inter_node_msgs": msgs, "msgs_per_op": msgs / K,
            "kernels": kinds, "oracle": bool(ref), "properties_failed": fails}
     log(json.dumps(out))
