@@ -238,13 +238,14 @@ struct gg_engine {
     bool f_dirty = true;      // some F row may be non-zero (reset must clear them)
     bool db_decided = false;  // ensure_db ran since the topology was installed
     bool sync_alloc = false;  // alloc_sync ran since the topology was installed
+    bool no_mark = false;     // GG_NO_MARK=1 at the install: no marking rounds (round_prep every round)
     uint64_t* d_F[2] = {nullptr, nullptr};
     uint8_t* d_flg[2] = {nullptr, nullptr};
-    uint8_t* d_cand = nullptr;       // [rows] candidate bytes
+    uint8_t* d_cand = nullptr;       // [2][rows] candidate bytes by round parity
     uint8_t* d_zmark = nullptr;      // [rows] stale-F-row marks
     uint8_t* d_tile_cand = nullptr;  // [tile_bytes]
     gg::TileWork* d_work = nullptr;  // [tiles] live-tile worklist (sparse sync/mask rounds)
-    uint32_t* d_n_work = nullptr;    // [2] live tiles, candidate nodes
+    uint32_t* d_n_work = nullptr;    // [2][2] live tiles, candidate nodes, by round parity
     uint32_t* d_bcount = nullptr;    // [compact blocks + 1] split compaction (large graphs)
     uint64_t prep_cap = 1024;        // round_prep's grid cap in rounds without timers (GG_PREP_BLOCKS)
     uint32_t* d_nodes = nullptr;     // [n_own] candidate-node list (sparse lean rounds)
@@ -490,7 +491,8 @@ int reset_device_state(gg_engine* e) {
     e->quiet = 2;
     e->f_dirty = !e->db_ok || e->P > 1;  // (sharded: the exchange writes the ghosts' F rows)
     for (int b = 0; b < 4; ++b) seg(e->d_fired[b], e->rows / 8, 0);
-    seg(e->d_cand, e->rows, 0);
+    seg(e->d_cand, 2 * e->rows, 0);
+    seg(e->d_n_work, 16, 0);
     seg(e->d_zmark, e->rows, 0);
     seg(e->d_tile_cand, e->tile_bytes, 0);
     seg(e->d_act, 16, 0);
@@ -606,10 +608,12 @@ void launch_expand(const gg::RoundArgs& a, bool syncw, bool maskw, hipStream_t s
 
 // expand_stream grid: one resident wave of blocks (node groups walk their
 // items grid-stride), so no partial second wave of blocks trails the round.
-template <int G, bool MASKW, bool DB = false>
+template <int G, bool MASKW, int DB = 0>
 void launch_stream_t(const gg::RoundArgs& a, hipStream_t s) {
     static int resident = 0;
-    auto kern = MASKW ? gg::expand_stream_masked<G, 2> : (DB ? gg::expand_stream_db<G, 2> : gg::expand_stream<G, 2>);
+    auto kern = MASKW ? gg::expand_stream_masked<G, 2>
+                      : (DB == 2 ? gg::expand_stream_db_mark<G, 2>
+                                 : (DB ? gg::expand_stream_db<G, 2> : gg::expand_stream<G, 2>));
     if (!resident) {
         int dev = 0, cus = 0, per_cu = 0;
         (void)hipGetDevice(&dev);
@@ -625,9 +629,14 @@ void launch_stream_t(const gg::RoundArgs& a, hipStream_t s) {
 
 template <int G>
 void launch_stream_m(const gg::RoundArgs& a, bool maskw, hipStream_t s) {
-    if (maskw) launch_stream_t<G, true>(a, s);
-    else if (a.db) launch_stream_t<G, false, true>(a, s);
-    else launch_stream_t<G, false>(a, s);
+    if (maskw) {
+        launch_stream_t<G, true>(a, s);
+    } else if (a.db) {
+        launch_stream_t<G, false, 1>(a, s);
+        if (a.mark_cand) launch_stream_t<G, false, 2>(a, s);  // the rounds that are not busy
+    } else {
+        launch_stream_t<G, false>(a, s);
+    }
 }
 
 template <int G, int WPL = 2>
@@ -917,6 +926,13 @@ void db_advance(gg_engine* e, int64_t r, bool db) {
     e->d_base = e->d_sets[e->set_cur];
 }
 
+// Marking rounds are for single double-buffered engines on symmetric graphs
+// without hubs (no ghost senders to mark receivers for, no hub_mark; a node's
+// receivers are its in-list); GG_NO_MARK=1 keeps round_prep.
+bool mark_ok(const gg_engine* e) {
+    return !e->no_mark && e->symmetric && e->P == 1 && e->n_ghost == 0 && e->n_hubs == 0 && e->n_mchunks == 0 && !e->cfg.batch_ticks;
+}
+
 // Which kernel path round r takes (gg_round_stats.path, diagnostics): the host
 // decides it from the round number, the windows and the buffers, so a replayed
 // batch reports the same bits as the enqueued one. db: db_round(e, r) before
@@ -927,6 +943,7 @@ uint64_t path_of(const gg_engine* e, int64_t r, bool db) {
     for (int k = 0; k < 5; ++k) maskw |= window_at(e, r - 3 + k) != nullptr;
     const bool syncw = e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks + 2;
     uint64_t p = maskw ? GG_PATH_MASKED : 0;
+    if (db && mark_ok(e) && !(e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks)) p |= GG_PATH_NO_PREP;
     if (db) return p | GG_PATH_DB;
     if (syncw && !maskw && e->d_srec) return p | GG_PATH_SYNC_STREAM;
     const bool lean = !syncw && (!maskw || (e->symmetric && e->n_hubs == 0 && e->nwp >= 2));
@@ -960,11 +977,14 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.F_cur = e->d_F[r & 1];
     a.flg_prev = e->d_flg[(r + 1) & 1];
     a.flg_cur = e->d_flg[r & 1];
-    a.cand = e->d_cand;
+    a.cand = e->d_cand + (size_t)(r & 1) * e->rows;
+    a.cand_next = e->d_cand + (size_t)((r + 1) & 1) * e->rows;
+    a.flg_prev_w = e->d_flg[(r + 1) & 1];
     a.zmark = e->d_zmark;
     a.tile_cand = e->d_tile_cand;
     a.work = e->d_work;
-    a.n_work = e->d_n_work;
+    a.n_work = e->d_n_work + 2 * (r & 1);
+    a.n_work_next = e->d_n_work + 2 * ((r + 1) & 1);
     a.bcount = e->d_bcount;
     a.nodes = e->d_nodes;
     a.act = e->d_act;
@@ -1049,6 +1069,13 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     const int64_t base = (int64_t)e->cfg.sync_base_ticks;
     const bool syncw_prep = e->cfg.enable_sync && r >= base;
     const bool syncw = e->cfg.enable_sync && r >= base + 2;
+    // marking rounds (RoundArgs::mark_cand): this double-buffered round's expand
+    // marks round r+1's candidates when r+1 is one too (before the timers), and
+    // such a round r+1 launches no round_prep (round 0: nothing to mark yet)
+    if (db && mark_ok(e) && !syncw_prep) {
+        a.prep_in_compact = 1;
+        a.mark_cand = (db_round(e, r + 1) && !(e->cfg.enable_sync && r + 1 >= base)) ? 1u : 0u;
+    }
     // streaming rounds: no sync event reaches the expand; partition windows only
     // on symmetric graphs without hubs at W >= 128 (expand_stream<.., MASKW>)
     // streamed sync rounds (sync_records + expand_stream_sync [+ hub_sync_*]): no masks
@@ -1102,7 +1129,9 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             const uint64_t blocks = std::max<uint64_t>(
                 1, std::min<uint64_t>((a.n_own + gg::kBlock - 1) / gg::kBlock, syncw_prep ? sync_cap : prep_cap));
             dim3 grid((unsigned)blocks), block(gg::kBlock);
-            if (syncw_prep) {
+            if (a.prep_in_compact) {
+                // the expand of r-1 marked this round's candidates; compact_round sums the rings
+            } else if (syncw_prep) {
                 if (maskw) hipLaunchKernelGGL((gg::round_prep<true, true>), grid, block, 0, e->stream, a);
                 else hipLaunchKernelGGL((gg::round_prep<true, false>), grid, block, 0, e->stream, a);
             } else {
@@ -1623,15 +1652,16 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     // the streamed-sync buffers: before the first round that reaches a timer
     // (ensure_sync), not here; GG_SYNC_EAGER=1 allocates them with the topology
     e->sync_alloc = false;
+    e->no_mark = test_knob("GG_NO_MARK") && atoi(test_knob("GG_NO_MARK"));
     const size_t rowbytes = e->rows * e->nwp * 8;
     e->tile_nodes = gg::kBlock / lanes_per_node((uint32_t)e->nwp);
     const uint64_t ntiles = (n_own + e->tile_nodes - 1) / e->tile_nodes;
     e->tile_bytes = (ntiles + 8) / 8 * 8;
-    HIPCHK(hipMalloc(&e->d_cand, e->rows));
+    HIPCHK(hipMalloc(&e->d_cand, 2 * e->rows));
     HIPCHK(hipMalloc(&e->d_zmark, e->rows));
     HIPCHK(hipMalloc(&e->d_tile_cand, e->tile_bytes));
     HIPCHK(hipMalloc(&e->d_work, std::max<uint64_t>(1, ntiles) * sizeof(gg::TileWork)));
-    HIPCHK(hipMalloc(&e->d_n_work, 2 * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&e->d_n_work, 4 * sizeof(uint32_t)));
     e->prep_cap = test_knob("GG_PREP_BLOCKS") ? (uint64_t)std::max(1, atoi(test_knob("GG_PREP_BLOCKS"))) : 1024;
     {  // split compaction when one atomic per block would serialise (compact_round)
         const uint64_t per_block = (uint64_t)gg::kBlock * gg::kCompactQ;

@@ -136,11 +136,22 @@ struct RoundArgs {
     uint64_t* F_cur;
     const uint8_t* flg_prev;    // [rows] FL_* of round r-1
     uint8_t* flg_cur;
-    uint8_t* cand;              // [rows] candidate bytes of this round (cleared by expand)
+    uint8_t* flg_prev_w;        // flg_prev, writable (marking rounds clear a processed node's byte)
+    uint8_t* cand;              // [rows] candidate bytes of this round (cleared by expand); two
+                                // arrays by round parity, so marks for round r+1 made during r
+                                // (cand_next) never meet round r's reads and clears
+    uint8_t* cand_next;         // [rows] candidate bytes of round r+1
+    uint32_t mark_cand;         // marking lean rounds (double-buffered, single engine): the expand
+                                // kernel marks round r+1's candidates itself — every node whose set
+                                // changes, and its receivers — and clears the node's flag byte of
+                                // r-1, so round r+1 needs no round_prep (prep_in_compact)
+    uint32_t prep_in_compact;   // no round_prep this round: compact_round sums the rings of r-1
+                                // (round r-1 was a marking round, or r is the first round)
     uint8_t* zmark;             // [rows] F row of this parity is stale (node active 2 rounds ago)
     uint8_t* tile_cand;         // [n_tiles rounded to 8] tile has a candidate (sparse rounds)
     struct TileWork* work;      // live tiles of a sparse round (compact_round; expand_round)
-    uint32_t* n_work;           // [2]: live tiles, candidate nodes
+    uint32_t* n_work;           // [2]: live tiles, candidate nodes (two pairs by round parity)
+    uint32_t* n_work_next;      // [2] round r+1's pair: zeroed by this round's compact_round
     uint32_t* bcount;           // [compact blocks + 1] split compaction (large graphs): per-block counts -> offsets
     uint32_t* nodes;            // candidate nodes of a sparse lean round (compact_round; expand_stream)
     uint32_t* act;              // [4] ring: nodes that became active in round r (slot r&3), summed by round_prep
@@ -324,9 +335,19 @@ __device__ __forceinline__ bool busy_round(const RoundArgs& a) {
     const double act = (double)a.act[(a.round - 1) & 3];
     return 2.0 * act * (double)a.n_edges >= (double)a.n_own * (double)a.n_own;
 }
+// Round r-1 was busy (the same test one round earlier, from the act ring).
+__device__ __forceinline__ bool busy_prev(const RoundArgs& a) {
+    const double act = (double)a.act[(a.round - 2) & 3];
+    return 2.0 * act * (double)a.n_edges >= (double)a.n_own * (double)a.n_own;
+}
 // Dense lean round: expand_stream visits every node, round_prep marks nothing
-// and expand_round exits.
-__device__ __forceinline__ bool dense_round(const RoundArgs& a) { return a.stream_ok && busy_round(a); }
+// and expand_round exits. A round without round_prep (prep_in_compact) after a
+// busy round is dense whatever its own count: a busy round's expand marks no
+// candidates (expand_stream_db takes it, not the marking kernel), so the round
+// after it visits every node and marks for the next one.
+__device__ __forceinline__ bool dense_round(const RoundArgs& a) {
+    return a.stream_ok && (busy_round(a) || (a.prep_in_compact && busy_prev(a)));
+}
 
 // Flags-first streaming round: fewer than half of the in-edges name a sender
 // that was ACT last round (an F row that is not zero), so expand_stream looks
@@ -508,19 +529,11 @@ __device__ __forceinline__ void flush_counters(const RoundArgs& a, unsigned long
     if (threadIdx.x == 0) stamp(a, kind, t_start);
 }
 
-// ---------------------------------------------------------------------------
-// round_prep: one thread per owned node (64 consecutive nodes per wave, so a
-// wave owns whole words of the fired bitmap). In dense rounds the per-node
-// flag/stale-row work moves into expand_stream and no candidates are marked,
-// so without sync timers the launch is a no-op.
-template <bool SYNCW, bool MASKW>
-__global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
-    __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
-    const unsigned long long t_start = clock100();
-    // Round r-1's rings from their spread slots (one slot per lane, summed per wave):
-    // this kernel decides dense/sparse from its own sum, block 0 publishes the sums
-    // for the round's later launches and clears round r's slots (nothing in this
-    // kernel adds to them).
+// Round r-1's rings (act, act_deg, tot) from their spread slots: every wave sums
+// the act slots for its own dense/sparse choice; block 0 publishes the three
+// sums for the round's later launches and clears round r's slots (nothing in
+// the calling kernel adds to them). Returns this round's dense choice.
+__device__ __forceinline__ bool rings_in(const RoundArgs& a) {
     const int lane = threadIdx.x & 63;
     const int pr = (int)((a.round - 1) & 3), cr = (int)(a.round & 3);
     const unsigned long long act_prev = wave_sum((unsigned long long)a.act_s[pr * kSlots + lane]);
@@ -536,9 +549,26 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
             a.act[pr] = (uint32_t)act_prev;
             a.act_deg[pr] = d;
             if (a.tot) a.tot[pr] = (a.round > 0 ? a.tot[(a.round - 2) & 3] : 0ull) + n;
-            a.n_work[0] = a.n_work[1] = 0;  // compact_round runs after this kernel
         }
     }
+    return dense;
+}
+
+// ---------------------------------------------------------------------------
+// round_prep: one thread per owned node (64 consecutive nodes per wave, so a
+// wave owns whole words of the fired bitmap). In dense rounds the per-node
+// flag/stale-row work moves into expand_stream and no candidates are marked,
+// so without sync timers the launch is a no-op.
+template <bool SYNCW, bool MASKW>
+__global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
+    __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
+    const unsigned long long t_start = clock100();
+    // Round r-1's rings from their spread slots (one slot per lane, summed per wave):
+    // this kernel decides dense/sparse from its own sum, block 0 publishes the sums
+    // for the round's later launches and clears round r's slots (nothing in this
+    // kernel adds to them).
+    const bool dense = rings_in(a);
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.n_work[0] = a.n_work[1] = 0;  // compact_round runs after this kernel
     if (a.sat) {  // last round's digest bits in (readers of this round see rounds < r only)
         const uint64_t nw = (a.n_own + 63) / 64;
         for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < nw; t += (uint64_t)gridDim.x * kBlock) {
@@ -637,9 +667,14 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
     }
     // the per-node bytes of the next node are loaded before this node's stores:
     // two nodes' worth of loads in flight per thread (the grid is capped)
+    // (timer rounds: the out-list bounds and the timer count too, for every node —
+    // 12 coalesced bytes a node — so a firing node or an answered read has no
+    // dependent load: C2's timer rounds were three memory latencies per node)
     struct PrepIn {
         uint64_t w1, w2, w3;  // fired words of r-1, r-2, r-3
+        int64_t o0, o1;       // out_ptr[i], out_ptr[i+1] (SYNCW)
         int32_t sn;           // sync_next
+        uint32_t sk;          // sync_k (SYNCW)
         uint8_t f, fc, pa;    // flg_prev, flg_cur, pushany
     };
     auto load_in = [&](uint64_t i, PrepIn& p) {
@@ -653,6 +688,9 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
             p.w2 = a.fired_m2[rp >> 6];
             p.w3 = a.fired_m3[rp >> 6];
             p.sn = a.sync_next[i];
+            p.o0 = a.out_ptr[i];
+            p.o1 = a.out_ptr[i + 1];
+            p.sk = a.sync_k[i];
             if (a.push_marked) p.pa = a.pushany[rp];
         }
     };
@@ -704,8 +742,13 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                     if (!cur.pa) st &= (uint8_t)~SE_FM3;
                     c_bytes += 1;
                 } else if ((f & FL_ACT) || fm3) {  // senders mark their (owned) receivers
-                    o0 = a.out_ptr[i];
-                    o1 = a.out_ptr[i + 1];
+                    if constexpr (SYNCW) {
+                        o0 = cur.o0;
+                        o1 = cur.o1;
+                    } else {
+                        o0 = a.out_ptr[i];
+                        o1 = a.out_ptr[i + 1];
+                    }
                     const bool hub = a.hub_deg && o1 - o0 > (int64_t)a.hub_deg;
                     if (hub) o1 = o0;  // hub_mark does it
                     // a pusher that is not active reaches only the peers it pushed to
@@ -736,10 +779,8 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
             }
             if constexpr (SYNCW) {
                 if (a.sstate) a.sstate[rep] = st;
-                if (fm1 || (int64_t)cur.sn == a.round) {
-                    o0 = a.out_ptr[i];
-                    o1 = a.out_ptr[i + 1];
-                }
+                o0 = cur.o0;
+                o1 = cur.o1;
                 // reads v sent in r-1 arrive now; each answered by a read_ok (:131)
                 if (fm1) {
                     if constexpr (MASKW) {
@@ -763,7 +804,7 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                         for (int64_t e = o0; e < o1; ++e)
                             c_dropped += masked<MASKW>(a, 3, rep, a.out_col[e] & kColMask, e) ? 1 : 0;
                     }
-                    const uint32_t kk = a.sync_k[i] + 1;
+                    const uint32_t kk = cur.sk + 1;
                     a.sync_k[i] = kk;
                     a.sync_next[i] = (int32_t)(a.round + gg_sync_interval(a.seed, gid_of(a, i), kk,
                                                                           a.sync_base, a.sync_jitter));
@@ -876,7 +917,12 @@ __global__ __launch_bounds__(kBlock) void compact_round(RoundArgs a) {
     __shared__ uint32_t s_cnt[kBlock / 64];
     __shared__ uint32_t s_base;
     const unsigned long long t_start = clock100();
-    if (dense_round(a)) {
+    // a round without round_prep: the first compaction launch sums the rings
+    // (the split path's later launches read what it published)
+    const bool dense = (a.prep_in_compact && PH != 2) ? (rings_in(a) || busy_prev(a)) : dense_round(a);
+    // round r+1's counts start from zero (round r-1, their last user, is done)
+    if (PH != 2 && blockIdx.x == 0 && threadIdx.x == 0 && a.n_work_next) a.n_work_next[0] = a.n_work_next[1] = 0;
+    if (dense) {
         noop_exit(a, K_PREP, t_start);
         return;
     }
@@ -1464,7 +1510,7 @@ __device__ __forceinline__ uint32_t active_senders(const uint64_t* abits, const 
     return m & ((1u << D) - 1u);
 }
 
-template <int G, int WPL, bool MASKW, bool DB = false>
+template <int G, int WPL, bool MASKW, bool DB = false, bool MARK = false>
 __device__ __forceinline__ void stream_body(RoundArgs a) {
     static_assert(WPL == 2, "DMA slots hold 16 bytes per lane");
     constexpr int NGB = kBlock / G;  // node groups per block
@@ -1472,7 +1518,11 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t s_slots[(kBlock / 64) * (D + 1) * 1024];
     __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
     const unsigned long long t_start = clock100();
-    if (!a.stream_ok) {
+    // marking rounds launch two kernels: expand_stream_db takes the busy ones
+    // (every node, nothing marked) and expand_stream_db_mark the others (the
+    // candidate list, or every node after a busy round; the next round's
+    // candidates marked)
+    if (!a.stream_ok || (MARK ? busy_round(a) : (DB && a.mark_cand && !busy_round(a)))) {
         noop_exit(a, K_STREAM, t_start);
         return;
     }
@@ -1750,6 +1800,21 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             if (m0.ca) a.cand[rep] = 0;
         }
         const unsigned long long deg = a.symmetric ? nin : (unsigned long long)(a.out_ptr[i + 1] - a.out_ptr[i]);
+        if constexpr (db && MARK) {
+            {
+                // round r+1's candidates, marked here instead of by a round_prep pass
+                // over every flag byte: a node whose set changed moves its row forward
+                // and is a sender (its receivers). Its flag byte of r-1 was read above
+                // (m0.fl) and is not read again: cleared, so no stale ACT byte waits
+                // for round r+1 to clear it (that round's round_prep would mark it)
+                if (lg == 0 && m0.fl) a.flg_prev_w[rep] = 0;
+                if (any) {  // (symmetric: mark_ok) the out-list is the in-list
+                    if (lg == 0) a.cand_next[rep] = CA_NODE;
+                    const uint32_t* oc = a.in_col + m0.p0;
+                    for (uint32_t e = (uint32_t)lg; e < m0.deg; e += G) a.cand_next[oc[e] & kColMask] = CA_NODE;
+                }
+            }
+        }
         c_new += T;
         const unsigned long long fs = deg * (unsigned long long)T - cl_recip;
         c_fwd += fs;
@@ -1766,7 +1831,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             // row_ptr + cand + flag bytes + col (+ a sender bit, flags-first), own row + gathered
             // sender rows, F / base / flag writes
             c_bytes += (dense ? 0 : 4) + 8 + 2 + (db ? 1 : 0) + 4 * nin + (ff ? (nin + 7) / 8 : 0) +
-                       (full ? 0 : rowb) + (any ? 1 : 0);
+                       (full ? 0 : rowb) + (any ? 1 : 0) + ((MARK && any) ? nin + 1 : 0);
         }
         // this lane's F / base chunk stores
         c_bytes += db ? ((lane_new || cp) ? 16 : 0) : ((lane_new || zm) ? 16 : 0) + (lane_new ? 16 : 0);
@@ -1815,6 +1880,16 @@ template <int G, int WPL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GG_STREAM_WAVES_PER_EU)))
 void expand_stream_db(RoundArgs a) {
     stream_body<G, WPL, false, true>(a);
+}
+
+// ... of marking rounds (RoundArgs::mark_cand) that are not busy: the same, and
+// each node whose set changes marks itself and its receivers as candidates of
+// round r+1 (the marking needs four more registers: a kernel of its own, so the
+// busy rounds keep 5 waves/SIMD).
+template <int G, int WPL>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+void expand_stream_db_mark(RoundArgs a) {
+    stream_body<G, WPL, false, true, true>(a);
 }
 
 // Which of a lane's D senders (columns c, the first n valid) were ACT last round
@@ -2425,7 +2500,7 @@ __global__ __launch_bounds__(kBlock) void expand_stream_sync(RoundArgs a) {
                             a.pushb[o0 + e0 + b] = nz ? 1 : 0;
                             pushed |= nz;
                             // the receiver's candidate byte for round r+1 (round_prep skips the walk)
-                            if (nz && a.mark_next && pc[b] < a.n_own) a.cand[a.own0 + pc[b]] = CA_NODE;
+                            if (nz && a.mark_next && pc[b] < a.n_own) a.cand_next[a.own0 + pc[b]] = CA_NODE;
                         }
                     }
                     cb_new += pn;
@@ -3370,7 +3445,7 @@ __global__ __launch_bounds__(kBlock) void hub_sync_push(RoundArgs a) {
             if (lg == 0) {
                 if (a.pushb) a.pushb[e] = nz ? 1 : 0;
                 pushed |= nz;
-                if (nz && a.mark_next && w < a.n_own) a.cand[a.own0 + w] = CA_NODE;
+                if (nz && a.mark_next && w < a.n_own) a.cand_next[a.own0 + w] = CA_NODE;
             }
         }
         if (lg == 0 && e1 > e0) c_bytes += (uint64_t)(e1 - e0) * (8 + 2 * 8ull * a.nwp + 1);

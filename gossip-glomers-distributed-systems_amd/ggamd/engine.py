@@ -121,7 +121,7 @@ STAT_FIELDS = [f for f, _ in GGRoundStats._fields_]
 DIAG_FIELDS = ("round", "kernel_ms", "work_rows", "work_gathers", "prep_ms", "expand_ms", "stream_ms",
                "prep_bytes", "expand_bytes", "stream_bytes", "sent_bytes", "path")
 # gg_round_stats.path bits (gossip.h GG_PATH_*)
-PATH_STREAM, PATH_DB, PATH_SYNC_STREAM, PATH_TILES, PATH_MASKED, PATH_BATCHED = 1, 2, 4, 8, 16, 32
+PATH_STREAM, PATH_DB, PATH_SYNC_STREAM, PATH_TILES, PATH_MASKED, PATH_BATCHED, PATH_NO_PREP = 1, 2, 4, 8, 16, 32, 64
 COUNT_FIELDS = [f for f in STAT_FIELDS if f not in DIAG_FIELDS]
 
 GG_SYMBOLS = [

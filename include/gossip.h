@@ -129,6 +129,8 @@ typedef struct {
 #define GG_PATH_TILES 8u        /* tile path (expand_round) */
 #define GG_PATH_MASKED 16u      /* a partition window touches rounds r-3..r+1 */
 #define GG_PATH_BATCHED 32u     /* batched gossip (expand_batched) */
+#define GG_PATH_NO_PREP 64u     /* no round_prep launch: the previous round's expand marked this round's
+                                   candidates (double-buffered rounds of a single engine before the timers) */
 
 /* Inter-node messages of a round = fwd_sent + pushes + acks + reads + read_oks. */
 

@@ -63,3 +63,44 @@ def test_prep_quad_path_equals_oracle(hip_lib, cpu_lib):
     p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stderr[-3000:]
     assert json.loads(p.stdout.strip().splitlines()[-1]) == []
+
+
+@pytest.mark.parametrize("no_mark", ["0", "1"])
+def test_marking_rounds_equal_oracle(hip_lib, cpu_lib, monkeypatch, no_mark):
+    """Marking rounds (GG_PATH_NO_PREP): in double-buffered rounds before the
+    timers the expand kernel marks the next round's candidates (a changed node
+    and its receivers) and clears its flag byte of r-1, and those rounds launch
+    no round_prep; GG_NO_MARK=1 keeps round_prep. Sparse and dense rounds,
+    injections spread over the rounds, the hand-over to the timer rounds, one
+    multi-round step and single steps: every round equals O2."""
+    import random
+
+    import numpy as np
+
+    from ggamd import topology as T
+    from ggamd.engine import PATH_DB, PATH_NO_PREP
+    from ggamd.workload import uniform_injections
+    from helpers import Scenario, diff_stats, make_engine
+    monkeypatch.setenv("GG_NO_MARK", no_mark)
+    monkeypatch.setenv("GG_DB", "1")
+    rnd = random.Random(5)
+    scs = [Scenario(T.tree(6000, 4), 256, 34, [(n, v, v % 7) for n, v, _ in uniform_injections(6000, 200, 1)],
+                    seed=2, sync_base=14, sync_jitter=3),
+           Scenario(T.random_regular(5000, 6, seed=3), 128, 30, [(rnd.randrange(5000), v, rnd.randrange(12))
+                                                                  for v in range(120)], seed=4, sync_base=9),
+           Scenario(T.grid_links(60, seed=5), 512, 26, uniform_injections(3600, 400, 6), seed=7, enable_sync=False)]
+    for k, sc in enumerate(scs):
+        c = make_engine(cpu_lib, sc)
+        want = c.step(sc.rounds)
+        for mode in ("whole", "single"):
+            g = make_engine(hip_lib, sc, device=0)
+            st = g.step(sc.rounds) if mode == "whole" else [g.step(1)[0] for _ in range(sc.rounds)]
+            d = diff_stats(want, st)
+            assert not d, (k, mode, d[:6])
+            assert np.array_equal(g.read_bits(), c.read_bits()), (k, mode)
+            assert np.array_equal(g.delivery_rounds(), c.delivery_rounds()), (k, mode)
+            n_np = sum(1 for s in st if s["path"] & PATH_NO_PREP)
+            assert any(s["path"] & PATH_DB for s in st), k
+            assert (n_np > 3) if no_mark == "0" else (n_np == 0), (k, mode, [s["path"] for s in st])
+            g.close()
+        c.close()
