@@ -317,6 +317,17 @@ struct gg_engine {
     BatchKey graph_key;
     bool graph_broken = false;
 
+    // device-driven exchange over IPC-mapped peer windows (gg_dist_ipc_*)
+    bool ipc = false;
+    uint8_t* d_win = nullptr;            // this engine's window (uncached): flags, 2 receive buffers
+    uint64_t win_rbuf = 0;               // receive buffer bytes (xroff[P] rounded up)
+    std::vector<void*> peer_map;         // [P] opened peer windows
+    uint8_t** d_peer_win = nullptr;      // [P] the same on the device
+    uint64_t* d_peer_off = nullptr;      // [P] this engine's segment offset in peer q's receive buffer
+    uint64_t* d_peer_rbuf = nullptr;     // [P] peer q's receive buffer bytes
+    uint64_t send_mask = 0, recv_mask = 0;
+    uint64_t xseq = 0;                   // exchange sequence number (one per sharded round, never reset)
+    uint32_t* d_xticket = nullptr;       // [2] unpack's last-block counter, error word
     ncclComm_t comm = nullptr;  // engine-owned RCCL communicator over the lane group's parts
     gg_transport xport{};       // or the caller's transport (gg_dist_transport_init)
     bool have_xport = false;
@@ -418,6 +429,15 @@ void gg_engine::free_topology() {
     dfree(d_xcnt);
     dfree(d_segbytes);
     dfree(d_payload);
+    for (void*& m : peer_map)
+        if (m) (void)hipIpcCloseMemHandle(m);
+    peer_map.clear();
+    dfree(d_peer_win);
+    dfree(d_peer_off);
+    dfree(d_peer_rbuf);
+    dfree(d_xticket);
+    dfree(d_win);
+    ipc = false;
     if (h_segbytes) (void)hipHostFree(h_segbytes);
     h_segbytes = nullptr;
     n_xtiles = 0;
@@ -2525,6 +2545,11 @@ static int fold_pending(gg_engine* e) {
             HIPCHK(hipMemcpyAsync(e->dist_sent.data(), e->d_payload, e->dist_k * 8, hipMemcpyDeviceToHost, e->stream));
     }
     HIPCHK(hipStreamSynchronize(e->stream));
+    if (e->ipc) {
+        uint32_t err = 0;
+        HIPCHK(hipMemcpy(&err, e->d_xticket + 1, 4, hipMemcpyDeviceToHost));
+        if (err) return e->fail(GG_EIO, "device-driven exchange: a peer did not arrive within the wait bound");
+    }
     for (uint32_t k = 0; k < e->dist_k; ++k) {
         gg_round_stats s;
         fold_stats(e, e->h_counters + (size_t)k * gg::kSlots * gg::kCounters, e->dist_round_of[k], &s);
@@ -2538,6 +2563,24 @@ static int fold_pending(gg_engine* e) {
 }
 
 }  // extern "C"
+
+// The device-driven exchange's kernel arguments for this round (peer_win null:
+// no IPC exchange).
+static gg::IpcArgs ipc_args(const gg_engine* e) {
+    gg::IpcArgs ip{};
+    if (!e->ipc) return ip;
+    ip.peer_win = e->d_peer_win;
+    ip.peer_off = e->d_peer_off;
+    ip.peer_rbuf = e->d_peer_rbuf;
+    ip.my_win = reinterpret_cast<uint64_t*>(e->d_win);
+    ip.rbuf = e->win_rbuf;
+    ip.send_mask = e->send_mask;
+    ip.recv_mask = e->recv_mask;
+    ip.seq = e->xseq;
+    ip.ticket = e->d_xticket;
+    ip.err = e->d_xticket + 1;
+    return ip;
+}
 
 // One sharded round up to the exchange: the round's kernels, then (vertex
 // parts) the pack of this round's ghost payloads. host_sizes: in exact mode,
@@ -2614,12 +2657,13 @@ static int dist_begin(gg_engine* e, gg_exchange* x, bool host_sizes) {
             pa.nwp = (uint32_t)e->nwp;
             pa.stride = e->xstride;
             pa.sync = sync ? 1 : 0;
+            pa.ipc = ipc_args(e);
             hipLaunchKernelGGL(gg::pack_ghosts, dim3(std::min<uint32_t>(e->n_xtiles, 4096)), dim3(gg::kBlock), 0,
                                e->stream, pa);
             HIPCHK(hipGetLastError());
         }
         hipLaunchKernelGGL(gg::finish_pack, dim3(1), dim3(64), 0, e->stream, e->d_xcnt, e->d_xsend, e->d_xsoff, P,
-                           e->part, e->xstride, e->d_segbytes, e->d_payload + e->dist_k);
+                           e->part, e->xstride, e->d_segbytes, e->d_payload + e->dist_k, ipc_args(e));
         HIPCHK(hipGetLastError());
         for (uint32_t q = 0; q < P; ++q) {  // peers: the parts of this lane group
             const uint32_t pr = e->peer_rank(q);
@@ -2628,7 +2672,10 @@ static int dist_begin(gg_engine* e, gg_exchange* x, bool host_sizes) {
             e->xsend_bytes[pr] = e->xsoff[q + 1] - e->xsoff[q];
             e->xrecv_bytes[pr] = e->xroff[q + 1] - e->xroff[q];
         }
-        if (e->xexact && host_sizes) {
+        if (e->ipc) {  // the pack kernels deliver the segments: nothing for a caller to move
+            std::fill(e->xsend_bytes.begin(), e->xsend_bytes.end(), 0);
+            std::fill(e->xrecv_bytes.begin(), e->xrecv_bytes.end(), 0);
+        } else if (e->xexact && host_sizes) {
             HIPCHK(hipMemcpyAsync(e->h_segbytes, e->d_segbytes, P * 8, hipMemcpyDeviceToHost, e->stream));
             HIPCHK(hipStreamSynchronize(e->stream));
             for (uint32_t q = 0; q < P; ++q)
@@ -2676,6 +2723,8 @@ int gg_dist_round_end(gg_engine* e, gg_round_stats* out) {
         ua.nwp = (uint32_t)e->nwp;
         ua.stride = e->xstride;
         ua.round = (uint32_t)r;
+        ua.ipc = ipc_args(e);
+        if (e->ipc) ua.in = e->d_win + gg::kWinHdr + (e->xseq & 1) * e->win_rbuf;
         const uint64_t cap = 2 * e->n_ghost * (e->nwp >= 2 ? 1 + e->nwp / 2 : 1);  // 16-byte pieces, at most
         const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((cap + gg::kBlock - 1) / gg::kBlock, 2048));
         hipLaunchKernelGGL(gg::unpack_ghosts, dim3(blocks), dim3(gg::kBlock), 0, e->stream, ua);
@@ -2686,6 +2735,7 @@ int gg_dist_round_end(gg_engine* e, gg_round_stats* out) {
         HIPCHK(hipGetLastError());
     }
     e->dist_k++;
+    if (e->P > 1) e->xseq++;  // every part of the lane group counts the same rounds
     retire_round(e, r);
     e->round++;
     e->dist_open = false;
@@ -2842,10 +2892,92 @@ int gg_dist_comm_init(gg_engine* e, const uint8_t* id_in) {
     return GG_OK;
 }
 
+// ---- device-driven exchange (IPC-mapped windows) ----------------------------
+namespace {
+struct IpcBlob {
+    uint32_t magic, part, parts, lgrp;
+    uint64_t rbuf;          // receive buffer bytes of the exporting engine
+    uint64_t roff[64];      // where source part q's segment lands in its receive buffer (xroff[q])
+    hipIpcMemHandle_t handle;
+};
+static_assert(sizeof(IpcBlob) <= GG_IPC_BLOB_BYTES, "IPC blob size");
+constexpr uint32_t kIpcMagic = 0x43504947u;  // "GIPC"
+}  // namespace
+
+int gg_dist_ipc_export(gg_engine* e, uint8_t* blob) {
+    if (!e || !blob) return GG_EINVAL;
+    if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
+    if (e->P < 2) return e->fail(GG_EINVAL, "no vertex parts: nothing to exchange");
+    if (e->comm || e->have_xport || e->ipc) return e->fail(GG_EINVAL, "exchange transport already set");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (!e->d_win) {
+        e->win_rbuf = (e->xroff[e->P] + 255) / 256 * 256;
+        const uint64_t bytes = gg::kWinHdr + 2 * std::max<uint64_t>(e->win_rbuf, 256);
+        // uncached: stores from the peers' pack kernels and this engine's reads meet in HBM
+        HIPCHK(hipExtMallocWithFlags(reinterpret_cast<void**>(&e->d_win), bytes, hipDeviceMallocUncached));
+        HIPCHK(hipMemset(e->d_win, 0, bytes));
+        HIPCHK(hipMalloc(&e->d_xticket, 8));
+        HIPCHK(hipMemset(e->d_xticket, 0, 8));
+    }
+    IpcBlob b{};
+    b.magic = kIpcMagic;
+    b.part = e->part;
+    b.parts = e->P;
+    b.lgrp = e->lgrp;
+    b.rbuf = std::max<uint64_t>(e->win_rbuf, 256);
+    for (uint32_t q = 0; q < e->P; ++q) b.roff[q] = e->xroff[q];
+    HIPCHK(hipIpcGetMemHandle(&b.handle, e->d_win));
+    std::memset(blob, 0, GG_IPC_BLOB_BYTES);
+    std::memcpy(blob, &b, sizeof(b));
+    return GG_OK;
+}
+
+int gg_dist_ipc_import(gg_engine* e, const uint8_t* blobs) {
+    if (!e || !blobs) return GG_EINVAL;
+    if (!e->d_win) return e->fail(GG_EINVAL, "gg_dist_ipc_import: call gg_dist_ipc_export first");
+    if (e->ipc) return e->fail(GG_EINVAL, "exchange transport already set");
+    const uint32_t P = e->P;
+    std::vector<IpcBlob> b(P);
+    for (uint32_t q = 0; q < P; ++q) {
+        std::memcpy(&b[q], blobs + (size_t)q * GG_IPC_BLOB_BYTES, sizeof(IpcBlob));
+        if (b[q].magic != kIpcMagic || b[q].part != q || b[q].parts != P || b[q].lgrp != e->lgrp)
+            return e->fail(GG_EINVAL, "gg_dist_ipc_import: blob " + std::to_string(q) +
+                                          " is not part " + std::to_string(q) + " of this lane group");
+    }
+    HIPCHK(hipSetDevice(e->device));
+    std::vector<uint8_t*> win(P, nullptr);
+    std::vector<uint64_t> off(P, 0), rb(P, 0);
+    e->peer_map.assign(P, nullptr);
+    e->send_mask = e->recv_mask = 0;
+    for (uint32_t q = 0; q < P; ++q) {
+        const bool snd = q != e->part && e->xsoff[q + 1] > e->xsoff[q];
+        const bool rcv = q != e->part && e->xroff[q + 1] > e->xroff[q];
+        if (!snd && !rcv) continue;
+        void* m = nullptr;
+        HIPCHK(hipIpcOpenMemHandle(&m, b[q].handle, hipIpcMemLazyEnablePeerAccess));
+        e->peer_map[q] = m;
+        win[q] = static_cast<uint8_t*>(m);
+        off[q] = b[q].roff[e->part];
+        rb[q] = b[q].rbuf;
+        if (snd) e->send_mask |= 1ull << q;
+        if (rcv) e->recv_mask |= 1ull << q;
+    }
+    HIPCHK(hipMalloc(&e->d_peer_win, P * sizeof(uint8_t*)));
+    HIPCHK(hipMalloc(&e->d_peer_off, P * 8));
+    HIPCHK(hipMalloc(&e->d_peer_rbuf, P * 8));
+    HIPCHK(hipMemcpy(e->d_peer_win, win.data(), P * sizeof(uint8_t*), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->d_peer_off, off.data(), P * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->d_peer_rbuf, rb.data(), P * 8, hipMemcpyHostToDevice));
+    e->ipc = true;
+    e->xseq = 0;
+    return GG_OK;
+}
+
 int gg_dist_transport_init(gg_engine* e, const gg_transport* t) {
     if (!e || !t || !t->group_start || !t->send || !t->recv || !t->group_end) return GG_EINVAL;
     if (e->world < 2) return e->fail(GG_EINVAL, "not a sharded engine (world == 1)");
-    if (e->comm || e->have_xport) return e->fail(GG_EINVAL, "exchange transport already set");
+    if (e->comm || e->have_xport || e->ipc) return e->fail(GG_EINVAL, "exchange transport already set");
     e->xport = *t;
     e->have_xport = true;
     return GG_OK;
@@ -2910,8 +3042,8 @@ extern "C" {
 int gg_dist_step(gg_engine* e, uint32_t n_rounds) {
     if (!e) return GG_EINVAL;
     const uint32_t P = e->P;
-    if (P > 1 && !e->comm && !e->have_xport)
-        return e->fail(GG_EINVAL, "no communicator (gg_dist_comm_init or gg_dist_transport_init)");
+    if (P > 1 && !e->comm && !e->have_xport && !e->ipc)
+        return e->fail(GG_EINVAL, "no communicator (gg_dist_comm_init, gg_dist_transport_init or gg_dist_ipc_import)");
     auto peer = [&](uint32_t q) {  // shares edges with part q (capacities are non-zero both ways)
         return q != e->part && e->xsoff.size() > q + 1 && e->xsoff[q + 1] > e->xsoff[q];
     };
@@ -2920,7 +3052,7 @@ int gg_dist_step(gg_engine* e, uint32_t n_rounds) {
         gg_exchange x{};
         int rc = dist_begin(e, &x, false);
         if (rc) return rc;
-        if (P > 1) {
+        if (P > 1 && !e->ipc) {  // (IPC: the pack kernels delivered the segments already)
             for (uint32_t q = 0; q < P; ++q) {
                 sb[q] = e->xsoff[q + 1] - e->xsoff[q];
                 rb[q] = e->xroff[q + 1] - e->xroff[q];

@@ -3663,6 +3663,57 @@ __global__ void build_edge_mask(const int64_t* in_ptr, const uint32_t* in_col, u
 // (nwp >= 2). A quiet round sends headers only.
 constexpr uint32_t XK_SET = 0x80000000u;
 
+// Device-driven exchange (gg_dist_ipc_*): every engine exports one window of
+// uncached HBM — flags, then two receive buffers by the parity of the exchange
+// sequence number seq (one per round, never reset) — and maps its peers'
+// windows. The sender packs each peer's segment straight into the peer's
+// receive buffer over xGMI, fences (system scope) and sets the peer's ready
+// slot to seq + 1; the receiver's unpack waits for those slots, reads, and its
+// last block sets each sender's consumed slot to seq + 1; a sender waits for
+// consumed >= seq - 1 before packing into a buffer (seq - 2 used it last). No
+// host wait, no collective call: the round is a fixed launch sequence.
+// Waits are bounded (kSpinLimit sleeps, ~15 s): a peer that never arrives sets
+// the engine's error word instead of hanging the GPU.
+constexpr uint64_t kWinHdr = 4096;         // flags area at the start of a window
+constexpr uint32_t kWinReady = 0;          // u64 ready[64]: by source part
+constexpr uint32_t kWinConsumed = 512;     // u64 consumed[64]: by receiving part
+constexpr uint32_t kSpinLimit = 1u << 25;
+
+// Wait until flags[q] >= want for every q in mask (system-scope acquire loads).
+// One thread calls it; false (and err set) after the bound.
+__device__ __forceinline__ bool wait_flags(const uint64_t* flags, uint64_t mask, uint64_t want, uint32_t* err) {
+    for (; mask; mask &= mask - 1) {
+        const int q = __ffsll((long long)mask) - 1;
+        uint32_t it = 0;
+        while (__hip_atomic_load(flags + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+            if (++it > kSpinLimit) {
+                atomicOr(err, 1u);
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(16);
+        }
+    }
+    return true;
+}
+
+struct IpcArgs {
+    uint8_t* const* peer_win;  // [parts] mapped peer windows (nullptr: no IPC exchange)
+    const uint64_t* peer_off;  // [parts] where this engine's segment lands in peer q's receive buffer
+    const uint64_t* peer_rbuf; // [parts] peer q's receive buffer bytes (the parity stride)
+    uint64_t* my_win;          // this engine's window
+    uint64_t rbuf;             // this engine's receive buffer bytes
+    uint64_t send_mask;        // parts this engine sends to
+    uint64_t recv_mask;        // parts this engine receives from
+    uint64_t seq;              // exchange sequence number of this round
+    uint32_t* ticket;          // unpack's last-block counter
+    uint32_t* err;             // bit 0: a wait ran out
+};
+
+// Peer q's segment for this engine in this round's receive buffer.
+__device__ __forceinline__ uint8_t* ipc_segment(const IpcArgs& ip, uint32_t q) {
+    return ip.peer_win[q] + kWinHdr + (ip.seq & 1) * ip.peer_rbuf[q] + ip.peer_off[q];
+}
+
 struct XchgTile {
     uint32_t peer;   // part index of the destination
     uint32_t k0;     // first send entry of the tile (global send-list index)
@@ -3685,6 +3736,7 @@ struct PackArgs {
     const uint64_t* seg_off;    // [parts] byte offset of each peer's segment in `out`
     uint32_t nwp, stride;
     int32_t sync;               // sets may be read next round
+    IpcArgs ipc;                // device-driven exchange: segments go straight to the peers
 };
 
 __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
@@ -3693,6 +3745,12 @@ __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
     __shared__ uint32_t s_base, s_tot;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t cpe = x.nwp >= 2 ? 1 + x.nwp / 2 : 1;  // 16-byte chunks per entry
+    if (x.ipc.peer_win) {  // the peers' buffers of this parity are free once they read seq - 2
+        if (threadIdx.x == 0 && x.ipc.seq >= 2)
+            wait_flags(reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(x.ipc.my_win) + kWinConsumed),
+                       x.ipc.send_mask, x.ipc.seq - 1, x.ipc.err);
+        __syncthreads();
+    }
     for (uint32_t ti = blockIdx.x; ti < x.n_tiles; ti += gridDim.x) {
         const XchgTile t = x.tiles[ti];
         const uint32_t k = t.k0 + threadIdx.x;
@@ -3738,7 +3796,8 @@ __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
             s_head[pos] = idx | XK_SET;
         }
         __syncthreads();
-        uint8_t* seg = x.out + x.seg_off[t.peer] + 16 + (uint64_t)s_base * x.stride;
+        uint8_t* seg = (x.ipc.peer_win ? ipc_segment(x.ipc, t.peer) : x.out + x.seg_off[t.peer]) + 16 +
+                       (uint64_t)s_base * x.stride;
         for (uint32_t e = threadIdx.x; e < s_tot * cpe; e += kBlock) {
             const uint32_t j = e / cpe, ch = e % cpe;
             const uint32_t hd = s_head[j], rr = s_row[j];
@@ -3774,12 +3833,13 @@ __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
         }
         __syncthreads();  // LDS reuse
     }
+    if (x.ipc.peer_win) __threadfence_system();  // this thread's segment stores performed before finish_pack's flags
 }
 
 // After pack_ghosts: each peer's header, its byte count for an exact-size
 // exchange, the round's payload bytes; counters reset for the next round.
 __global__ void finish_pack(uint32_t* cnt, uint8_t* out, const uint64_t* seg_off, uint32_t parts, uint32_t self,
-                            uint32_t stride, unsigned long long* seg_bytes, unsigned long long* payload) {
+                            uint32_t stride, unsigned long long* seg_bytes, unsigned long long* payload, IpcArgs ip) {
     const uint32_t q = threadIdx.x;
     unsigned long long pay = 0;
     if (q < parts) {
@@ -3789,8 +3849,13 @@ __global__ void finish_pack(uint32_t* cnt, uint8_t* out, const uint64_t* seg_off
             ulonglong2 h;
             h.x = n;
             h.y = (unsigned long long)n * stride;
-            *reinterpret_cast<ulonglong2*>(out + seg_off[q]) = h;
+            *reinterpret_cast<ulonglong2*>(ip.peer_win ? ipc_segment(ip, q) : out + seg_off[q]) = h;
             pay = (unsigned long long)n * stride;
+            if (ip.peer_win) {  // the segment is complete at system scope: peer q may read it
+                __threadfence_system();
+                __hip_atomic_store(reinterpret_cast<uint64_t*>(ip.peer_win[q] + kWinReady) + self, ip.seq + 1,
+                                   __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
         seg_bytes[q] = peer ? 16 + (unsigned long long)n * stride : 0ull;
         cnt[q] = 0;
@@ -3823,6 +3888,7 @@ struct UnpackArgs {
     uint64_t ghost0, n_ghost;
     uint32_t nwp, stride;
     uint32_t round;
+    IpcArgs ipc;                 // device-driven exchange: `in` is this round's receive buffer
 };
 
 // Every received entry into its ghost row (kind F: F row, flag ACT, stamp;
@@ -3830,6 +3896,9 @@ struct UnpackArgs {
 __global__ __launch_bounds__(kBlock) void unpack_ghosts(UnpackArgs x) {
     __shared__ uint32_t s_src[64], s_pref[65];
     const uint32_t cpe = x.nwp >= 2 ? 1 + x.nwp / 2 : 1;
+    if (threadIdx.x == 0 && x.ipc.peer_win)  // every source's segment of this round has landed
+        wait_flags(reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(x.ipc.my_win) + kWinReady),
+                   x.ipc.recv_mask, x.ipc.seq + 1, x.ipc.err);
     if (threadIdx.x == 0) {
         uint32_t tot = 0, m = 0;
         for (uint32_t p = 0; p < x.parts; ++p) {
@@ -3880,6 +3949,20 @@ __global__ __launch_bounds__(kBlock) void unpack_ghosts(UnpackArgs x) {
     }
     const unsigned long long s = wave_sum(nact);
     if ((threadIdx.x & 63) == 0 && s) atomicAdd(x.act_cur + (blockIdx.x % kSlots), (uint32_t)s);
+    if (x.ipc.peer_win) {  // the last block to finish tells every source its buffer is free
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            if (atomicAdd(x.ipc.ticket, 1u) == gridDim.x - 1) {
+                *x.ipc.ticket = 0;
+                for (uint64_t m = x.ipc.recv_mask; m; m &= m - 1) {
+                    const int p = __ffsll((long long)m) - 1;
+                    __hip_atomic_store(reinterpret_cast<uint64_t*>(x.ipc.peer_win[p] + kWinConsumed) + x.self,
+                                       x.ipc.seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            }
+        }
+    }
 }
 
 // Ghosts whose F row of round r-2 sits in this round's buffer and that sent no

@@ -134,10 +134,15 @@ class ShardedRunner:
         self._views = {}   # (ptr, bytes, on_device) -> tensor view of engine memory
         self._streams = {}  # stream ptr -> torch.cuda.ExternalStream
         want = transport or os.environ.get("GG_DIST_TRANSPORT", "engine")
-        if want not in ("engine", "torch"):
-            raise ValueError(f"transport {want!r}: 'engine' or 'torch'")
+        if want not in ("engine", "torch", "ipc"):
+            raise ValueError(f"transport {want!r}: 'engine', 'torch' or 'ipc'")
         self.host_xport = None
-        if self.nccl:
+        if want == "ipc" and eng.parts > 1:
+            # device-driven exchange: the parts map each other's windows once; the
+            # rounds need no collective and no host wait (gossip.h gg_dist_ipc_*)
+            self.engine_comm = True
+            _ipc_connect([eng], self.group, self.rank, self.world, eng.parts)
+        elif self.nccl:
             self.engine_comm = want == "engine" and self._init_engine_comm()
         else:  # gloo: the engine's own sequencing only when asked (transport="engine")
             self.engine_comm = transport == "engine" and eng.parts > 1
@@ -147,6 +152,7 @@ class ShardedRunner:
             self.engine_comm = True  # lane groups only: nothing to exchange, gg_dist_step runs the rounds
         if self.engine_comm:
             self.transport = "none (lane groups only)" if eng.parts == 1 else (
+                "device-driven: IPC-mapped peer windows, kernel flag hand-over" if want == "ipc" else
                 "engine RCCL send/recv" if self.nccl else "engine sequencing, gloo host transport")
         else:
             self.transport = "torch all_to_all_single" if self.nccl else "gloo via host"
@@ -289,6 +295,25 @@ class ShardedRunner:
         return out
 
 
+def _ipc_connect(engines: list[Engine], group, rank: int, world: int, P: int) -> None:
+    """Every process exports its engines' windows (one blob each, engines in
+    lane-group order), one all_gather of the blobs, and each engine imports the
+    P blobs of its own lane group in part order."""
+    from .engine import IPC_BLOB_BYTES
+    mine = b"".join(e.dist_ipc_export() for e in engines)
+    t = torch.frombuffer(bytearray(mine), dtype=torch.uint8)
+    if dist.get_backend(group) == "nccl":
+        t = t.to(torch.device("cuda", torch.cuda.current_device()))
+    got = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(got, t, group=group)
+    allb = [g.cpu().numpy().tobytes() for g in got]  # allb[r][h * BLOB:]: engine h of rank r
+    B = IPC_BLOB_BYTES
+    for h, e in enumerate(engines):
+        g = rank // P  # the process's lane group index (rank = group * P + part)
+        blobs = b"".join(allb[g * P + q][h * B:(h + 1) * B] for q in range(P))
+        e.dist_ipc_import(blobs)
+
+
 def _sum_rounds(a: list[dict], b: list[dict]) -> list[dict]:
     """Per-round counters of two engines over disjoint lanes, summed (seen_hash mod 2^64)."""
     out = []
@@ -317,7 +342,7 @@ class HalvesRunner:
     node has remote neighbours (R-MAT, random long links) this is the overlap
     that interior-first ordering cannot give: there are no interior nodes."""
 
-    def __init__(self, engines: list[Engine], device: torch.device, group=None):
+    def __init__(self, engines: list[Engine], device: torch.device, group=None, transport: str | None = None):
         assert len(engines) == 2
         self.engs = engines
         self.device, self.group = device, group
@@ -331,8 +356,12 @@ class HalvesRunner:
         self.nccl = dist.get_backend(group) == "nccl"
         glob = (lambda r: r) if group is None else (lambda r: dist.get_global_rank(group, r))
         self.xports = []
+        want = transport or os.environ.get("GG_DIST_TRANSPORT", "engine")
         if P == 1:
             self.transport = "none (lane groups only)"
+        elif want == "ipc":
+            _ipc_connect(engines, group, self.rank, self.world, P)
+            self.transport = "device-driven: IPC-mapped peer windows, two lane halves per GPU"
         elif self.nccl:
             ok = all(e.dist_comm_available()[0] for e in engines)
             flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)

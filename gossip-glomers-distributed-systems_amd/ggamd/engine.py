@@ -121,6 +121,7 @@ STAT_FIELDS = [f for f, _ in GGRoundStats._fields_]
 DIAG_FIELDS = ("round", "kernel_ms", "work_rows", "work_gathers", "prep_ms", "expand_ms", "stream_ms",
                "prep_bytes", "expand_bytes", "stream_bytes", "sent_bytes", "path")
 # gg_round_stats.path bits (gossip.h GG_PATH_*)
+IPC_BLOB_BYTES = 1024  # gossip.h GG_IPC_BLOB_BYTES
 PATH_STREAM, PATH_DB, PATH_SYNC_STREAM, PATH_TILES, PATH_MASKED, PATH_BATCHED, PATH_NO_PREP = 1, 2, 4, 8, 16, 32, 64
 COUNT_FIELDS = [f for f in STAT_FIELDS if f not in DIAG_FIELDS]
 
@@ -133,6 +134,7 @@ GG_SYMBOLS = [
     "gg_read_bits_nodes", "gg_delivery_rounds_nodes",
     "gg_dist_round_begin", "gg_dist_round_end", "gg_dist_flush", "gg_dist_owned", "gg_dist_info",
     "gg_dist_comm_available", "gg_dist_comm_id", "gg_dist_comm_init", "gg_dist_transport_init", "gg_dist_step",
+    "gg_dist_ipc_export", "gg_dist_ipc_import",
 ]
 
 _LIBS: dict[str, C.CDLL] = {}
@@ -179,6 +181,8 @@ def load_library(path: str) -> C.CDLL:
     lib.gg_dist_comm_id.argtypes = [C.c_void_p, C.c_void_p]
     lib.gg_dist_comm_init.argtypes = [C.c_void_p, C.c_void_p]
     lib.gg_dist_step.argtypes = [C.c_void_p, C.c_uint32]
+    lib.gg_dist_ipc_export.argtypes = [C.c_void_p, C.c_void_p]
+    lib.gg_dist_ipc_import.argtypes = [C.c_void_p, C.c_void_p]
     lib.gg_dist_transport_init.argtypes = [C.c_void_p, P(GGTransport)]
     lib.gg_delivery_rounds_nodes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
     if hasattr(lib, "gg_topology_generate"):
@@ -423,6 +427,18 @@ class Engine:
         if rc:
             raise RuntimeError(f"gg_dist_comm_id failed ({rc})")
         return bytes(buf)
+
+    def dist_ipc_export(self) -> bytes:
+        """This part's exchange window as a GG_IPC_BLOB_BYTES blob (device-driven exchange)."""
+        buf = (C.c_uint8 * IPC_BLOB_BYTES)()
+        self._ok(self.lib.gg_dist_ipc_export(self.h, buf))
+        return bytes(buf)
+
+    def dist_ipc_import(self, blobs: bytes) -> None:
+        """Map the windows of every part of this lane group (P blobs, part order)."""
+        assert len(blobs) == self.parts * IPC_BLOB_BYTES
+        buf = (C.c_uint8 * len(blobs)).from_buffer_copy(blobs)
+        self._ok(self.lib.gg_dist_ipc_import(self.h, buf))
 
     def dist_comm_init(self, uid: bytes) -> None:
         assert len(uid) == 128

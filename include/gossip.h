@@ -290,9 +290,25 @@ typedef struct {
     int (*group_end)(void* user);
 } gg_transport;
 int gg_dist_transport_init(gg_engine* e, const gg_transport* t);
-/* n sharded rounds with the engine's exchange (RCCL or the transport; none needed
- * when the engine has no other vertex part). */
+/* n sharded rounds with the engine's exchange (RCCL, the transport or IPC; none
+ * needed when the engine has no other vertex part). */
 int gg_dist_step(gg_engine* e, uint32_t n_rounds);
+
+/* Device-driven exchange (no host wait, no collective call per round): every part
+ * of a lane group exports one window of uncached device memory (flags and two
+ * receive buffers) as a blob of GG_IPC_BLOB_BYTES (gg_dist_ipc_export), the caller
+ * hands every part all P blobs of its lane group in part order, and
+ * gg_dist_ipc_import maps the peers' windows (hipIpcOpenMemHandle; peers are other
+ * processes, on this GPU or another of the node). From then on gg_dist_step packs
+ * each peer's segment straight into the peer's receive buffer over xGMI and the
+ * kernels hand rounds over with flags in the windows (bounded waits: a peer that
+ * never arrives gives GG_EIO at the next flush instead of a hang); the round is a
+ * fixed launch sequence on the engine stream. Every part must run the same number
+ * of sharded rounds (they count them); a new topology drops the windows (export
+ * and import again). gg_dist_round_begin reports zero bytes to move. */
+#define GG_IPC_BLOB_BYTES 1024
+int gg_dist_ipc_export(gg_engine* e, uint8_t* blob /* GG_IPC_BLOB_BYTES */);
+int gg_dist_ipc_import(gg_engine* e, const uint8_t* blobs /* P x GG_IPC_BLOB_BYTES, part order */);
 
 /* gg_read_bits / gg_delivery_rounds for a list of owned nodes (any engine). */
 int gg_read_bits_nodes(gg_engine* e, const uint32_t* nodes, uint64_t n, uint64_t* out);

@@ -698,3 +698,87 @@ def test_sharded_db_paths_equal_oracle(hip_lib, cpu_lib, world, db):
             else:
                 assert n_db == 0, (k, rank)
         ref.close()
+
+
+def _ipc_worker(rank, world, port, lib, scenarios, q, lane_groups, env):
+    import torch
+    import torch.distributed as dist
+
+    from ggamd.dist import ShardedRunner
+    from helpers import apply
+    os.environ.update(env or {})
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        out = []
+        dev = torch.device("cuda", 0)
+        for sc in scenarios:
+            e = make_engine(lib, sc, rank=rank, world=world, device=0, lane_groups=lane_groups)
+            r = ShardedRunner(e, dev, transport="ipc")
+            assert r.transport.startswith("device-driven"), r.transport
+            half = sc.rounds // 2
+            first = r.step(half) + r.step(sc.rounds - half)
+            owned = e.dist_owned()
+            res = (first, owned, e.read_bits_nodes(owned), e.delivery_rounds_nodes(owned))
+            # a second episode after gg_reset: the exchange's sequence numbers go on
+            e.reset()
+            for n, v, rr in sc.injections:
+                e.broadcast(int(n), int(v), int(rr))
+            again = r.step(sc.rounds)
+            out.append(res + (again,))
+            e.close()
+        q.put((rank, out))
+    except BaseException as exc:  # report instead of leaving the parent waiting
+        q.put((rank, f"rank {rank} failed: {exc!r}"))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,lane_groups", [(2, 1), (3, 1), (4, 2), (8, 1)])
+def test_ipc_exchange_equals_oracle(hip_lib, cpu_lib, world, lane_groups):
+    """The device-driven exchange (gg_dist_ipc_*): every rank a process with an
+    engine on the one GPU, windows mapped with hipIpcOpenMemHandle, segments
+    packed straight into the peers' receive buffers and handed over by kernel
+    flags — no collective and no host wait per round. Counters of every round,
+    node sets and delivery rounds equal O2, and a second episode after gg_reset
+    equals the first."""
+    from ggamd import topology as T
+    from ggamd.workload import uniform_injections
+    scs = [Scenario(T.tree(3000, 4), 256, 30, uniform_injections(3000, 200, 5), seed=9, sync_base=6, sync_jitter=3,
+                    windows=[("seeded", 3, 9, 77)]),
+           Scenario(T.grid_links(40, seed=11), 64, 36, uniform_injections(1600, 64, 6), seed=10, sync_base=8,
+                    sync_jitter=4),
+           Scenario(T.rmat(2048, 8, seed=22), 128, 26, uniform_injections(2048, 100, 9), seed=14, sync_base=8,
+                    sync_jitter=4)]
+    scs = [sc for sc in scs if sc.W >= 64 * lane_groups]  # a lane group holds whole 64-lane words
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ipc_worker, args=(r, world, port, hip_lib, scs, qq, lane_groups, None))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, got = qq.get(timeout=170)
+        assert not isinstance(got, str), got
+        res[r] = got
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for k, sc in enumerate(scs):
+        ref = make_engine(cpu_lib, sc)
+        want = ref.step(sc.rounds)
+        tot_own = []
+        for rank in range(world):
+            stats, owned, bits, dr, again = res[rank][k]
+            d = diff_stats(want, stats)
+            assert not d, (k, rank, d[:8])
+            assert not diff_stats(want, again), (k, rank, "second episode")
+            if lane_groups == 1:  # (a lane-group engine holds its own lanes only)
+                assert np.array_equal(bits, ref.read_bits_nodes(owned)), (k, rank)
+                assert np.array_equal(dr, ref.delivery_rounds_nodes(owned)), (k, rank)
+            if rank < world // lane_groups:
+                tot_own.append(owned)
+        assert np.array_equal(np.sort(np.concatenate(tot_own)), np.arange(sc.topo.n_nodes)), k
+        ref.close()
