@@ -132,6 +132,10 @@ def main():
                     help="N = 1: after the timed region, episodes rotating this many distinct seeded injection "
                          "sets (every step re-captures its launch graph and uploads its injections; 0: skip)")
     ap.add_argument("--no-check", action="store_true", help="skip the N > 1 single-engine check")
+    ap.add_argument("--xchg", default=os.environ.get("GG_DIST_TRANSPORT", "engine"), choices=["engine", "ipc", "torch"],
+                    help="N > 1 exchange between vertex parts: engine = the engine's grouped RCCL send/recv; "
+                         "ipc = device-driven (IPC-mapped peer windows, kernel flags, captured batches of rounds, "
+                         "no host wait); torch = torch all_to_all")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 "
                     "(nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
     args = ap.parse_args()
@@ -187,7 +191,8 @@ def main():
         engs = [eng]
         if world > 1:
             from ggamd.dist import ShardedRunner
-            runner = ShardedRunner(eng, device)
+            runner = ShardedRunner(eng, device, transport=args.xchg if args.backend == "nccl" or args.xchg == "ipc"
+                                   else None)
         parallelism = f"vertex-range x{world}" if world > 1 else "single GPU"
         scaling = "weak"
         workload = ("C2: tree4 of 2^20 nodes per GPU, 1024 messages broadcast in round 0 at seeded uniform "
@@ -210,7 +215,7 @@ def main():
             E = engs[0].generate(**gen)
             engs[1].generate(**gen)
             eng = engs[0]
-            runner = HalvesRunner(engs, device)
+            runner = HalvesRunner(engs, device, transport=args.xchg)
         else:
             eng = Engine(V, K, seed=seed, enable_sync=True, device=local, rank=rank, world=world,
                          lane_groups=L)
@@ -218,7 +223,8 @@ def main():
             engs = [eng]
             if P > 1:
                 from ggamd.dist import ShardedRunner
-                runner = ShardedRunner(eng, device, transport=None if args.backend == "nccl" else "engine")
+                runner = ShardedRunner(eng, device, transport=args.xchg if args.backend == "nccl" or args.xchg == "ipc"
+                                       else "engine")
         if world == 1:
             parallelism = "single GPU"
         elif P == 1:

@@ -179,6 +179,8 @@ struct gg_engine {
     uint32_t* d_grow = nullptr;    // [n_ghost] range shard in locality order: ghost row of the g-th ghost
                                    // in exchange order (ascending id)
     bool have_topo = false, symmetric = true;
+    bool part_rows = false;        // built from a caller's own rows (gg_topology_part*): per-edge window
+                                   // bits are over those rows
     std::vector<int64_t> host_rp;  // vertex-sharded: the caller's row offsets (gg_set_partition)
     uint32_t* d_gid = nullptr;     // sharded only (single engine: row == id)
     // exchange: owned rows each rank needs (concatenated per destination) and
@@ -316,6 +318,9 @@ struct gg_engine {
     double step_event_ms = 0.0;           // HIP-event time of the last gg_step (device)
     BatchKey graph_key;
     bool graph_broken = false;
+    hipGraphExec_t dist_exec = nullptr;   // gg_dist_step's captured batch of sharded rounds (IPC / no exchange)
+    BatchKey dist_key;
+    uint32_t dist_key_k0 = 0;             // ... and the counter slot it starts at
 
     // device-driven exchange over IPC-mapped peer windows (gg_dist_ipc_*)
     bool ipc = false;
@@ -326,8 +331,8 @@ struct gg_engine {
     uint64_t* d_peer_off = nullptr;      // [P] this engine's segment offset in peer q's receive buffer
     uint64_t* d_peer_rbuf = nullptr;     // [P] peer q's receive buffer bytes
     uint64_t send_mask = 0, recv_mask = 0;
-    uint64_t xseq = 0;                   // exchange sequence number (one per sharded round, never reset)
-    uint32_t* d_xticket = nullptr;       // [2] unpack's last-block counter, error word
+    uint32_t* d_xticket = nullptr;       // [4] unpack's last-block counter, error word, exchange sequence
+                                         // number (u64: one per sharded round, never reset; on the device)
     ncclComm_t comm = nullptr;  // engine-owned RCCL communicator over the lane group's parts
     gg_transport xport{};       // or the caller's transport (gg_dist_transport_init)
     bool have_xport = false;
@@ -356,6 +361,8 @@ static void dfree(T*& p) {
 void gg_engine::free_topology() {
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
     graph_exec = nullptr;
+    if (dist_exec) (void)hipGraphExecDestroy(dist_exec);
+    dist_exec = nullptr;
     if (d_out_col == d_in_col) d_out_col = nullptr;
     if (d_out_ptr == d_in_ptr) d_out_ptr = nullptr;
     dfree(d_out_col);
@@ -446,6 +453,7 @@ void gg_engine::free_topology() {
         dfree(w.d_ebits);
     }
     have_topo = false;
+    part_rows = false;
 }
 
 static void rccl_destroy(ncclComm_t c);
@@ -2265,7 +2273,9 @@ int gg_topology_part(gg_engine* e, const uint64_t* part_lo, const int64_t* row_p
         if (g.col) (void)hipFree(g.col);
         return e->fail(GG_EIO, std::string("gg_topology_part upload: ") + hipGetErrorString(ue));
     }
-    return install_shard(e, g, plo, nullptr);
+    const int rc = install_shard(e, g, plo, nullptr);
+    if (rc == GG_OK) e->part_rows = true;  // per-edge window bits: over the caller's own rows
+    return rc;
 }
 
 int gg_topology_export(gg_engine* e, int64_t* row_ptr, int32_t* col, uint64_t cap, uint64_t* nnz_out) {
@@ -2335,9 +2345,9 @@ int gg_set_partition(gg_engine* e, int64_t a, int64_t b, const uint64_t* bits) {
     if (!e || !bits) return GG_EINVAL;
     if (!e->have_topo) return e->fail(GG_EINVAL, "gg_set_partition: install the topology first");
     if (!e->symmetric) return e->fail(GG_EINVAL, "gg_set_partition: per-edge windows need a symmetric topology");
-    if (e->P > 1 && e->host_rp.empty())
+    if (e->P > 1 && e->host_rp.empty() && !e->part_rows)
         return e->fail(GG_EINVAL, "gg_set_partition: a shard built by gg_topology_generate holds no whole-graph "
-                                  "row offsets (use gg_topology, or seeded/group windows)");
+                                  "row offsets (use gg_topology or gg_topology_part, or seeded/group windows)");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
     const uint64_t V = e->V, n_own = e->n_own;
@@ -2576,10 +2586,92 @@ static gg::IpcArgs ipc_args(const gg_engine* e) {
     ip.rbuf = e->win_rbuf;
     ip.send_mask = e->send_mask;
     ip.recv_mask = e->recv_mask;
-    ip.seq = e->xseq;
+    ip.seq = reinterpret_cast<uint64_t*>(e->d_xticket + 2);
     ip.ticket = e->d_xticket;
     ip.err = e->d_xticket + 1;
     return ip;
+}
+
+// The pack of round r's ghost payloads (vertex parts): set marks, pack_ghosts
+// (IPC: straight into the peers' receive buffers), finish_pack (headers, sizes,
+// the payload bytes of counter slot `slot`; IPC: the peers' ready flags).
+static int enqueue_pack(gg_engine* e, int64_t r, uint32_t slot) {
+    // sets may be read in r+1 by callbacks (fired in r-1) and pushes (fired in r-2)
+    const bool sync = e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks + 1;
+    if (sync && e->n_ghost) {
+        hipLaunchKernelGGL(gg::mark_set_needs, dim3((unsigned)((e->n_ghost + 255) / 256)), dim3(256), 0,
+                           e->stream, e->d_fired[(r - 1) & 3], e->d_gout_ptr, e->d_gout_sidx, e->ghost0,
+                           e->n_ghost, e->d_needmark);
+        HIPCHK(hipGetLastError());
+    }
+    if (e->ipc && e->send_mask) {  // the peers' buffers of this round's parity are free
+        hipLaunchKernelGGL(gg::ipc_wait, dim3(1), dim3(64), 0, e->stream, ipc_args(e), 0);
+        HIPCHK(hipGetLastError());
+    }
+    if (e->n_xtiles) {
+        gg::PackArgs pa{};
+        pa.F_cur = e->d_F[r & 1];
+        pa.base = e->d_base;
+        // a double-buffered round wrote no F rows: the payload's are set(r) & ~set(r-1)
+        pa.set_prev = e->db_active ? e->d_sets[(r + 1) & 1] : nullptr;
+        pa.flg_cur = e->d_flg[r & 1];
+        pa.fired_m2 = e->d_fired[(r - 2) & 3];
+        pa.needmark = e->d_needmark;
+        pa.send_idx = e->d_send_idx;
+        pa.tiles = e->d_xtiles;
+        pa.n_tiles = e->n_xtiles;
+        pa.cnt = e->d_xcnt;
+        pa.out = e->d_xsend;
+        pa.seg_off = e->d_xsoff;
+        pa.nwp = (uint32_t)e->nwp;
+        pa.stride = e->xstride;
+        pa.sync = sync ? 1 : 0;
+        pa.ipc = ipc_args(e);
+        hipLaunchKernelGGL(gg::pack_ghosts, dim3(std::min<uint32_t>(e->n_xtiles, 4096)), dim3(gg::kBlock), 0,
+                           e->stream, pa);
+        HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(gg::finish_pack, dim3(1), dim3(64), 0, e->stream, e->d_xcnt, e->d_xsend, e->d_xsoff, e->P,
+                       e->part, e->xstride, e->d_segbytes, e->d_payload + slot, ipc_args(e));
+    HIPCHK(hipGetLastError());
+    return GG_OK;
+}
+
+// The received ghost payloads of round r into the ghost rows (IPC: once every
+// source's ready flag says they landed; then the sources' consumed flags).
+static int enqueue_unpack(gg_engine* e, int64_t r) {
+    if (!e->n_ghost) return GG_OK;
+    gg::UnpackArgs ua{};
+    ua.F_cur = e->d_F[r & 1];
+    ua.base = e->d_base;
+    ua.flg_cur = e->d_flg[r & 1];
+    ua.stamp = e->d_stamp;
+    ua.grow = e->d_grow;
+    ua.act_cur = e->d_act_s + (r & 3) * gg::kSlots;
+    ua.in = e->d_xrecv;
+    ua.seg_off = e->d_xroff;
+    ua.gfirst = e->d_gfirst;
+    ua.parts = e->P;
+    ua.self = e->part;
+    ua.ghost0 = e->ghost0;
+    ua.n_ghost = e->n_ghost;
+    ua.nwp = (uint32_t)e->nwp;
+    ua.stride = e->xstride;
+    ua.round = (uint32_t)r;
+    ua.ipc = ipc_args(e);
+    if (e->ipc && e->recv_mask) {  // every source's segment of this round has landed
+        hipLaunchKernelGGL(gg::ipc_wait, dim3(1), dim3(64), 0, e->stream, ua.ipc, 1);
+        HIPCHK(hipGetLastError());
+    }
+    const uint64_t cap = 2 * e->n_ghost * (e->nwp >= 2 ? 1 + e->nwp / 2 : 1);  // 16-byte pieces, at most
+    const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((cap + gg::kBlock - 1) / gg::kBlock, 2048));
+    hipLaunchKernelGGL(gg::unpack_ghosts, dim3(blocks), dim3(gg::kBlock), 0, e->stream, ua);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(gg::clear_stale_ghosts, dim3((unsigned)((e->n_ghost + 255) / 256)), dim3(256), 0, e->stream,
+                       e->d_F[r & 1], e->d_flg[r & 1], e->d_stamp, e->ghost0, e->n_ghost, (uint32_t)e->nwp,
+                       (uint32_t)r);
+    HIPCHK(hipGetLastError());
+    return GG_OK;
 }
 
 // One sharded round up to the exchange: the round's kernels, then (vertex
@@ -2631,40 +2723,7 @@ static int dist_begin(gg_engine* e, gg_exchange* x, bool host_sizes) {
     e->xsend_off.assign(e->world, 0);
     e->xrecv_off.assign(e->world, 0);
     if (P > 1) {
-        // sets may be read in r+1 by callbacks (fired in r-1) and pushes (fired in r-2)
-        const bool sync = e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks + 1;
-        if (sync && e->n_ghost) {
-            hipLaunchKernelGGL(gg::mark_set_needs, dim3((unsigned)((e->n_ghost + 255) / 256)), dim3(256), 0,
-                               e->stream, e->d_fired[(r - 1) & 3], e->d_gout_ptr, e->d_gout_sidx, e->ghost0,
-                               e->n_ghost, e->d_needmark);
-            HIPCHK(hipGetLastError());
-        }
-        if (e->n_xtiles) {
-            gg::PackArgs pa{};
-            pa.F_cur = e->d_F[r & 1];
-            pa.base = e->d_base;
-            // a double-buffered round wrote no F rows: the payload's are set(r) & ~set(r-1)
-            pa.set_prev = e->db_active ? e->d_sets[(r + 1) & 1] : nullptr;
-            pa.flg_cur = e->d_flg[r & 1];
-            pa.fired_m2 = e->d_fired[(r - 2) & 3];
-            pa.needmark = e->d_needmark;
-            pa.send_idx = e->d_send_idx;
-            pa.tiles = e->d_xtiles;
-            pa.n_tiles = e->n_xtiles;
-            pa.cnt = e->d_xcnt;
-            pa.out = e->d_xsend;
-            pa.seg_off = e->d_xsoff;
-            pa.nwp = (uint32_t)e->nwp;
-            pa.stride = e->xstride;
-            pa.sync = sync ? 1 : 0;
-            pa.ipc = ipc_args(e);
-            hipLaunchKernelGGL(gg::pack_ghosts, dim3(std::min<uint32_t>(e->n_xtiles, 4096)), dim3(gg::kBlock), 0,
-                               e->stream, pa);
-            HIPCHK(hipGetLastError());
-        }
-        hipLaunchKernelGGL(gg::finish_pack, dim3(1), dim3(64), 0, e->stream, e->d_xcnt, e->d_xsend, e->d_xsoff, P,
-                           e->part, e->xstride, e->d_segbytes, e->d_payload + e->dist_k, ipc_args(e));
-        HIPCHK(hipGetLastError());
+        if ((rc = enqueue_pack(e, r, e->dist_k))) return rc;
         for (uint32_t q = 0; q < P; ++q) {  // peers: the parts of this lane group
             const uint32_t pr = e->peer_rank(q);
             e->xsend_off[pr] = e->xsoff[q];
@@ -2705,43 +2764,14 @@ int gg_dist_round_end(gg_engine* e, gg_round_stats* out) {
     if (!e || !e->dist_open) return GG_EINVAL;
     HIPCHK(hipSetDevice(e->device));
     const int64_t r = e->round;
-    if (e->n_ghost) {
-        gg::UnpackArgs ua{};
-        ua.F_cur = e->d_F[r & 1];
-        ua.base = e->d_base;
-        ua.flg_cur = e->d_flg[r & 1];
-        ua.stamp = e->d_stamp;
-        ua.grow = e->d_grow;
-        ua.act_cur = e->d_act_s + (r & 3) * gg::kSlots;
-        ua.in = e->d_xrecv;
-        ua.seg_off = e->d_xroff;
-        ua.gfirst = e->d_gfirst;
-        ua.parts = e->P;
-        ua.self = e->part;
-        ua.ghost0 = e->ghost0;
-        ua.n_ghost = e->n_ghost;
-        ua.nwp = (uint32_t)e->nwp;
-        ua.stride = e->xstride;
-        ua.round = (uint32_t)r;
-        ua.ipc = ipc_args(e);
-        if (e->ipc) ua.in = e->d_win + gg::kWinHdr + (e->xseq & 1) * e->win_rbuf;
-        const uint64_t cap = 2 * e->n_ghost * (e->nwp >= 2 ? 1 + e->nwp / 2 : 1);  // 16-byte pieces, at most
-        const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((cap + gg::kBlock - 1) / gg::kBlock, 2048));
-        hipLaunchKernelGGL(gg::unpack_ghosts, dim3(blocks), dim3(gg::kBlock), 0, e->stream, ua);
-        HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(gg::clear_stale_ghosts, dim3((unsigned)((e->n_ghost + 255) / 256)), dim3(256), 0, e->stream,
-                           e->d_F[r & 1], e->d_flg[r & 1], e->d_stamp, e->ghost0, e->n_ghost, (uint32_t)e->nwp,
-                           (uint32_t)r);
-        HIPCHK(hipGetLastError());
-    }
+    int rc = enqueue_unpack(e, r);
+    if (rc) return rc;
     e->dist_k++;
-    if (e->P > 1) e->xseq++;  // every part of the lane group counts the same rounds
     retire_round(e, r);
     e->round++;
     e->dist_open = false;
     if (out) {
-        int rc = fold_pending(e);
-        if (rc) return rc;
+        if ((rc = fold_pending(e))) return rc;
         *out = e->dist_done.back();
         e->dist_done.pop_back();
     }
@@ -2908,7 +2938,7 @@ int gg_dist_ipc_export(gg_engine* e, uint8_t* blob) {
     if (!e || !blob) return GG_EINVAL;
     if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
     if (e->P < 2) return e->fail(GG_EINVAL, "no vertex parts: nothing to exchange");
-    if (e->comm || e->have_xport || e->ipc) return e->fail(GG_EINVAL, "exchange transport already set");
+    if (e->ipc) return e->fail(GG_EINVAL, "exchange transport already set");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
     if (!e->d_win) {
@@ -2917,8 +2947,8 @@ int gg_dist_ipc_export(gg_engine* e, uint8_t* blob) {
         // uncached: stores from the peers' pack kernels and this engine's reads meet in HBM
         HIPCHK(hipExtMallocWithFlags(reinterpret_cast<void**>(&e->d_win), bytes, hipDeviceMallocUncached));
         HIPCHK(hipMemset(e->d_win, 0, bytes));
-        HIPCHK(hipMalloc(&e->d_xticket, 8));
-        HIPCHK(hipMemset(e->d_xticket, 0, 8));
+        HIPCHK(hipMalloc(&e->d_xticket, 16));
+        HIPCHK(hipMemset(e->d_xticket, 0, 16));
     }
     IpcBlob b{};
     b.magic = kIpcMagic;
@@ -2970,7 +3000,6 @@ int gg_dist_ipc_import(gg_engine* e, const uint8_t* blobs) {
     HIPCHK(hipMemcpy(e->d_peer_off, off.data(), P * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->d_peer_rbuf, rb.data(), P * 8, hipMemcpyHostToDevice));
     e->ipc = true;
-    e->xseq = 0;
     return GG_OK;
 }
 
@@ -3039,9 +3068,406 @@ struct XGroup {
 
 extern "C" {
 
+}  // extern "C"
+
+// ---- gg_topology_part_directed: a rank's own rows of a directed topology -----
+// Each node keeps only its own row (broadcast.go:40-45); a receiver's in-list is
+// made of other ranks' rows, so the ranks hand each other the reverse of their
+// cut edges (one exchange of (receiver, sender) pairs over the engine's RCCL
+// communicator or the caller's transport, staged through device memory), and
+// every rank then builds its owned rows, ghosts (remote nodes adjacent in or out),
+// send lists and ghost -> owned lists from local data only.
+static int exchange_reverse_edges(gg_engine* e, const std::vector<uint64_t>& plo, const int64_t* orp,
+                                  const int32_t* ocol, std::vector<int64_t>& irp, std::vector<uint32_t>& icol) {
+    const uint32_t P = e->P, me = e->part;
+    const uint64_t lo = plo[me], hi = plo[me + 1], n = hi - lo;
+    auto owner = [&](uint64_t u) -> uint32_t {
+        return (uint32_t)(std::upper_bound(plo.begin(), plo.end(), u) - plo.begin()) - 1;
+    };
+    std::vector<std::vector<uint64_t>> out(P);  // (receiver << 32 | sender) per receiver's part
+    for (uint64_t i = 0; i < n; ++i)
+        for (int64_t k = orp[i]; k < orp[i + 1]; ++k) {
+            const uint64_t u = (uint64_t)ocol[k];
+            out[owner(u)].push_back(u << 32 | (lo + i));
+        }
+    std::vector<uint64_t> scnt(P), rcnt(P, 0);
+    for (uint32_t q = 0; q < P; ++q) scnt[q] = out[q].size();
+    uint64_t* d_cnt = nullptr;
+    HIPCHK(hipMalloc(&d_cnt, 2 * P * 8));
+    HIPCHK(hipMemcpy(d_cnt, scnt.data(), P * 8, hipMemcpyHostToDevice));
+    {
+        XGroup g(e);
+        for (uint32_t q = 0; q < P; ++q) {
+            if (q == me) continue;
+            g.send(d_cnt + q, 8, q);
+            g.recv(d_cnt + P + q, 8, q);
+        }
+        const int rc = g.close();
+        if (rc) {
+            dfree(d_cnt);
+            return rc;
+        }
+    }
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipMemcpy(rcnt.data(), d_cnt + P, P * 8, hipMemcpyDeviceToHost));
+    dfree(d_cnt);
+    rcnt[me] = 0;
+    uint64_t stot = 0, rtot = 0;
+    std::vector<uint64_t> soff(P + 1, 0), roff(P + 1, 0);
+    for (uint32_t q = 0; q < P; ++q) {
+        soff[q + 1] = soff[q] + (q == me ? 0 : scnt[q]);
+        roff[q + 1] = roff[q] + rcnt[q];
+    }
+    stot = soff[P];
+    rtot = roff[P];
+    std::vector<uint64_t> pairs(out[me]);  // this part's own links
+    uint64_t *d_s = nullptr, *d_r = nullptr;
+    HIPCHK(hipMalloc(&d_s, std::max<uint64_t>(1, stot) * 8));
+    HIPCHK(hipMalloc(&d_r, std::max<uint64_t>(1, rtot) * 8));
+    for (uint32_t q = 0; q < P; ++q)
+        if (q != me && scnt[q]) HIPCHK(hipMemcpy(d_s + soff[q], out[q].data(), scnt[q] * 8, hipMemcpyHostToDevice));
+    int rc = GG_OK;
+    {
+        XGroup g(e);
+        for (uint32_t q = 0; q < P; ++q) {
+            if (q == me) continue;
+            if (scnt[q]) g.send(d_s + soff[q], scnt[q] * 8, q);
+            if (rcnt[q]) g.recv(d_r + roff[q], rcnt[q] * 8, q);
+        }
+        rc = g.close();
+    }
+    if (rc == GG_OK) {
+        pairs.resize(pairs.size() + rtot);
+        const hipError_t ce = hipStreamSynchronize(e->stream);
+        const hipError_t ce2 = ce == hipSuccess && rtot
+                                   ? hipMemcpy(pairs.data() + out[me].size(), d_r, rtot * 8, hipMemcpyDeviceToHost)
+                                   : ce;
+        if (ce2 != hipSuccess) rc = e->fail(GG_EIO, std::string("reverse edges: ") + hipGetErrorString(ce2));
+    }
+    dfree(d_s);
+    dfree(d_r);
+    if (rc) return rc;
+    std::sort(pairs.begin(), pairs.end());  // by receiver, then sender: in-lists ascending by sender id
+    irp.assign(n + 1, 0);
+    icol.resize(pairs.size());
+    for (size_t k = 0; k < pairs.size(); ++k) {
+        const uint64_t u = pairs[k] >> 32;
+        if (u < lo || u >= hi) return e->fail(GG_EIO, "internal: a reverse edge for another part");
+        irp[u - lo + 1]++;
+        icol[k] = (uint32_t)pairs[k];
+    }
+    for (uint64_t i = 0; i < n; ++i) irp[i + 1] += irp[i];
+    return GG_OK;
+}
+
+// The sharded install of gg_topology, from one part's own out-lists and in-lists
+// (global ids, ascending) instead of the whole graph: owned rows in id order
+// (range mode), ghosts by source part and id, send lists, ghost -> owned lists.
+static int install_part_rows(gg_engine* e, const std::vector<uint64_t>& plo, const int64_t* orp, const int32_t* ocolg,
+                             const std::vector<int64_t>& irp, const std::vector<uint32_t>& icolg) {
+    const uint32_t P = e->P, me = e->part;
+    const uint64_t lo = plo[me], hi = plo[me + 1], n_own = hi - lo;
+    auto owner = [&](uint64_t u) -> uint32_t {
+        return (uint32_t)(std::upper_bound(plo.begin(), plo.end(), u) - plo.begin()) - 1;
+    };
+    bool sym = true;  // this part's rows: every out-list equals its in-list
+    for (uint64_t i = 0; i < n_own && sym; ++i) {
+        if (orp[i + 1] - orp[i] != irp[i + 1] - irp[i]) sym = false;
+        for (int64_t k = 0; sym && k < orp[i + 1] - orp[i]; ++k)
+            if ((uint32_t)ocolg[orp[i] + k] != icolg[irp[i] + k]) sym = false;
+    }
+    e->symmetric = sym;
+    e->range_mode = true;
+    e->range_lo = lo;
+    e->range_hi = hi;
+    e->own_row.clear();
+    e->loc_of.clear();
+    e->n_own = n_own;
+    std::vector<std::vector<uint32_t>> gfrom(P), sendl(P);
+    std::vector<uint32_t> peers;
+    for (uint64_t i = 0; i < n_own; ++i) {
+        peers.clear();
+        auto visit = [&](uint32_t u) {
+            const uint32_t q = owner(u);
+            if (q == me) return;
+            gfrom[q].push_back(u);
+            peers.push_back(q);
+        };
+        for (int64_t k = orp[i]; k < orp[i + 1]; ++k) visit((uint32_t)ocolg[k]);
+        for (int64_t k = irp[i]; k < irp[i + 1]; ++k) visit(icolg[k]);
+        std::sort(peers.begin(), peers.end());
+        peers.erase(std::unique(peers.begin(), peers.end()), peers.end());
+        for (uint32_t q : peers) sendl[q].push_back((uint32_t)i);  // owned rows ascend with ids
+    }
+    std::vector<uint32_t> ghosts;
+    e->send_off.assign(P + 1, 0);
+    e->recv_off.assign(P + 1, 0);
+    for (uint32_t q = 0; q < P; ++q) {
+        auto& g = gfrom[q];
+        std::sort(g.begin(), g.end());
+        g.erase(std::unique(g.begin(), g.end()), g.end());
+        ghosts.insert(ghosts.end(), g.begin(), g.end());
+        e->recv_off[q + 1] = e->recv_off[q] + g.size();
+        e->send_off[q + 1] = e->send_off[q] + sendl[q].size();
+    }
+    e->n_ghost = ghosts.size();
+    e->ghost0 = (n_own + 63) / 64 * 64;
+    e->rows = std::max<uint64_t>(64, (e->ghost0 + e->n_ghost + 63) / 64 * 64);
+    if (e->rows > 0x7fffffffull) return e->fail(GG_EINVAL, "local rows exceed 2^31");
+    e->gid.assign(e->rows, ~0u);
+    for (uint64_t i = 0; i < n_own; ++i) e->gid[i] = (uint32_t)(lo + i);
+    for (uint64_t k = 0; k < ghosts.size(); ++k) e->gid[e->ghost0 + k] = ghosts[k];
+    auto row_of = [&](uint32_t u) -> uint32_t {
+        if (u >= lo && u < hi) return (uint32_t)(u - lo);
+        const uint32_t q = owner(u);
+        const uint32_t* g0 = ghosts.data() + e->recv_off[q];
+        const uint32_t* g1 = ghosts.data() + e->recv_off[q + 1];
+        return (uint32_t)(e->ghost0 + e->recv_off[q] + (std::lower_bound(g0, g1, u) - g0));
+    };
+    std::vector<uint32_t> icol(irp[n_own]), ocol(sym ? 0 : orp[n_own]);
+    host_parallel(n_own, [&](uint64_t a, uint64_t b) {
+        for (uint64_t i = a; i < b; ++i) {
+            const int32_t* ob = ocolg + orp[i];
+            const int32_t* oe = ocolg + orp[i + 1];
+            for (int64_t k = irp[i]; k < irp[i + 1]; ++k) {
+                const uint32_t u = icolg[k];
+                const bool recip = sym || std::binary_search(ob, oe, (int32_t)u);
+                icol[k] = row_of(u) | (recip ? gg::kRecipBit : 0u);
+            }
+            if (!sym)
+                for (int64_t k = orp[i]; k < orp[i + 1]; ++k) ocol[k] = row_of((uint32_t)ocolg[k]);
+        }
+    });
+    std::vector<int64_t> gcnt(e->n_ghost + 1, 0);
+    for (uint64_t k = 0; k < icol.size() && e->n_ghost; ++k) {
+        const uint32_t ru = icol[k] & gg::kColMask;
+        if (ru >= e->ghost0) gcnt[ru - e->ghost0 + 1]++;
+    }
+    std::vector<uint32_t> gocol;
+    if (e->n_ghost) {
+        for (uint64_t g = 0; g < e->n_ghost; ++g) gcnt[g + 1] += gcnt[g];
+        gocol.resize(gcnt[e->n_ghost]);
+        std::vector<int64_t> fill(gcnt.begin(), gcnt.end() - 1);
+        for (uint64_t i = 0; i < n_own; ++i)
+            for (int64_t k = irp[i]; k < irp[i + 1]; ++k) {
+                const uint32_t ru = icol[k] & gg::kColMask;
+                if (ru >= e->ghost0) gocol[fill[ru - e->ghost0]++] = (uint32_t)i;
+            }
+    }
+    e->n_in_edges = icol.size();
+    e->n_out_edges = sym ? icol.size() : ocol.size();
+    HIPCHK(hipMalloc(&e->d_in_ptr, (n_own + 1) * 8));
+    HIPCHK(hipMalloc(&e->d_in_col, std::max<size_t>(1, icol.size()) * 4));
+    HIPCHK(hipMemcpy(e->d_in_ptr, irp.data(), (n_own + 1) * 8, hipMemcpyHostToDevice));
+    if (!icol.empty()) HIPCHK(hipMemcpy(e->d_in_col, icol.data(), icol.size() * 4, hipMemcpyHostToDevice));
+    if (sym) {
+        e->d_out_ptr = e->d_in_ptr;
+        e->d_out_col = e->d_in_col;
+    } else {
+        HIPCHK(hipMalloc(&e->d_out_ptr, (n_own + 1) * 8));
+        HIPCHK(hipMalloc(&e->d_out_col, std::max<size_t>(1, ocol.size()) * 4));
+        HIPCHK(hipMemcpy(e->d_out_ptr, orp, (n_own + 1) * 8, hipMemcpyHostToDevice));
+        if (!ocol.empty()) HIPCHK(hipMemcpy(e->d_out_col, ocol.data(), ocol.size() * 4, hipMemcpyHostToDevice));
+    }
+    HIPCHK(hipMalloc(&e->d_gid, e->rows * 4));
+    HIPCHK(hipMemcpy(e->d_gid, e->gid.data(), e->rows * 4, hipMemcpyHostToDevice));
+    std::vector<uint32_t> sidx;
+    for (uint32_t q = 0; q < P; ++q) sidx.insert(sidx.end(), sendl[q].begin(), sendl[q].end());
+    HIPCHK(hipMalloc(&e->d_send_idx, std::max<size_t>(1, sidx.size()) * 4));
+    if (!sidx.empty()) HIPCHK(hipMemcpy(e->d_send_idx, sidx.data(), sidx.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&e->d_gout_ptr, (e->n_ghost + 1) * 8));
+    HIPCHK(hipMemcpy(e->d_gout_ptr, gcnt.data(), (e->n_ghost + 1) * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&e->d_gout_col, std::max<size_t>(1, gocol.size()) * 4));
+    if (!gocol.empty()) HIPCHK(hipMemcpy(e->d_gout_col, gocol.data(), gocol.size() * 4, hipMemcpyHostToDevice));
+    // the send entry of every ghost -> owned edge: the owned row's position in the
+    // send list to the ghost's part (send lists hold owned rows, ascending)
+    std::vector<uint32_t> gsidx(gocol.size());
+    {
+        uint32_t p = 0;
+        for (uint64_t g = 0; g < e->n_ghost; ++g) {
+            while (g >= e->recv_off[p + 1]) ++p;
+            const auto& sl = sendl[p];
+            for (int64_t k = gcnt[g]; k < gcnt[g + 1]; ++k) {
+                const auto it = std::lower_bound(sl.begin(), sl.end(), gocol[k]);
+                if (it == sl.end() || *it != gocol[k]) return e->fail(GG_EIO, "internal: ghost edge without a send entry");
+                gsidx[k] = (uint32_t)(e->send_off[p] + (it - sl.begin()));
+            }
+        }
+    }
+    HIPCHK(hipMalloc(&e->d_gout_sidx, std::max<size_t>(1, gsidx.size()) * 4));
+    if (!gsidx.empty()) HIPCHK(hipMemcpy(e->d_gout_sidx, gsidx.data(), gsidx.size() * 4, hipMemcpyHostToDevice));
+    if (int rc = setup_exchange(e)) return rc;
+    e->part_rows = true;
+    return finish_topology(e, irp.data(), sym ? nullptr : orp);
+}
+
+extern "C" int gg_topology_part_directed(gg_engine* e, const uint64_t* part_lo, const int64_t* row_ptr,
+                                         const int32_t* col, uint64_t nnz) {
+    if (!e || !part_lo || !row_ptr || (nnz && !col)) return GG_EINVAL;
+    if (e->P < 2) return e->fail(GG_EINVAL, "gg_topology_part_directed: not a vertex-sharded engine");
+    if (!e->comm && !e->have_xport)
+        return e->fail(GG_EINVAL, "gg_topology_part_directed: the reverse edges need gg_dist_comm_init or "
+                                  "gg_dist_transport_init first");
+    const uint32_t P = e->P;
+    std::vector<uint64_t> plo(part_lo, part_lo + P + 1);
+    if (plo[0] != 0 || plo[P] != e->V) return e->fail(GG_EINVAL, "part_lo must run from 0 to n_nodes");
+    for (uint32_t q = 0; q < P; ++q)
+        if (plo[q + 1] < plo[q]) return e->fail(GG_EINVAL, "part_lo not ascending");
+    const uint64_t lo = plo[e->part], hi = plo[e->part + 1], n = hi - lo;
+    if (n == 0) return e->fail(GG_EINVAL, "empty part");
+    if (row_ptr[0] != 0 || (uint64_t)row_ptr[n] != nnz) return e->fail(GG_EINVAL, "row_ptr[0]/row_ptr[n] mismatch");
+    for (uint64_t i = 0; i < n; ++i) {
+        if (row_ptr[i + 1] < row_ptr[i]) return e->fail(GG_EINVAL, "row_ptr not monotone");
+        for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; ++k) {
+            if (col[k] < 0 || (uint64_t)col[k] >= e->V) return e->fail(GG_EINVAL, "neighbour id out of range");
+            if (k > row_ptr[i] && col[k] <= col[k - 1]) return e->fail(GG_EINVAL, "neighbour list not ascending/unique");
+        }
+    }
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->free_topology();
+    e->have_topo = false;
+    e->host_rp.clear();
+    e->windows.erase(std::remove_if(e->windows.begin(), e->windows.end(), [](const Window& w) { return w.edges; }),
+                     e->windows.end());
+    std::vector<int64_t> irp;
+    std::vector<uint32_t> icol;
+    int rc = exchange_reverse_edges(e, plo, row_ptr, col, irp, icol);
+    if (rc) return rc;
+    return install_part_rows(e, plo, row_ptr, col, irp, icol);
+}
+
+// gg_dist_step when the exchange needs no host: the device-driven exchange (IPC)
+// or none (lane groups only). Rounds go in batches that fill the pending counter
+// slots; a batch is captured once into a hipGraph (kernels, the exchange's pack
+// and unpack, the counter clear) and replayed while its shape — first round,
+// length, first counter slot, the rounds that inject, lanes injected so far,
+// windows, buffers — is unchanged; the injections and each round's offsets into
+// them are uploaded before the launch and read on the device (as in gg_step). No
+// host wait anywhere: the counters come back with gg_dist_flush.
+static int dist_step_batched(gg_engine* e, uint32_t n_rounds) {
+    HIPCHK(hipSetDevice(e->device));
+    int rc = materialize_windows(e);
+    if (rc) return rc;
+    if ((rc = ensure_db(e))) return rc;
+    if ((rc = ensure_sync(e, e->round + (int64_t)n_rounds - 1))) return rc;
+    if (e->dist_round_of.size() < kMaxBatch) e->dist_round_of.resize(kMaxBatch);
+    if (e->dist_path.size() < kMaxBatch) e->dist_path.resize(kMaxBatch);
+    if (e->dist_sent.size() < kMaxBatch) e->dist_sent.resize(kMaxBatch);
+    if (!e->d_injtab) {
+        HIPCHK(hipMalloc(&e->d_injtab, (kMaxBatch + 1) * sizeof(uint32_t)));
+        HIPCHK(hipHostMalloc(&e->h_injtab, (kMaxBatch + 1) * sizeof(uint32_t)));
+    }
+    static const bool no_graph = ab_knob("GG_NO_GRAPH") != nullptr;
+    const size_t slot = (size_t)gg::kSlots * gg::kCounters;
+    uint32_t done = 0;
+    while (done < n_rounds) {
+        if (e->dist_k == kMaxBatch && (rc = fold_pending(e))) return rc;
+        const uint32_t k0 = e->dist_k;
+        const uint32_t m = std::min<uint32_t>(n_rounds - done, kMaxBatch - k0);
+        const int64_t r0 = e->round;
+        // injections of the batch behind the pending rounds' (their kernels may not have run)
+        std::vector<size_t> off;
+        const size_t base = e->inj_off;
+        const size_t total = pack_injections(e, r0, m, off, base);
+        if (total == (size_t)-1) return GG_EIO;
+        e->inj_dev_hash = 0;  // d_inj holds sharded rounds' pairs
+        if (total)
+            HIPCHK(hipMemcpyAsync(e->d_inj + 2 * base, e->h_inj + 2 * base, total * 8, hipMemcpyHostToDevice,
+                                  e->stream));
+        // the pinned table slots of this batch are not those of a pending batch (slots k0..k0+m)
+        for (uint32_t k = 0; k <= m; ++k) e->h_injtab[k0 + k] = (uint32_t)(base + off[k]);
+        HIPCHK(hipMemcpyAsync(e->d_injtab + k0, e->h_injtab + k0, (m + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
+                              e->stream));
+        e->inj_off += total;
+        e->injtab_dev_hash = ~0ull;  // gg_step's table cache no longer matches d_injtab
+        const bool save_db = e->db_active, save_fd = e->f_dirty;
+        const int save_set = e->set_cur;
+        auto enqueue = [&]() -> int {
+            e->db_active = save_db;
+            e->f_dirty = save_fd;
+            e->set_cur = save_set;
+            e->d_base = e->d_sets[save_set];
+            HIPCHK(hipMemsetAsync(e->d_counters + k0 * slot, 0, (size_t)m * slot * 8, e->stream));
+            for (uint32_t k = 0; k < m; ++k) {
+                e->round = r0 + k;
+                const uint32_t ni = (uint32_t)(off[k + 1] - off[k]);
+                int rc2 = enqueue_round(e, e->d_inj, ni, e->d_counters + (k0 + k) * slot, e->d_injtab + k0 + k);
+                if (rc2) return rc2;
+                if (e->P > 1) {
+                    if ((rc2 = enqueue_pack(e, r0 + k, k0 + k))) return rc2;
+                    if ((rc2 = enqueue_unpack(e, r0 + k))) return rc2;
+                }
+            }
+            return GG_OK;
+        };
+        BatchKey key;
+        key.r0 = r0;
+        key.m = m;
+        key.windows = e->windows.size();
+        key.inj_buf = e->d_inj;
+        key.db_state = (e->db_active ? 2 : 0) | e->set_cur;
+        {
+            uint64_t p = gg_mix64(m);
+            for (size_t k = 0; k < m; ++k) p = gg_mix64(p ^ (off[k + 1] > off[k] ? 2 * k + 1 : 2 * k));
+            key.inj_hash = p;
+            uint64_t u = gg_mix64(~0ull);
+            for (int64_t q = r0 - 1; q < r0 + (int64_t)m; ++q) u = gg_mix64(u ^ lanes_through(e, q));
+            key.u_hash = u;
+        }
+        if (no_graph || e->graph_broken || m < 4) {  // (a capture costs more than a few rounds' launches)
+            if ((rc = enqueue())) return rc;
+        } else {
+            if (!(e->dist_exec && key == e->dist_key && k0 == e->dist_key_k0)) {
+                if (e->dist_exec) (void)hipGraphExecDestroy(e->dist_exec);
+                e->dist_exec = nullptr;
+                hipGraph_t g = nullptr;
+                bool ok = hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+                const int rc2 = ok ? enqueue() : GG_OK;
+                if (ok) ok = hipStreamEndCapture(e->stream, &g) == hipSuccess && g && rc2 == GG_OK;
+                hipGraphExec_t ge = nullptr;
+                if (ok) ok = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) == hipSuccess;
+                if (g) (void)hipGraphDestroy(g);
+                if (!ok) {
+                    (void)hipGetLastError();
+                    e->graph_broken = true;  // direct launches from now on
+                    if ((rc = enqueue())) return rc;
+                } else {
+                    e->dist_exec = ge;
+                    e->dist_key = key;
+                    e->dist_key_k0 = k0;
+                }
+            }
+            if (e->dist_exec) HIPCHK(hipGraphLaunch(e->dist_exec, e->stream));
+        }
+        // host state after the batch (a replayed graph enqueued nothing)
+        e->db_active = save_db;
+        e->f_dirty = save_fd;
+        e->set_cur = save_set;
+        for (uint32_t k = 0; k < m; ++k) {
+            const bool dbk = db_round(e, r0 + k);
+            e->dist_round_of[k0 + k] = r0 + k;
+            e->dist_path[k0 + k] = path_of(e, r0 + k, dbk);
+            db_advance(e, r0 + k, dbk);
+            retire_round(e, r0 + k);
+        }
+        e->round = r0 + m;
+        e->dist_k = k0 + m;
+        e->ctr_dirty = std::max(e->ctr_dirty, e->dist_k);
+        done += m;
+    }
+    return GG_OK;
+}
+
+extern "C" {
+
 int gg_dist_step(gg_engine* e, uint32_t n_rounds) {
     if (!e) return GG_EINVAL;
+    if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
+    if (e->world < 2) return e->fail(GG_EINVAL, "not a sharded engine (world == 1): use gg_step");
+    if (e->dist_open) return e->fail(GG_EINVAL, "round already open");
     const uint32_t P = e->P;
+    if (e->ipc || P == 1) return dist_step_batched(e, n_rounds);
     if (P > 1 && !e->comm && !e->have_xport && !e->ipc)
         return e->fail(GG_EINVAL, "no communicator (gg_dist_comm_init, gg_dist_transport_init or gg_dist_ipc_import)");
     auto peer = [&](uint32_t q) {  // shares edges with part q (capacities are non-zero both ways)

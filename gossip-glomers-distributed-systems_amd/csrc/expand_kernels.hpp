@@ -3669,9 +3669,11 @@ constexpr uint32_t XK_SET = 0x80000000u;
 // windows. The sender packs each peer's segment straight into the peer's
 // receive buffer over xGMI, fences (system scope) and sets the peer's ready
 // slot to seq + 1; the receiver's unpack waits for those slots, reads, and its
-// last block sets each sender's consumed slot to seq + 1; a sender waits for
-// consumed >= seq - 1 before packing into a buffer (seq - 2 used it last). No
-// host wait, no collective call: the round is a fixed launch sequence.
+// last block sets each sender's consumed slot to seq + 1 and advances seq; a
+// sender waits for consumed >= seq - 1 before packing into a buffer (seq - 2
+// used it last). seq lives in device memory, so the round is a fixed launch
+// sequence with no host wait and no collective call, and a captured batch of
+// rounds replays for any seq.
 // Waits are bounded (kSpinLimit sleeps, ~15 s): a peer that never arrives sets
 // the engine's error word instead of hanging the GPU.
 constexpr uint64_t kWinHdr = 4096;         // flags area at the start of a window
@@ -3704,14 +3706,30 @@ struct IpcArgs {
     uint64_t rbuf;             // this engine's receive buffer bytes
     uint64_t send_mask;        // parts this engine sends to
     uint64_t recv_mask;        // parts this engine receives from
-    uint64_t seq;              // exchange sequence number of this round
+    uint64_t* seq;             // exchange sequence number of this round (advanced by unpack)
     uint32_t* ticket;          // unpack's last-block counter
     uint32_t* err;             // bit 0: a wait ran out
 };
 
-// Peer q's segment for this engine in this round's receive buffer.
-__device__ __forceinline__ uint8_t* ipc_segment(const IpcArgs& ip, uint32_t q) {
-    return ip.peer_win[q] + kWinHdr + (ip.seq & 1) * ip.peer_rbuf[q] + ip.peer_off[q];
+// One 64-thread block before pack_ghosts (which = 0: the peers consumed round
+// seq - 2, whose buffers this round reuses) or before unpack_ghosts (which = 1:
+// every source's segment of round seq has landed): lane q waits for part q. A
+// single small block spins, so the kernels it guards hold no CU while a peer on
+// the same GPU still needs one.
+__global__ void ipc_wait(IpcArgs ip, int which) {
+    const uint32_t q = threadIdx.x;
+    const uint64_t seq = *ip.seq;
+    const uint64_t mask = which ? ip.recv_mask : ip.send_mask;
+    if (q >= 64 || !((mask >> q) & 1ull)) return;
+    if (which == 0 && seq < 2) return;
+    const uint64_t* flags =
+        reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(ip.my_win) + (which ? kWinReady : kWinConsumed));
+    wait_flags(flags, 1ull << q, which ? seq + 1 : seq - 1, ip.err);
+}
+
+// Peer q's segment for this engine in round seq's receive buffer.
+__device__ __forceinline__ uint8_t* ipc_segment(const IpcArgs& ip, uint32_t q, uint64_t seq) {
+    return ip.peer_win[q] + kWinHdr + (seq & 1) * ip.peer_rbuf[q] + ip.peer_off[q];
 }
 
 struct XchgTile {
@@ -3745,12 +3763,7 @@ __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
     __shared__ uint32_t s_base, s_tot;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t cpe = x.nwp >= 2 ? 1 + x.nwp / 2 : 1;  // 16-byte chunks per entry
-    if (x.ipc.peer_win) {  // the peers' buffers of this parity are free once they read seq - 2
-        if (threadIdx.x == 0 && x.ipc.seq >= 2)
-            wait_flags(reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(x.ipc.my_win) + kWinConsumed),
-                       x.ipc.send_mask, x.ipc.seq - 1, x.ipc.err);
-        __syncthreads();
-    }
+    const uint64_t seq = x.ipc.peer_win ? *x.ipc.seq : 0;  // (ipc_wait ran before: the buffers are free)
     for (uint32_t ti = blockIdx.x; ti < x.n_tiles; ti += gridDim.x) {
         const XchgTile t = x.tiles[ti];
         const uint32_t k = t.k0 + threadIdx.x;
@@ -3796,7 +3809,7 @@ __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
             s_head[pos] = idx | XK_SET;
         }
         __syncthreads();
-        uint8_t* seg = (x.ipc.peer_win ? ipc_segment(x.ipc, t.peer) : x.out + x.seg_off[t.peer]) + 16 +
+        uint8_t* seg = (x.ipc.peer_win ? ipc_segment(x.ipc, t.peer, seq) : x.out + x.seg_off[t.peer]) + 16 +
                        (uint64_t)s_base * x.stride;
         for (uint32_t e = threadIdx.x; e < s_tot * cpe; e += kBlock) {
             const uint32_t j = e / cpe, ch = e % cpe;
@@ -3842,6 +3855,7 @@ __global__ void finish_pack(uint32_t* cnt, uint8_t* out, const uint64_t* seg_off
                             uint32_t stride, unsigned long long* seg_bytes, unsigned long long* payload, IpcArgs ip) {
     const uint32_t q = threadIdx.x;
     unsigned long long pay = 0;
+    const uint64_t seq = ip.peer_win ? *ip.seq : 0;
     if (q < parts) {
         const uint32_t n = cnt[q];
         const bool peer = q != self && seg_off[q + 1] > seg_off[q];  // segments with capacity only
@@ -3849,11 +3863,11 @@ __global__ void finish_pack(uint32_t* cnt, uint8_t* out, const uint64_t* seg_off
             ulonglong2 h;
             h.x = n;
             h.y = (unsigned long long)n * stride;
-            *reinterpret_cast<ulonglong2*>(ip.peer_win ? ipc_segment(ip, q) : out + seg_off[q]) = h;
+            *reinterpret_cast<ulonglong2*>(ip.peer_win ? ipc_segment(ip, q, seq) : out + seg_off[q]) = h;
             pay = (unsigned long long)n * stride;
             if (ip.peer_win) {  // the segment is complete at system scope: peer q may read it
                 __threadfence_system();
-                __hip_atomic_store(reinterpret_cast<uint64_t*>(ip.peer_win[q] + kWinReady) + self, ip.seq + 1,
+                __hip_atomic_store(reinterpret_cast<uint64_t*>(ip.peer_win[q] + kWinReady) + self, seq + 1,
                                    __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
@@ -3896,9 +3910,10 @@ struct UnpackArgs {
 __global__ __launch_bounds__(kBlock) void unpack_ghosts(UnpackArgs x) {
     __shared__ uint32_t s_src[64], s_pref[65];
     const uint32_t cpe = x.nwp >= 2 ? 1 + x.nwp / 2 : 1;
-    if (threadIdx.x == 0 && x.ipc.peer_win)  // every source's segment of this round has landed
-        wait_flags(reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(x.ipc.my_win) + kWinReady),
-                   x.ipc.recv_mask, x.ipc.seq + 1, x.ipc.err);
+    const uint64_t seq = x.ipc.peer_win ? *x.ipc.seq : 0;
+    if (x.ipc.peer_win)  // this round's receive buffer
+        x.in = reinterpret_cast<const uint8_t*>(x.ipc.my_win) + kWinHdr + (seq & 1) * x.ipc.rbuf;
+    // (IPC: ipc_wait ran before — every source's segment of this round has landed)
     if (threadIdx.x == 0) {
         uint32_t tot = 0, m = 0;
         for (uint32_t p = 0; p < x.parts; ++p) {
@@ -3958,8 +3973,9 @@ __global__ __launch_bounds__(kBlock) void unpack_ghosts(UnpackArgs x) {
                 for (uint64_t m = x.ipc.recv_mask; m; m &= m - 1) {
                     const int p = __ffsll((long long)m) - 1;
                     __hip_atomic_store(reinterpret_cast<uint64_t*>(x.ipc.peer_win[p] + kWinConsumed) + x.self,
-                                       x.ipc.seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                                       seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
+                *x.ipc.seq = seq + 1;  // every block of this launch has read seq
             }
         }
     }

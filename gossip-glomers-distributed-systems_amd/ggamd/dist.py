@@ -383,8 +383,15 @@ class HalvesRunner:
             self.transport = "engine sequencing, gloo host transport, two lane halves per GPU"
 
     def step(self, n_rounds: int, reduce: bool = True) -> list[dict]:
-        for _ in range(n_rounds):
-            for e in self.engs:  # half A's round, then half B's: B's kernels run during A's exchange
-                e.dist_step(1)
+        if self.transport.startswith("device-driven"):
+            # both halves' rounds are enqueued at once on their own streams; the
+            # kernels' flags order each half's rounds with its peers, and the two
+            # streams overlap one half's exchange with the other half's kernels
+            for e in self.engs:
+                e.dist_step(n_rounds)
+        else:
+            for _ in range(n_rounds):
+                for e in self.engs:  # half A's round, then half B's: B's kernels run during A's exchange
+                    e.dist_step(1)
         local = _sum_rounds(self.engs[0].dist_flush(), self.engs[1].dist_flush())
         return ShardedRunner.reduce(self, local) if reduce else local

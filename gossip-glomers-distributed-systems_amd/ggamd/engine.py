@@ -128,7 +128,7 @@ COUNT_FIELDS = [f for f in STAT_FIELDS if f not in DIAG_FIELDS]
 GG_SYMBOLS = [
     "gg_abi_version", "gg_create", "gg_destroy", "gg_last_error", "gg_topology",
     "gg_partition_seeded", "gg_partition_groups", "gg_set_partition", "gg_broadcast", "gg_broadcast_many",
-    "gg_lane_of", "gg_step", "gg_topology_part",
+    "gg_lane_of", "gg_step", "gg_topology_part", "gg_topology_part_directed",
     "gg_current_round", "gg_step_device_ms", "gg_read", "gg_read_bits", "gg_delivery_rounds", "gg_reset",
     "gg_device_bytes",
     "gg_read_bits_nodes", "gg_delivery_rounds_nodes",
@@ -156,6 +156,7 @@ def load_library(path: str) -> C.CDLL:
     lib.gg_last_error.restype = C.c_char_p
     lib.gg_topology.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
     lib.gg_topology_part.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
+    lib.gg_topology_part_directed.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
     lib.gg_partition_seeded.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_uint64]
     lib.gg_partition_groups.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]
     lib.gg_set_partition.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]
@@ -275,6 +276,15 @@ class Engine:
         rp = np.ascontiguousarray(row_ptr, np.int64)
         cl = np.ascontiguousarray(col, np.int32)
         self._ok(self.lib.gg_topology_part(self.h, plo.ctypes.data, rp.ctypes.data, cl.ctypes.data, cl.size))
+
+    def topology_part_directed(self, part_lo, row_ptr, col):
+        """gg_topology_part_directed: this rank's own rows, which may be directed;
+        the in-lists come from the other parts (needs the engine's exchange
+        first: dist_comm_init or dist_transport_init)."""
+        plo = np.ascontiguousarray(part_lo, np.uint64)
+        rp = np.ascontiguousarray(row_ptr, np.int64)
+        cl = np.ascontiguousarray(col, np.int32)
+        self._ok(self.lib.gg_topology_part_directed(self.h, plo.ctypes.data, rp.ctypes.data, cl.ctypes.data, cl.size))
 
     def generate(self, kind: str, n: int, k: int = 0, seed: int = 0, a: float = 0.0, b: float = 0.0,
                  c: float = 0.0) -> int:

@@ -379,7 +379,7 @@ public:
             while (run < n && st[n - 1 - run].new_bits == 0) ++run;
             x.quiet_run = run == n ? x.quiet_run + n : run;
             x.queued = false;
-            x.frozen = sym_ && k + 1 < engines_.size() && x.quiet_run >= (opt_.batch ? opt_.batch + 1 : 1);
+            x.frozen = can_freeze() && k + 1 < engines_.size() && x.quiet_run >= (opt_.batch ? opt_.batch + 1 : 1);
         }
         pending_.clear();
         round_ += n;
@@ -387,6 +387,14 @@ public:
     }
 
     size_t engine_count() const { return engines_.size(); }
+
+    // Freezing an engine after a quiet round is safe only while every message is
+    // delivered: on a symmetric topology each node then holds every value of its
+    // component, so sync rounds can only repair losses and there are none. This
+    // front end installs no partition windows and drops nothing (the simulated
+    // network is Maelstrom's); a windowed engine would need its sync rounds to heal
+    // a cut, and a frozen one would answer reads with stale sets.
+    bool can_freeze() const { return sym_ && !windows_; }
 
 private:
     struct Slot {
@@ -550,6 +558,7 @@ private:
     std::vector<int64_t> rp_;
     std::vector<int32_t> col_;
     bool sym_ = true;
+    bool windows_ = false;  // partition windows installed (none today: see can_freeze)
     int64_t V_ = 0;
     int64_t n_nodes_ = 0;
     std::map<uint32_t, std::vector<int64_t>> pending_;

@@ -153,9 +153,19 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
  * ids, ascending and unique per row. The topology must be symmetric (u lists v
  * iff v lists u), as Maelstrom's are: links inside the part are checked, links to
  * other parts are the caller's promise. Ghosts and send lists are built on the
- * device. Per-edge windows (gg_set_partition) need gg_topology's whole graph. */
+ * device. */
 int gg_topology_part(gg_engine* e, const uint64_t* part_lo, const int64_t* row_ptr, const int32_t* col,
                      uint64_t nnz);
+/* The same for rows that may be directed (u lists v without v listing u): a
+ * receiver's in-list is made of other parts' rows, so the ranks of the lane group
+ * exchange the reverse of their cut edges once, over the engine's RCCL
+ * communicator or the caller's transport — call gg_dist_comm_init or
+ * gg_dist_transport_init first (collective over the lane group). No rank holds
+ * another's rows; owned nodes keep id order. Per-edge windows (gg_set_partition)
+ * on an engine built by either function take bits over the caller's own rows (a
+ * symmetric topology and mask; links to other parts are the caller's promise). */
+int gg_topology_part_directed(gg_engine* e, const uint64_t* part_lo, const int64_t* row_ptr, const int32_t* col,
+                              uint64_t nnz);
 
 /* Partition windows [round_from, round_to): a message sent in such a round
  * between nodes of different groups is dropped. Windows must not overlap.

@@ -890,6 +890,9 @@ int gg_dist_step(gg_engine* e, uint32_t) { return e ? e->fail(GG_EIO, "CPU oracl
 int gg_topology_part(gg_engine* e, const uint64_t*, const int64_t*, const int32_t*, uint64_t) {
     return e ? e->fail(GG_ENOSYS, "CPU oracle: sharded engines take the whole graph (gg_topology)") : GG_EINVAL;
 }
+int gg_topology_part_directed(gg_engine* e, const uint64_t*, const int64_t*, const int32_t*, uint64_t) {
+    return e ? e->fail(GG_ENOSYS, "CPU oracle: sharded engines take the whole graph (gg_topology)") : GG_EINVAL;
+}
 int gg_dist_transport_init(gg_engine* e, const gg_transport*) {
     return e ? e->fail(GG_EIO, "CPU oracle: the engine-driven exchange is the HIP engine's") : GG_EINVAL;
 }

@@ -484,16 +484,29 @@ def _check_against_oracle(cpu_lib, scs, res, world, lane_groups=1):
 
 
 @pytest.mark.parametrize("build", ["host_csr", "device"])
-@pytest.mark.parametrize("transport", ["torch", "engine"])
+@pytest.mark.parametrize("transport", ["torch", "engine", "ipc"])
 def test_world8_equals_oracle(hip_lib, cpu_lib, build, transport):
     """World 8 (BASELINE's GPU count) as 8 ranks on this GPU, vertex-range
     sharded 8 ways, against the CPU oracle O2: the C4 and C5 shapes, host-CSR
     partitions (gg_topology: locality order) and device-built ones
     (gg_topology_generate: native ranges), over the Python all-to-all-v
-    sequencing and over the engine's own gg_dist_step sequencing."""
+    sequencing, over the engine's own gg_dist_step sequencing, and over the
+    device-driven exchange (IPC-mapped windows, captured batches of rounds)."""
     scs = _world8_scenarios()
     res = _run(hip_lib, scs, 8, env={"GG_HUB_DEG": "24", "GG_XCHG_MODE": "exact"},
                generate=(build == "device"), transport=transport, timeout=240)
+    _check_against_oracle(cpu_lib, scs, res, 8)
+
+
+def test_world8_c4_shape_full_width_equals_oracle(hip_lib, cpu_lib):
+    """The C4 shape at BASELINE's width (W = 4096 lanes: 512-byte rows, the
+    widest node group of the kernels) on 8 device-built ranks, sync timers firing
+    during propagation, over the device-driven exchange, against O2."""
+    from ggamd import topology as T
+    from ggamd.workload import uniform_injections
+    scs = [Scenario(T.rmat(4096, 16, seed=61), 4096, 22, uniform_injections(4096, 4096, 62), seed=63, sync_base=6,
+                    sync_jitter=3, gen=dict(kind="rmat", n=4096, k=16, seed=61, a=0.57, b=0.19, c=0.19))]
+    res = _run(hip_lib, scs, 8, env={"GG_HUB_DEG": "24"}, generate=True, transport="ipc", timeout=240)
     _check_against_oracle(cpu_lib, scs, res, 8)
 
 
@@ -539,18 +552,21 @@ def _halves_worker(rank, world, port, lib, scenarios, q, parts, env):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,parts", [(2, 2), (4, 4), (4, 2)])
-def test_lane_halves_equal_oracle(hip_lib, cpu_lib, world, parts):
+@pytest.mark.parametrize("world,parts,transport", [(2, 2, "engine"), (4, 4, "engine"), (4, 2, "engine"),
+                                                  (4, 4, "ipc"), (8, 8, "ipc")])
+def test_lane_halves_equal_oracle(hip_lib, cpu_lib, world, parts, transport):
     """ggamd.dist.HalvesRunner: two engines per process over the two halves of
-    its lanes, device-built vertex parts, the engines' own exchange over gloo,
-    half A's round then half B's: per-rank counters (summed over ranks) and
-    every node's set and delivery rounds equal O2."""
+    its lanes, device-built vertex parts, the engines' own exchange over gloo
+    (half A's round then half B's) or device-driven (both halves' rounds
+    enqueued at once on their own streams): per-rank counters (summed over
+    ranks) and every node's set and delivery rounds equal O2."""
     scs = [sc for sc in _world8_scenarios() if sc.W >= 256]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_halves_worker, args=(r, world, port, hip_lib, scs, q, parts,
-                                                      {"GG_HUB_DEG": "24", "GG_XCHG_MODE": "exact"}))
+                                                      {"GG_HUB_DEG": "24", "GG_XCHG_MODE": "exact",
+                                                       "GG_DIST_TRANSPORT": transport}))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -781,4 +797,114 @@ def test_ipc_exchange_equals_oracle(hip_lib, cpu_lib, world, lane_groups):
             if rank < world // lane_groups:
                 tot_own.append(owned)
         assert np.array_equal(np.sort(np.concatenate(tot_own)), np.arange(sc.topo.n_nodes)), k
+        ref.close()
+
+
+def _slice_bits(words, a, b):
+    """Bits [a, b) of a uint64 bit array, re-based to bit 0."""
+    n = b - a
+    out = np.zeros((n + 63) // 64, np.uint64)
+    for k in range(n):
+        x = a + k
+        if (int(words[x >> 6]) >> (x & 63)) & 1:
+            out[k >> 6] |= np.uint64(1) << np.uint64(k & 63)
+    return out
+
+
+def _own_rows_worker(rank, world, port, lib, scenarios, bounds, q, directed):
+    import torch
+    import torch.distributed as dist
+
+    from ggamd.dist import ShardedRunner
+    from ggamd.engine import Engine
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        out = []
+        dev = torch.device("cuda", 0)
+        for sc, plo in zip(scenarios, bounds):
+            t = sc.topo
+            lo, hi = int(plo[rank]), int(plo[rank + 1])
+            rp = t.row_ptr[lo:hi + 1] - t.row_ptr[lo]  # this rank's rows only
+            col = t.col[t.row_ptr[lo]:t.row_ptr[hi]]
+            e = Engine(t.n_nodes, sc.W, seed=sc.seed, sync_base=sc.sync_base, sync_jitter=sc.sync_jitter,
+                       enable_sync=sc.enable_sync, track_delivery=True, device=0, rank=rank, world=world,
+                       library=lib)
+            r = ShardedRunner(e, dev, transport="engine")  # the reverse edges travel over it
+            if directed:
+                e.topology_part_directed(plo, rp, col)
+            else:
+                e.topology_part(plo, rp, col)
+            for w in sc.windows:
+                if w[0] == "seeded":
+                    e.partition_seeded(w[1], w[2], w[3])
+                elif w[0] == "groups":
+                    e.partition_groups(w[1], w[2], w[3])
+                else:  # per-edge bits over this rank's own rows
+                    e.set_partition(w[1], w[2], _slice_bits(w[3], int(t.row_ptr[lo]), int(t.row_ptr[hi])))
+            for n, v, rr in sc.injections:
+                e.broadcast(int(n), int(v), int(rr))
+            stats = r.step(sc.rounds)
+            owned = e.dist_owned()
+            out.append((stats, owned, e.read_bits_nodes(owned), e.delivery_rounds_nodes(owned)))
+            e.close()
+        q.put((rank, out))
+    except BaseException as exc:
+        q.put((rank, f"rank {rank} failed: {exc!r}"))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("directed", [True, False])
+def test_own_rows_directed_and_edge_windows_equal_oracle(hip_lib, cpu_lib, directed):
+    """Each of 3 ranks holds only its own rows (uneven ranges). Directed rows
+    (gg_topology_part_directed): the in-lists come from the other ranks' rows
+    through one exchange of reverse edges, with seeded and group windows and sync
+    timers. Symmetric rows (gg_topology_part) with per-edge windows whose bits
+    each rank gives over its own rows only. Against O2 given the whole graph."""
+    from helpers import random_scenario, symmetric_cut, symmetric_random_scenario
+    rnd = random.Random(71 + directed)
+    world = 3
+    scs = []
+    for k in range(4):
+        if directed:
+            sc = random_scenario(rnd, max_v=400, directed_p=0.4, W=128, rounds=45)
+            while sc.topo.n_nodes < 30:
+                sc = random_scenario(rnd, max_v=400, directed_p=0.4, W=128, rounds=45)
+        else:
+            sc = symmetric_random_scenario(rnd, max_v=400, W=128, rounds=45, edge_windows=2)
+            while sc.topo.n_nodes < 30:
+                sc = symmetric_random_scenario(rnd, max_v=400, W=128, rounds=45, edge_windows=2)
+        scs.append(sc)
+    if not directed:
+        assert any(w[0] == "edges" for sc in scs for w in sc.windows)
+    bounds = []
+    for sc in scs:
+        V = sc.topo.n_nodes
+        cuts = sorted(rnd.sample(range(1, V), world - 1))
+        bounds.append(np.array([0] + cuts + [V], np.uint64))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_own_rows_worker, args=(r, world, port, hip_lib, scs, bounds, q, directed))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, got = q.get(timeout=170)
+        assert not isinstance(got, str), got
+        res[r] = got
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for k, sc in enumerate(scs):
+        ref = make_engine(cpu_lib, sc)
+        want = ref.step(sc.rounds)
+        for rank in range(world):
+            stats, owned, bits, dr = res[rank][k]
+            d = diff_stats(want, stats)
+            assert not d, (k, rank, d[:8])
+            assert np.array_equal(bits, ref.read_bits_nodes(owned)), (k, rank)
+            assert np.array_equal(dr, ref.delivery_rounds_nodes(owned)), (k, rank)
         ref.close()
