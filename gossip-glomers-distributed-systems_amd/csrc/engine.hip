@@ -1557,7 +1557,7 @@ int gg_create(const gg_config* cfg, gg_engine** out) {
     // the exchange kernels keep one LDS slot per source part (unpack_ghosts) and
     // one lane per destination part (finish_pack, a 64-thread block)
     if (cfg->world / L > 63) return GG_EINVAL;
-    if (cfg->batch_ticks && cfg->world != 1) return GG_EINVAL;  // batched gossip: one engine
+    if (cfg->batch_ticks && L != 1) return GG_EINVAL;  // batched gossip: vertex parts, no lane groups
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GG_EIO;
     auto* e = new gg_engine();
@@ -2643,7 +2643,7 @@ static int enqueue_unpack(gg_engine* e, int64_t r) {
     if (!e->n_ghost) return GG_OK;
     gg::UnpackArgs ua{};
     ua.F_cur = e->d_F[r & 1];
-    ua.base = e->d_base;
+    ua.base = (e->cfg.batch_ticks && e->d_bset[0]) ? e->d_bset[r & 1] : e->d_base;
     ua.flg_cur = e->d_flg[r & 1];
     ua.stamp = e->d_stamp;
     ua.grow = e->d_grow;

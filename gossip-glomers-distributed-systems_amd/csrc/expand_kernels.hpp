@@ -2795,6 +2795,20 @@ __global__ __launch_bounds__(kBlock) void expand_batched(RoundArgs a) {
             c_new += T;
         }
     }
+    // sharded: the ghosts' sync timers (the same pure function of seed, node id and
+    // k their owner runs), so their fired bits (reads answered here, pushes, the
+    // sets the exchange ships) are known without crossing the exchange
+    if (sync && a.n_ghost) {
+        for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < a.n_ghost; g += (uint64_t)gridDim.x * kBlock) {
+            const uint64_t row = a.ghost0 + g;
+            if ((int64_t)a.sync_next[row] != a.round) continue;
+            atomicOr(a.fired_cur + (row >> 6), 1ull << (row & 63));
+            const uint32_t kk = a.sync_k[row] + 1;
+            a.sync_k[row] = kk;
+            a.sync_next[row] =
+                (int32_t)(a.round + gg_sync_interval(a.seed, gid_of(a, row), kk, a.sync_base, a.sync_jitter));
+        }
+    }
     unsigned long long acc[C_NUM];
 #pragma unroll
     for (int k = 0; k < C_NUM; ++k) acc[k] = 0;
@@ -3890,7 +3904,8 @@ __global__ void mark_set_needs(const uint64_t* fired_m1, const int64_t* gout_ptr
 
 struct UnpackArgs {
     uint64_t* F_cur;
-    uint64_t* base;
+    uint64_t* base;              // where kind S (a whole set) goes: the ghost's base row, or in batched
+                                 // gossip with sync the set buffer of this round (read as bset_prev next round)
     uint8_t* flg_cur;
     uint32_t* stamp;             // [n_ghost] last round a ghost's F row arrived (by ghost row)
     const uint32_t* grow;        // [n_ghost] ghost row of the g-th ghost in exchange order, or nullptr (same)

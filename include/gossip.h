@@ -93,7 +93,10 @@ typedef struct {
                                    values. Sync timers: the read_ok callback adds what it lacked to
                                    the pending values and sends each peer one push with everything the
                                    peer's reply lacked; partition windows drop batches as in parity
-                                   mode. Single engine (world == 1). */
+                                   mode. One engine, or vertex parts (world > 1, lane_groups == 1:
+                                   each engine runs its ghosts' timers, the exchange ships batches as
+                                   F rows and the sets callbacks and pushes read as kind S); lane
+                                   groups are refused (GG_EINVAL). The CPU oracle O2 is one engine. */
 } gg_config;
 
 typedef struct {

@@ -30,7 +30,8 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, lib, scenarios, q, lane_groups=1, env=None, generate=False, transport=None):
+def _worker(rank, world, port, lib, scenarios, q, lane_groups=1, env=None, generate=False, transport=None,
+            kw=None):
     import torch
     import torch.distributed as dist
 
@@ -41,7 +42,8 @@ def _worker(rank, world, port, lib, scenarios, q, lane_groups=1, env=None, gener
         out = []
         dev = torch.device("cuda", 0)
         for sc in scenarios:
-            e = make_engine(lib, sc, rank=rank, world=world, device=0, lane_groups=lane_groups, generate=generate)
+            e = make_engine(lib, sc, rank=rank, world=world, device=0, lane_groups=lane_groups, generate=generate,
+                            **(kw or {}))
             r = ShardedRunner(e, dev, transport=transport)
             if transport == "engine" and e.parts > 1:  # gg_dist_step's own sequencing, over gloo
                 assert r.host_xport is not None, r.transport
@@ -60,12 +62,12 @@ def _worker(rank, world, port, lib, scenarios, q, lane_groups=1, env=None, gener
         dist.destroy_process_group()
 
 
-def _run(lib, scenarios, world, lane_groups=1, env=None, generate=False, transport=None, timeout=150):
+def _run(lib, scenarios, world, lane_groups=1, env=None, generate=False, transport=None, timeout=150, kw=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, lib, scenarios, q, lane_groups, env, generate,
-                                               transport))
+                                               transport, kw))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -908,3 +910,53 @@ def test_own_rows_directed_and_edge_windows_equal_oracle(hip_lib, cpu_lib, direc
             assert np.array_equal(bits, ref.read_bits_nodes(owned)), (k, rank)
             assert np.array_equal(dr, ref.delivery_rounds_nodes(owned)), (k, rank)
         ref.close()
+
+
+def _batched_scenarios():
+    """Batched gossip across a vertex cut: sync timers firing while batches are
+    in flight (pushes and callbacks read ghost sets), seeded and edge windows,
+    client broadcasts spread over the rounds."""
+    from ggamd import topology as T
+    from ggamd.workload import uniform_injections
+    from helpers import symmetric_cut
+    rnd = random.Random(31)
+    grid = T.grid_links(40, seed=32)
+    return [
+        Scenario(T.tree(3000, 4), 256, 36, [(n, v, v % 9) for n, v, _ in uniform_injections(3000, 200, 33)],
+                 seed=34, sync_base=6, sync_jitter=3, windows=[("seeded", 3, 9, 35)]),
+        Scenario(grid, 128, 40, [(n, v, v % 5) for n, v, _ in uniform_injections(1600, 100, 36)], seed=37,
+                 sync_base=7, sync_jitter=3, windows=[("seeded", 2, 8, 5), ("edges", 5, 14, symmetric_cut(grid, rnd, 0.3))]),
+        Scenario(T.random_regular(2500, 6, seed=38), 64, 30, uniform_injections(2500, 64, 39), seed=40,
+                 enable_sync=False),
+        random_scenario(random.Random(41), max_v=300, W=128, rounds=45),
+    ]
+
+
+@pytest.mark.parametrize("world,transport", [(2, "torch"), (3, "engine"), (3, "ipc")])
+@pytest.mark.parametrize("B", [2, 3])
+def test_batched_sharded_equals_oracle(hip_lib, cpu_lib, world, transport, B):
+    """Batched gossip (gg_config.batch_ticks) on vertex parts: every engine runs
+    its ghosts' timers, batches cross the cut as F rows and the sets read by
+    pushes and callbacks as kind S into the set buffer of the round. Counters
+    of every round, sets and delivery rounds equal the single O2 engine."""
+    scs = _batched_scenarios()
+    res = _run(hip_lib, scs, world, transport=transport, kw={"batch_ticks": B})
+    for k, sc in enumerate(scs):
+        ref = make_engine(cpu_lib, sc, batch_ticks=B)
+        want = ref.step(sc.rounds)
+        bits = np.zeros((sc.topo.n_nodes, sc.W // 64), np.uint64)
+        dr = np.full((sc.topo.n_nodes, sc.W), -1, np.int32)
+        for rank in range(world):
+            stats, owned, b, d = res[rank][k]
+            assert not diff_stats(want, stats), (k, rank, diff_stats(want, stats)[:10])
+            bits[owned.astype(np.int64)] = b
+            dr[owned.astype(np.int64)] = d
+        assert np.array_equal(bits, ref.read_bits()), k
+        assert np.array_equal(dr, ref.delivery_rounds()), k
+        ref.close()
+
+
+def test_batched_refuses_lane_groups(hip_lib):
+    from ggamd.engine import Engine, GGError
+    with pytest.raises(GGError):
+        Engine(10, 128, batch_ticks=2, world=2, rank=0, lane_groups=2, library=hip_lib)
