@@ -552,6 +552,8 @@ int reset_device_state(gg_engine* e) {
     ra.seed = e->cfg.seed;
     ra.sync_base = e->cfg.sync_base_ticks;
     ra.sync_jitter = e->cfg.sync_jitter_ticks;
+    ra.sync_mix = gg_mix64(e->cfg.seed ^ GG_TAG_SYNC);
+    ra.sync_rcp = gg_sync_rcp(e->cfg.sync_jitter_ticks);
     if (e->err == "internal: reset segment table full") return GG_EIO;
     const uint64_t blocks = std::min<uint64_t>(std::max<uint64_t>(1, rowbytes / 16384), 4096);
     hipLaunchKernelGGL(gg::reset_state, dim3((unsigned)blocks), dim3(gg::kBlock), 0, e->stream, ra);
@@ -1091,6 +1093,8 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.seed = e->cfg.seed;
     a.sync_base = e->cfg.sync_base_ticks;
     a.sync_jitter = e->cfg.sync_jitter_ticks;
+    a.sync_mix = gg_mix64(e->cfg.seed ^ GG_TAG_SYNC);
+    a.sync_rcp = gg_sync_rcp(e->cfg.sync_jitter_ticks);
     a.enable_sync = e->cfg.enable_sync;
     // timers fire from round sync_base on (round_prep: timers, read_ok counts);
     // the first callbacks and pushes reach the expand kernels two rounds later

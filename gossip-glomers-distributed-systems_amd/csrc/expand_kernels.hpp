@@ -261,6 +261,7 @@ struct RoundArgs {
                                 // expand_stream takes it when it is dense (dense_round)
     int64_t round;
     uint64_t seed;
+    uint64_t sync_mix, sync_rcp;  // gg_sync_interval_rcp's constants (gg_mix64(seed ^ GG_TAG_SYNC), gg_sync_rcp)
     uint32_t sync_base, sync_jitter;
     int32_t enable_sync;
 };
@@ -806,8 +807,8 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                     }
                     const uint32_t kk = cur.sk + 1;
                     a.sync_k[i] = kk;
-                    a.sync_next[i] = (int32_t)(a.round + gg_sync_interval(a.seed, gid_of(a, i), kk,
-                                                                          a.sync_base, a.sync_jitter));
+                    a.sync_next[i] = (int32_t)(a.round + gg_sync_interval_rcp(a.sync_mix, a.sync_rcp, gid_of(a, i), kk,
+                                                                              a.sync_base, a.sync_jitter));
                 }
             }
         }
@@ -836,8 +837,8 @@ __global__ __launch_bounds__(kBlock) void round_prep(RoundArgs a) {
                     fire = true;
                     const uint32_t kk = a.sync_k[row] + 1;
                     a.sync_k[row] = kk;
-                    a.sync_next[row] = (int32_t)(a.round + gg_sync_interval(a.seed, gid_of(a, row), kk, a.sync_base,
-                                                                            a.sync_jitter));
+                    a.sync_next[row] = (int32_t)(a.round + gg_sync_interval_rcp(a.sync_mix, a.sync_rcp, gid_of(a, row), kk,
+                                                                                a.sync_base, a.sync_jitter));
                 }
                 if (a.sstate) {
                     st = (uint8_t)((a.flg_prev[row] & (FL_ACT | FL_LAG)) | (bit_at(a.fired_m2, row) ? SE_FM2 : 0) |
@@ -2764,7 +2765,7 @@ __global__ __launch_bounds__(kBlock) void expand_batched(RoundArgs a) {
                     atomicOr(a.fired_cur + (rep >> 6), 1ull << (rep & 63));
                     const uint32_t kk = a.sync_k[i] + 1;
                     a.sync_k[i] = kk;
-                    a.sync_next[i] = (int32_t)(a.round + gg_sync_interval(a.seed, g, kk, a.sync_base, a.sync_jitter));
+                    a.sync_next[i] = (int32_t)(a.round + gg_sync_interval_rcp(a.sync_mix, a.sync_rcp, g, kk, a.sync_base, a.sync_jitter));
                 }
                 // (6) the batch: one message per out-neighbour but the single deliverer
                 const bool single = src != kPendMixed && src != kPendNone;
@@ -2806,7 +2807,7 @@ __global__ __launch_bounds__(kBlock) void expand_batched(RoundArgs a) {
             const uint32_t kk = a.sync_k[row] + 1;
             a.sync_k[row] = kk;
             a.sync_next[row] =
-                (int32_t)(a.round + gg_sync_interval(a.seed, gid_of(a, row), kk, a.sync_base, a.sync_jitter));
+                (int32_t)(a.round + gg_sync_interval_rcp(a.sync_mix, a.sync_rcp, gid_of(a, row), kk, a.sync_base, a.sync_jitter));
         }
     }
     unsigned long long acc[C_NUM];
@@ -3578,6 +3579,7 @@ struct ResetArgs {
     uint64_t n_own, ghost0, n_ghost;  // timers: owned rows and ghost rows
     const uint32_t* gid;
     uint64_t seed;
+    uint64_t sync_mix, sync_rcp;  // gg_sync_interval_rcp's constants (gg_mix64(seed ^ GG_TAG_SYNC), gg_sync_rcp)
     uint32_t sync_base, sync_jitter;
     // an F buffer whose rows are zero where their flag byte is: only the flagged
     // rows and the flags are cleared (or nullptr)
@@ -3624,8 +3626,8 @@ __global__ __launch_bounds__(kBlock) void reset_state(ResetArgs ra) {
     for (uint64_t t = t0; t < ra.n_own + ra.n_ghost; t += stride) {
         const uint64_t i = t < ra.n_own ? t : ra.ghost0 + (t - ra.n_own);
         ra.sync_k[i] = 0;
-        ra.sync_next[i] = (int32_t)gg_sync_interval(ra.seed, ra.gid ? (uint64_t)ra.gid[i] : i, 0, ra.sync_base,
-                                                    ra.sync_jitter);
+        ra.sync_next[i] = (int32_t)gg_sync_interval_rcp(ra.sync_mix, ra.sync_rcp, ra.gid ? (uint64_t)ra.gid[i] : i, 0,
+                                                        ra.sync_base, ra.sync_jitter);
     }
 }
 

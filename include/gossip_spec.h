@@ -45,6 +45,36 @@ GG_HD uint32_t gg_sync_interval(uint64_t seed, uint64_t v, uint32_t k, uint32_t 
     return base + (uint32_t)((h % (100ull * jitter)) / 100ull);
 }
 
+/* High 64 bits of a 64 x 64-bit product. */
+GG_HD uint64_t gg_umulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(a, b);
+#else
+    return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+/* gg_sync_interval with the per-run constants precomputed: seedmix =
+ * gg_mix64(seed ^ GG_TAG_SYNC) and rcp = floor((2^64 - 1) / m), m = 100 * jitter
+ * (gg_sync_rcp). Bit-identical: q = floor(h * rcp / 2^64) is floor(h / m) or one
+ * less, since h/m - h*rcp/2^64 = h (1 + s) / (m 2^64) < 1 with s = (2^64 - 1) mod m
+ * < m; so h - q m < 2m and one subtraction gives h mod m. The device's timers
+ * take this form (a 64-bit remainder by a run-time divisor is a long
+ * instruction sequence on the GPU, paid by every wave holding a firing node). */
+GG_HD uint64_t gg_sync_rcp(uint32_t jitter) {
+    return jitter ? ~0ull / (100ull * jitter) : 0ull;
+}
+
+GG_HD uint32_t gg_sync_interval_rcp(uint64_t seedmix, uint64_t rcp, uint64_t v, uint32_t k,
+                                    uint32_t base, uint32_t jitter) {
+    if (jitter == 0) return base;
+    const uint64_t m = 100ull * jitter;
+    const uint64_t h = gg_mix64(seedmix ^ gg_mix64((v << 20) ^ (uint64_t)k));
+    uint64_t r = h - gg_umulhi64(h, rcp) * m;
+    if (r >= m) r -= m;
+    return base + (uint32_t)(r < (1ull << 32) ? (uint32_t)r / 100u : r / 100ull);
+}
+
 /* Side (0/1) of node v in the seeded bisection of one partition window. */
 GG_HD uint32_t gg_part_group(uint64_t seed, uint64_t epoch_seed, uint64_t v) {
     return (uint32_t)(gg_mix64(gg_mix64(seed ^ GG_TAG_PART ^ epoch_seed) ^ v) & 1ull);
