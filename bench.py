@@ -402,6 +402,31 @@ def main():
                 dist.destroy_process_group()
             raise SystemExit(1)
 
+    # every timed episode's global counters against the CPU oracle O2's run of the
+    # same workload (tests/golden/bench_c2.json, made by make_bench_golden.py for
+    # 2^20 x N nodes); a differing episode fails the run
+    oracle_check = None
+    gold_p = os.path.join(REPO, "tests", "golden", "bench_c2.json")
+    if cfg == "C2" and K == 1024 and seed == BASE_SEED + 2 and os.path.exists(gold_p):
+        gold = next((g for g in json.load(open(gold_p))["runs"].values() if g["nodes"] == V and g["lanes"] == K),
+                    None)
+        if gold is not None:
+            want = gold["rounds"]
+            M = (1 << 64) - 1
+            diffs = [f"episode {k} round {j} {f}: {ep[j][f] & M} != O2 {want[j][f] & M}"
+                     for k, ep in enumerate(per_ep) for j in range(min(len(ep), len(want))) for f in COUNT_FIELDS
+                     if (ep[j][f] & M) != (want[j][f] & M)]
+            if len(want) != R:
+                diffs.append(f"quiescence round count {R} != O2 {len(want)}")
+            if diffs:
+                if rank == 0:
+                    print("bench: counters differ from O2:", diffs[:8], file=sys.stderr)
+                if world > 1:
+                    dist.destroy_process_group()
+                raise SystemExit(1)
+            oracle_check = (f"all {len(per_ep)} timed episodes: every round's global counters and delivery hash "
+                            f"equal O2's run of this workload (tests/golden/bench_c2.json, {V} nodes)")
+
     if rank == 0:
         value = deliveries / elapsed
         out = {
@@ -434,6 +459,7 @@ def main():
                 "hbm_bytes_rank0": hbm_bytes,
                 "setup_s_rank0": setup_s,
                 "check": check,
+                "oracle_check": oracle_check,
                 "fresh_injections": fresh,
             },
             "roofline": {

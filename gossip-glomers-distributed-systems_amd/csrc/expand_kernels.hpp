@@ -1601,6 +1601,13 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
     };
 
     uint32_t k = blockIdx.x * NGB + threadIdx.x / G;
+    // an all-full double-buffered round: every owned set is row 0's, so each lane
+    // puts its chunk of it in its own-row LDS slot once (no own-row DMA overwrites
+    // it) instead of every node DMA-ing the same row, and the loop only writes the
+    // rows moving forward
+    if (db && full)
+        *reinterpret_cast<ulonglong2*>(my + D * 1024 + lane16) =
+            *reinterpret_cast<const ulonglong2*>(a.base_prev + a.own0 * a.nwp + off);
     Meta m0, m1;
     uint32_t c0[D], c1[D];
     const uint32_t n0 = node_of(k), n1 = node_of(k + stride);
@@ -1618,8 +1625,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         // (a) DMA node i's own row and its first D sender rows (masked rounds:
         // and the words of the window bitmaps covering its first D in-edges)
         // (an all-full double-buffered round: every owned set is the same, row 0's)
-        if (!hub && (!full || db))
-            dma16((const void*)((db ? a.base_prev : a.base) + (full ? a.own0 : rep) * a.nwp + off), my + D * 1024);
+        if (!hub && !full) dma16((const void*)((db ? a.base_prev : a.base) + rep * a.nwp + off), my + D * 1024);
         uint64_t mw[3][2];
         if constexpr (MASKW) {
 #pragma unroll

@@ -3,12 +3,19 @@
 two reset_state launches (the last complete episode), each with its duration
 and the idle gap before it, and per-kernel sums; the episode's wall span versus
 its summed kernel time shows how much of a step is launch gaps.
-Usage: tools/trace_episode.py kernel_trace.csv [episode index from the end, default 2]"""
+Usage: tools/trace_episode.py kernel_trace.csv|results.db [episode index from the end, default 2]"""
 import csv
 import sys
 from collections import defaultdict
 
-rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+if sys.argv[1].endswith(".db"):  # rocprofv3's default SQLite output: its `kernels` view
+    import sqlite3
+    db = sqlite3.connect(sys.argv[1])
+    rows = [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e}
+            for n, s, e in db.execute("select name, start, end from kernels")]
+else:
+    rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 back = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 resets = [i for i, r in enumerate(rows) if "reset_state" in r["Kernel_Name"]]
 if len(resets) < back + 1:
