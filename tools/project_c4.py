@@ -16,7 +16,14 @@ Scale-up to 10^8 nodes (--scale S): kernel times and payloads multiplied by
 the single-engine ratio S of the dense rounds (measured: C4 at 10^8 vs the
 rehearsal size), stated as a projection, not a measurement.
 
-Usage: python tools/project_c4.py profiles/r3/r3_c4_rehearsal_2p22_p8_ordered.json [--halves H.json] [--scale S]
+Host time per round (--host-us U): time the host spends on a round's critical
+path, added to every round (the engine's RCCL exchange in exact-size mode
+waits for each round's segment sizes before it enqueues the payload, round 3:
+~70 us of enqueue per round behind that wait; the device-driven exchange has
+none — its whole episode is enqueued ahead in one graph, 17 us per C4 round
+measured, profiles/r4/ipc/).
+
+Usage: python tools/project_c4.py profiles/r3/r3_c4_rehearsal_2p22_p8_ordered.json [--halves H.json] [--scale S] [--host-us U]
 """
 import argparse
 import json
@@ -32,12 +39,13 @@ def main():
     ap.add_argument("--halves")
     ap.add_argument("--links", default="64,76.5,153", help="GB/s per link and direction")
     ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--host-us", type=float, default=0.0, help="host time per round on the critical path")
     args = ap.parse_args()
     d = json.load(open(args.rehearsal))
     P = d["config"]["parts"]
     h = json.load(open(args.halves)) if args.halves else None
     out = {"rehearsal": args.rehearsal, "halves": args.halves, "parts": P, "lane_groups": d["config"]["lane_groups"],
-           "nodes": d["config"]["nodes"], "scale": args.scale, "projections": []}
+           "nodes": d["config"]["nodes"], "scale": args.scale, "host_us_per_round": args.host_us, "projections": []}
     single = sum(r["single_ms"] for r in rounds_of(d)) * args.scale
     for link in [float(x) for x in args.links.split(",")]:
         B = link * 1e9 * min(7, max(1, P - 1))
@@ -45,15 +53,16 @@ def main():
         for i, r in enumerate(rounds_of(d)):
             c = r["rank_ms_max"] * args.scale
             x = r["payload_bytes_max"] * args.scale / B * 1e3
-            t_after += c + x
-            t_ovl += max(c, x)
+            hst = args.host_us * 1e-3
+            t_after += c + x + hst
+            t_ovl += max(c, x) + hst
             if h:
                 hr = rounds_of(h)[i]
                 # a GPU holds two lane-half ranks: both halves' kernels and payloads
                 c2 = 2 * hr["rank_ms_mean"] * args.scale if hr["rank_ms_max"] < 1.2 * hr["rank_ms_mean"] else \
                     (hr["rank_ms_max"] + hr["rank_ms_mean"]) * args.scale
                 x2 = 2 * hr["payload_bytes_max"] * args.scale / B * 1e3
-                t_half += max(c2, x2)
+                t_half += max(c2, x2) + hst
         p = {"link_GBps": link, "single_ms": single, "exchange_after_ms": t_after,
              "speedup_exchange_after": single / t_after, "overlap_bound_ms": t_ovl,
              "speedup_overlap_bound": single / t_ovl}
