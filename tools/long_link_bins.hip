@@ -120,8 +120,9 @@ static inline uint64_t mix(uint64_t x) {
     return x ^ (x >> 33);
 }
 
-int main() {
-    const uint32_t V = 1u << 26;
+int main(int argc, char** argv) {
+    const int LV = argc > 1 ? atoi(argv[1]) : 26;  // receivers = 2^LV (2^30: C5's size; ~60 GB host, 64 GB HBM)
+    const uint32_t V = 1u << LV;
     const uint64_t E = 2ull * V;  // two long-link senders per receiver (edge e = 2v + j)
     const uint32_t nbins = V / kBin;
     std::vector<uint32_t> src(E);
@@ -179,7 +180,7 @@ int main() {
     };
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-    printf("V = 2^26 receivers, %llu long-link slots, %u bins of %u receivers\n", (unsigned long long)E, nbins, kBin);
+    printf("V = 2^%d receivers, %llu long-link slots, %u bins of %u receivers\n", LV, (unsigned long long)E, nbins, kBin);
     for (int grid : {cus * 8, cus * 32}) {
         const float t = timeit([&] { hipLaunchKernelGGL(pull_far<4>, dim3(grid), dim3(256), 0, 0, F, d_src, V, o1); });
         printf("pull (random 8-byte gathers), grid %5d: %.3f ms, %.1f G rows/s\n", grid, t, E / (t * 1e-3) / 1e9);
@@ -214,6 +215,7 @@ int main() {
     if (bad) return 1;
     // ---- window pull: sender windows of 2^LW nodes, items by (XCD, window, receiver)
     for (int LW : {16, 17, 18}) {
+        if (LV > 26) break;  // the window layout's host tables grow as V^2
         const uint32_t nw = V >> LW;
         std::vector<uint64_t> cntw(nw + 1, 0), cntbw((uint64_t)nbins * nw + 1, 0);
         auto wkey = [&](uint32_t w) { return (uint64_t)(w % 8) * (nw / 8) + w / 8; };
