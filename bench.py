@@ -57,8 +57,9 @@ MAIN_KERNELS = {"prep": ["round_prep"], "expand": ["expand_round", "expand_round
 KIND_KERNELS = {
     "prep": ["round_prep", "compact_round", "mark_injections", "hub_mark", "sync_records"],
     "expand": ["expand_round", "expand_round_lean"],
-    "stream": ["expand_stream", "expand_stream_db", "expand_stream_masked", "expand_stream1", "expand_stream_sync",
-               "hub_chunks", "hub_finish", "hub_sync_chunks", "hub_sync_finish", "hub_sync_push", "expand_batched"],
+    "stream": ["expand_stream", "expand_stream_db", "expand_stream_db_mark", "expand_stream_masked", "expand_stream1",
+               "expand_stream_sync", "hub_chunks", "hub_finish", "hub_sync_chunks", "hub_sync_finish", "hub_sync_push",
+               "expand_batched"],
 }
 TRAFFIC_JSON = {"C2": os.path.join(REPO, "profiles", "traffic.json"),  # committed PMC passes per config
                 "C4": os.path.join(REPO, "profiles", "traffic_C4.json")}
