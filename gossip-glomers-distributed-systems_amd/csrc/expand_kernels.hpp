@@ -3777,7 +3777,16 @@ struct PackArgs {
     uint32_t nwp, stride;
     int32_t sync;               // sets may be read next round
     IpcArgs ipc;                // device-driven exchange: segments go straight to the peers
+    // finish_pack's work, done by the last block to finish (ticket): no launch of its own
+    uint32_t* ticket;           // last-block counter (reset by that block)
+    uint32_t parts, self;
+    unsigned long long* seg_bytes;
+    unsigned long long* payload;
 };
+
+__device__ __forceinline__ void finish_pack_body(uint32_t* cnt, uint8_t* out, const uint64_t* seg_off, uint32_t parts,
+                                                 uint32_t self, uint32_t stride, unsigned long long* seg_bytes,
+                                                 unsigned long long* payload, const IpcArgs& ip);
 
 __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
     __shared__ uint32_t s_row[2 * kBlock], s_head[2 * kBlock];
@@ -3868,13 +3877,31 @@ __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
         }
         __syncthreads();  // LDS reuse
     }
-    if (x.ipc.peer_win) __threadfence_system();  // this thread's segment stores performed before finish_pack's flags
+    if (x.ipc.peer_win) __threadfence_system();  // this thread's segment stores performed before the ready flags
+    // the last block to finish runs finish_pack (every block's counts and stores are in)
+    __shared__ uint32_t s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const uint32_t t = atomicAdd(x.ticket, 1u);
+        s_last = t == gridDim.x - 1 ? 1u : 0u;
+        if (s_last) {
+            *x.ticket = 0;
+            __threadfence();
+        }
+    }
+    __syncthreads();
+    if (s_last && threadIdx.x < 64) finish_pack_body(x.cnt, x.out, x.seg_off, x.parts, x.self, x.stride, x.seg_bytes,
+                                                     x.payload, x.ipc);
 }
 
 // After pack_ghosts: each peer's header, its byte count for an exact-size
 // exchange, the round's payload bytes; counters reset for the next round.
-__global__ void finish_pack(uint32_t* cnt, uint8_t* out, const uint64_t* seg_off, uint32_t parts, uint32_t self,
-                            uint32_t stride, unsigned long long* seg_bytes, unsigned long long* payload, IpcArgs ip) {
+// (threads 0..63 of one block; pack_ghosts' last block, or a launch of its own
+// when no tile has entries to pack)
+__device__ __forceinline__ void finish_pack_body(uint32_t* cnt, uint8_t* out, const uint64_t* seg_off, uint32_t parts,
+                                                 uint32_t self, uint32_t stride, unsigned long long* seg_bytes,
+                                                 unsigned long long* payload, const IpcArgs& ip) {
     const uint32_t q = threadIdx.x;
     unsigned long long pay = 0;
     const uint64_t seq = ip.peer_win ? *ip.seq : 0;
@@ -3898,6 +3925,11 @@ __global__ void finish_pack(uint32_t* cnt, uint8_t* out, const uint64_t* seg_off
     }
     pay = wave_sum(pay);
     if (threadIdx.x == 0) *payload = pay;
+}
+
+__global__ void finish_pack(uint32_t* cnt, uint8_t* out, const uint64_t* seg_off, uint32_t parts, uint32_t self,
+                            uint32_t stride, unsigned long long* seg_bytes, unsigned long long* payload, IpcArgs ip) {
+    finish_pack_body(cnt, out, seg_off, parts, self, stride, seg_bytes, payload, ip);
 }
 
 // Sync rounds: ghosts that fired in r-1 run their callback in r+1 and read the
@@ -3926,6 +3958,8 @@ struct UnpackArgs {
     uint32_t nwp, stride;
     uint32_t round;
     IpcArgs ipc;                 // device-driven exchange: `in` is this round's receive buffer
+    uint32_t* stale_ticket;      // non-null: the last block clears the stale ghost rows (clear_stale_ghosts'
+                                 // work; few ghosts, so no launch of its own)
 };
 
 // Every received entry into its ghost row (kind F: F row, flag ACT, stamp;
@@ -3987,6 +4021,26 @@ __global__ __launch_bounds__(kBlock) void unpack_ghosts(UnpackArgs x) {
     }
     const unsigned long long s = wave_sum(nact);
     if ((threadIdx.x & 63) == 0 && s) atomicAdd(x.act_cur + (blockIdx.x % kSlots), (uint32_t)s);
+    if (x.stale_ticket) {  // the last block: ghosts whose F row of r-2 sits here and that sent none this round
+        __shared__ uint32_t s_last;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            s_last = atomicAdd(x.stale_ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
+            if (s_last) {
+                *x.stale_ticket = 0;
+                __threadfence();
+            }
+        }
+        __syncthreads();
+        if (s_last)
+            for (uint64_t g = threadIdx.x; g < x.n_ghost; g += kBlock) {
+                const uint64_t row = x.ghost0 + g;
+                if (!(x.flg_cur[row] & FL_ACT) || x.stamp[g] == x.round) continue;
+                for (uint32_t w = 0; w < x.nwp; ++w) x.F_cur[row * x.nwp + w] = 0;
+                x.flg_cur[row] = 0;
+            }
+    }
     if (x.ipc.peer_win) {  // the last block to finish tells every source its buffer is free
         __syncthreads();
         if (threadIdx.x == 0) {
