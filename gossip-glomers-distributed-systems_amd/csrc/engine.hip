@@ -219,6 +219,9 @@ struct gg_engine {
     std::vector<int64_t> dist_round_of;        // round of each pending slot
     std::vector<uint64_t> dist_path;           // its kernel path (GG_PATH_*)
     uint64_t last_path = 0;                    // path of the round enqueue_round enqueued last
+    bool last_mark = false;                    // ... and whether it marks round r+1's candidates (mark_cand):
+                                               // then the unpack of its exchange marks the owned receivers of
+                                               // the ghosts that sent an F row (round r+1 runs no round_prep)
     std::vector<uint64_t> dist_sent;           // payload bytes sent in each pending slot
     std::vector<gg_round_stats> dist_done;     // folded, not yet flushed
     size_t inj_off = 0;                        // pinned injection ring offset (async rounds)
@@ -958,11 +961,12 @@ void db_advance(gg_engine* e, int64_t r, bool db) {
     e->d_base = e->d_sets[e->set_cur];
 }
 
-// Marking rounds are for single double-buffered engines on symmetric graphs
-// without hubs (no ghost senders to mark receivers for, no hub_mark; a node's
-// receivers are its in-list); GG_NO_MARK=1 keeps round_prep.
+// Marking rounds are for double-buffered engines on symmetric graphs without
+// hubs (no hub_mark; a node's receivers are its in-list); on vertex parts the
+// exchange's unpack marks the owned receivers of the ghosts that sent an F row
+// (round_prep's ghost pass); GG_NO_MARK=1 keeps round_prep.
 bool mark_ok(const gg_engine* e) {
-    return !e->no_mark && e->symmetric && e->P == 1 && e->n_ghost == 0 && e->n_hubs == 0 && e->n_mchunks == 0 && !e->cfg.batch_ticks;
+    return !e->no_mark && e->symmetric && e->n_hubs == 0 && e->n_mchunks == 0 && !e->cfg.batch_ticks;
 }
 
 // Which kernel path round r takes (gg_round_stats.path, diagnostics): the host
@@ -1110,6 +1114,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         a.prep_in_compact = 1;
         a.mark_cand = (db_round(e, r + 1) && !(e->cfg.enable_sync && r + 1 >= base)) ? 1u : 0u;
     }
+    e->last_mark = a.mark_cand != 0;
     // streaming rounds: no sync event reaches the expand; partition windows only
     // on symmetric graphs without hubs at W >= 128 (expand_stream<.., MASKW>)
     // streamed sync rounds (sync_records + expand_stream_sync [+ hub_sync_*]): no masks
@@ -2680,6 +2685,11 @@ static int enqueue_unpack(gg_engine* e, int64_t r) {
     ua.stride = e->xstride;
     ua.round = (uint32_t)r;
     ua.ipc = ipc_args(e);
+    if (e->last_mark) {  // round r+1 runs no round_prep: the active ghosts mark their owned receivers here
+        ua.cand_mark = e->d_cand + (size_t)((r + 1) & 1) * e->rows;
+        ua.gout_ptr = e->d_gout_ptr;
+        ua.gout_col = e->d_gout_col;
+    }
     if (e->ipc && e->recv_mask) {  // every source's segment of this round has landed
         hipLaunchKernelGGL(gg::ipc_wait, dim3(1), dim3(64), 0, e->stream, ua.ipc, 1);
         HIPCHK(hipGetLastError());

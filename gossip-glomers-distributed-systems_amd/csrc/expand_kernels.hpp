@@ -3960,6 +3960,9 @@ struct UnpackArgs {
     IpcArgs ipc;                 // device-driven exchange: `in` is this round's receive buffer
     uint32_t* stale_ticket;      // non-null: the last block clears the stale ghost rows (clear_stale_ghosts'
                                  // work; few ghosts, so no launch of its own)
+    uint8_t* cand_mark;          // non-null (marking rounds): round r+1's candidate bytes; a ghost that sent
+    const int64_t* gout_ptr;     // an F row marks its owned receivers (ghost -> owned CSR), round_prep's
+    const uint32_t* gout_col;    // ghost pass moved here
 };
 
 // Every received entry into its ghost row (kind F: F row, flag ACT, stamp;
@@ -4013,6 +4016,8 @@ __global__ __launch_bounds__(kBlock) void unpack_ghosts(UnpackArgs x) {
                 x.flg_cur[row] = FL_ACT;
                 x.stamp[g] = x.round;
                 ++nact;
+                if (x.cand_mark)
+                    for (int64_t q = x.gout_ptr[g]; q < x.gout_ptr[g + 1]; ++q) x.cand_mark[x.gout_col[q]] = CA_NODE;
             }
         } else {
             const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(ent + 16 * ch);

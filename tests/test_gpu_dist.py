@@ -684,15 +684,18 @@ def test_topology_part_refusals(hip_lib):
     e.close()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-@pytest.mark.parametrize("db", ["GG_DB", "GG_NO_DB"])
-def test_sharded_db_paths_equal_oracle(hip_lib, cpu_lib, world, db):
+@pytest.mark.parametrize("world,db,mark", [(2, "GG_DB", "1"), (4, "GG_DB", "1"), (2, "GG_DB", "0"),
+                                           (2, "GG_NO_DB", "1"), (4, "GG_NO_DB", "1")])
+def test_sharded_db_paths_equal_oracle(hip_lib, cpu_lib, world, db, mark):
     """Both lean-round paths of a sharded engine, forced (GG_DB: double-buffered
     sets — ghost senders' F rows from the exchange, pack_ghosts with set_prev,
     materialize_F and clear_stale_ghosts at the hand-over to the sync rounds;
-    GG_NO_DB: the F-row kernels), against O2; gg_round_stats.path says which ran."""
+    GG_NO_DB: the F-row kernels), against O2; gg_round_stats.path says which ran.
+    Double-buffered rounds on symmetric graphs are marking rounds (the expand
+    marks the next round's owned candidates, the exchange's unpack the owned
+    receivers of active ghosts: no round_prep) unless GG_NO_MARK=1."""
     from ggamd import topology as T
-    from ggamd.engine import PATH_DB
+    from ggamd.engine import PATH_DB, PATH_NO_PREP
     from ggamd.workload import uniform_injections
     scs = [Scenario(T.tree(3000, 4), 256, 34, uniform_injections(3000, 200, 41), seed=42, sync_base=6, sync_jitter=3),
            Scenario(T.random_regular(2500, 8, seed=43), 128, 30,
@@ -700,7 +703,7 @@ def test_sharded_db_paths_equal_oracle(hip_lib, cpu_lib, world, db):
                     sync_jitter=2),
            Scenario(T.grid_links(44, seed=46), 512, 36, uniform_injections(44 * 44, 300, 47), seed=48, sync_base=9,
                     sync_jitter=4, windows=[("seeded", 12, 16, 3)])]
-    res = _run(hip_lib, scs, world, env={db: "1"})
+    res = _run(hip_lib, scs, world, env={db: "1", "GG_NO_MARK": "0" if mark == "1" else "1"})
     for k, sc in enumerate(scs):
         ref = make_engine(cpu_lib, sc)
         want = ref.step(sc.rounds)
@@ -711,10 +714,12 @@ def test_sharded_db_paths_equal_oracle(hip_lib, cpu_lib, world, db):
             assert np.array_equal(bits, ref.read_bits_nodes(owned)), (k, rank)
             assert np.array_equal(dr, ref.delivery_rounds_nodes(owned)), (k, rank)
             n_db = sum(1 for s in stats if s["path"] & PATH_DB)
+            n_np = sum(1 for s in stats if s["path"] & PATH_NO_PREP)
             if db == "GG_DB":
                 assert n_db >= 4, (k, rank, [s["path"] for s in stats])
+                assert (n_np >= 3) if mark == "1" else (n_np == 0), (k, rank, [s["path"] for s in stats])
             else:
-                assert n_db == 0, (k, rank)
+                assert n_db == 0 and n_np == 0, (k, rank)
         ref.close()
 
 
