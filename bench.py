@@ -133,10 +133,12 @@ def main():
                     help="N = 1: after the timed region, episodes rotating this many distinct seeded injection "
                          "sets (every step re-captures its launch graph and uploads its injections; 0: skip)")
     ap.add_argument("--no-check", action="store_true", help="skip the N > 1 single-engine check")
-    ap.add_argument("--xchg", default=os.environ.get("GG_DIST_TRANSPORT", "engine"), choices=["engine", "ipc", "torch"],
+    ap.add_argument("--xchg", default=os.environ.get("GG_DIST_TRANSPORT", "auto"),
+                    choices=["auto", "engine", "ipc", "torch"],
                     help="N > 1 exchange between vertex parts: engine = the engine's grouped RCCL send/recv; "
                          "ipc = device-driven (IPC-mapped peer windows, kernel flags, captured batches of rounds, "
-                         "no host wait); torch = torch all_to_all")
+                         "no host wait); torch = torch all_to_all; auto (default) = ipc on RCCL jobs when every "
+                         "rank maps its peers and two validation rounds match O2, else engine")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 "
                     "(nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
     args = ap.parse_args()
@@ -179,65 +181,115 @@ def main():
     cfg = args.config
     free0 = torch.cuda.mem_get_info(local)[0]
     t_setup = time.perf_counter()
-    runner = None
-    if cfg == "C2":
-        V = (args.nodes or (1 << 20)) * world
-        K = args.lanes or 1024
-        seed = BASE_SEED + 2
-        topo = T.tree(V, 4)
-        gen = None
-        E = int(topo.nnz)
-        eng = Engine(V, K, seed=seed, enable_sync=True, device=local, rank=rank, world=world)
-        eng.topology(topo)
-        engs = [eng]
-        if world > 1:
-            from ggamd.dist import ShardedRunner
-            runner = ShardedRunner(eng, device, transport=args.xchg if args.backend == "nccl" or args.xchg == "ipc"
-                                   else None)
-        parallelism = f"vertex-range x{world}" if world > 1 else "single GPU"
-        scaling = "weak"
-        workload = ("C2: tree4 of 2^20 nodes per GPU, 1024 messages broadcast in round 0 at seeded uniform "
-                    "nodes, sync on, no partitions; one step = one episode to quiescence")
-    else:
-        V = args.nodes or 100_000_000
-        K = args.lanes or 4096
-        seed = BASE_SEED + 4
-        topo = None
-        gen = dict(kind="rmat", n=V, k=16, seed=seed, a=0.57, b=0.19, c=0.19)
-        P = args.parts
-        if world % P:
-            raise SystemExit(f"--parts {P} does not divide the world size {world}")
-        L = world // P
-        if args.halves == 2 and P > 1:
-            from ggamd.dist import HalvesRunner
-            g, q = divmod(rank, P)
-            engs = [Engine(V, K, seed=seed, enable_sync=True, device=local, rank=(2 * g + h) * P + q,
-                           world=2 * world, lane_groups=2 * L) for h in range(2)]
-            E = engs[0].generate(**gen)
-            engs[1].generate(**gen)
-            eng = engs[0]
-            runner = HalvesRunner(engs, device, transport=args.xchg)
-        else:
-            eng = Engine(V, K, seed=seed, enable_sync=True, device=local, rank=rank, world=world,
-                         lane_groups=L)
-            E = eng.generate(**gen)  # this rank's rows of the graph, built in its GPU's HBM (gossip_gen.h)
+
+    def setup(xchg):
+        runner = None
+        if cfg == "C2":
+            V = (args.nodes or (1 << 20)) * world
+            K = args.lanes or 1024
+            seed = BASE_SEED + 2
+            topo = T.tree(V, 4)
+            gen = None
+            E = int(topo.nnz)
+            eng = Engine(V, K, seed=seed, enable_sync=True, device=local, rank=rank, world=world)
+            eng.topology(topo)
             engs = [eng]
-            if P > 1:
+            if world > 1:
                 from ggamd.dist import ShardedRunner
-                runner = ShardedRunner(eng, device, transport=args.xchg if args.backend == "nccl" or args.xchg == "ipc"
-                                       else "engine")
-        if world == 1:
-            parallelism = "single GPU"
-        elif P == 1:
-            parallelism = f"message lanes x{world} (every GPU: whole graph, {K // world} lanes)"
+                runner = ShardedRunner(eng, device, transport=xchg if args.backend == "nccl" or xchg == "ipc" else None)
+            parallelism = f"vertex-range x{world}" if world > 1 else "single GPU"
+            scaling = "weak"
+            workload = ("C2: tree4 of 2^20 nodes per GPU, 1024 messages broadcast in round 0 at seeded uniform "
+                        "nodes, sync on, no partitions; one step = one episode to quiescence")
         else:
-            parallelism = (f"{L} lane groups x {P} vertex parts (each GPU: 1/{P} of the nodes + ghosts, "
-                           f"{K // L} lanes" + (", as two engines of half the lanes each, exchange of one "
-                                                "overlapping the other's kernels)" if len(engs) == 2 else ")"))
-        scaling = "strong"
-        workload = (f"C4: R-MAT (.57,.19,.19,.05) edge factor 16, symmetrized, {V} nodes, {K} messages "
-                    "broadcast in round 0 at seeded uniform nodes, sync on, no partitions; graph built "
-                    "in HBM by the on-device generator; one step = one episode to quiescence")
+            V = args.nodes or 100_000_000
+            K = args.lanes or 4096
+            seed = BASE_SEED + 4
+            topo = None
+            gen = dict(kind="rmat", n=V, k=16, seed=seed, a=0.57, b=0.19, c=0.19)
+            P = args.parts
+            if world % P:
+                raise SystemExit(f"--parts {P} does not divide the world size {world}")
+            L = world // P
+            if args.halves == 2 and P > 1:
+                from ggamd.dist import HalvesRunner
+                g, q = divmod(rank, P)
+                engs = [Engine(V, K, seed=seed, enable_sync=True, device=local, rank=(2 * g + h) * P + q,
+                               world=2 * world, lane_groups=2 * L) for h in range(2)]
+                E = engs[0].generate(**gen)
+                engs[1].generate(**gen)
+                eng = engs[0]
+                runner = HalvesRunner(engs, device, transport=xchg)
+            else:
+                eng = Engine(V, K, seed=seed, enable_sync=True, device=local, rank=rank, world=world,
+                             lane_groups=L)
+                E = eng.generate(**gen)  # this rank's rows of the graph, built in its GPU's HBM (gossip_gen.h)
+                engs = [eng]
+                if P > 1:
+                    from ggamd.dist import ShardedRunner
+                    runner = ShardedRunner(eng, device, transport=xchg if args.backend == "nccl" or xchg == "ipc" else "engine")
+            if world == 1:
+                parallelism = "single GPU"
+            elif P == 1:
+                parallelism = f"message lanes x{world} (every GPU: whole graph, {K // world} lanes)"
+            else:
+                parallelism = (f"{L} lane groups x {P} vertex parts (each GPU: 1/{P} of the nodes + ghosts, "
+                               f"{K // L} lanes" + (", as two engines of half the lanes each, exchange of one "
+                                                    "overlapping the other's kernels)" if len(engs) == 2 else ")"))
+            scaling = "strong"
+            workload = (f"C4: R-MAT (.57,.19,.19,.05) edge factor 16, symmetrized, {V} nodes, {K} messages "
+                        "broadcast in round 0 at seeded uniform nodes, sync on, no partitions; graph built "
+                        "in HBM by the on-device generator; one step = one episode to quiescence")
+
+        return runner, V, K, seed, topo, gen, E, eng, engs, parallelism, scaling, workload
+
+    # N > 1 exchange: "auto" = the device-driven one (no host wait, captured rounds)
+    # if every rank can map its peers and two validation rounds through it finish
+    # (their global counters equal O2's where tests/golden/bench_c2.json has them),
+    # else the engine's RCCL send/recv, rebuilt from scratch on every rank
+    xchg = args.xchg
+    xchg_note = None
+    if xchg == "auto":
+        xchg = "ipc" if (world > 1 and (cfg == "C2" or args.parts > 1)) else "engine"
+    if args.xchg == "auto" and xchg == "ipc":
+        ok, built, got = 1, None, [0, 0]
+        try:  # (every rank makes the same collective calls whatever fails)
+            built = setup("ipc")
+            rn, V0, K0, seed0, _, _, _, _, engs0, _, _, _ = built
+            arr0 = injection_arrays(uniform_injections(V0, K0, seed0))
+            for e in engs0:
+                e.reset()
+                inject(e, arr0)
+            got = [s["new_bits"] for s in rn.step(2, reduce=False)]
+            if os.environ.get("GG_BENCH_IPC_FAIL") == str(rank):  # test hook: the fallback path
+                raise RuntimeError("GG_BENCH_IPC_FAIL")
+        except Exception as exc:  # noqa: BLE001 — any failure: every rank falls back
+            ok = 0
+            print(f"bench: rank {rank}: device-driven exchange unavailable ({exc!r}); falling back", file=sys.stderr)
+        v = allreduce_i64([1 - ok] + [int(x) for x in got])
+        ok = v[0] == 0 and sum(v[1:]) > 0
+        gold_p = os.path.join(REPO, "tests", "golden", "bench_c2.json")
+        if ok and cfg == "C2" and os.path.exists(gold_p):
+            g = next((g for g in json.load(open(gold_p))["runs"].values()
+                      if g["nodes"] == built[1] and g["lanes"] == built[2]), None)
+            if g is not None and v[1:] != [g["rounds"][0]["new_bits"], g["rounds"][1]["new_bits"]]:
+                ok = False
+                if rank == 0:
+                    print(f"bench: device-driven validation rounds differ from O2: {v[1:]}; falling back",
+                          file=sys.stderr)
+        if ok:
+            runner, V, K, seed, topo, gen, E, eng, engs, parallelism, scaling, workload = built
+        else:
+            if built is not None:
+                for e in built[8]:
+                    e.close()
+            built = None
+            torch.cuda.synchronize()
+            xchg = "engine"
+            xchg_note = "device-driven exchange failed its setup or validation on some rank: fell back to --xchg engine"
+            runner, V, K, seed, topo, gen, E, eng, engs, parallelism, scaling, workload = setup(xchg)
+    else:
+        runner, V, K, seed, topo, gen, E, eng, engs, parallelism, scaling, workload = setup(xchg)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
     inj = uniform_injections(V, K, seed)
@@ -453,6 +505,7 @@ def main():
                 "exchange": (runner.transport if runner is not None else
                              ("none: lane groups never exchange; one all_reduce of the counters "
                               "after the timed episodes" if world > 1 else None)),
+                "exchange_note": xchg_note,
                 "lane_groups": world // args.parts if cfg == "C4" else 1,
                 "vertex_parts": args.parts if cfg == "C4" else world,
                 "exchange_bytes_per_round_rank0": xbytes,

@@ -300,13 +300,20 @@ def _ipc_connect(engines: list[Engine], group, rank: int, world: int, P: int) ->
     lane-group order), one all_gather of the blobs, and each engine imports the
     P blobs of its own lane group in part order."""
     from .engine import IPC_BLOB_BYTES
-    mine = b"".join(e.dist_ipc_export() for e in engines)
+    err = None
+    try:
+        mine = b"".join(e.dist_ipc_export() for e in engines)
+    except Exception as exc:  # still join the all_gather (zero blobs: every importer refuses them)
+        err = exc
+        mine = bytes(IPC_BLOB_BYTES * len(engines))
     t = torch.frombuffer(bytearray(mine), dtype=torch.uint8)
     if dist.get_backend(group) == "nccl":
         t = t.to(torch.device("cuda", torch.cuda.current_device()))
     got = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(got, t, group=group)
     allb = [g.cpu().numpy().tobytes() for g in got]  # allb[r][h * BLOB:]: engine h of rank r
+    if err is not None:
+        raise err
     B = IPC_BLOB_BYTES
     for h, e in enumerate(engines):
         g = rank // P  # the process's lane group index (rank = group * P + part)
