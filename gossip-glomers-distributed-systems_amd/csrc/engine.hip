@@ -647,8 +647,9 @@ template <int G, bool MASKW, int DB = 0>
 void launch_stream_t(const gg::RoundArgs& a, hipStream_t s) {
     static int resident = 0;
     auto kern = MASKW ? gg::expand_stream_masked<G, 2>
-                      : (DB == 2 ? gg::expand_stream_db_mark<G, 2>
-                                 : (DB ? gg::expand_stream_db<G, 2> : gg::expand_stream<G, 2>));
+                      : (DB == 3 ? gg::expand_stream_db<G, 2, 3>
+                                 : (DB == 2 ? gg::expand_stream_db_mark<G, 2>
+                                            : (DB ? gg::expand_stream_db<G, 2> : gg::expand_stream<G, 2>)));
     if (!resident) {
         int dev = 0, cus = 0, per_cu = 0;
         (void)hipGetDevice(&dev);
@@ -667,7 +668,8 @@ void launch_stream_m(const gg::RoundArgs& a, bool maskw, hipStream_t s) {
     if (maskw) {
         launch_stream_t<G, true>(a, s);
     } else if (a.db) {
-        launch_stream_t<G, false, 1>(a, s);
+        if (a.n_edges < 4ull * a.n_own) launch_stream_t<G, false, 3>(a, s);  // mean in-degree < 4: 3 rows a batch
+        else launch_stream_t<G, false, 1>(a, s);
         if (a.mark_cand) launch_stream_t<G, false, 2>(a, s);  // the rounds that are not busy
     } else {
         launch_stream_t<G, false>(a, s);

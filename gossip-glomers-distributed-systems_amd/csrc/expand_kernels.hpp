@@ -67,6 +67,13 @@ namespace gg {
 #define GG_STREAM_WAVES_PER_EU 4
 #endif
 constexpr int kStreamRows = GG_STREAM_ROWS;
+// ... in the marking kernel: three rows keep it at 95 VGPRs, 5 waves/SIMD (four:
+// 101, four waves). With three in both kernels C2 ran 1.613 -> 1.568 ms/step and
+// C3 at 2M nodes 6.58 -> 6.82 ms (in-degree 8 wants four in the busy rounds)
+#ifndef GG_MARK_ROWS
+#define GG_MARK_ROWS 3
+#endif
+constexpr int kMarkRows = GG_MARK_ROWS;
 // Sender rows a lane of expand_stream1 (W = 64) keeps in flight.
 #ifndef GG_STREAM1_ROWS
 #define GG_STREAM1_ROWS 8
@@ -1511,11 +1518,11 @@ __device__ __forceinline__ uint32_t active_senders(const uint64_t* abits, const 
     return m & ((1u << D) - 1u);
 }
 
-template <int G, int WPL, bool MASKW, bool DB = false, bool MARK = false>
+template <int G, int WPL, bool MASKW, bool DB = false, bool MARK = false, int D = kStreamRows>
 __device__ __forceinline__ void stream_body(RoundArgs a) {
     static_assert(WPL == 2, "DMA slots hold 16 bytes per lane");
     constexpr int NGB = kBlock / G;  // node groups per block
-    constexpr int D = kStreamRows;   // sender rows per DMA batch
+    // D: sender rows per DMA batch
     __shared__ __attribute__((aligned(16))) uint8_t s_slots[(kBlock / 64) * (D + 1) * 1024];
     __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
     const unsigned long long t_start = clock100();
@@ -1883,20 +1890,23 @@ void expand_stream_masked(RoundArgs a) {
 }
 
 // Double-buffered lean rounds (RoundArgs::db): sets of r-1 in, sets of r out.
-template <int G, int WPL>
+// D = 3 sender rows per batch on graphs with a mean in-degree below 4 (the host
+// picks: C2 1.60 -> 1.56 ms/step), 4 above (C3 at 2M nodes: 6.58 vs 6.80 ms).
+template <int G, int WPL, int D = kStreamRows>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GG_STREAM_WAVES_PER_EU)))
 void expand_stream_db(RoundArgs a) {
-    stream_body<G, WPL, false, true>(a);
+    stream_body<G, WPL, false, true, false, D>(a);
 }
 
 // ... of marking rounds (RoundArgs::mark_cand) that are not busy: the same, and
 // each node whose set changes marks itself and its receivers as candidates of
 // round r+1 (the marking needs four more registers: a kernel of its own, so the
-// busy rounds keep 5 waves/SIMD).
+// busy rounds keep 5 waves/SIMD; with kMarkRows = 3 sender rows per batch it
+// fits 5 waves too).
 template <int G, int WPL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
 void expand_stream_db_mark(RoundArgs a) {
-    stream_body<G, WPL, false, true, true>(a);
+    stream_body<G, WPL, false, true, true, kMarkRows>(a);
 }
 
 // Which of a lane's D senders (columns c, the first n valid) were ACT last round
