@@ -299,6 +299,9 @@ struct gg_engine {
     int32_t* d_dr = nullptr;
     unsigned long long* d_counters = nullptr;
     unsigned long long* h_counters = nullptr;  // pinned
+    unsigned long long* d_ep = nullptr;  // gg_run_episodes: each episode's folded counter rows
+    unsigned long long* h_ep = nullptr;  // pinned
+    size_t ep_cap = 0;                   // bytes of each
     uint32_t* d_inj = nullptr;
     uint32_t* h_inj = nullptr;  // pinned
     uint32_t* d_injtab = nullptr;  // [kMaxBatch + 1] first pair of each round of a batch (gg_step)
@@ -472,6 +475,8 @@ gg_engine::~gg_engine() {
     dfree(d_counters);
     dfree(d_inj);
     if (h_counters) (void)hipHostFree(h_counters);
+    dfree(d_ep);
+    if (h_ep) (void)hipHostFree(h_ep);
     if (h_inj) (void)hipHostFree(h_inj);
     if (h_injtab) (void)hipHostFree(h_injtab);
     dfree(d_injtab);
@@ -660,6 +665,8 @@ void launch_stream_t(const gg::RoundArgs& a, hipStream_t s) {
     const uint64_t ngb = gg::kBlock / G;
     uint64_t blocks = (a.n_own + ngb - 1) / ngb;
     blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)resident));
+    // block lists: a block's 256 granules of 16 nodes cover its share of the nodes
+    if (DB && a.block_lists) blocks = std::max<uint64_t>(blocks, (a.n_own + gg::kBllMax - 1) / gg::kBllMax);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(gg::kBlock), 0, s, a);
 }
 
@@ -668,9 +675,11 @@ void launch_stream_m(const gg::RoundArgs& a, bool maskw, hipStream_t s) {
     if (maskw) {
         launch_stream_t<G, true>(a, s);
     } else if (a.db) {
+        // the marking kernel first: in rounds with block lists it sums round r-1's
+        // rings and publishes them for the other one
+        if (a.mark_cand) launch_stream_t<G, false, 2>(a, s);  // the rounds that are not busy
         if (a.n_edges < 4ull * a.n_own) launch_stream_t<G, false, 3>(a, s);  // mean in-degree < 4: 3 rows a batch
         else launch_stream_t<G, false, 1>(a, s);
-        if (a.mark_cand) launch_stream_t<G, false, 2>(a, s);  // the rounds that are not busy
     } else {
         launch_stream_t<G, false>(a, s);
     }
@@ -1191,7 +1200,13 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             hipLaunchKernelGGL(gg::mark_injections, dim3(gg::kMarkInjBlocks), dim3(256), 0, e->stream, a);
             HIPCHK(hipGetLastError());
         }
-        {
+        // block lists (RoundArgs::block_lists): a marking round on one engine needs
+        // no compact_round — its two double-buffered expand kernels list their
+        // blocks' candidates themselves (C2: one launch and a list pass less a round)
+        static const bool no_bll = ab_knob("GG_BLOCK_LISTS") && atoi(ab_knob("GG_BLOCK_LISTS")) == 0;  // A/B
+        a.block_lists = (a.prep_in_compact && a.mark_cand && a.db && a.stream_ok && !sync_stream && !maskw &&
+                         e->P == 1 && e->n_hubs == 0 && !no_bll) ? 1u : 0u;
+        if (!a.block_lists) {
             const uint64_t groups = (a.n_own + 7) / 8;  // >= tile groups
             const uint64_t per_block = (uint64_t)gg::kBlock * gg::kCompactQ;
             const uint64_t nb = (groups + per_block - 1) / per_block;
@@ -1354,7 +1369,8 @@ size_t pack_injections(gg_engine* e, int64_t r0, uint32_t n, std::vector<size_t>
 // replayed kernels are exactly the captured launches; only host launch cost is
 // saved. GG_NO_GRAPH=1 disables it.
 template <class F>
-int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& off, size_t total, F&& enqueue) {
+int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& off, size_t total, F&& enqueue,
+              bool wait = true) {
     static const bool no_graph = ab_knob("GG_NO_GRAPH") != nullptr;
     uint64_t h = gg_mix64(total);
     for (size_t t = 0; t < 2 * total; ++t) h = gg_mix64(h ^ e->h_inj[t]);
@@ -1385,6 +1401,7 @@ int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& o
         e->injtab_dev_hash = th;
     }
     if (no_graph || m < 4 || e->graph_broken) {
+        if (!wait) return enqueue();  // (gg_run_episodes: timed and synchronised by the caller)
         HIPCHK(hipEventRecord(e->ev[0], e->stream));
         int rc = enqueue();
         if (rc) return rc;
@@ -1417,7 +1434,7 @@ int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& o
         hipGraph_t g = nullptr;
         if (hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
             e->graph_broken = true;
-            return run_batch(e, r0, m, off, 0, enqueue);
+            return run_batch(e, r0, m, off, 0, enqueue, wait);
         }
         const int rc = enqueue();
         const hipError_t ec = hipStreamEndCapture(e->stream, &g);
@@ -1426,11 +1443,15 @@ int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& o
             if (g) (void)hipGraphDestroy(g);
             (void)hipGetLastError();
             e->graph_broken = true;  // fall back to direct launches for good
-            return run_batch(e, r0, m, off, 0, enqueue);
+            return run_batch(e, r0, m, off, 0, enqueue, wait);
         }
         (void)hipGraphDestroy(g);
         e->graph_exec = ge;
         e->graph_key = key;
+    }
+    if (!wait) {
+        HIPCHK(hipGraphLaunch(e->graph_exec, e->stream));
+        return GG_OK;
     }
     HIPCHK(hipEventRecord(e->ev[0], e->stream));
     HIPCHK(hipGraphLaunch(e->graph_exec, e->stream));
@@ -2472,6 +2493,99 @@ int gg_lane_of(const gg_engine* e, int64_t message) {
 
 int64_t gg_current_round(const gg_engine* e) { return e ? e->round : -1; }
 
+namespace {
+
+// One batch of m <= kMaxBatch rounds from e->round, enqueued (captured once,
+// replayed after): each round's 64 counter slots are folded on the device into
+// one row at d_counters + kMaxBatch * kSlots * kCounters and copied to
+// h_counters. wait: synchronise and time it (run_batch). paths: each round's
+// path bits (host-known).
+int enqueue_step_batch(gg_engine* e, uint32_t m, bool wait, std::vector<uint64_t>& paths) {
+    const int64_t r0 = e->round;
+    int rc = ensure_events(e, 2);
+    if (rc) return rc;
+    if (e->inj_ev_live) {  // h_inj reuse: only the copy out of it must be done (not e.g. a reset)
+        HIPCHK(hipEventSynchronize(e->inj_ev));
+        e->inj_ev_live = false;
+    }
+    std::vector<size_t> off;
+    const size_t total = pack_injections(e, r0, m, off);
+    if (total == (size_t)-1) return GG_EIO;
+    const int64_t save_round = e->round;
+    const bool save_db = e->db_active, save_fd = e->f_dirty;
+    const int save_set = e->set_cur;
+    auto enqueue_batch = [&]() -> int {
+        e->db_active = save_db;  // (a failed capture may have run it once already)
+        e->f_dirty = save_fd;
+        e->set_cur = save_set;
+        e->d_base = e->d_sets[save_set];
+        HIPCHK(hipMemsetAsync(e->d_counters, 0, (size_t)m * gg::kSlots * gg::kCounters * 8, e->stream));
+        for (uint32_t k = 0; k < m; ++k) {
+            const uint32_t ni = (uint32_t)(off[k + 1] - off[k]);
+            e->round = r0 + k;
+            int rc2 = enqueue_round(e, e->d_inj, ni, e->d_counters + (size_t)k * gg::kSlots * gg::kCounters,
+                                    e->d_injtab + k);
+            if (rc2) return rc2;
+        }
+        // fold the 64 slots of each round on the device: one 256-byte row per round to the host
+        unsigned long long* folded = e->d_counters + (size_t)kMaxBatch * gg::kSlots * gg::kCounters;
+        hipLaunchKernelGGL(gg::fold_slots, dim3(m), dim3(gg::kCounters), 0, e->stream, e->d_counters, folded);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(e->h_counters, folded, (size_t)m * gg::kCounters * 8, hipMemcpyDeviceToHost,
+                              e->stream));
+        return GG_OK;
+    };
+    rc = run_batch(e, r0, m, off, total, enqueue_batch, wait);
+    e->ctr_dirty = std::max(e->ctr_dirty, m);
+    e->round = save_round + m;
+    // the double-buffer state after the batch (a replayed graph enqueued nothing)
+    e->db_active = save_db;
+    e->f_dirty = save_fd;
+    e->set_cur = save_set;
+    paths.assign(m, 0);
+    for (uint32_t k = 0; k < m; ++k) {
+        const bool dbk = db_round(e, r0 + k);
+        paths[k] = path_of(e, r0 + k, dbk);
+        db_advance(e, r0 + k, dbk);
+    }
+    return rc;
+}
+
+// The host side of a batch's rounds once their folded counter rows are in `rows`.
+void finish_step_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<uint64_t>& paths,
+                       const unsigned long long* rows, gg_round_stats* out, bool retire) {
+    for (uint32_t k = 0; k < m; ++k) {
+        gg_round_stats s;
+        fold_stats(e, rows + (size_t)k * gg::kCounters, r0 + k, &s, 1);
+        s.path = paths[k];
+        e->quiet = s.new_bits ? 0 : e->quiet + 1;
+        if (out) out[k] = s;
+        if (retire) retire_round(e, r0 + k);
+    }
+}
+
+// gg_reset's host part: round 0, no pending acks, no lane history; keep_schedule:
+// the lanes and client broadcasts stay (gg_run_episodes restores them itself).
+void reset_host_state(gg_engine* e, bool keep_schedule) {
+    e->dist_k = 0;
+    e->dist_done.clear();
+    e->inj_off = 0;
+    if (!keep_schedule) {
+        e->lanes.clear();
+        e->lane_value.clear();
+        e->inj.clear();
+    }
+    e->dirty_parity = (int)(e->round & 1);
+    e->round = 0;
+    e->pend_acks = e->pend_ackdrop = 0;
+    e->hash_total = 0;
+    e->dist_open = false;
+    e->u_hist.clear();
+    e->u_bits.clear();
+}
+
+}  // namespace
+
 int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
     if (!e) return GG_EINVAL;
     if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
@@ -2482,66 +2596,75 @@ int gg_step(gg_engine* e, uint32_t n, gg_round_stats* out) {
     if ((rc = ensure_db(e))) return rc;
     if ((rc = ensure_sync(e, e->round + (int64_t)n - 1))) return rc;
     uint32_t done = 0;
-    std::vector<size_t> off;
+    std::vector<uint64_t> paths;
     e->step_event_ms = 0.0;
     while (done < n) {
         const uint32_t m = std::min<uint32_t>(kMaxBatch, n - done);
         const int64_t r0 = e->round;
-        if ((rc = ensure_events(e, 2))) return rc;
-        if (e->inj_ev_live) {  // h_inj reuse: only the copy out of it must be done (not e.g. a reset)
-            HIPCHK(hipEventSynchronize(e->inj_ev));
-            e->inj_ev_live = false;
-        }
-        const size_t total = pack_injections(e, r0, m, off);
-        if (total == (size_t)-1) return GG_EIO;
-        const int64_t save_round = e->round;
-        const bool save_db = e->db_active, save_fd = e->f_dirty;
-        const int save_set = e->set_cur;
-        auto enqueue_batch = [&]() -> int {
-            e->db_active = save_db;  // (a failed capture may have run it once already)
-            e->f_dirty = save_fd;
-            e->set_cur = save_set;
-            e->d_base = e->d_sets[save_set];
-            HIPCHK(hipMemsetAsync(e->d_counters, 0, (size_t)m * gg::kSlots * gg::kCounters * 8, e->stream));
-            for (uint32_t k = 0; k < m; ++k) {
-                const uint32_t ni = (uint32_t)(off[k + 1] - off[k]);
-                e->round = r0 + k;
-                int rc2 = enqueue_round(e, e->d_inj, ni, e->d_counters + (size_t)k * gg::kSlots * gg::kCounters,
-                                        e->d_injtab + k);
-                if (rc2) return rc2;
-            }
-            // fold the 64 slots of each round on the device: one 256-byte row per round to the host
-            unsigned long long* folded = e->d_counters + (size_t)kMaxBatch * gg::kSlots * gg::kCounters;
-            hipLaunchKernelGGL(gg::fold_slots, dim3(m), dim3(gg::kCounters), 0, e->stream, e->d_counters, folded);
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipMemcpyAsync(e->h_counters, folded, (size_t)m * gg::kCounters * 8, hipMemcpyDeviceToHost,
-                                  e->stream));
-            return GG_OK;
-        };
-        rc = run_batch(e, r0, m, off, total, enqueue_batch);
-        e->ctr_dirty = std::max(e->ctr_dirty, m);
-        e->round = save_round + m;
-        // the double-buffer state after the batch (a replayed graph enqueued nothing)
-        e->db_active = save_db;
-        e->f_dirty = save_fd;
-        e->set_cur = save_set;
-        std::vector<uint64_t> paths(m);
-        for (uint32_t k = 0; k < m; ++k) {
-            const bool dbk = db_round(e, r0 + k);
-            paths[k] = path_of(e, r0 + k, dbk);
-            db_advance(e, r0 + k, dbk);
-        }
-        if (rc) return rc;
+        if ((rc = enqueue_step_batch(e, m, true, paths))) return rc;
         HIPCHK(hipStreamSynchronize(e->stream));
-        for (uint32_t k = 0; k < m; ++k) {
-            gg_round_stats s;
-            fold_stats(e, e->h_counters + (size_t)k * gg::kCounters, r0 + k, &s, 1);
-            s.path = paths[k];
-            e->quiet = s.new_bits ? 0 : e->quiet + 1;
-            if (out) out[done + k] = s;
-            retire_round(e, r0 + k);
-        }
+        finish_step_batch(e, r0, m, paths, e->h_counters, out ? out + done : nullptr, true);
         done += m;
+    }
+    return GG_OK;
+}
+
+int gg_run_episodes(gg_engine* e, uint32_t n, uint32_t episodes, gg_round_stats* out) {
+    if (!e) return GG_EINVAL;
+    if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
+    if (e->P != 1) return e->fail(GG_EINVAL, "vertex-sharded engine: use gg_dist_round_begin/end");
+    if (e->round != 0) return e->fail(GG_EINVAL, "gg_run_episodes: call it right after gg_reset and the broadcasts");
+    if (n < 1 || n > kMaxBatch || episodes < 1) return e->fail(GG_EINVAL, "gg_run_episodes: bad sizes");
+    HIPCHK(hipSetDevice(e->device));
+    int rc = materialize_windows(e);
+    if (rc) return rc;
+    if ((rc = ensure_db(e))) return rc;
+    if ((rc = ensure_sync(e, (int64_t)n - 1))) return rc;
+    if ((rc = ensure_events(e, 2))) return rc;
+    // every episode's folded counter rows in a device ring, read back once
+    const size_t rows_b = (size_t)n * gg::kCounters * 8, need = rows_b * episodes;
+    if (need > e->ep_cap) {
+        HIPCHK(hipStreamSynchronize(e->stream));
+        dfree(e->d_ep);
+        if (e->h_ep) (void)hipHostFree(e->h_ep);
+        e->h_ep = nullptr;
+        e->ep_cap = 0;
+        HIPCHK(hipMalloc(&e->d_ep, need));
+        HIPCHK(hipHostMalloc(&e->h_ep, need));
+        e->ep_cap = need;
+    }
+    const auto inj0 = e->inj;
+    const LaneTable lanes0 = e->lanes;
+    const std::vector<int64_t> lv0 = e->lane_value;
+    const int quiet0 = e->quiet;
+    std::vector<std::vector<uint64_t>> paths(episodes);
+    const unsigned long long* folded = e->d_counters + (size_t)kMaxBatch * gg::kSlots * gg::kCounters;
+    HIPCHK(hipEventRecord(e->ev[0], e->stream));
+    for (uint32_t k = 0; k < episodes; ++k) {
+        if (k) {  // gg_reset + the same broadcasts, without gg_reset's wait
+            reset_host_state(e, true);
+            e->inj = inj0;
+            e->lanes = lanes0;
+            e->lane_value = lv0;
+            e->quiet = 0;  // the last episode's quiet rounds are not known yet: clear every per-round array
+            if ((rc = reset_device_state(e))) return rc;
+        }
+        if ((rc = enqueue_step_batch(e, n, false, paths[k]))) return rc;
+        HIPCHK(hipMemcpyAsync(e->d_ep + (size_t)k * n * gg::kCounters, folded, rows_b, hipMemcpyDeviceToDevice,
+                              e->stream));
+    }
+    HIPCHK(hipEventRecord(e->ev[1], e->stream));
+    HIPCHK(hipMemcpyAsync(e->h_ep, e->d_ep, need, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
+    e->step_event_ms = (double)ms / episodes;
+    for (uint32_t k = 0; k < episodes; ++k) {  // each episode's stats from round 0's state
+        e->hash_total = 0;
+        e->pend_acks = e->pend_ackdrop = 0;
+        e->quiet = k ? 2 : quiet0;  // (what a reset leaves)
+        finish_step_batch(e, 0, n, paths[k], e->h_ep + (size_t)k * n * gg::kCounters, out ? out + (size_t)k * n : nullptr,
+                          k + 1 == episodes);
     }
     return GG_OK;
 }
@@ -3700,19 +3823,7 @@ int gg_delivery_rounds_nodes(gg_engine* e, const uint32_t* nodes, uint64_t n, in
 int gg_reset(gg_engine* e) {
     if (!e) return GG_EINVAL;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    e->dist_k = 0;
-    e->dist_done.clear();
-    e->inj_off = 0;
-    e->lanes.clear();
-    e->lane_value.clear();
-    e->inj.clear();
-    e->dirty_parity = (int)(e->round & 1);
-    e->round = 0;
-    e->pend_acks = e->pend_ackdrop = 0;
-    e->hash_total = 0;
-    e->dist_open = false;
-    e->u_hist.clear();
-    e->u_bits.clear();
+    reset_host_state(e, false);
     if (!e->have_topo) return GG_OK;
     HIPCHK(hipSetDevice(e->device));
     return reset_device_state(e);

@@ -74,6 +74,7 @@ constexpr int kStreamRows = GG_STREAM_ROWS;
 #define GG_MARK_ROWS 3
 #endif
 constexpr int kMarkRows = GG_MARK_ROWS;
+constexpr uint32_t kBllMax = 4096;  // block lists: nodes of a block's slice (kBlock x 16 candidate bytes)
 // Sender rows a lane of expand_stream1 (W = 64) keeps in flight.
 #ifndef GG_STREAM1_ROWS
 #define GG_STREAM1_ROWS 8
@@ -154,6 +155,9 @@ struct RoundArgs {
                                 // r-1, so round r+1 needs no round_prep (prep_in_compact)
     uint32_t prep_in_compact;   // no round_prep this round: compact_round sums the rings of r-1
                                 // (round r-1 was a marking round, or r is the first round)
+    uint32_t block_lists;       // ... and no compact_round either: the double-buffered expand
+                                // kernels sum the rings themselves and each block lists the
+                                // candidates of its own slice of the nodes in LDS (single engine)
     uint8_t* zmark;             // [rows] F row of this parity is stale (node active 2 rounds ago)
     uint8_t* tile_cand;         // [n_tiles rounded to 8] tile has a candidate (sparse rounds)
     struct TileWork* work;      // live tiles of a sparse round (compact_round; expand_round)
@@ -550,9 +554,16 @@ __device__ __forceinline__ bool rings_in(const RoundArgs& a) {
     if (blockIdx.x == 0 && threadIdx.x < kSlots) {
         const unsigned long long d = wave_sum(a.act_deg_s[pr * kSlots + lane]);
         const unsigned long long n = wave_sum(a.tot_s[pr * kSlots + lane]);
+        // round r's slots, and round r+1's: a round r+1 with block lists sums
+        // its predecessor's slots while its own blocks add to its own, so it
+        // finds them cleared and clears round r+2's (below)
+        const int nr = (int)((a.round + 1) & 3);
         a.act_s[cr * kSlots + lane] = 0;
         a.act_deg_s[cr * kSlots + lane] = 0;
         a.tot_s[cr * kSlots + lane] = 0;
+        a.act_s[nr * kSlots + lane] = 0;
+        a.act_deg_s[nr * kSlots + lane] = 0;
+        a.tot_s[nr * kSlots + lane] = 0;
         if (lane == 0) {
             a.act[pr] = (uint32_t)act_prev;
             a.act_deg[pr] = d;
@@ -560,6 +571,54 @@ __device__ __forceinline__ bool rings_in(const RoundArgs& a) {
         }
     }
     return dense;
+}
+
+// Round r-1's rings as a kernel of round r sees them. Published (rings_in ran
+// earlier in the round) or, in rounds with block lists, summed from r-1's slots
+// by every wave, with block 0 publishing them for round r+1 and clearing round
+// r+1's slots (round r's were cleared in round r-1; this round's blocks add to
+// them). Both expand kernels of such a round publish the same values.
+struct RingView {
+    unsigned long long act, act_deg, tot;  // round r-1: nodes active, their degrees, cumulative new bits
+    unsigned long long act_m2;             // round r-2: nodes active
+};
+template <bool SUM = true>
+__device__ __forceinline__ RingView ring_view(const RoundArgs& a) {
+    RingView v;
+    const int pr = (int)((a.round - 1) & 3), p2 = (int)((a.round - 2) & 3);
+    v.act_m2 = a.act[p2];
+    if (!SUM || !a.block_lists) {
+        v.act = a.act[pr];
+        v.act_deg = a.act_deg ? a.act_deg[pr] : 0ull;
+        v.tot = a.tot ? a.tot[pr] : 0ull;
+        return v;
+    }
+    const int lane = threadIdx.x & 63;
+    v.act = wave_sum((unsigned long long)a.act_s[pr * kSlots + lane]);
+    v.act_deg = a.act_deg ? wave_sum(a.act_deg_s[pr * kSlots + lane]) : 0ull;
+    const unsigned long long n = a.tot ? wave_sum(a.tot_s[pr * kSlots + lane]) : 0ull;
+    v.tot = a.tot ? (a.round > 0 ? a.tot[p2] : 0ull) + n : 0ull;
+    if (blockIdx.x == 0 && threadIdx.x < kSlots) {
+        const int nr = (int)((a.round + 1) & 3);
+        a.act_s[nr * kSlots + lane] = 0;
+        a.act_deg_s[nr * kSlots + lane] = 0;
+        a.tot_s[nr * kSlots + lane] = 0;
+        if (lane == 0) {
+            a.act[pr] = (uint32_t)v.act;
+            if (a.act_deg) a.act_deg[pr] = v.act_deg;
+            if (a.tot) a.tot[pr] = v.tot;
+            if (a.n_work_next) a.n_work_next[0] = a.n_work_next[1] = 0;
+        }
+    }
+    return v;
+}
+__device__ __forceinline__ bool busy_count(const RoundArgs& a, unsigned long long act) {
+    return 2.0 * (double)act * (double)a.n_edges >= (double)a.n_own * (double)a.n_own;
+}
+// ff_round() from a ring view
+__device__ __forceinline__ bool ff_view(const RoundArgs& a, const RingView& rv) {
+    return a.ff_ok && a.stream_ok && a.act_deg && rv.act_deg >= a.ff_min &&
+           16.0 * (double)rv.act_deg < (double)a.ff_ok * (double)a.n_edges;
 }
 
 // ---------------------------------------------------------------------------
@@ -1526,22 +1585,134 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t s_slots[(kBlock / 64) * (D + 1) * 1024];
     __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
     const unsigned long long t_start = clock100();
+    // round r-1's rings: summed by the marking kernel in rounds with block lists
+    // (launched first: the other kernel reads what its block 0 published)
+    const RingView rv = ring_view<MARK>(a);
+    const bool busy = busy_count(a, rv.act);
     // marking rounds launch two kernels: expand_stream_db takes the busy ones
     // (every node, nothing marked) and expand_stream_db_mark the others (the
     // candidate list, or every node after a busy round; the next round's
     // candidates marked)
-    if (!a.stream_ok || (MARK ? busy_round(a) : (DB && a.mark_cand && !busy_round(a)))) {
+    if (!a.stream_ok || (MARK ? busy : (DB && a.mark_cand && !busy))) {
         noop_exit(a, K_STREAM, t_start);
         return;
     }
-    const bool dense = dense_round(a);
-    const uint32_t n_items = dense ? (uint32_t)a.n_own : a.n_work[1];
-    if ((uint64_t)blockIdx.x * NGB >= n_items) {  // sparse round: no item reaches this block
+    // dense_round(): a round without round_prep after a busy round is dense too
+    const bool dense = busy || (a.prep_in_compact && busy_count(a, rv.act_m2));
+    // block lists (sparse rounds without compact_round): thread t of block b
+    // takes the 16 nodes of granule t * grid + b (one 16-byte load of candidate
+    // bytes; the host sizes the grid so 256 granules a block cover every node),
+    // the block lists their candidates in LDS by a block scan and its node
+    // groups walk that list. Granules interleaved over the blocks: the wave
+    // fronts of sparse rounds are runs of consecutive nodes (C2, a tree in BFS
+    // order: subtrees), which contiguous slices left to a few blocks (rounds
+    // 4-9 took 2x as long)
+    // (marking kernel only: the host sets block_lists in marking rounds, where the
+    // other kernel takes only busy, dense rounds)
+    const bool bl = MARK && a.block_lists && !dense;
+    __shared__ uint16_t s_list[kBllMax];
+    __shared__ uint32_t s_lcnt[kBlock / 64];
+    uint32_t n_items = dense ? (uint32_t)a.n_own : 0u;
+    if (bl) {
+        const uint64_t n16 = ((uint64_t)threadIdx.x * gridDim.x + blockIdx.x) * 16;  // rows: a multiple of 64
+        const uint32_t t16 = threadIdx.x * 16;
+        ulonglong2 x = make_ulonglong2(0ull, 0ull);
+        if (n16 < a.n_own) x = *reinterpret_cast<const ulonglong2*>(a.cand + a.own0 + n16);
+        const unsigned long long lo7 = 0x7f7f7f7f7f7f7f7full;
+        unsigned long long m0 = (((x.x & lo7) + lo7) | x.x) & ~lo7, m1 = (((x.y & lo7) + lo7) | x.y) & ~lo7;
+        const uint32_t c = (uint32_t)(__popcll(m0) + __popcll(m1));
+        const int ln = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        uint32_t incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (ln >= o) incl += y;
+        }
+        if (ln == 63) s_lcnt[wv] = incl;
+        __syncthreads();
+        uint32_t pos = incl - c, tot = 0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) {
+            const uint32_t v = s_lcnt[w];
+            pos += w < wv ? v : 0u;
+            tot += v;
+        }
+        for (; m0; m0 &= m0 - 1) s_list[pos++] = (uint16_t)(t16 + (__ffsll(m0) - 1) / 8);
+        for (; m1; m1 &= m1 - 1) s_list[pos++] = (uint16_t)(t16 + 8 + (__ffsll(m1) - 1) / 8);
+        __syncthreads();
+        n_items = tot;
+    } else if (!dense) {
+        n_items = a.n_work[1];
+    }
+    // list entry t * 16 + j: node j of thread t's granule
+    auto bl_node = [&](uint32_t x) -> uint32_t { return ((x >> 4) * gridDim.x + blockIdx.x) * 16u + (x & 15u); };
+    if (bl ? n_items == 0 : (uint64_t)blockIdx.x * NGB >= n_items) {  // sparse round: no item reaches this block
         noop_exit(a, K_STREAM, t_start);
         return;
     }
-    const bool ff = !MASKW && ff_round(a);  // flags-first gathers (block-uniform)
-    const bool full = !MASKW && all_full(a);  // nothing can arrive: no gathers, no own rows
+    const bool ff = !MASKW && ff_view(a, rv);  // flags-first gathers (block-uniform)
+    // nothing can arrive (all_full()): no gathers, no own rows
+    const bool full = !MASKW && a.tot && inj_n(a) == 0 && rv.tot == a.full_new;
+    if (DB && !MASKW && full) {
+        // an all-full double-buffered round (e.g. the quiescence round that ends an
+        // episode): every owned set is the universe, row 0's, so nothing arrives
+        // and a node's only work is moving that row forward if its row in this
+        // buffer is two rounds old (ACT in r-1), and its flag and candidate bytes.
+        // No gathers: U nodes a group per iteration, their bytes loaded together
+        // (the general loop below pays a memory round trip per node)
+        const int lg = threadIdx.x % G;
+        const uint32_t off = (uint32_t)lg * WPL, stride = bl ? (uint32_t)NGB : gridDim.x * NGB;
+        const uint32_t k = (bl ? 0u : blockIdx.x * NGB) + threadIdx.x / G;
+        auto node_of = [&](uint32_t q) -> uint32_t {
+            return q < n_items ? (dense ? q : (bl ? bl_node(s_list[q]) : a.nodes[q])) : ~0u;
+        };
+        Row<WPL> U0;
+        {
+            const ulonglong2 u = *reinterpret_cast<const ulonglong2*>(a.base_prev + a.own0 * a.nwp + off);
+            U0.w[0] = u.x;
+            U0.w[1] = u.y;
+        }
+        constexpr int U = 4;
+        uint32_t c_act = 0;
+        unsigned long long c_by = 0;
+        for (uint32_t kk = k; kk < n_items; kk += U * stride) {
+            uint32_t nd[U];
+            uint8_t fl[U], ca[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) nd[u] = node_of(kk + u * stride);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                fl[u] = ca[u] = 0;
+                if (nd[u] != ~0u) {
+                    fl[u] = a.flg_prev[a.own0 + nd[u]];
+                    ca[u] = a.cand[a.own0 + nd[u]];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (nd[u] == ~0u) continue;
+                const uint64_t rep = a.own0 + nd[u];
+                if (fl[u] & FL_ACT) {
+                    store_row_nt(a.base + rep * a.nwp + off, U0);
+                    c_by += 16;
+                }
+                if (lg == 0) {
+                    a.flg_cur[rep] = 0;
+                    if (ca[u]) a.cand[rep] = 0;
+                    if (MARK && fl[u]) a.flg_prev_w[rep] = 0;
+                    c_act += 1;
+                    c_by += (dense ? 0 : 4) + 8 + 2 + 1;
+                }
+            }
+        }
+        unsigned long long acc[C_NUM];
+#pragma unroll
+        for (int q = 0; q < C_NUM; ++q) acc[q] = 0;
+        acc[C_ACTIVE] = c_act;
+        acc[C_BYTES] = c_by;
+        flush_counters(a, acc, s_red, t_start, K_STREAM);
+        return;
+    }
     // double-buffered round: own and sender rows are sets of r-1 (base_prev); in a
     // lean round without a dropped message so far a sender's set holds nothing new
     // for v beyond its F row (it forwarded every older value to v), so claims are
@@ -1566,7 +1737,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
     const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
     uint8_t* const my = &s_slots[(threadIdx.x >> 6) * (D + 1) * 1024];
     const uint32_t lane16 = (threadIdx.x & 63) * 16;
-    const uint32_t stride = gridDim.x * NGB;
+    const uint32_t stride = bl ? (uint32_t)NGB : gridDim.x * NGB;
     const unsigned long long rowb = 8ull * a.nwp;
 
     // node ids are < 2^31 (gg_create), so 32-bit ids and in-degrees keep the
@@ -1579,7 +1750,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
     constexpr uint32_t kNone = ~0u;
     constexpr uint32_t kHubBit = 0x80000000u;  // node ids < 2^31
     auto node_of = [&](uint32_t k) -> uint32_t {
-        return k < n_items ? (dense ? (uint32_t)k : a.nodes[k]) : kNone;
+        return k < n_items ? (dense ? (uint32_t)k : (bl ? bl_node(s_list[k]) : a.nodes[k])) : kNone;
     };
     auto fetch_meta = [&](uint32_t n, Meta& m) {
         m.node = n;
@@ -1607,7 +1778,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             c[b] = ((uint32_t)b < m.deg) ? a.in_col[m.p0 + b] : 0u;
     };
 
-    uint32_t k = blockIdx.x * NGB + threadIdx.x / G;
+    uint32_t k = (bl ? 0u : blockIdx.x * NGB) + threadIdx.x / G;
     // an all-full double-buffered round: every owned set is row 0's, so each lane
     // puts its chunk of it in its own-row LDS slot once (no own-row DMA overwrites
     // it) instead of every node DMA-ing the same row, and the loop only writes the
@@ -2900,7 +3071,7 @@ __global__ void build_rev(const int64_t* in_ptr, const uint32_t* in_col, const i
 __global__ __launch_bounds__(kBlock) void pack_act_bits(RoundArgs a) {
     static_assert(FL_ACT == 1, "the bit gather assumes FL_ACT is bit 0");
     const unsigned long long t_start = clock100();
-    if (!ff_round(a)) {
+    if (!ff_view(a, ring_view(a))) {
         noop_exit(a, K_PREP, t_start);
         return;
     }

@@ -129,7 +129,7 @@ GG_SYMBOLS = [
     "gg_abi_version", "gg_create", "gg_destroy", "gg_last_error", "gg_topology",
     "gg_partition_seeded", "gg_partition_groups", "gg_set_partition", "gg_broadcast", "gg_broadcast_many",
     "gg_lane_of", "gg_step", "gg_topology_part", "gg_topology_part_directed",
-    "gg_current_round", "gg_step_device_ms", "gg_read", "gg_read_bits", "gg_delivery_rounds", "gg_reset",
+    "gg_current_round", "gg_step_device_ms", "gg_run_episodes", "gg_read", "gg_read_bits", "gg_delivery_rounds", "gg_reset",
     "gg_device_bytes",
     "gg_read_bits_nodes", "gg_delivery_rounds_nodes",
     "gg_dist_round_begin", "gg_dist_round_end", "gg_dist_flush", "gg_dist_owned", "gg_dist_info",
@@ -165,6 +165,7 @@ def load_library(path: str) -> C.CDLL:
     lib.gg_lane_of.argtypes = [C.c_void_p, C.c_int64]
     lib.gg_step.argtypes = [C.c_void_p, C.c_uint32, P(GGRoundStats)]
     lib.gg_step_device_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+    lib.gg_run_episodes.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(GGRoundStats)]
     lib.gg_current_round.argtypes = [C.c_void_p]
     lib.gg_current_round.restype = C.c_int64
     lib.gg_read.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, P(C.c_uint64)]
@@ -344,8 +345,19 @@ class Engine:
             return arr
         return [stats_dict(arr[i]) for i in range(n_rounds)]
 
+    def run_episodes(self, n_rounds: int, episodes: int, raw: bool = False):
+        """gg_run_episodes: right after reset() and the broadcasts, `episodes`
+        episodes of that schedule, n_rounds each, with one host wait; per episode
+        its rounds' stats (raw=True: one ctypes array, episode k at k * n_rounds)."""
+        arr = (GGRoundStats * (n_rounds * episodes))()
+        self._ok(self.lib.gg_run_episodes(self.h, n_rounds, episodes, arr))
+        if raw:
+            return arr
+        return [[stats_dict(arr[k * n_rounds + i]) for i in range(n_rounds)] for k in range(episodes)]
+
     def step_device_ms(self) -> float:
-        """HIP-event device time of the last step() call (whole launch sequence)."""
+        """HIP-event device time of the last step() call (whole launch sequence;
+        after run_episodes: per episode)."""
         x = C.c_double(0.0)
         self._ok(self.lib.gg_step_device_ms(self.h, C.byref(x)))
         return x.value

@@ -21,6 +21,8 @@
  *                             rebroadcastAllExcept (`:50-57`) / SyncBroadcast
  *                             (`:81-122`) / HandleRead (`:124-132`) / broadcast_ok
  *                             (`main.go:38-40`) event of those rounds
+ * gg_run_episodes             repeated gg_reset + broadcasts + gg_step with one host
+ *                             wait (a workload replayed many times; new)
  * gg_read / gg_read_bits      client `read` -> HandleRead `broadcast.go:124-132`
  * gg_delivery_rounds          observation only (first round each value was seen)
  * gg_dist_*                   one engine per GPU: locality-ordered vertex ranges with
@@ -52,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 6
+#define GG_ABI_VERSION 7
 
 #define GG_OK 0
 #define GG_EIO (-5)
@@ -198,6 +200,18 @@ int64_t gg_current_round(const gg_engine* e);
 /* Device time of the last gg_step measured with HIP events on the engine's
  * stream around the whole launch sequence (0 for the CPU oracle). */
 int gg_step_device_ms(const gg_engine* e, double* ms);
+/* A serving loop of whole episodes without a host round trip between them:
+ * called right after gg_reset and the client broadcasts of one episode (current
+ * round 0), runs `episodes` episodes of that schedule, each = n_rounds rounds;
+ * episode k > 0 first does what gg_reset + the same broadcasts would. The
+ * result equals `episodes` x (gg_reset; the same broadcasts; gg_step(n_rounds))
+ * — out[k * n_rounds + i] (may be NULL) receives round i of episode k, and the
+ * engine is left at the end of the last episode — but the episodes are queued
+ * back to back on the engine's stream and the host waits once, at the end.
+ * Single engine (not vertex-sharded), 1 <= n_rounds <= 256. gg_step_device_ms
+ * then gives the device time per episode. (Host side of a Maelstrom run that
+ * replays one broadcast workload many times; the reference has no counterpart.) */
+int gg_run_episodes(gg_engine* e, uint32_t n_rounds, uint32_t episodes, gg_round_stats* out);
 
 /* HandleRead: the values node holds, ascending. n_out = count (even if > cap). */
 int gg_read(gg_engine* e, uint32_t node, int64_t* out, uint64_t cap, uint64_t* n_out);

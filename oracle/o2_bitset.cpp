@@ -765,6 +765,30 @@ int gg_step_device_ms(const gg_engine* e, double* ms) {
     return GG_OK;
 }
 
+// gossip.h: episodes x (gg_reset; the schedule held now; gg_step(n_rounds)).
+int gg_run_episodes(gg_engine* e, uint32_t n_rounds, uint32_t episodes, gg_round_stats* out) {
+    if (!e) return GG_EINVAL;
+    if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
+    if (e->P != 1) return e->fail(GG_EINVAL, "vertex-sharded engine: use gg_dist_round_begin/end");
+    if (e->round != 0) return e->fail(GG_EINVAL, "gg_run_episodes: call it right after gg_reset and the broadcasts");
+    if (n_rounds < 1 || n_rounds > 256 || episodes < 1) return e->fail(GG_EINVAL, "gg_run_episodes: bad sizes");
+    const auto inj0 = e->inj;
+    const auto lanes0 = e->lanes;
+    const auto lv0 = e->lane_value;
+    for (uint32_t k = 0; k < episodes; ++k) {
+        if (k) {
+            int rc = gg_reset(e);
+            if (rc) return rc;
+            e->inj = inj0;
+            e->lanes = lanes0;
+            e->lane_value = lv0;
+        }
+        int rc = gg_step(e, n_rounds, out ? out + (size_t)k * n_rounds : nullptr);
+        if (rc) return rc;
+    }
+    return GG_OK;
+}
+
 int gg_dist_info(const gg_engine* e, uint64_t* n_own, uint64_t* n_ghost, uint64_t* n_send) {
     if (!e || !e->have_topo) return GG_EINVAL;
     const uint64_t n = e->hi - e->lo;
