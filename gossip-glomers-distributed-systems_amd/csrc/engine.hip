@@ -1200,12 +1200,12 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
             hipLaunchKernelGGL(gg::mark_injections, dim3(gg::kMarkInjBlocks), dim3(256), 0, e->stream, a);
             HIPCHK(hipGetLastError());
         }
-        // block lists (RoundArgs::block_lists): a marking round on one engine needs
+        // block lists (RoundArgs::block_lists): a marking round needs
         // no compact_round — its two double-buffered expand kernels list their
         // blocks' candidates themselves (C2: one launch and a list pass less a round)
         static const bool no_bll = ab_knob("GG_BLOCK_LISTS") && atoi(ab_knob("GG_BLOCK_LISTS")) == 0;  // A/B
         a.block_lists = (a.prep_in_compact && a.mark_cand && a.db && a.stream_ok && !sync_stream && !maskw &&
-                         e->P == 1 && e->n_hubs == 0 && !no_bll) ? 1u : 0u;
+                         e->n_hubs == 0 && !no_bll) ? 1u : 0u;
         if (!a.block_lists) {
             const uint64_t groups = (a.n_own + 7) / 8;  // >= tile groups
             const uint64_t per_block = (uint64_t)gg::kBlock * gg::kCompactQ;

@@ -155,9 +155,9 @@ struct RoundArgs {
                                 // r-1, so round r+1 needs no round_prep (prep_in_compact)
     uint32_t prep_in_compact;   // no round_prep this round: compact_round sums the rings of r-1
                                 // (round r-1 was a marking round, or r is the first round)
-    uint32_t block_lists;       // ... and no compact_round either: the double-buffered expand
-                                // kernels sum the rings themselves and each block lists the
-                                // candidates of its own slice of the nodes in LDS (single engine)
+    uint32_t block_lists;       // ... and no compact_round either: the marking kernel sums the
+                                // rings itself and each of its blocks lists the candidates of
+                                // its own granules of the owned nodes in LDS
     uint8_t* zmark;             // [rows] F row of this parity is stale (node active 2 rounds ago)
     uint8_t* tile_cand;         // [n_tiles rounded to 8] tile has a candidate (sparse rounds)
     struct TileWork* work;      // live tiles of a sparse round (compact_round; expand_round)
