@@ -351,15 +351,25 @@ def main():
     # its counters read back and checked like the loop's — with one host wait, so
     # no host round trip idles the GPU between episodes (the loop of synchronous
     # reset/broadcast/step calls is timed beside it: per_call_ms_per_step)
-    pipelined = runner is None
+    # (vertex parts: gg_dist_run_episodes over the device-driven exchange, every rank alike)
+    dist_pipe = (runner is not None and getattr(runner, "can_run_episodes", False)
+                 and os.environ.get("GG_BENCH_DIST_EPISODES", "0") == "1")
+    pipelined = runner is None or dist_pipe
     if pipelined and args.warmup > 0:  # (its counter ring is allocated here)
         eng.reset()
         inject(eng, inj_arr)
-        eng.run_episodes(R, args.steps, raw=True)
+        if dist_pipe:
+            runner.run_episodes(R, args.steps)
+        else:
+            eng.run_episodes(R, args.steps, raw=True)
     barrier()
     t0 = time.perf_counter()
     local_stats = []
-    if pipelined:
+    if dist_pipe:
+        eng.reset()
+        inject(eng, inj_arr)
+        local_stats = runner.run_episodes(R, args.steps)
+    elif pipelined:
         eng.reset()
         inject(eng, inj_arr)
         arr = eng.run_episodes(R, args.steps, raw=True)
@@ -371,7 +381,8 @@ def main():
     elapsed = t1 - t0
     per_call_ms = None
     if pipelined:
-        local_stats = [[arr[k * R + i] for i in range(R)] for k in range(args.steps)]
+        if not dist_pipe:
+            local_stats = [[arr[k * R + i] for i in range(R)] for k in range(args.steps)]
         ev_pipe = [eng.step_device_ms()] * args.steps
         barrier()
         c0 = time.perf_counter()
@@ -542,7 +553,7 @@ def main():
                 "setup_s_rank0": setup_s,
                 "check": check,
                 "oracle_check": oracle_check,
-                "timed_loop": ("gg_run_episodes: the K episodes (each a reset, the same client broadcasts and "
+                "timed_loop": (("gg_dist_run_episodes" if dist_pipe else "gg_run_episodes") + ": the K episodes (each a reset, the same client broadcasts and "
                                "R rounds, its counters read back) queued back to back, one host wait; "
                                "roofline.per_call_ms_per_step times the same episodes as K synchronous "
                                "reset/broadcast/step calls" if pipelined else

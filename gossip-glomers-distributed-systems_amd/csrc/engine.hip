@@ -3676,6 +3676,81 @@ int gg_dist_step(gg_engine* e, uint32_t n_rounds) {
     return GG_OK;
 }
 
+int gg_dist_run_episodes(gg_engine* e, uint32_t n, uint32_t episodes, gg_round_stats* out) {
+    if (!e) return GG_EINVAL;
+    if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
+    if (e->world < 2) return e->fail(GG_EINVAL, "not a sharded engine (world == 1): use gg_run_episodes");
+    if (!(e->ipc || e->P == 1)) return e->fail(GG_EINVAL, "gg_dist_run_episodes: needs the device-driven exchange");
+    if (e->dist_open || e->dist_k || e->round != 0)
+        return e->fail(GG_EINVAL, "gg_dist_run_episodes: call it right after gg_reset and the broadcasts");
+    if (n < 1 || n > kMaxBatch || episodes < 1) return e->fail(GG_EINVAL, "gg_dist_run_episodes: bad sizes");
+    HIPCHK(hipSetDevice(e->device));
+    // every episode's raw counter slots (and payload bytes) in a device ring, read back once
+    const size_t slot = (size_t)gg::kSlots * gg::kCounters;
+    const size_t ctr_b = (size_t)n * slot * 8, pay_b = (size_t)n * 8, per = ctr_b + pay_b, need = per * episodes;
+    if (need > e->ep_cap) {
+        HIPCHK(hipStreamSynchronize(e->stream));
+        dfree(e->d_ep);
+        if (e->h_ep) (void)hipHostFree(e->h_ep);
+        e->h_ep = nullptr;
+        e->ep_cap = 0;
+        HIPCHK(hipMalloc(&e->d_ep, need));
+        HIPCHK(hipHostMalloc(&e->h_ep, need));
+        e->ep_cap = need;
+    }
+    const auto inj0 = e->inj;
+    const LaneTable lanes0 = e->lanes;
+    const std::vector<int64_t> lv0 = e->lane_value;
+    int rc = ensure_events(e, 2);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(e->ev[0], e->stream));
+    for (uint32_t k = 0; k < episodes; ++k) {
+        if (k) {  // gg_reset + the same broadcasts, without gg_reset's wait
+            reset_host_state(e, true);
+            e->inj = inj0;
+            e->lanes = lanes0;
+            e->lane_value = lv0;
+            e->quiet = 0;
+            if ((rc = reset_device_state(e))) return rc;
+        }
+        // (episode k > 0 packs the same pairs into the same pinned ring slots an
+        // earlier episode's copy may still be reading: identical bytes)
+        if ((rc = dist_step_batched(e, n))) return rc;
+        auto* dst = reinterpret_cast<uint8_t*>(e->d_ep) + (size_t)k * per;
+        HIPCHK(hipMemcpyAsync(dst, e->d_counters, ctr_b, hipMemcpyDeviceToDevice, e->stream));
+        if (e->d_payload) HIPCHK(hipMemcpyAsync(dst + ctr_b, e->d_payload, pay_b, hipMemcpyDeviceToDevice, e->stream));
+    }
+    HIPCHK(hipEventRecord(e->ev[1], e->stream));
+    HIPCHK(hipMemcpyAsync(e->h_ep, e->d_ep, need, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
+    e->step_event_ms = (double)ms / episodes;
+    if (e->ipc) {
+        uint32_t err = 0;
+        HIPCHK(hipMemcpy(&err, e->d_xticket + 1, 4, hipMemcpyDeviceToHost));
+        if (err) return e->fail(GG_EIO, "device-driven exchange: a peer did not arrive within the wait bound");
+    }
+    for (uint32_t k = 0; k < episodes; ++k) {
+        e->hash_total = 0;
+        e->pend_acks = e->pend_ackdrop = 0;
+        const auto* src = reinterpret_cast<const uint8_t*>(e->h_ep) + (size_t)k * per;
+        const auto* ctr = reinterpret_cast<const unsigned long long*>(src);
+        const auto* pay = reinterpret_cast<const unsigned long long*>(src + ctr_b);
+        for (uint32_t j = 0; j < n; ++j) {
+            gg_round_stats s;
+            fold_stats(e, ctr + (size_t)j * slot, e->dist_round_of[j], &s);
+            s.path = e->dist_path[j];
+            s.sent_bytes = e->d_payload ? pay[j] : 0;
+            e->quiet = s.new_bits ? 0 : e->quiet + 1;
+            if (out) out[(size_t)k * n + j] = s;
+        }
+    }
+    e->dist_k = 0;  // (folded here: gg_dist_flush has nothing pending)
+    e->inj_off = 0;
+    return GG_OK;
+}
+
 }  // extern "C"
 
 // Local rows of owned nodes (GG_EINVAL if one is not owned).

@@ -271,6 +271,17 @@ class ShardedRunner:
         local = self.eng.dist_flush()
         return self.reduce(local) if reduce else local
 
+    @property
+    def can_run_episodes(self) -> bool:
+        """gg_dist_run_episodes applies: the device-driven exchange, or lane groups only."""
+        return self.engine_comm and (self.transport.startswith("device-driven") or self.eng.parts == 1)
+
+    def run_episodes(self, n_rounds: int, episodes: int) -> list[list[dict]]:
+        """Right after reset() and the broadcasts on this rank (every rank calls
+        it alike): `episodes` episodes of n_rounds rounds back to back on the
+        device, one host wait; this rank's stats per episode (not reduced)."""
+        return self.eng.dist_run_episodes(n_rounds, episodes)
+
     def reduce(self, local: list[dict]) -> list[dict]:
         """Sum the per-rank counters of each round (seen_hash mod 2^64)."""
         if not local:

@@ -134,7 +134,7 @@ GG_SYMBOLS = [
     "gg_read_bits_nodes", "gg_delivery_rounds_nodes",
     "gg_dist_round_begin", "gg_dist_round_end", "gg_dist_flush", "gg_dist_owned", "gg_dist_info",
     "gg_dist_comm_available", "gg_dist_comm_id", "gg_dist_comm_init", "gg_dist_transport_init", "gg_dist_step",
-    "gg_dist_ipc_export", "gg_dist_ipc_import",
+    "gg_dist_ipc_export", "gg_dist_ipc_import", "gg_dist_run_episodes",
 ]
 
 _LIBS: dict[str, C.CDLL] = {}
@@ -183,6 +183,7 @@ def load_library(path: str) -> C.CDLL:
     lib.gg_dist_comm_id.argtypes = [C.c_void_p, C.c_void_p]
     lib.gg_dist_comm_init.argtypes = [C.c_void_p, C.c_void_p]
     lib.gg_dist_step.argtypes = [C.c_void_p, C.c_uint32]
+    lib.gg_dist_run_episodes.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(GGRoundStats)]
     lib.gg_dist_ipc_export.argtypes = [C.c_void_p, C.c_void_p]
     lib.gg_dist_ipc_import.argtypes = [C.c_void_p, C.c_void_p]
     lib.gg_dist_transport_init.argtypes = [C.c_void_p, P(GGTransport)]
@@ -476,6 +477,13 @@ class Engine:
     def dist_step(self, n_rounds: int) -> None:
         """n sharded rounds with the engine's own RCCL exchange; counters pending (dist_flush)."""
         self._ok(self.lib.gg_dist_step(self.h, n_rounds))
+
+    def dist_run_episodes(self, n_rounds: int, episodes: int) -> list[list[dict]]:
+        """gg_dist_run_episodes (device-driven exchange or lane groups only): this
+        engine's own stats of every round of every episode, one host wait."""
+        arr = (GGRoundStats * (n_rounds * episodes))()
+        self._ok(self.lib.gg_dist_run_episodes(self.h, n_rounds, episodes, arr))
+        return [[stats_dict(arr[k * n_rounds + i]) for i in range(n_rounds)] for k in range(episodes)]
 
     def dist_flush(self) -> list[dict]:
         n = C.c_uint64(0)

@@ -320,6 +320,13 @@ int gg_dist_transport_init(gg_engine* e, const gg_transport* t);
 /* n sharded rounds with the engine's exchange (RCCL, the transport or IPC; none
  * needed when the engine has no other vertex part). */
 int gg_dist_step(gg_engine* e, uint32_t n_rounds);
+/* gg_run_episodes for the device-driven sharded round (after gg_dist_ipc_import,
+ * or lane groups only): right after gg_reset and the broadcasts, `episodes`
+ * episodes of n_rounds gg_dist_step rounds, episode k > 0 first doing what
+ * gg_reset + the same broadcasts would; this engine's own per-round stats (not
+ * summed over ranks) in out[k * n_rounds + i], one host wait at the end. Every
+ * rank of the job calls it with the same sizes. */
+int gg_dist_run_episodes(gg_engine* e, uint32_t n_rounds, uint32_t episodes, gg_round_stats* out);
 
 /* Device-driven exchange (no host wait, no collective call per round): every part
  * of a lane group exports one window of uncached device memory (flags and two

@@ -911,6 +911,9 @@ int gg_dist_ipc_export(gg_engine*, uint8_t*) { return GG_EIO; }  // no device me
 int gg_dist_ipc_import(gg_engine*, const uint8_t*) { return GG_EIO; }
 int gg_dist_comm_init(gg_engine* e, const uint8_t*) { return e ? e->fail(GG_EIO, "CPU oracle: no RCCL") : GG_EINVAL; }
 int gg_dist_step(gg_engine* e, uint32_t) { return e ? e->fail(GG_EIO, "CPU oracle: no RCCL") : GG_EINVAL; }
+int gg_dist_run_episodes(gg_engine* e, uint32_t, uint32_t, gg_round_stats*) {
+    return e ? e->fail(GG_EIO, "CPU oracle: no device-driven exchange") : GG_EINVAL;
+}
 int gg_topology_part(gg_engine* e, const uint64_t*, const int64_t*, const int32_t*, uint64_t) {
     return e ? e->fail(GG_ENOSYS, "CPU oracle: sharded engines take the whole graph (gg_topology)") : GG_EINVAL;
 }

@@ -965,3 +965,79 @@ def test_batched_refuses_lane_groups(hip_lib):
     from ggamd.engine import Engine, GGError
     with pytest.raises(GGError):
         Engine(10, 128, batch_ticks=2, world=2, rank=0, lane_groups=2, library=hip_lib)
+
+
+def _episodes_worker(rank, world, port, lib, scenarios, q, lane_groups, episodes):
+    import torch
+    import torch.distributed as dist
+
+    from ggamd.dist import ShardedRunner
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        out = []
+        dev = torch.device("cuda", 0)
+        for sc in scenarios:
+            e = make_engine(lib, sc, rank=rank, world=world, device=0, lane_groups=lane_groups)
+            r = ShardedRunner(e, dev, transport="ipc")
+            assert r.can_run_episodes, r.transport
+            eps = [r.reduce(ep) for ep in r.run_episodes(sc.rounds, episodes)]
+            owned = e.dist_owned()
+            bits = e.read_bits_nodes(owned)
+            # a synchronous episode after it starts from the state it left
+            e.reset()
+            for n, v, rr in sc.injections:
+                e.broadcast(int(n), int(v), int(rr))
+            again = r.step(sc.rounds)
+            out.append((eps, owned, bits, again))
+            e.close()
+        q.put((rank, out))
+    except BaseException as exc:  # report instead of leaving the parent waiting
+        q.put((rank, f"rank {rank} failed: {exc!r}"))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,lane_groups", [(2, 1), (3, 1), (4, 2)])
+def test_ipc_run_episodes_equal_oracle(hip_lib, cpu_lib, world, lane_groups):
+    """gg_dist_run_episodes: episodes of the device-driven sharded round queued
+    back to back (reset and broadcasts of episode k > 0 on the device, one host
+    wait): every episode's summed counters equal O2's episode, the node sets
+    after the last one equal O2's, and a synchronous episode after it too."""
+    from ggamd import topology as T
+    from ggamd.workload import uniform_injections
+    scs = [Scenario(T.tree(3000, 4), 256, 30, uniform_injections(3000, 200, 5), seed=9, sync_base=6, sync_jitter=3),
+           Scenario(T.grid_links(40, seed=11), 64, 36, uniform_injections(1600, 64, 6), seed=10, sync_base=8,
+                    sync_jitter=4),
+           Scenario(T.random_regular(2048, 6, seed=3), 128, 26, uniform_injections(2048, 100, 9), seed=14,
+                    sync_base=8, sync_jitter=4, windows=[("seeded", 2, 7, 5)])]
+    scs = [sc for sc in scs if sc.W >= 64 * lane_groups]
+    episodes = 3
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_episodes_worker, args=(r, world, port, hip_lib, scs, qq, lane_groups, episodes))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, got = qq.get(timeout=170)
+        assert not isinstance(got, str), got
+        res[r] = got
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for k, sc in enumerate(scs):
+        ref = make_engine(cpu_lib, sc)
+        want = ref.step(sc.rounds)
+        for rank in range(world):
+            eps, owned, bits, again = res[rank][k]
+            assert len(eps) == episodes
+            for j, ep in enumerate(eps):
+                d = diff_stats(want, ep)
+                assert not d, (k, rank, j, d[:8])
+            assert not diff_stats(want, again), (k, rank, "synchronous episode after")
+            if lane_groups == 1:
+                assert np.array_equal(bits, ref.read_bits_nodes(owned)), (k, rank)
+        ref.close()
