@@ -353,7 +353,7 @@ def main():
     # reset/broadcast/step calls is timed beside it: per_call_ms_per_step)
     # (vertex parts: gg_dist_run_episodes over the device-driven exchange, every rank alike)
     dist_pipe = (runner is not None and getattr(runner, "can_run_episodes", False)
-                 and os.environ.get("GG_BENCH_DIST_EPISODES", "0") == "1")
+                 and os.environ.get("GG_BENCH_DIST_EPISODES", "1") != "0")
     pipelined = runner is None or dist_pipe
     if pipelined and args.warmup > 0:  # (its counter ring is allocated here)
         eng.reset()
