@@ -359,7 +359,16 @@ def main():
         eng.reset()
         inject(eng, inj_arr)
         if dist_pipe:
-            runner.run_episodes(R, args.steps)
+            fail = 0
+            try:
+                runner.run_episodes(R, args.steps)
+            except Exception as exc:  # noqa: BLE001 — every rank agrees below, then falls back
+                fail = 1
+                print(f"bench: rank {rank}: gg_dist_run_episodes failed ({exc!r}); timing synchronous calls",
+                      file=sys.stderr)
+            if allreduce_i64([fail])[0]:
+                dist_pipe = False
+                pipelined = False
         else:
             eng.run_episodes(R, args.steps, raw=True)
     barrier()
