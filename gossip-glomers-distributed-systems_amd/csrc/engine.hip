@@ -2639,6 +2639,7 @@ int gg_run_episodes(gg_engine* e, uint32_t n, uint32_t episodes, gg_round_stats*
     const int quiet0 = e->quiet;
     std::vector<std::vector<uint64_t>> paths(episodes);
     const unsigned long long* folded = e->d_counters + (size_t)kMaxBatch * gg::kSlots * gg::kCounters;
+    int quiet_end = 0;  // trailing quiet rounds of an episode: every episode's, they are the same
     HIPCHK(hipEventRecord(e->ev[0], e->stream));
     for (uint32_t k = 0; k < episodes; ++k) {
         if (k) {  // gg_reset + the same broadcasts, without gg_reset's wait
@@ -2646,12 +2647,22 @@ int gg_run_episodes(gg_engine* e, uint32_t n, uint32_t episodes, gg_round_stats*
             e->inj = inj0;
             e->lanes = lanes0;
             e->lane_value = lv0;
-            e->quiet = 0;  // the last episode's quiet rounds are not known yet: clear every per-round array
+            e->quiet = quiet_end;  // (reset clears the per-round F arrays only where they can be dirty)
             if ((rc = reset_device_state(e))) return rc;
         }
         if ((rc = enqueue_step_batch(e, n, false, paths[k]))) return rc;
         HIPCHK(hipMemcpyAsync(e->d_ep + (size_t)k * n * gg::kCounters, folded, rows_b, hipMemcpyDeviceToDevice,
                               e->stream));
+        if (k == 0 && episodes > 1) {
+            // the episodes are identical, so the first one's trailing quiet rounds
+            // (its folded rows reach h_counters inside the replayed sequence) tell
+            // every later reset how much of the F buffers an episode leaves dirty:
+            // one host wait, after the first episode only
+            HIPCHK(hipStreamSynchronize(e->stream));
+            int q = 2;  // what a reset leaves
+            for (uint32_t j = 0; j < n; ++j) q = e->h_counters[(size_t)j * gg::kCounters + gg::C_NEW] ? 0 : q + 1;
+            quiet_end = q;
+        }
     }
     HIPCHK(hipEventRecord(e->ev[1], e->stream));
     HIPCHK(hipMemcpyAsync(e->h_ep, e->d_ep, need, hipMemcpyDeviceToHost, e->stream));
