@@ -207,7 +207,9 @@ int gg_step_device_ms(const gg_engine* e, double* ms);
  * result equals `episodes` x (gg_reset; the same broadcasts; gg_step(n_rounds))
  * — out[k * n_rounds + i] (may be NULL) receives round i of episode k, and the
  * engine is left at the end of the last episode — but the episodes are queued
- * back to back on the engine's stream and the host waits once, at the end.
+ * back to back on the engine's stream and the host waits only after the first
+ * episode (its trailing quiet rounds tell the later resets which buffers an
+ * episode leaves dirty) and at the end.
  * Single engine (not vertex-sharded), 1 <= n_rounds <= 256. gg_step_device_ms
  * then gives the device time per episode. (Host side of a Maelstrom run that
  * replays one broadcast workload many times; the reference has no counterpart.) */
