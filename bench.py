@@ -6,33 +6,40 @@ lockstep rounds until the round after the last delivery (quiescence, fixed
 during warmup). `value` = all (node,msg) deliveries of the timed episodes on
 all ranks / the max-over-ranks wall time.
 
---config C2 (default; BASELINE.json configs[1]): a 4-ary tree (Maelstrom
-  `tree4`) of 2^20 nodes per GPU, K = 1024 fresh messages broadcast by clients
-  at seeded uniform nodes in round 0, sync timers on, no partitions. On N GPUs
-  the tree has N * 2^20 nodes, vertex-range sharded (locality order) with one
-  exchange of ghost payloads per round ("scaling": "weak"): the engine's own
-  grouped RCCL send/recv on its stream.
---config C4 (configs[3], the 100M-node config the >= 6x scaling target is
-  quoted on): R-MAT (.57,.19,.19,.05), edge factor 16, 10^8 nodes, K = 4096
-  messages in round 0. Strong scaling over a 2-D grid of ranks, N = L x P
-  (--parts P, default 1): P vertex parts (each rank builds only its node range
-  of the graph on its GPU, with ghost copies of the adjacent remote nodes, and
-  exchanges one filtered ghost payload per round with the other parts of its
-  lane group over RCCL) times L = N / P lane groups (each a slice of the 4096
-  message lanes; lane groups never exchange anything). P = 1: every GPU holds
-  the whole CSR and 4096/N lanes, no exchange at all. The per-round counters
-  are summed with one all_reduce after the timed episodes.
+Headline (--config C2, default; BASELINE.json configs[1]): a 4-ary tree
+  (Maelstrom `tree4`) of 2^20 nodes per GPU, K = 1024 fresh messages broadcast
+  by clients at seeded uniform nodes in round 0, sync timers on, no partitions.
+  On N GPUs the tree has N * 2^20 nodes, vertex-range sharded (locality order)
+  with one exchange of ghost payloads per round ("scaling": "weak").
+--config C4 (configs[3]) as the headline: R-MAT (.57,.19,.19,.05), edge factor
+  16, 10^8 nodes, K = 4096, strong scaling over N = L x P ranks (--parts P).
 
-N > 1: after the timed region rank 0 runs one episode of a single unsharded
-engine over the whole graph on its own GPU and every round's global counters
-must equal it, else the run exits with status 1.
+Legs (--legs, default C4,C5 after a C2 headline; in the same JSON line under
+"legs", every N including 1): the two configs the north-star targets are
+quoted on, each built in HBM by the on-device generators and self-checked —
+  C4  10^8-node R-MAT, W = 4096, STRONG scaling: N vertex parts (two lane
+      halves per GPU, one half's exchange under the other half's kernels);
+      ms/step, deliveries/s, HBM per GPU, the dominant kernel's roofline;
+  C5  2^30-node grid + one long link per node, W = 64, N vertex parts: HBM per
+      GPU, rounds to full delivery, episode time.
+  Checks: every timed episode equals the checking episode counter by counter;
+  P1 / KAT-3 / ACK (ggamd.checks; C4's components from the exported graph);
+  N > 1: every round's global counters equal one unsharded engine on rank 0.
 
-Usage: python bench.py [--config C2|C4] [--parts P] [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+N > 1 exchange (--xchg auto): the device-driven IPC exchange when every rank
+maps its peers and one whole C2 episode through it equals O2's run of the
+same workload (tests/golden/bench_c2.json, every counter and the delivery
+hash); else the engine's grouped RCCL send/recv. A failure later in the timed
+region rebuilds every rank on the engine exchange and times that.
+
+Usage: python bench.py [--config C2|C4] [--parts P] [--gpus N] [--steps K] [--warmup W]
+                       [--legs C4,C5|none] [--leg-steps S] [--no-cpu-baseline]
 For N > 1 launch under torch.distributed.run (one process per GPU).
 """
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -46,6 +53,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "(node,msg) deliveries/sec at 1/2/4/8 GPUs; % of HBM roofline; msgs/op"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+M64 = (1 << 64) - 1
 
 KERNELS = {"prep": "round_prep", "expand": "expand_round", "stream": "expand_stream"}
 # the kernels one round launches exactly one of, per kind (the launch count of a kind)
@@ -62,8 +70,14 @@ KIND_KERNELS = {
                "expand_batched"],
 }
 TRAFFIC_JSON = {"C2": os.path.join(REPO, "profiles", "traffic.json"),  # committed PMC passes per config
-                "C4": os.path.join(REPO, "profiles", "traffic_C4.json")}
+                "C4": os.path.join(REPO, "profiles", "traffic_C4.json"),
+                "C5": os.path.join(REPO, "profiles", "traffic_C5.json")}
 CPU_LIB = os.path.join(REPO, "oracle", "_build", "libgossip_cpu.so")
+GOLD_C2 = os.path.join(REPO, "tests", "golden", "bench_c2.json")
+# the random-row request ceiling (rows of <= 128 B gathered by a per-node index,
+# tools/gather_bench.hip): what a kernel whose rows are one line
+# each can reach, where the byte roofline cannot be
+ROW_CEILING_PER_S = 47e9
 
 
 def pmc_traffic(kind: str, shape: dict):
@@ -116,70 +130,197 @@ def cpu_counts():
     return os.cpu_count() or 1, aff or 1
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="C2", choices=["C2", "C4"])
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--nodes", type=int, help="C2: nodes per GPU (2^20); C4: nodes (10^8)")
-    ap.add_argument("--lanes", type=int, help="C2: 1024; C4: 4096")
-    ap.add_argument("--parts", type=int, default=1, help="C4: vertex parts P (world = lane groups x P)")
-    ap.add_argument("--halves", type=int, default=1, choices=[1, 2],
-                    help="C4 with --parts > 1: 2 = two engines per GPU over the two halves of its lanes, "
-                         "one half's exchange overlapping the other half's kernels (ggamd.dist.HalvesRunner)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--fresh-sets", type=int, default=4,
-                    help="N = 1: after the timed region, episodes rotating this many distinct seeded injection "
-                         "sets (every step re-captures its launch graph and uploads its injections; 0: skip)")
-    ap.add_argument("--no-check", action="store_true", help="skip the N > 1 single-engine check")
-    ap.add_argument("--xchg", default=os.environ.get("GG_DIST_TRANSPORT", "auto"),
-                    choices=["auto", "engine", "ipc", "torch"],
-                    help="N > 1 exchange between vertex parts: engine = the engine's grouped RCCL send/recv; "
-                         "ipc = device-driven (IPC-mapped peer windows, kernel flags, captured batches of rounds, "
-                         "no host wait); torch = torch all_to_all; auto (default) = ipc on RCCL jobs when every "
-                         "rank maps its peers and two validation rounds match O2, else engine")
-    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 "
-                    "(nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
-    args = ap.parse_args()
+def roofline(rounds_local: list[dict], nwp: int, n_own: int, E_own: int, shape: dict) -> dict:
+    """The dominant kernel kind's roofline over a run's rounds (this rank):
+    per-kind device times (first block start to last block end of each launch,
+    stamped by the kernels) and the algorithmic bytes each launch had to move
+    (counted by the kernels). line_frac: the same launches priced
+    as random-row requests — every row a node moved or gathered is
+    ceil(row bytes / 128) lines — against the measured random-row ceiling;
+    the byte roofline is out of reach for gathers of rows this small."""
+    kinds = {}
+    n = max(1, len(rounds_local))
+    for kind, name in KERNELS.items():
+        ms = sum(s[kind + "_ms"] for s in rounds_local)
+        by = sum(s[kind + "_bytes"] for s in rounds_local)
+        if kind == "stream":
+            name = "expand_stream / expand_stream_db / expand_stream1"
+        kinds[kind] = {"kernel": name, "launches": len(rounds_local), "total_ms": ms, "bytes": by,
+                       "avg_launch_ms": ms / n, "GBps": by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0}
+    dom = max(kinds, key=lambda k: kinds[k]["total_ms"])
+    D = kinds[dom]
+    traffic, traffic_src = pmc_traffic(dom, shape)
+    lines_per_row = max(1, (8 * nwp + 127) // 128)
+    # rows moved by the round's kernels: gathered sender rows + own row read + row written
+    rows = sum(s["work_gathers"] + 2 * s["work_rows"] for s in rounds_local)
+    round_ms = sum(s["kernel_ms"] for s in rounds_local)
+    lines_per_s = rows * lines_per_row / (round_ms * 1e-3) if round_ms > 0 else 0.0
+    round_bytes = sum(s["prep_bytes"] + s["expand_bytes"] + s["stream_bytes"] for s in rounds_local)
+    return {
+        "bound": "hbm",
+        "kernel": D["kernel"],
+        "kind": dom,
+        "kind_kernels": "every kernel stamping this kind per round: " + ", ".join(KIND_KERNELS[dom]),
+        "achieved": D["GBps"],
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": D["GBps"] / HBM_PEAK_GBS,
+        "traffic": traffic,
+        "traffic_source": traffic_src,
+        "algorithmic_bytes_per_launch": D["bytes"] / n,
+        "avg_launch_ms": D["avg_launch_ms"],
+        "launches": D["launches"],
+        "dense_bytes_per_round": dense_bytes_per_round(n_own, E_own, nwp),
+        "line_frac": lines_per_s / ROW_CEILING_PER_S,
+        "line_model": {"rows_moved": rows, "lines_per_row": lines_per_row, "line_bytes": 128,
+                       "lines_per_s": lines_per_s, "ceiling_lines_per_s": ROW_CEILING_PER_S,
+                       "over": "every kernel of the timed rounds (round device time)",
+                       "note": "rows = sender rows gathered + 2 x nodes visited (own row read, and "
+                               "written: counted for every visited node, an upper bound), from the "
+                               "kernels' work counters; columns and flag bytes stream and are not "
+                               "counted"},
+        "timing": "per launch: device clock (s_memrealtime) from the first block start to the last "
+                  "block end of that kernel, stamped by every block (no-op launches included, as in "
+                  "rocprofv3's average)",
+        "kernels": {k: dict(d) for k, d in kinds.items()},
+        "round_GBps": round_bytes / (round_ms * 1e-3) / 1e9 if round_ms > 0 else 0.0,
+    }
 
-    import torch
-    import torch.distributed as dist
 
+class Job:
+    """This process's rank, device and collectives (one process per GPU)."""
+
+    def __init__(self, backend: str, gpus: int):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != gpus and self.world == 1 and gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+        self.backend = backend
+        if backend == "gloo":  # rehearsal: every rank on the one visible GPU
+            self.local = 0
+        torch.cuda.set_device(self.local)
+        self.device = torch.device("cuda", self.local)
+        if self.world > 1:
+            to = datetime.timedelta(seconds=int(os.environ.get("GG_BENCH_PG_TIMEOUT", "600")))
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=self.device, timeout=to)
+            else:
+                dist.init_process_group(backend, timeout=to)
+
+    def barrier(self):
+        if self.world > 1:
+            if self.backend == "nccl":
+                self.dist.barrier(device_ids=[self.local])
+            else:
+                self.dist.barrier()
+        self.torch.cuda.synchronize()
+
+    def allreduce(self, vals, op: str = "sum") -> list[int]:
+        if self.world == 1:
+            return [int(v) for v in vals]
+        t = self.torch.tensor([int(v) for v in vals], dtype=self.torch.int64,
+                              device=self.device if self.backend == "nccl" else "cpu")
+        R = self.dist.ReduceOp
+        self.dist.all_reduce(t, op={"sum": R.SUM, "max": R.MAX, "min": R.MIN}[op])
+        return t.cpu().tolist()
+
+    def agree(self, ok: bool) -> bool:
+        """True iff every rank is ok (every rank calls it at the same point)."""
+        return self.allreduce([0 if ok else 1])[0] == 0
+
+    def gather_i64(self, v: int) -> list[int]:
+        """Every rank's value, by rank."""
+        vals = [0] * self.world
+        vals[self.rank] = int(v)
+        return self.allreduce(vals)
+
+    def free_bytes(self) -> int:
+        return self.torch.cuda.mem_get_info(self.local)[0]
+
+    def close(self):
+        if self.world > 1:
+            self.barrier()
+            self.dist.destroy_process_group()
+
+
+def reduce_counts(stats, job: Job, fields):
+    """Sum one episode's per-round counters over the ranks (seen_hash mod 2^64)."""
+    flat = []
+    for s in stats:
+        for f in fields:
+            v = s[f] & M64
+            flat.append(v - (1 << 64) if v >= (1 << 63) else v)
+    tot = job.allreduce(flat)
+    out, k = [], 0
+    for s in stats:
+        d = dict(s)
+        for f in fields:
+            d[f] = tot[k] & M64
+            k += 1
+        out.append(d)
+    return out
+
+
+def count_diffs(a_eps, b_eps, fields, label_a, label_b, limit=8):
+    out = []
+    for a, b in zip(a_eps, b_eps):
+        for f in fields:
+            if (a[f] & M64) != (b[f] & M64):
+                out.append(f"round {b['round']} {f}: {label_a} {a[f] & M64} != {label_b} {b[f] & M64}")
+                if len(out) >= limit:
+                    return out
+    if len(a_eps) != len(b_eps):
+        out.append(f"{label_a} has {len(a_eps)} rounds, {label_b} {len(b_eps)}")
+    return out
+
+
+def gold_c2(nodes: int, lanes: int):
+    """O2's per-round global counters of the C2 workload (tests/golden/bench_c2.json)."""
+    if not os.path.exists(GOLD_C2):
+        return None
+    return next((g for g in json.load(open(GOLD_C2))["runs"].values() if g["nodes"] == nodes and g["lanes"] == lanes),
+                None)
+
+
+def peer_info(job: Job) -> dict:
+    """Where the ranks' GPUs are: distinct devices or not, and peer access from this one."""
+    torch = job.torch
+    if job.world == 1:
+        return {}
+    try:
+        uuid = str(torch.cuda.get_device_properties(job.local).uuid)
+    except Exception:  # noqa: BLE001
+        uuid = f"local{job.local}"
+    import hashlib
+    h = int.from_bytes(hashlib.sha1(uuid.encode()).digest()[:7], "little")
+    uuids = job.gather_i64(h)
+    locals_ = job.gather_i64(job.local)
+    acc = {}
+    for q in range(job.world):
+        if q != job.rank and locals_[q] != job.local:
+            try:
+                acc[q] = bool(torch.cuda.can_device_access_peer(job.local, locals_[q]))
+            except Exception:  # noqa: BLE001
+                acc[q] = None
+    return {"distinct_devices": len(set(uuids)) == job.world, "devices": len(set(uuids)),
+            "local_device_of_rank": locals_, "can_access_peer_from_rank0": acc if job.rank == 0 else None}
+
+
+# ---------------------------------------------------------------------------
+# headline (C2 weak scaling; or --config C4)
+
+def headline(job: Job, args) -> tuple[dict | None, dict]:
+    torch, world, rank, local = job.torch, job.world, job.rank, job.local
     from ggamd import topology as T
     from ggamd.engine import COUNT_FIELDS, Engine, stats_dict
     from ggamd.workload import BASE_SEED, inject, injection_arrays, uniform_injections
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world == 1 and args.gpus > 1:
-        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
-    if args.backend == "gloo":  # rehearsal: every rank on the one visible GPU
-        local = 0
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
-    if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
-        else:
-            dist.init_process_group(args.backend)
-
-    def barrier():
-        if world > 1:
-            if args.backend == "nccl":
-                dist.barrier(device_ids=[local])
-            else:
-                dist.barrier()
-        torch.cuda.synchronize()
-
-    def allreduce_i64(vals, op=None):
-        t = torch.tensor(vals, dtype=torch.int64, device=device if args.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=op or dist.ReduceOp.SUM)
-        return t.cpu().tolist()
-
     cfg = args.config
-    free0 = torch.cuda.mem_get_info(local)[0]
+    free0 = job.free_bytes()
     t_setup = time.perf_counter()
 
     def setup(xchg):
@@ -196,7 +337,8 @@ def main():
             engs = [eng]
             if world > 1:
                 from ggamd.dist import ShardedRunner
-                runner = ShardedRunner(eng, device, transport=xchg if args.backend == "nccl" or xchg == "ipc" else None)
+                runner = ShardedRunner(eng, job.device,
+                                       transport=xchg if args.backend == "nccl" or xchg == "ipc" else "engine")
             parallelism = f"vertex-range x{world}" if world > 1 else "single GPU"
             scaling = "weak"
             workload = ("C2: tree4 of 2^20 nodes per GPU, 1024 messages broadcast in round 0 at seeded uniform "
@@ -219,7 +361,7 @@ def main():
                 E = engs[0].generate(**gen)
                 engs[1].generate(**gen)
                 eng = engs[0]
-                runner = HalvesRunner(engs, device, transport=xchg)
+                runner = HalvesRunner(engs, job.device, transport=xchg)
             else:
                 eng = Engine(V, K, seed=seed, enable_sync=True, device=local, rank=rank, world=world,
                              lane_groups=L)
@@ -227,7 +369,8 @@ def main():
                 engs = [eng]
                 if P > 1:
                     from ggamd.dist import ShardedRunner
-                    runner = ShardedRunner(eng, device, transport=xchg if args.backend == "nccl" or xchg == "ipc" else "engine")
+                    runner = ShardedRunner(eng, job.device,
+                                           transport=xchg if args.backend == "nccl" or xchg == "ipc" else "engine")
             if world == 1:
                 parallelism = "single GPU"
             elif P == 1:
@@ -240,168 +383,178 @@ def main():
             workload = (f"C4: R-MAT (.57,.19,.19,.05) edge factor 16, symmetrized, {V} nodes, {K} messages "
                         "broadcast in round 0 at seeded uniform nodes, sync on, no partitions; graph built "
                         "in HBM by the on-device generator; one step = one episode to quiescence")
+        return dict(runner=runner, V=V, K=K, seed=seed, topo=topo, gen=gen, E=E, eng=eng, engs=engs,
+                    parallelism=parallelism, scaling=scaling, workload=workload)
 
-        return runner, V, K, seed, topo, gen, E, eng, engs, parallelism, scaling, workload
+    def close_all(b):
+        if b is not None:
+            for e in b["engs"]:
+                e.close()
+        torch.cuda.synchronize()
 
     # N > 1 exchange: "auto" = the device-driven one (no host wait, captured rounds)
-    # if every rank can map its peers and two validation rounds through it finish
-    # (their global counters equal O2's where tests/golden/bench_c2.json has them),
-    # else the engine's RCCL send/recv, rebuilt from scratch on every rank
+    # if every rank can map its peers and one whole episode through it equals O2
+    # (every round's global counters, C2: tests/golden/bench_c2.json), else the
+    # engine's RCCL send/recv, rebuilt from scratch on every rank
     xchg = args.xchg
-    xchg_note = None
+    notes = []
+    validation = None
     if xchg == "auto":
         xchg = "ipc" if (world > 1 and (cfg == "C2" or args.parts > 1)) else "engine"
     if args.xchg == "auto" and xchg == "ipc":
-        ok, built, got = 1, None, [0, 0]
-        try:  # (every rank makes the same collective calls whatever fails)
-            built = setup("ipc")
-            rn, V0, K0, seed0, _, _, _, _, engs0, _, _, _ = built
-            arr0 = injection_arrays(uniform_injections(V0, K0, seed0))
-            for e in engs0:
-                e.reset()
-                inject(e, arr0)
-            got = [s["new_bits"] for s in rn.step(2, reduce=False)]
-            if os.environ.get("GG_BENCH_IPC_FAIL") == str(rank):  # test hook: the fallback path
-                raise RuntimeError("GG_BENCH_IPC_FAIL")
-        except Exception as exc:  # noqa: BLE001 — any failure: every rank falls back
-            ok = 0
-            print(f"bench: rank {rank}: device-driven exchange unavailable ({exc!r}); falling back", file=sys.stderr)
-        v = allreduce_i64([1 - ok] + [int(x) for x in got])
-        ok = v[0] == 0 and sum(v[1:]) > 0
-        gold_p = os.path.join(REPO, "tests", "golden", "bench_c2.json")
-        if ok and cfg == "C2" and os.path.exists(gold_p):
-            g = next((g for g in json.load(open(gold_p))["runs"].values()
-                      if g["nodes"] == built[1] and g["lanes"] == built[2]), None)
-            if g is not None and v[1:] != [g["rounds"][0]["new_bits"], g["rounds"][1]["new_bits"]]:
-                ok = False
-                if rank == 0:
-                    print(f"bench: device-driven validation rounds differ from O2: {v[1:]}; falling back",
-                          file=sys.stderr)
-        if ok:
-            runner, V, K, seed, topo, gen, E, eng, engs, parallelism, scaling, workload = built
-        else:
-            if built is not None:
-                for e in built[8]:
-                    e.close()
-            built = None
-            torch.cuda.synchronize()
+        built, validation = validate_ipc(job, args, setup)
+        if built is None:
             xchg = "engine"
-            xchg_note = "device-driven exchange failed its setup or validation on some rank: fell back to --xchg engine"
-            runner, V, K, seed, topo, gen, E, eng, engs, parallelism, scaling, workload = setup(xchg)
+            notes.append(f"device-driven exchange failed its validation ({validation['result']}): "
+                         "every rank rebuilt on --xchg engine")
+            b = setup(xchg)
+        else:
+            b = built
     else:
-        runner, V, K, seed, topo, gen, E, eng, engs, parallelism, scaling, workload = setup(xchg)
+        b = setup(xchg)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
-    inj = uniform_injections(V, K, seed)
+    inj = uniform_injections(b["V"], b["K"], b["seed"])
     inj_arr = injection_arrays(inj)  # converted once, outside the timed loop
 
-    def run_rounds(n):
-        if runner is None:
-            return eng.step(n, raw=True)  # dicts built after the timed region
-        return runner.step(n, reduce=False)
+    def quiescence(bb) -> int:
+        for e in bb["engs"]:
+            e.reset()
+            inject(e, inj_arr)
+        R = 0
+        while True:
+            rn = bb["runner"]
+            st = rn.step(1, reduce=False)[0] if rn else bb["eng"].step(1)[0]
+            if os.environ.get("GG_BENCH_DEBUG") and R < 3:
+                print(f"bench: rank {rank} quiescence round {R} new_bits {st['new_bits']}", file=sys.stderr, flush=True)
+            nb = job.allreduce([st["new_bits"]])[0]
+            R += 1
+            if nb == 0 and R > 1:
+                return R
+            if R > 400:
+                raise RuntimeError("no quiescence within 400 rounds")
 
-    # warmup 0: the quiescence round R from per-round global counts
-    for e in engs:
-        e.reset()
-        inject(e, inj_arr)
-    R = 0
-    while True:
-        st = runner.step(1, reduce=False)[0] if runner else eng.step(1)[0]
-        nb = st["new_bits"]
-        if world > 1:  # sum over the ranks
-            nb = allreduce_i64([nb])[0]
-        R += 1
-        if nb == 0 and R > 1:
-            break
-        if R > 400:
-            raise RuntimeError("no quiescence within 400 rounds")
+    R = quiescence(b)  # warmup 0: the quiescence round R from per-round global counts
     torch.cuda.synchronize()
     # after the first episode: the engine's second set buffer (double-buffered
     # rounds) is allocated at its first step
-    hbm_bytes = free0 - torch.cuda.mem_get_info(local)[0]
+    hbm_bytes = free0 - job.free_bytes()
 
     event_ms = []
 
-    def episode():
-        for e in engs:
+    def episode(bb):
+        for e in bb["engs"]:
             e.reset()
             inject(e, inj_arr)
-        st = run_rounds(R)
-        if runner is None:
-            event_ms.append(eng.step_device_ms())
-        return st
-
-    def quiescence_rounds(arrs):  # single engine: rounds to the round after the last delivery
-        eng.reset()
-        inject(eng, arrs)
-        n = 0
-        while True:
-            n += 1
-            if eng.step(1)[0]["new_bits"] == 0 and n > 1:
-                return n
-            if n > 400:
-                raise RuntimeError("no quiescence within 400 rounds")
+        rn = bb["runner"]
+        if rn is None:
+            st = bb["eng"].step(R, raw=True)
+            event_ms.append(bb["eng"].step_device_ms())
+            return st
+        return rn.step(R, reduce=False)
 
     for _ in range(max(0, args.warmup - 1)):
-        episode()
+        wst = episode(b)
+        if os.environ.get("GG_BENCH_DEBUG") and b["runner"] is not None:
+            print(f"bench: rank {rank} warmup episode new_bits {[x['new_bits'] for x in wst][:6]}",
+                  file=sys.stderr, flush=True)
+            w2 = episode(b)
+            print(f"bench: rank {rank} second replay new_bits {[x['new_bits'] for x in w2][:4]}",
+                  file=sys.stderr, flush=True)
+            for e in b["engs"]:
+                e.reset()
+                inject(e, inj_arr)
+            w3 = [b["runner"].step(1, reduce=False)[0] for _ in range(R)]
+            print(f"bench: rank {rank} single steps new_bits {[x['new_bits'] for x in w3][:4]}",
+                  file=sys.stderr, flush=True)
+            for e in b["engs"]:
+                e.reset()
+                inject(e, inj_arr)
+            w4 = b["runner"].step(5, reduce=False) + b["runner"].step(R - 5, reduce=False)
+            print(f"bench: rank {rank} 5 + rest new_bits {[x['new_bits'] for x in w4][:7]}",
+                  file=sys.stderr, flush=True)
     event_ms.clear()
 
     # one engine per rank (no vertex parts): the K episodes go back to back through
     # gg_run_episodes — each still a reset, the same client broadcasts and R rounds,
     # its counters read back and checked like the loop's — with one host wait, so
-    # no host round trip idles the GPU between episodes (the loop of synchronous
-    # reset/broadcast/step calls is timed beside it: per_call_ms_per_step)
-    # (vertex parts: gg_dist_run_episodes over the device-driven exchange, every rank alike)
-    dist_pipe = (runner is not None and getattr(runner, "can_run_episodes", False)
-                 and os.environ.get("GG_BENCH_DIST_EPISODES", "1") != "0")
-    pipelined = runner is None or dist_pipe
-    if pipelined and args.warmup > 0:  # (its counter ring is allocated here)
-        eng.reset()
-        inject(eng, inj_arr)
-        if dist_pipe:
-            fail = 0
-            try:
-                runner.run_episodes(R, args.steps)
-            except Exception as exc:  # noqa: BLE001 — every rank agrees below, then falls back
-                fail = 1
-                print(f"bench: rank {rank}: gg_dist_run_episodes failed ({exc!r}); timing synchronous calls",
-                      file=sys.stderr)
-            if allreduce_i64([fail])[0]:
-                dist_pipe = False
-                pipelined = False
+    # no host round trip idles the GPU between episodes; vertex parts over the
+    # device-driven exchange: gg_dist_run_episodes, every rank alike. A failure there
+    # (every rank agrees) rebuilds every rank on the engine exchange.
+    def mode_of(bb):
+        rn = bb["runner"]
+        if rn is None:
+            return "single"
+        if getattr(rn, "can_run_episodes", False) and os.environ.get("GG_BENCH_DIST_EPISODES", "1") != "0":
+            return "dist_pipe"
+        return "sync"
+
+    def timed(bb, mode, warm: bool):
+        """(elapsed s, this rank's stats per episode); raises on an exchange failure."""
+        eng, rn = bb["eng"], bb["runner"]
+        if warm and mode != "sync" and args.warmup > 0:  # (its counter ring is allocated here)
+            eng.reset()
+            inject(eng, inj_arr)
+            if mode == "dist_pipe":
+                if os.environ.get("GG_BENCH_EPISODES_FAIL") == str(rank):  # test hook: the rebuild path
+                    raise RuntimeError("GG_BENCH_EPISODES_FAIL")
+                rn.run_episodes(R, args.steps)
+            else:
+                eng.run_episodes(R, args.steps, raw=True)
+        job.barrier()
+        t0 = time.perf_counter()
+        if mode == "dist_pipe":
+            eng.reset()
+            inject(eng, inj_arr)
+            local = rn.run_episodes(R, args.steps)
+        elif mode == "single":
+            eng.reset()
+            inject(eng, inj_arr)
+            arr = eng.run_episodes(R, args.steps, raw=True)
         else:
-            eng.run_episodes(R, args.steps, raw=True)
-    barrier()
-    t0 = time.perf_counter()
-    local_stats = []
-    if dist_pipe:
-        eng.reset()
-        inject(eng, inj_arr)
-        local_stats = runner.run_episodes(R, args.steps)
-    elif pipelined:
-        eng.reset()
-        inject(eng, inj_arr)
-        arr = eng.run_episodes(R, args.steps, raw=True)
-    else:
-        for _ in range(args.steps):
-            local_stats.append(episode())
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+            local = [episode(bb) for _ in range(args.steps)]
+        job.barrier()
+        el = time.perf_counter() - t0
+        if mode == "single":
+            local = [[arr[k * R + i] for i in range(R)] for k in range(args.steps)]
+        return el, local
+
+    mode = mode_of(b)
+    fail = None
+    try:
+        elapsed, local_stats = timed(b, mode, True)
+    except Exception as exc:  # noqa: BLE001 — every rank agrees below
+        fail = exc
+        print(f"bench: rank {rank}: timed {mode} run failed ({exc!r})", file=sys.stderr)
+    if not job.agree(fail is None):
+        if mode == "single" or xchg == "engine":
+            raise SystemExit(f"bench: the timed run failed on some rank ({fail!r})")
+        # the device-driven exchange failed after its validation: every rank
+        # closes its engines and rebuilds on the engine exchange (ADVICE r4: the
+        # IPC runner cannot be reused — its error word stays set)
+        close_all(b)
+        xchg = "engine"
+        notes.append(f"the timed {mode} run failed on some rank: every rank rebuilt on --xchg engine")
+        b = setup(xchg)
+        R2 = quiescence(b)
+        if R2 != R:
+            raise SystemExit(f"bench: the rebuilt job quiesces after {R2} rounds, not {R}")
+        mode = mode_of(b)
+        elapsed, local_stats = timed(b, mode, False)
+    runner, eng, engs, V, K, seed = b["runner"], b["eng"], b["engs"], b["V"], b["K"], b["seed"]
+    pipelined = mode in ("single", "dist_pipe")
     per_call_ms = None
     if pipelined:
-        if not dist_pipe:
-            local_stats = [[arr[k * R + i] for i in range(R)] for k in range(args.steps)]
         ev_pipe = [eng.step_device_ms()] * args.steps
-        barrier()
+        job.barrier()
         c0 = time.perf_counter()
         for _ in range(args.steps):
-            episode()
-        barrier()
+            episode(b)
+        job.barrier()
         per_call_ms = (time.perf_counter() - c0) / args.steps * 1e3
         event_ms[:] = ev_pipe
         if world > 1:
-            per_call_ms = float(allreduce_i64([int(per_call_ms * 1e6)], dist.ReduceOp.MAX)[0]) / 1e6
+            per_call_ms = float(job.allreduce([int(per_call_ms * 1e6)], "max")[0]) / 1e6
 
     # fresh episodes (N = 1): every step broadcasts a different seeded value set, as
     # in a workload whose clients keep sending new values: the injections and each
@@ -411,7 +564,18 @@ def main():
     fresh = None
     if world == 1 and args.fresh_sets > 0:
         sets = [injection_arrays(uniform_injections(V, K, seed + 7919 * (i + 1))) for i in range(args.fresh_sets)]
-        rounds_of = [quiescence_rounds(a) for a in sets]
+
+        def q_rounds(arrs):
+            eng.reset()
+            inject(eng, arrs)
+            n = 0
+            while True:
+                n += 1
+                if eng.step(1)[0]["new_bits"] == 0 and n > 1:
+                    return n
+                if n > 400:
+                    raise RuntimeError("no quiescence within 400 rounds")
+        rounds_of = [q_rounds(a) for a in sets]
         n_fresh = max(args.fresh_sets, min(args.steps, 2 * args.fresh_sets))
         torch.cuda.synchronize()
         f0 = time.perf_counter()
@@ -429,49 +593,45 @@ def main():
                  "note": "each step uploads its own injection pairs and round offsets, then replays the "
                          "captured launch sequence, which reads both from device memory (the timed `value` "
                          "repeats one set, whose pairs stay resident)"}
-    if runner is None:
+    if mode == "single":
         local_stats = [[stats_dict(a[i]) for i in range(R)] for a in local_stats]
     if world > 1:
-        elapsed = float(allreduce_i64([int(elapsed * 1e9)], dist.ReduceOp.MAX)[0]) / 1e9
-        per_ep = [reduce_counts(s, allreduce_i64, COUNT_FIELDS) for s in local_stats]
+        elapsed = float(job.allreduce([int(elapsed * 1e9)], "max")[0]) / 1e9
+        per_ep = [reduce_counts(s, job, COUNT_FIELDS) for s in local_stats]
     else:
         per_ep = local_stats
     deliveries = sum(s["new_bits"] for ep in per_ep for s in ep)
     msgs = sum(s["fwd_sent"] + s["pushes"] + s["acks"] + s["reads"] + s["read_oks"] for s in per_ep[-1])
+    if os.environ.get("GG_BENCH_DEBUG"):
+        print(f"bench: rank {rank} R {R} rounds {[len(ep) for ep in local_stats]} new_bits of episode 0 "
+              f"{[x['new_bits'] for x in local_stats[0]]}", file=sys.stderr, flush=True)
+        print(f"bench: rank {rank} mode {mode}: local round 0 of the episodes "
+              f"{[{f: ep[0][f] for f in ('new_bits', 'fwd_sent', 'pushes')} for ep in local_stats]}; "
+              f"global {[{f: ep[0][f] for f in ('new_bits', 'fwd_sent', 'pushes')} for ep in per_ep]}",
+              file=sys.stderr, flush=True)
 
-    # roofline of the dominant kernel: per-kind device times (first block start
-    # to last block end of each launch, stamped by the kernels) and the bytes
-    # each launch had to move (counted by the kernels); this rank's
     dinfo = None
     if runner is not None:
         dinfo = eng.dist_info()
+        dinfo.update(peer_info(job))
         n_own = dinfo["owned"]
-        if topo is not None:
+        if b["topo"] is not None:
             owned = eng.dist_owned().astype(np.int64)
-            E_own = int((topo.row_ptr[owned + 1] - topo.row_ptr[owned]).sum())
+            E_own = int((b["topo"].row_ptr[owned + 1] - b["topo"].row_ptr[owned]).sum())
         else:
-            E_own = E  # generate() returned this rank's adjacency entries
+            E_own = b["E"]  # generate() returned this rank's adjacency entries
     else:
-        n_own, E_own = V, E
+        n_own, E_own = V, b["E"]
     nwp = next_pow2(K // 64 // (world // args.parts * len(engs) if cfg == "C4" else 1))
     rounds_local = [s for ep in local_stats for s in ep]
-    kinds = {}
-    for kind, name in KERNELS.items():
-        ms = sum(s[kind + "_ms"] for s in rounds_local)
-        by = sum(s[kind + "_bytes"] for s in rounds_local)
-        if kind == "stream":  # one of the two per lean round (double-buffered rounds)
-            name = "expand_stream / expand_stream_db"
-        kinds[kind] = {"kernel": name, "launches": len(rounds_local), "total_ms": ms, "bytes": by,
-                       "avg_launch_ms": ms / len(rounds_local),
-                       "GBps": by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0}
-    dom = max(kinds, key=lambda k: kinds[k]["total_ms"])
-    D = kinds[dom]
-    achieved = D["GBps"]
     shape = {"config": cfg, "nodes": V // world if cfg == "C2" else V, "lanes": K, "world": world,
              "parts": args.parts if cfg == "C4" else world, "halves": len(engs)}
-    traffic, traffic_src = pmc_traffic(dom, shape)
-    round_ms = sum(s["kernel_ms"] for s in rounds_local)
-    round_bytes = sum(s["prep_bytes"] + s["expand_bytes"] + s["stream_bytes"] for s in rounds_local)
+    roof = roofline(rounds_local, nwp, n_own, E_own, shape)
+    roof["event_ms_per_step"] = (sum(event_ms) / len(event_ms)) if event_ms else None
+    roof["per_call_ms_per_step"] = per_call_ms
+    roof["stamp_ms_per_step"] = sum(s["kernel_ms"] for s in rounds_local) / args.steps
+    roof["timing"] += ("; cross-check: HIP events on the engine stream around episodes 1..K-1 of the "
+                       "pipelined run (event_ms_per_step)")
     xbytes = None
     if runner is not None:  # payload bytes this rank sent per round (mean over the timed rounds)
         xbytes = sum(s["sent_bytes"] for s in rounds_local) / len(rounds_local)
@@ -480,148 +640,437 @@ def main():
     check = None
     if world > 1 and not args.no_check:
         bad = 0
+        close_all(b)  # free every rank's shard before rank 0 builds the whole graph
         if rank == 0:
-            for e in engs:
-                e.close()  # free this rank's shard before building the whole graph
             ref = Engine(V, K, seed=seed, enable_sync=True, device=local)
-            if gen is None:
-                ref.topology(topo)
+            if b["gen"] is None:
+                ref.topology(b["topo"])
             else:
-                ref.generate(**gen)
+                ref.generate(**b["gen"])
             inject(ref, inj_arr)
             want = ref.step(R)
             ref.close()
-            diffs = [f"round {a['round']} {f}: sharded {a[f]} != single {b[f]}"
-                     for a, b in zip(per_ep[-1], want) for f in COUNT_FIELDS if a[f] != b[f]]
+            diffs = count_diffs(per_ep[-1], want, COUNT_FIELDS, "sharded", "single")
             bad = len(diffs)
             if diffs:
-                print("bench: sharded run differs from the single engine:", diffs[:8], file=sys.stderr)
-        bad = allreduce_i64([bad])[0]
+                print("bench: sharded run differs from the single engine:", diffs, file=sys.stderr)
+        bad = job.allreduce([bad])[0]
         check = "every round's global counters equal one unsharded engine" if bad == 0 else "FAILED"
         if bad:
-            if world > 1:
-                dist.destroy_process_group()
+            job.close()
             raise SystemExit(1)
 
     # every timed episode's global counters against the CPU oracle O2's run of the
     # same workload (tests/golden/bench_c2.json, made by make_bench_golden.py for
     # 2^20 x N nodes); a differing episode fails the run
     oracle_check = None
-    gold_p = os.path.join(REPO, "tests", "golden", "bench_c2.json")
-    if cfg == "C2" and K == 1024 and seed == BASE_SEED + 2 and os.path.exists(gold_p):
-        gold = next((g for g in json.load(open(gold_p))["runs"].values() if g["nodes"] == V and g["lanes"] == K),
-                    None)
+    if cfg == "C2" and K == 1024 and seed == BASE_SEED + 2:
+        gold = gold_c2(V, K)
         if gold is not None:
             want = gold["rounds"]
-            M = (1 << 64) - 1
-            diffs = [f"episode {k} round {j} {f}: {ep[j][f] & M} != O2 {want[j][f] & M}"
-                     for k, ep in enumerate(per_ep) for j in range(min(len(ep), len(want))) for f in COUNT_FIELDS
-                     if (ep[j][f] & M) != (want[j][f] & M)]
+            diffs = [d for k, ep in enumerate(per_ep) for d in
+                     count_diffs(ep, want[:len(ep)], COUNT_FIELDS, f"episode {k}", "O2", 2)]
             if len(want) != R:
                 diffs.append(f"quiescence round count {R} != O2 {len(want)}")
             if diffs:
                 if rank == 0:
                     print("bench: counters differ from O2:", diffs[:8], file=sys.stderr)
-                if world > 1:
-                    dist.destroy_process_group()
+                job.close()
                 raise SystemExit(1)
             oracle_check = (f"all {len(per_ep)} timed episodes: every round's global counters and delivery hash "
                             f"equal O2's run of this workload (tests/golden/bench_c2.json, {V} nodes)")
 
-    if rank == 0:
-        value = deliveries / elapsed
-        out = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "deliveries/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": scaling,
-            "vs_baseline": None,
-            "dtype": "u64",
-            "data": f"synthetic (seeded {'tree4' if cfg == 'C2' else 'R-MAT'} topology, seeded client broadcasts)",
-            "config": {
-                "workload": workload,
-                "nodes": V, "edges": E, "lanes": K, "rounds_per_step": R,
-                "deliveries_per_step": deliveries // args.steps,
-                "inter_node_msgs_per_step": msgs,
-                "msgs_per_op": msgs / K,
-                "parallelism": parallelism,
-                "exchange": (runner.transport if runner is not None else
-                             ("none: lane groups never exchange; one all_reduce of the counters "
-                              "after the timed episodes" if world > 1 else None)),
-                "exchange_note": xchg_note,
-                "lane_groups": world // args.parts if cfg == "C4" else 1,
-                "vertex_parts": args.parts if cfg == "C4" else world,
-                "exchange_bytes_per_round_rank0": xbytes,
-                "shard": dinfo,
-                "hbm_bytes_rank0": hbm_bytes,
-                "setup_s_rank0": setup_s,
-                "check": check,
-                "oracle_check": oracle_check,
-                "timed_loop": (("gg_dist_run_episodes" if dist_pipe else "gg_run_episodes") + ": the K episodes (each a reset, the same client broadcasts and "
-                               "R rounds, its counters read back) queued back to back, one host wait; "
-                               "roofline.per_call_ms_per_step times the same episodes as K synchronous "
-                               "reset/broadcast/step calls" if pipelined else
-                               "one synchronous reset/broadcast/step call sequence per episode"),
-                "fresh_injections": fresh,
-            },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": D["kernel"],
-                "kind": dom,
-                "kind_kernels": "every kernel stamping this kind per round: " + ", ".join(KIND_KERNELS[dom]),
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": D["bytes"] / D["launches"],
-                "avg_launch_ms": D["avg_launch_ms"],
-                "launches": D["launches"],
-                "dense_bytes_per_round": dense_bytes_per_round(n_own, E_own, nwp),
-                "timing": "per launch: device clock (s_memrealtime) from the first block start to the last "
-                          "block end of that kernel, stamped by every block (no-op launches included, as in "
-                          "rocprofv3's average); cross-check: HIP events around each step's launch sequence "
-                          "on the engine stream",
-                "kernels": {k: dict(d) for k, d in kinds.items()},
-                "round_GBps": round_bytes / (round_ms * 1e-3) / 1e9 if round_ms > 0 else 0.0,
-                "event_ms_per_step": (sum(event_ms) / len(event_ms)) if event_ms else None,
-                "per_call_ms_per_step": per_call_ms,
-                "stamp_ms_per_step": round_ms / args.steps,
-            },
-            "cpu_baseline": None,
+    close_all(b)
+    info = {"xchg": xchg, "validation": validation}
+    if rank != 0:
+        return None, info
+    value = deliveries / elapsed
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "deliveries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": b["scaling"],
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": f"synthetic (seeded {'tree4' if cfg == 'C2' else 'R-MAT'} topology, seeded client broadcasts)",
+        "config": {
+            "workload": b["workload"],
+            "nodes": V, "edges": b["E"], "lanes": K, "rounds_per_step": R,
+            "deliveries_per_step": deliveries // args.steps,
+            "inter_node_msgs_per_step": msgs,
+            "msgs_per_op": msgs / K,
+            "parallelism": b["parallelism"],
+            "exchange": (runner.transport if runner is not None else
+                         ("none: lane groups never exchange; one all_reduce of the counters "
+                          "after the timed episodes" if world > 1 else None)),
+            "exchange_note": "; ".join(notes) or None,
+            "exchange_validation": validation,
+            "lane_groups": world // args.parts if cfg == "C4" else 1,
+            "vertex_parts": args.parts if cfg == "C4" else world,
+            "exchange_bytes_per_round_rank0": xbytes,
+            "shard": dinfo,
+            "hbm_bytes_rank0": hbm_bytes,
+            "setup_s_rank0": setup_s,
+            "check": check,
+            "oracle_check": oracle_check,
+            "timed_loop": ({"single": "gg_run_episodes", "dist_pipe": "gg_dist_run_episodes"}.get(mode, "") +
+                           ": the K episodes (each a reset, the same client broadcasts and R rounds, its counters "
+                           "read back) queued back to back, one host wait; roofline.per_call_ms_per_step times the "
+                           "same episodes as K synchronous reset/broadcast/step calls" if pipelined else
+                           "one synchronous reset/broadcast/step call sequence per episode"),
+            "fresh_injections": fresh,
+        },
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    if world == 1 and not args.no_cpu_baseline and os.path.exists(CPU_LIB):
+        out["cpu_baseline"] = cpu_baseline(cfg, b["topo"], inj, V, K, seed, R)
+    return out, info
+
+
+def validate_ipc(job: Job, args, setup):
+    """Build the job on the device-driven exchange and run one whole episode
+    through it (C2: every round — at least 4, so the consumed-flag waits and the
+    reuse of each parity's buffers run — against O2's run of the same workload;
+    --config C4: 6 rounds that must finish). Returns (the built job or None,
+    a record of the validation). Every rank makes the same collective calls
+    whatever fails. Test hook GG_BENCH_IPC_FAIL=rank[:round]: that rank stops
+    exchanging after `round` rounds (default 0: at once) — its peers' waits
+    run out (GG_EIO) — and reports a failure."""
+    from ggamd.engine import COUNT_FIELDS
+    from ggamd.workload import inject, injection_arrays, uniform_injections
+    hook = os.environ.get("GG_BENCH_IPC_FAIL")
+    f_rank, f_round = (None, None)
+    if hook:
+        p = hook.split(":")
+        f_rank, f_round = int(p[0]), int(p[1]) if len(p) > 1 else 0
+    ok, built, local, gold, err = True, None, None, None, None
+    rounds = 6
+    try:
+        built = setup("ipc")
+        if args.config == "C2":
+            gold = gold_c2(built["V"], built["K"])
+            if gold is not None:
+                rounds = len(gold["rounds"])
+        arr = injection_arrays(uniform_injections(built["V"], built["K"], built["seed"]))
+        for e in built["engs"]:
+            e.reset()
+            inject(e, arr)
+        if os.environ.get("GG_BENCH_VAL_ROUNDS"):  # (debug)
+            rounds = int(os.environ["GG_BENCH_VAL_ROUNDS"])
+            gold = None
+        n = rounds if job.rank != f_rank else min(rounds, f_round)
+        local = built["runner"].step(n, reduce=False) if n else []
+        if job.rank == f_rank:
+            raise RuntimeError(f"GG_BENCH_IPC_FAIL: stopped after {n} rounds")
+    except Exception as exc:  # noqa: BLE001 — every rank falls back together
+        ok = False
+        err = repr(exc)
+        print(f"bench: rank {job.rank}: device-driven exchange failed its validation ({exc!r})", file=sys.stderr)
+    rec = {"rounds": rounds, "against": "tests/golden/bench_c2.json (O2), every counter and the delivery hash"
+           if gold is not None else "completion only (no golden run of this shape)"}
+    if job.agree(ok):
+        glob = reduce_counts(local, job, COUNT_FIELDS)
+        if os.environ.get("GG_BENCH_DEBUG"):
+            print(f"bench: rank {job.rank} validation local new_bits {[x['new_bits'] for x in local][:6]}",
+                  file=sys.stderr, flush=True)
+        diffs = count_diffs(glob, gold["rounds"], COUNT_FIELDS, "ipc", "O2") if gold is not None else []
+        if not diffs:
+            rec["result"] = "passed"
+            return built, rec
+        rec["result"] = "counters differ from O2: " + "; ".join(diffs[:4])
+        if job.rank == 0:
+            print(f"bench: device-driven validation episode differs from O2: {diffs}", file=sys.stderr)
+    else:
+        rec["result"] = f"failed on some rank (rank {job.rank}: {err})" if err else "failed on some rank"
+    if built is not None:
+        for e in built["engs"]:
+            e.close()
+    job.torch.cuda.synchronize()
+    return None, rec
+
+
+# ---------------------------------------------------------------------------
+# legs: C4 (10^8 R-MAT, W = 4096, strong scaling) and C5 (2^30 grid + links, W = 64)
+
+def run_leg(job: Job, args, name: str, xchg_pref: str) -> dict:
+    t0 = time.perf_counter()
+    try:
+        rec = leg(job, args, name, xchg_pref)
+    except LegAbort as exc:
+        rec = {"config": name, "error": str(exc)}
+    rec["leg_s"] = time.perf_counter() - t0
+    return rec
+
+
+class LegAbort(RuntimeError):
+    pass
+
+
+def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
+    """One leg; every phase ends in an agreement (all ranks ok, or LegAbort on
+    every rank), so no rank waits in a collective another rank skipped."""
+    torch, world, rank, local = job.torch, job.world, job.rank, job.local
+    from ggamd.checks import components, episode_failures, expected_from_components
+    from ggamd.engine import COUNT_FIELDS, Engine, stats_dict
+    from ggamd.workload import BASE_SEED, inject, injection_arrays, uniform_injections
+
+    if name == "C4":
+        V = args.c4_nodes or 100_000_000
+        K = 4096
+        seed = BASE_SEED + 4
+        gen = dict(kind="rmat", n=V, k=16, seed=seed, a=0.57, b=0.19, c=0.19)
+        workload = (f"C4: R-MAT (.57,.19,.19,.05) edge factor 16, symmetrized, {V} nodes, {K} messages broadcast "
+                    "in round 0 at seeded uniform nodes, sync on, no partitions; graph built in HBM by the "
+                    "on-device generator; strong scaling (the same graph at every N)")
+    else:
+        side = args.c5_side or 32768
+        V = side * side
+        K = 64
+        seed = BASE_SEED + 5
+        gen = dict(kind="grid_links", n=side, seed=seed)
+        workload = (f"C5: {side}x{side} 4-neighbour grid + one seeded long-range link per node, symmetrized, "
+                    f"{V} nodes, {K} messages broadcast in round 0 at seeded uniform nodes, sync on, no "
+                    "partitions; graph built in HBM by the on-device generator (each rank its own part)")
+    P = args.leg_parts or world
+    if world % P:
+        raise LegAbort(f"--leg-parts {P} does not divide the world size {world}")
+    L = world // P
+    halves = 2 if (name == "C4" and P > 1 and K // 64 // L >= 2 and args.leg_halves != 1) else 1
+    inj = uniform_injections(V, K, seed)
+    inj_arr = injection_arrays(inj)
+    log = (lambda *a: print(f"bench[{name}]:", *a, file=sys.stderr, flush=True)) if rank == 0 else (lambda *a: None)
+
+    def phase(fn, what):
+        ok, res, err = True, None, None
+        try:
+            res = fn()
+        except Exception as exc:  # noqa: BLE001
+            ok, err = False, exc
+            print(f"bench[{name}]: rank {rank}: {what} failed ({exc!r})", file=sys.stderr, flush=True)
+        if not job.agree(ok):
+            raise LegAbort(f"{what} failed on some rank" + (f" (rank {rank}: {err!r})" if err else ""))
+        return res
+
+    free0 = job.free_bytes()
+    tb = time.perf_counter()
+    engs = []
+
+    def build_engines():
+        if halves == 2:
+            g, q = divmod(rank, P)
+            for h in range(2):
+                engs.append(Engine(V, K, seed=seed, enable_sync=True, device=local, rank=(2 * g + h) * P + q,
+                                   world=2 * world, lane_groups=2 * L))
+        else:
+            engs.append(Engine(V, K, seed=seed, enable_sync=True, device=local, rank=rank, world=world,
+                               lane_groups=L))
+        E = 0
+        for e in engs:
+            E = e.generate(**gen)  # this rank's rows (gossip_gen.h); halves: the same rows twice
+        return E
+
+    def close_engs():
+        for e in engs:
+            e.close()
+        engs.clear()
+        torch.cuda.synchronize()
+
+    def build_runner(xchg):
+        if P == 1 and L == 1:
+            return None
+        if halves == 2:
+            from ggamd.dist import HalvesRunner
+            return HalvesRunner(engs, job.device, transport=xchg)
+        from ggamd.dist import ShardedRunner
+        return ShardedRunner(engs[0], job.device,
+                             transport=xchg if (args.backend == "nccl" or xchg == "ipc") else "engine")
+
+    try:
+        E_local = phase(build_engines, "engine build")
+        xchg = xchg_pref if P > 1 else "none"
+        runner = phase(lambda: build_runner(xchg), f"exchange setup ({xchg})")
+        setup_s = time.perf_counter() - tb
+        log(f"built in {setup_s:.1f} s: {len(engs)} engine(s) per GPU, P={P} L={L}, exchange {xchg}")
+        eng = engs[0]
+
+        def reset_all():
+            for e in engs:
+                e.reset()
+                inject(e, inj_arr)
+
+        # checking episode: one round at a time to quiescence (global counters)
+        def check_round():
+            if runner is None:
+                return eng.step(1)[0]
+            return runner.step(1, reduce=False)[0]
+
+        reset_all()
+        check = []
+        while True:
+            ok, st = True, None
+            try:
+                st = check_round()
+            except Exception as exc:  # noqa: BLE001
+                ok = False
+                print(f"bench[{name}]: rank {rank}: round {len(check)} failed ({exc!r})", file=sys.stderr)
+            vals = [0 if ok else 1] + ([(st[f] & M64) - (1 << 64) if (st[f] & M64) >= (1 << 63) else st[f]
+                                        for f in COUNT_FIELDS] if ok else [0] * len(COUNT_FIELDS))
+            tot = job.allreduce(vals)
+            if tot[0]:
+                raise LegAbort(f"checking episode: round {len(check)} failed on some rank")
+            g = dict(st)
+            for j, f in enumerate(COUNT_FIELDS):
+                g[f] = tot[1 + j] & M64
+            check.append(g)
+            if (g["new_bits"] == 0 and len(check) > 1) or len(check) >= 120:
+                break
+        R = len(check)
+        if check[-1]["new_bits"]:
+            raise LegAbort(f"no quiescence within {R} rounds")
+        hbm = job.gather_i64(free0 - job.free_bytes())
+        log(f"checking episode: {R} rounds, {sum(s['new_bits'] for s in check)} deliveries")
+
+        # timed episodes
+        event_ms = None
+
+        def timed():
+            nonlocal event_ms
+            job.barrier()
+            t0 = time.perf_counter()
+            if runner is None:
+                reset_all()
+                arr = eng.run_episodes(R, args.leg_steps, raw=True)
+                eps = [[stats_dict(arr[k * R + i]) for i in range(R)] for k in range(args.leg_steps)]
+                event_ms = eng.step_device_ms()
+            elif getattr(runner, "can_run_episodes", False):
+                reset_all()
+                eps = runner.run_episodes(R, args.leg_steps)
+            else:
+                eps = []
+                for _ in range(args.leg_steps):
+                    reset_all()
+                    eps.append(runner.step(R, reduce=False))
+            job.barrier()
+            return time.perf_counter() - t0, eps
+
+        res = None
+        try:
+            res = timed()
+        except Exception as exc:  # noqa: BLE001
+            print(f"bench[{name}]: rank {rank}: timed episodes failed ({exc!r})", file=sys.stderr, flush=True)
+        note = None
+        if not job.agree(res is not None):
+            if xchg != "ipc":
+                raise LegAbort("timed episodes failed on some rank")
+            # the device-driven exchange failed: rebuild every rank on the engine exchange
+            close_engs()
+            phase(build_engines, "engine rebuild")
+            xchg = "engine"
+            runner = phase(lambda: build_runner(xchg), "exchange setup (engine)")
+            eng = engs[0]
+            note = "the device-driven exchange failed in the timed episodes: rebuilt on the engine exchange"
+            res = phase(timed, "timed episodes (engine exchange)")
+        elapsed, eps_local = res
+        elapsed = float(job.allreduce([int(elapsed * 1e9)], "max")[0]) / 1e9
+        eps = [reduce_counts(ep, job, COUNT_FIELDS) for ep in eps_local] if world > 1 else eps_local
+        deliveries = sum(s["new_bits"] for ep in eps for s in ep)
+        fails = []
+        for k, ep in enumerate(eps):
+            d = count_diffs(ep, check, COUNT_FIELDS, f"timed episode {k}", "checking episode", 3)
+            fails += d
+        rounds_local = [s for ep in eps_local for s in ep]
+        sent = sum(s["sent_bytes"] for s in rounds_local) / max(1, len(rounds_local))
+        dinfo = eng.dist_info() if world > 1 else None
+        n_own = dinfo["owned"] if dinfo else V
+        nwp = next_pow2(K // 64 // (L * halves))
+        shape = {"config": name, "nodes": V, "lanes": K, "world": world, "parts": P, "halves": halves}
+        roof = roofline(rounds_local, nwp, n_own, E_local, shape) if rank == 0 else None
+        if roof is not None:
+            roof["event_ms_per_step"] = event_ms
+            roof["stamp_ms_per_step"] = sum(s["kernel_ms"] for s in rounds_local) / args.leg_steps
+        # the graph's global adjacency entries: lane group 0's parts hold every row once
+        nnz = job.allreduce([E_local if rank < P else 0])[0]
+        transport = runner.transport if runner is not None else None
+        if dinfo is not None:
+            dinfo.update(peer_info(job))
+
+        # properties and, N > 1, one unsharded engine on rank 0 (after every shard is freed)
+        export_c4 = []  # N = 1: the C4 graph for its components, exported before the engine goes
+        if world == 1 and name == "C4":
+            export_c4.append(phase(eng.export_topology, "graph export"))
+        close_engs()
+        srcs = [n for n, _, _ in inj]
+        checks = {}
+
+        def verify():
+            if rank != 0:
+                return []
+            bad = []
+            single = None
+            if world > 1:
+                t = time.perf_counter()
+                ref = Engine(V, K, seed=seed, enable_sync=True, device=local)
+                try:
+                    ref.generate(**gen)
+                    inject(ref, inj_arr)
+                    single = ref.step(R)
+                    topo = ref.export_topology() if name == "C4" else None
+                finally:
+                    ref.close()
+                torch.cuda.synchronize()
+                d = count_diffs(check, single, COUNT_FIELDS, "sharded", "single")
+                bad += d
+                checks["single_engine"] = ("every round's global counters equal one unsharded engine "
+                                           f"({time.perf_counter() - t:.1f} s)" if not d else "FAILED: " + "; ".join(d))
+            if name == "C4":
+                t = time.perf_counter()
+                if world == 1:
+                    topo = export_c4.pop()
+                lab, size, vol = components(topo.row_ptr, topo.col, device=f"cuda:{local}", log=log)
+                del topo
+                exp_d, exp_f = expected_from_components(lab, size, vol, srcs)
+                checks["components_s"] = time.perf_counter() - t
+            else:  # the grid spans every node: one component
+                exp_d, exp_f = V * K, K * (nnz - (V - 1))
+            bad += episode_failures(check, exp_d, exp_f)
+            checks["properties"] = ("P1 (deliveries = sum of source component sizes), KAT-3 (forwards = sum of "
+                                    "vol(comp) - |comp| + 1: no timer fired before quiescence) and ACK "
+                                    "(acks(r+1) = broadcasts delivered in r) hold on the checking episode")
+            checks["expected"] = {"deliveries": exp_d, "forwards": exp_f}
+            return bad
+
+        fails += phase(verify, "checks") or []
+        ok = not job.allreduce([len(fails)])[0]
+        checks["timed_episodes"] = "every timed episode equals the checking episode, counter by counter"
+        if fails:
+            checks["failures"] = fails[:12]
+        last = max((i for i, s in enumerate(check) if s["new_bits"]), default=-1)
+        rec = {
+            "config": name, "workload": workload, "nodes": V, "edges": nnz, "lanes": K, "n_gpus": world,
+            "scaling": "strong", "vertex_parts": P, "lane_groups": L, "lane_halves_per_gpu": halves,
+            "exchange": transport, "exchange_note": note,
+            "steps": args.leg_steps, "rounds_per_step": R, "rounds_to_full_delivery": last + 1,
+            "value": deliveries / elapsed, "unit": "deliveries/s",
+            "ms_per_step": elapsed / args.leg_steps * 1e3,
+            "deliveries_per_step": deliveries // args.leg_steps,
+            "hbm_bytes_per_gpu": hbm, "hbm_bytes_max": max(hbm),
+            "exchange_bytes_per_round_rank0": sent if world > 1 else None,
+            "shard": dinfo, "setup_s": setup_s,
+            "check": "passed" if ok else "FAILED", "checks": checks,
+            "roofline": roof,
         }
-        if world == 1 and not args.no_cpu_baseline and os.path.exists(CPU_LIB):
-            out["cpu_baseline"] = cpu_baseline(cfg, topo, inj, V, K, seed, R)
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        barrier()
-        dist.destroy_process_group()
+        return rec
+    finally:
+        close_engs()
 
 
-def reduce_counts(stats, allreduce_i64, fields):
-    """Sum one episode's per-round counters over the ranks (seen_hash mod 2^64)."""
-    M = (1 << 64) - 1
-    flat = []
-    for s in stats:
-        for f in fields:
-            v = s[f] & M
-            flat.append(v - (1 << 64) if v >= (1 << 63) else v)
-    tot = allreduce_i64(flat)
-    out, k = [], 0
-    for s in stats:
-        d = dict(s)
-        for f in fields:
-            d[f] = tot[k] & M
-            k += 1
-        out.append(d)
-    return out
-
+# ---------------------------------------------------------------------------
 
 def cpu_baseline(cfg, topo, inj, V, K, seed, R):
     """The oracle restatements on this host's cores (reported beside the GPU
@@ -631,7 +1080,7 @@ def cpu_baseline(cfg, topo, inj, V, K, seed, R):
     per-message Send/handler path in kind. Each leg is a bounded sample."""
     from ggamd import topology as T
     from ggamd.engine import Engine
-    from ggamd.workload import BASE_SEED, inject, uniform_injections
+    from ggamd.workload import inject, uniform_injections
     host_cpus, affinity = cpu_counts()
     # the CPU share this process is given: the runtime's declared thread budget
     # (OMP_NUM_THREADS: the GPU box's per-GPU share of its host cores), else every
@@ -711,6 +1160,59 @@ def o1_c1_leg():
             "deliveries_per_s": dl / dt, "messages": msgs, "seconds": dt,
             "sample": f"C1 (25-node tree4, {len(wl.injections)} client broadcasts over 200 rounds, sync on), "
                       f"{wl.max_rounds} rounds through O1's message-level network"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C2", choices=["C2", "C4"])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--nodes", type=int, help="C2: nodes per GPU (2^20); C4: nodes (10^8)")
+    ap.add_argument("--lanes", type=int, help="C2: 1024; C4: 4096")
+    ap.add_argument("--parts", type=int, default=1, help="--config C4: vertex parts P (world = lane groups x P)")
+    ap.add_argument("--halves", type=int, default=1, choices=[1, 2],
+                    help="--config C4 with --parts > 1: 2 = two engines per GPU over the two halves of its lanes, "
+                         "one half's exchange overlapping the other half's kernels (ggamd.dist.HalvesRunner)")
+    ap.add_argument("--legs", default=None,
+                    help="comma list of C4,C5 (default after a C2 headline: C4,C5; 'none' to skip)")
+    ap.add_argument("--leg-steps", type=int, default=3, help="timed episodes per leg")
+    ap.add_argument("--leg-parts", type=int, default=0, help="legs: vertex parts P (default N)")
+    ap.add_argument("--leg-halves", type=int, default=0, choices=[0, 1], help="legs: 1 = no lane halves for C4")
+    ap.add_argument("--c4-nodes", type=int, help="C4 leg nodes (10^8; smaller for rehearsals)")
+    ap.add_argument("--c5-side", type=int, help="C5 leg grid side (32768 = 2^30 nodes)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fresh-sets", type=int, default=4,
+                    help="N = 1: after the timed region, episodes rotating this many distinct seeded injection "
+                         "sets (every step re-captures its launch graph and uploads its injections; 0: skip)")
+    ap.add_argument("--no-check", action="store_true", help="skip the N > 1 single-engine check")
+    ap.add_argument("--xchg", default=os.environ.get("GG_DIST_TRANSPORT", "auto"),
+                    choices=["auto", "engine", "ipc", "torch"],
+                    help="N > 1 exchange between vertex parts: engine = the engine's grouped RCCL send/recv; "
+                         "ipc = device-driven (IPC-mapped peer windows, kernel flags, captured batches of rounds, "
+                         "no host wait); torch = torch all_to_all; auto (default) = ipc when every rank maps its "
+                         "peers and one whole validation episode through it equals O2, else engine")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 "
+                    "(nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
+    args = ap.parse_args()
+
+    job = Job(args.backend, args.gpus)
+    out, info = headline(job, args)
+    legs_arg = args.legs if args.legs is not None else ("C4,C5" if args.config == "C2" else "none")
+    names = [x.strip().upper() for x in legs_arg.split(",") if x.strip() and x.strip().lower() != "none"]
+    legs = {}
+    for name in names:
+        if name not in ("C4", "C5"):
+            raise SystemExit(f"--legs: unknown leg {name}")
+        pref = info["xchg"] if info["xchg"] in ("ipc", "engine") else "engine"
+        if args.backend != "nccl" and pref == "engine":
+            pref = "engine"  # (gloo rehearsal: the engine's sequencing over HostTransport)
+        legs[name] = run_leg(job, args, name, pref)
+    if job.rank == 0:
+        if names:
+            out["legs"] = legs
+        print(json.dumps(out), flush=True)
+    job.close()
 
 
 if __name__ == "__main__":

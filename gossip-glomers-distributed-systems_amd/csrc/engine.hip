@@ -48,7 +48,8 @@ constexpr int kMaxBlocks = 2048;
 // double-buffered lean rounds: the F-row kernels take them), GG_DB (double-buffered
 // lean rounds whatever the free memory), GG_SYNC_EAGER / GG_SYNC_ALLOC_ROUND (the
 // streamed-sync buffers with the topology / from a given round), GG_COMPACT_ATOMIC /
-// GG_COMPACT_SPLIT (one-launch or split compaction whatever the size).
+// GG_COMPACT_SPLIT (one-launch or split compaction whatever the size),
+// GG_IPC_SPIN_LIMIT (sleeps before a device-driven exchange wait gives up).
 const char* test_knob(const char* name) { return getenv(name); }
 // A/B switches of past measurements (GG_ALL_FULL, GG_NO_GRAPH, GG_SYNC_ALLPUSH,
 // GG_FLAGS_FIRST, GG_FF_FRAC16, GG_PREP_WIDE, GG_XCHG_EXACT_BYTES): read only in a -DGG_AB_KNOBS build.
@@ -997,6 +998,8 @@ uint64_t path_of(const gg_engine* e, int64_t r, bool db) {
     return p | (lean ? GG_PATH_STREAM : GG_PATH_TILES);
 }
 
+int zero_async(gg_engine* e, void* p, size_t bytes);
+
 // Enqueue round e->round (kernels only). inj: device pairs for this round.
 int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned long long* d_ctr,
                   const uint32_t* d_tab = nullptr) {
@@ -1138,7 +1141,7 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         if (e->d_bset[0]) {  // sync timers: this round's fired bits are set by the kernel
             a.bset_prev = e->d_bset[(r + 1) & 1];
             a.bset_cur = e->d_bset[r & 1];
-            HIPCHK(hipMemsetAsync(a.fired_cur, 0, e->rows / 8, e->stream));
+            if (int rz = zero_async(e, a.fired_cur, e->rows / 8)) return rz;
         }
         if (n_inj) {
             hipLaunchKernelGGL(gg::mark_injections, dim3(gg::kMarkInjBlocks), dim3(256), 0, e->stream, a);
@@ -1298,6 +1301,17 @@ void fold_stats(gg_engine* e, const unsigned long long* slots, int64_t round, gg
     s->work_gathers = c[gg::C_GATHERS];
     e->pend_acks = c[gg::C_NEXT_ACKS];
     e->pend_ackdrop = c[gg::C_NEXT_ACKDROP];
+}
+
+// Zero `bytes` (a multiple of 8, 16-byte aligned) on the engine stream with a
+// kernel of ours: every clear that can sit inside a captured batch (gg::zero_words).
+int zero_async(gg_engine* e, void* p, size_t bytes) {
+    const uint64_t n = bytes / 8;
+    if (!n) return GG_OK;
+    const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n / 2 + 255) / 256, 1024));
+    hipLaunchKernelGGL(gg::zero_words, dim3(blocks), dim3(256), 0, e->stream, reinterpret_cast<uint64_t*>(p), n);
+    HIPCHK(hipGetLastError());
+    return GG_OK;
 }
 
 int ensure_events(gg_engine* e, size_t n) {
@@ -2519,7 +2533,7 @@ int enqueue_step_batch(gg_engine* e, uint32_t m, bool wait, std::vector<uint64_t
         e->f_dirty = save_fd;
         e->set_cur = save_set;
         e->d_base = e->d_sets[save_set];
-        HIPCHK(hipMemsetAsync(e->d_counters, 0, (size_t)m * gg::kSlots * gg::kCounters * 8, e->stream));
+        if (int rz = zero_async(e, e->d_counters, (size_t)m * gg::kSlots * gg::kCounters * 8)) return rz;
         for (uint32_t k = 0; k < m; ++k) {
             const uint32_t ni = (uint32_t)(off[k + 1] - off[k]);
             e->round = r0 + k;
@@ -2620,7 +2634,7 @@ int gg_run_episodes(gg_engine* e, uint32_t n, uint32_t episodes, gg_round_stats*
     if (rc) return rc;
     if ((rc = ensure_db(e))) return rc;
     if ((rc = ensure_sync(e, (int64_t)n - 1))) return rc;
-    if ((rc = ensure_events(e, 2))) return rc;
+    if ((rc = ensure_events(e, 3))) return rc;
     // every episode's folded counter rows in a device ring, read back once
     const size_t rows_b = (size_t)n * gg::kCounters * 8, need = rows_b * episodes;
     if (need > e->ep_cap) {
@@ -2659,6 +2673,7 @@ int gg_run_episodes(gg_engine* e, uint32_t n, uint32_t episodes, gg_round_stats*
             // every later reset how much of the F buffers an episode leaves dirty:
             // one host wait, after the first episode only
             HIPCHK(hipStreamSynchronize(e->stream));
+            HIPCHK(hipEventRecord(e->ev[2], e->stream));  // the timed span: episodes 1..K-1 (no host wait)
             int q = 2;  // what a reset leaves
             for (uint32_t j = 0; j < n; ++j) q = e->h_counters[(size_t)j * gg::kCounters + gg::C_NEW] ? 0 : q + 1;
             quiet_end = q;
@@ -2668,8 +2683,10 @@ int gg_run_episodes(gg_engine* e, uint32_t n, uint32_t episodes, gg_round_stats*
     HIPCHK(hipMemcpyAsync(e->h_ep, e->d_ep, need, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     float ms = 0.f;
-    HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
-    e->step_event_ms = (double)ms / episodes;
+    // per episode: the episodes queued after the one host wait (the first one's
+    // span also holds its graph launch and, on a new batch shape, the capture)
+    HIPCHK(hipEventElapsedTime(&ms, e->ev[episodes > 1 ? 2 : 0], e->ev[1]));
+    e->step_event_ms = (double)ms / (episodes > 1 ? episodes - 1 : 1);
     for (uint32_t k = 0; k < episodes; ++k) {  // each episode's stats from round 0's state
         e->hash_total = 0;
         e->pend_acks = e->pend_ackdrop = 0;
@@ -2714,7 +2731,11 @@ static int fold_pending(gg_engine* e) {
     if (e->ipc) {
         uint32_t err = 0;
         HIPCHK(hipMemcpy(&err, e->d_xticket + 1, 4, hipMemcpyDeviceToHost));
-        if (err) return e->fail(GG_EIO, "device-driven exchange: a peer did not arrive within the wait bound");
+        if (err)
+            return e->fail(GG_EIO, "device-driven exchange: a peer did not arrive within the wait bound (" +
+                                       std::to_string(err) +
+                                       " wait(s) ran out; the exchange stays dead: install a new topology and "
+                                       "export/import again)");
     }
     for (uint32_t k = 0; k < e->dist_k; ++k) {
         gg_round_stats s;
@@ -2745,6 +2766,9 @@ static gg::IpcArgs ipc_args(const gg_engine* e) {
     ip.seq = reinterpret_cast<uint64_t*>(e->d_xticket + 2);
     ip.ticket = e->d_xticket;
     ip.err = e->d_xticket + 1;
+    static const uint32_t limit = test_knob("GG_IPC_SPIN_LIMIT") ? (uint32_t)strtoul(test_knob("GG_IPC_SPIN_LIMIT"), nullptr, 0)
+                                                                  : gg::kSpinLimit;
+    ip.spin_limit = limit;
     return ip;
 }
 
@@ -2879,7 +2903,7 @@ static int dist_begin(gg_engine* e, gg_exchange* x, bool host_sizes) {
     // (fold_pending has read the last one), and only as far as they were used:
     // a caller that folds every round (gg_dist_round_end with out) clears one slot
     if (e->dist_k == 0 && e->ctr_dirty) {
-        HIPCHK(hipMemsetAsync(e->d_counters, 0, e->ctr_dirty * slot * 8, e->stream));
+        if ((rc = zero_async(e, e->d_counters, e->ctr_dirty * slot * 8))) return rc;
         e->ctr_dirty = 0;
     }
     e->ctr_dirty = std::max(e->ctr_dirty, e->dist_k + 1);
@@ -3560,7 +3584,7 @@ static int dist_step_batched(gg_engine* e, uint32_t n_rounds) {
             e->f_dirty = save_fd;
             e->set_cur = save_set;
             e->d_base = e->d_sets[save_set];
-            HIPCHK(hipMemsetAsync(e->d_counters + k0 * slot, 0, (size_t)m * slot * 8, e->stream));
+            if (int rz = zero_async(e, e->d_counters + k0 * slot, (size_t)m * slot * 8)) return rz;
             for (uint32_t k = 0; k < m; ++k) {
                 e->round = r0 + k;
                 const uint32_t ni = (uint32_t)(off[k + 1] - off[k]);
@@ -3740,7 +3764,11 @@ int gg_dist_run_episodes(gg_engine* e, uint32_t n, uint32_t episodes, gg_round_s
     if (e->ipc) {
         uint32_t err = 0;
         HIPCHK(hipMemcpy(&err, e->d_xticket + 1, 4, hipMemcpyDeviceToHost));
-        if (err) return e->fail(GG_EIO, "device-driven exchange: a peer did not arrive within the wait bound");
+        if (err)
+            return e->fail(GG_EIO, "device-driven exchange: a peer did not arrive within the wait bound (" +
+                                       std::to_string(err) +
+                                       " wait(s) ran out; the exchange stays dead: install a new topology and "
+                                       "export/import again)");
     }
     for (uint32_t k = 0; k < episodes; ++k) {
         e->hash_total = 0;

@@ -3738,6 +3738,19 @@ __global__ void materialize_F(const uint64_t* set_q, const uint64_t* set_qm1, co
     }
 }
 
+// Zero n 8-byte words (16-byte stores, an 8-byte tail). Used instead of
+// hipMemsetAsync inside captured launch sequences: replays of a graph whose
+// memset node was captured in an engine's first batch were seen to fill the
+// counter slots with pointer-like words (16-byte pattern) instead of zeros,
+// depending on the process's other allocations (round 5, 2 ranks on one GPU).
+__global__ void zero_words(uint64_t* p, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t n2 = n / 2;
+    ulonglong2* q = reinterpret_cast<ulonglong2*>(p);
+    for (uint64_t k = i; k < n2; k += stride) q[k] = make_ulonglong2(0ull, 0ull);
+    if (i == 0 && (n & 1)) p[n - 1] = 0;
+}
+
 __global__ void fold_slots(const unsigned long long* ctr, unsigned long long* out) {
     const int j = threadIdx.x;
     const unsigned long long* c = ctr + (size_t)blockIdx.x * kSlots * kCounters;
@@ -3877,22 +3890,34 @@ constexpr uint32_t XK_SET = 0x80000000u;
 // used it last). seq lives in device memory, so the round is a fixed launch
 // sequence with no host wait and no collective call, and a captured batch of
 // rounds replays for any seq.
-// Waits are bounded (kSpinLimit sleeps, ~15 s): a peer that never arrives sets
-// the engine's error word instead of hanging the GPU.
+// Waits are bounded (IpcArgs::spin_limit sleeps, default kSpinLimit ≈ 15 s): a
+// peer that never arrives sets the engine's error word instead of hanging the
+// GPU. Once the word is set every later wait, pack and unpack of the engine
+// returns at once (the exchange is dead until a new topology is exported and
+// imported again), so a missing peer costs one bound, not one per wait of every
+// queued round: the word counts the waits that ran out (at most one per
+// engine, plus any running concurrently with the first).
 constexpr uint64_t kWinHdr = 4096;         // flags area at the start of a window
 constexpr uint32_t kWinReady = 0;          // u64 ready[64]: by source part
 constexpr uint32_t kWinConsumed = 512;     // u64 consumed[64]: by receiving part
 constexpr uint32_t kSpinLimit = 1u << 25;
 
+__device__ __forceinline__ bool ipc_failed(const uint32_t* err) {
+    return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+}
+
 // Wait until flags[q] >= want for every q in mask (system-scope acquire loads).
-// One thread calls it; false (and err set) after the bound.
-__device__ __forceinline__ bool wait_flags(const uint64_t* flags, uint64_t mask, uint64_t want, uint32_t* err) {
+// One thread calls it; false after the bound (err counts it) or as soon as
+// another wait of this engine has run out (err already set).
+__device__ __forceinline__ bool wait_flags(const uint64_t* flags, uint64_t mask, uint64_t want, uint32_t* err,
+                                           uint32_t limit) {
     for (; mask; mask &= mask - 1) {
         const int q = __ffsll((long long)mask) - 1;
         uint32_t it = 0;
         while (__hip_atomic_load(flags + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
-            if (++it > kSpinLimit) {
-                atomicOr(err, 1u);
+            if ((it & 255u) == 0u && ipc_failed(err)) return false;
+            if (++it > limit) {
+                atomicAdd(err, 1u);
                 return false;
             }
             __builtin_amdgcn_s_sleep(16);
@@ -3911,7 +3936,8 @@ struct IpcArgs {
     uint64_t recv_mask;        // parts this engine receives from
     uint64_t* seq;             // exchange sequence number of this round (advanced by unpack)
     uint32_t* ticket;          // unpack's last-block counter
-    uint32_t* err;             // bit 0: a wait ran out
+    uint32_t* err;             // waits that ran out (non-zero: the exchange is dead)
+    uint32_t spin_limit;       // sleeps before a wait gives up (kSpinLimit; GG_IPC_SPIN_LIMIT for tests)
 };
 
 // One 64-thread block before pack_ghosts (which = 0: the peers consumed round
@@ -3925,9 +3951,10 @@ __global__ void ipc_wait(IpcArgs ip, int which) {
     const uint64_t mask = which ? ip.recv_mask : ip.send_mask;
     if (q >= 64 || !((mask >> q) & 1ull)) return;
     if (which == 0 && seq < 2) return;
+    if (ipc_failed(ip.err)) return;
     const uint64_t* flags =
         reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(ip.my_win) + (which ? kWinReady : kWinConsumed));
-    wait_flags(flags, 1ull << q, which ? seq + 1 : seq - 1, ip.err);
+    wait_flags(flags, 1ull << q, which ? seq + 1 : seq - 1, ip.err, ip.spin_limit);
 }
 
 // Peer q's segment for this engine in round seq's receive buffer.
@@ -3975,6 +4002,9 @@ __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
     __shared__ uint32_t s_base, s_tot;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t cpe = x.nwp >= 2 ? 1 + x.nwp / 2 : 1;  // 16-byte chunks per entry
+    // a dead exchange (a wait ran out; ipc_wait, the only writer, ran before this
+    // launch, so every block reads the same word): store nothing into the peers
+    if (x.ipc.peer_win && ipc_failed(x.ipc.err)) return;
     const uint64_t seq = x.ipc.peer_win ? *x.ipc.seq : 0;  // (ipc_wait ran before: the buffers are free)
     for (uint32_t ti = blockIdx.x; ti < x.n_tiles; ti += gridDim.x) {
         const XchgTile t = x.tiles[ti];
@@ -4110,6 +4140,7 @@ __device__ __forceinline__ void finish_pack_body(uint32_t* cnt, uint8_t* out, co
 
 __global__ void finish_pack(uint32_t* cnt, uint8_t* out, const uint64_t* seg_off, uint32_t parts, uint32_t self,
                             uint32_t stride, unsigned long long* seg_bytes, unsigned long long* payload, IpcArgs ip) {
+    if (ip.peer_win && ipc_failed(ip.err)) return;
     finish_pack_body(cnt, out, seg_off, parts, self, stride, seg_bytes, payload, ip);
 }
 
@@ -4151,6 +4182,7 @@ struct UnpackArgs {
 __global__ __launch_bounds__(kBlock) void unpack_ghosts(UnpackArgs x) {
     __shared__ uint32_t s_src[64], s_pref[65];
     const uint32_t cpe = x.nwp >= 2 ? 1 + x.nwp / 2 : 1;
+    if (x.ipc.peer_win && ipc_failed(x.ipc.err)) return;  // a dead exchange: nothing landed
     const uint64_t seq = x.ipc.peer_win ? *x.ipc.seq : 0;
     if (x.ipc.peer_win)  // this round's receive buffer
         x.in = reinterpret_cast<const uint8_t*>(x.ipc.my_win) + kWinHdr + (seq & 1) * x.ipc.rbuf;

@@ -211,7 +211,8 @@ int gg_step_device_ms(const gg_engine* e, double* ms);
  * episode (its trailing quiet rounds tell the later resets which buffers an
  * episode leaves dirty) and at the end.
  * Single engine (not vertex-sharded), 1 <= n_rounds <= 256. gg_step_device_ms
- * then gives the device time per episode. (Host side of a Maelstrom run that
+ * then gives the device time per episode of episodes 1..K-1, the ones queued
+ * after the host wait (episode 0 alone when episodes == 1). (Host side of a Maelstrom run that
  * replays one broadcast workload many times; the reference has no counterpart.) */
 int gg_run_episodes(gg_engine* e, uint32_t n_rounds, uint32_t episodes, gg_round_stats* out);
 
@@ -338,7 +339,12 @@ int gg_dist_run_episodes(gg_engine* e, uint32_t n_rounds, uint32_t episodes, gg_
  * processes, on this GPU or another of the node). From then on gg_dist_step packs
  * each peer's segment straight into the peer's receive buffer over xGMI and the
  * kernels hand rounds over with flags in the windows (bounded waits: a peer that
- * never arrives gives GG_EIO at the next flush instead of a hang); the round is a
+ * never arrives gives GG_EIO at the next flush instead of a hang; the first wait
+ * that runs out marks the exchange dead, so every later wait, pack and unpack of
+ * this engine returns at once and the job fails after one bound, not one per
+ * queued round). A dead exchange stays dead: every later gg_dist_step, flush or
+ * gg_dist_run_episodes returns GG_EIO — gg_reset does not revive it; install a
+ * new topology and export and import the windows again (collectively). The round is a
  * fixed launch sequence on the engine stream. Every part must run the same number
  * of sharded rounds (they count them); a new topology drops the windows (export
  * and import again). gg_dist_round_begin reports zero bytes to move. */

@@ -1041,3 +1041,70 @@ def test_ipc_run_episodes_equal_oracle(hip_lib, cpu_lib, world, lane_groups):
             if lane_groups == 1:
                 assert np.array_equal(bits, ref.read_bits_nodes(owned)), (k, rank)
         ref.close()
+
+
+def _dead_peer_worker(rank, world, port, lib, q, rounds):
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    from ggamd import topology as T
+    from ggamd.dist import ShardedRunner
+    from ggamd.engine import GGError
+    from ggamd.workload import uniform_injections
+    os.environ["GG_IPC_SPIN_LIMIT"] = str(1 << 16)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        sc = Scenario(T.tree(3000, 4), 128, 30, uniform_injections(3000, 100, 5), seed=9, enable_sync=False)
+        e = make_engine(lib, sc, rank=rank, world=world, device=0)
+        r = ShardedRunner(e, torch.device("cuda", 0), transport="ipc")
+        t0 = time.perf_counter()
+        err1 = err2 = None
+        try:
+            r.step(rounds[rank], reduce=False)
+        except GGError as exc:
+            err1 = str(exc)
+        t1 = time.perf_counter()
+        try:  # a dead exchange stays dead, and its waits no longer spin
+            r.step(4, reduce=False) if err1 else None
+        except GGError as exc:
+            err2 = str(exc)
+        t2 = time.perf_counter()
+        dist.barrier()  # the short rank keeps its window mapped until the long one is done
+        e.close()
+        q.put((rank, (err1, err2, t1 - t0, t2 - t1)))
+    except BaseException as exc:  # noqa: BLE001
+        q.put((rank, f"rank {rank} failed: {exc!r}"))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ipc_dead_peer_fails_after_one_bound(hip_lib):
+    """a peer that stops exchanging costs its partner ONE wait bound.
+    Rank 1 runs 4 rounds, rank 0 runs 12 (8 rounds = 16 waits its peer never
+    answers). With a lowered bound (GG_IPC_SPIN_LIMIT) rank 0 gets GG_EIO with
+    exactly one wait counted as run out (every later wait, pack and unpack saw
+    the dead exchange and returned at once), and a further gg_dist_step fails
+    at once as well; rank 1 finishes cleanly."""
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dead_peer_worker, args=(r, 2, port, hip_lib, qq, (12, 4))) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, got = qq.get(timeout=120)
+        assert not isinstance(got, str), got
+        res[r] = got
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    err1, err2, t_first, t_again = res[0]
+    print(f"dead peer: first failure after {t_first:.3f} s, the next step's after {t_again:.3f} s")
+    assert err1 is not None and "EIO" in err1 and "(1 wait(s) ran out" in err1, err1
+    assert err2 is not None and "EIO" in err2, err2
+    assert t_again < max(0.5, t_first / 2), (t_first, t_again)
+    assert res[1][0] is None, res[1]

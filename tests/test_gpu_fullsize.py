@@ -23,6 +23,7 @@ pinned against it at 4K nodes (tests/test_golden.py).
 import numpy as np
 import pytest
 
+from ggamd.checks import components, expected_from_components
 from ggamd.engine import COUNT_FIELDS, Engine
 from ggamd.workload import BASE_SEED, inject, injection_arrays, uniform_injections
 
@@ -117,50 +118,6 @@ def test_c3_full_size_equals_o2(hip_lib, cpu_lib):
         c.close()
 
 
-def _components(row_ptr, col, device="cuda", chunk=1 << 29):
-    """Connected components of a symmetric CSR on the GPU (torch): min-label
-    propagation over every adjacency entry (rows and columns resident as int64
-    chunks) with pointer jumping, to a fixed point. Returns (label per node,
-    component size per label, degree sum per label) as CPU tensors."""
-    import time
-
-    import torch
-    dev = torch.device(device)
-    t0 = time.time()
-    V = row_ptr.size - 1
-    deg = torch.from_numpy(row_ptr[1:] - row_ptr[:-1]).to(dev)
-    E = int(col.size)
-    chunks = []  # (rows, cols) int64 on the device
-    for e0 in range(0, E, chunk):
-        e1 = min(E, e0 + chunk)
-        v0 = int(np.searchsorted(row_ptr, e0, side="right")) - 1
-        v1 = int(np.searchsorted(row_ptr, e1 - 1, side="right"))
-        rp = torch.from_numpy(np.clip(row_ptr[v0:v1 + 1], e0, e1) - e0).to(dev)
-        rows = torch.repeat_interleave(torch.arange(v0, v1, device=dev), rp[1:] - rp[:-1])
-        chunks.append((rows, torch.from_numpy(col[e0:e1]).to(dev).long()))
-    lab = torch.arange(V, dtype=torch.int64, device=dev)
-    it = 0
-    while True:
-        old = lab.clone()
-        for rows, cols in chunks:
-            lab.scatter_reduce_(0, rows, lab[cols], reduce="amin")
-        for _ in range(8):  # pointer jumping
-            lab = lab[lab]
-        it += 1
-        print(f"components: pass {it}, {time.time() - t0:.1f} s", flush=True)
-        if torch.equal(lab, old):
-            break
-    lab = lab.cpu().numpy()
-    del chunks, deg
-    torch.cuda.empty_cache()
-    # per-label sums on the host: the giant component's label would take every
-    # device atomic of a bincount on one address
-    size = np.bincount(lab, minlength=V)
-    vol = np.bincount(lab, weights=(row_ptr[1:] - row_ptr[:-1]).astype(np.float64), minlength=V)
-    print(f"components: {int((size > 0).sum())} labels, {time.time() - t0:.1f} s", flush=True)
-    return lab, size, vol
-
-
 def test_c4_full_size_lane_groups_equal_single(hip_lib):
     """Also, on the single engine: P1 (every message reaches exactly its
     source's connected component) and KAT-3 (no timer fires before
@@ -181,12 +138,9 @@ def test_c4_full_size_lane_groups_equal_single(hip_lib):
         e.close()
     assert want[-1]["new_bits"] == 0
     assert all(s["syncs_fired"] == 0 for s in want), "a sync timer fired before quiescence"
-    lab, size, vol = _components(topo.row_ptr, topo.col)
+    lab, size, vol = components(topo.row_ptr, topo.col)
     del topo
-    src = [n for n, _, _ in inj_l]
-    comp = lab[np.asarray(src, np.int64)]
-    p1 = int(size[comp].sum())
-    kat3 = int(round(float(vol[comp].sum()))) - p1 + K
+    p1, kat3 = expected_from_components(lab, size, vol, [n for n, _, _ in inj_l])
     assert sum(s["new_bits"] for s in want) == p1, "P1: deliveries != sum of source component sizes"
     assert sum(s["fwd_sent"] for s in want) == kat3, "KAT-3: forwards != sum of vol(comp) - (|comp| - 1)"
     for a, b in zip(want, want[1:]):
