@@ -425,8 +425,6 @@ def headline(job: Job, args) -> tuple[dict | None, dict]:
         while True:
             rn = bb["runner"]
             st = rn.step(1, reduce=False)[0] if rn else bb["eng"].step(1)[0]
-            if os.environ.get("GG_BENCH_DEBUG") and R < 3:
-                print(f"bench: rank {rank} quiescence round {R} new_bits {st['new_bits']}", file=sys.stderr, flush=True)
             nb = job.allreduce([st["new_bits"]])[0]
             R += 1
             if nb == 0 and R > 1:
@@ -454,25 +452,7 @@ def headline(job: Job, args) -> tuple[dict | None, dict]:
         return rn.step(R, reduce=False)
 
     for _ in range(max(0, args.warmup - 1)):
-        wst = episode(b)
-        if os.environ.get("GG_BENCH_DEBUG") and b["runner"] is not None:
-            print(f"bench: rank {rank} warmup episode new_bits {[x['new_bits'] for x in wst][:6]}",
-                  file=sys.stderr, flush=True)
-            w2 = episode(b)
-            print(f"bench: rank {rank} second replay new_bits {[x['new_bits'] for x in w2][:4]}",
-                  file=sys.stderr, flush=True)
-            for e in b["engs"]:
-                e.reset()
-                inject(e, inj_arr)
-            w3 = [b["runner"].step(1, reduce=False)[0] for _ in range(R)]
-            print(f"bench: rank {rank} single steps new_bits {[x['new_bits'] for x in w3][:4]}",
-                  file=sys.stderr, flush=True)
-            for e in b["engs"]:
-                e.reset()
-                inject(e, inj_arr)
-            w4 = b["runner"].step(5, reduce=False) + b["runner"].step(R - 5, reduce=False)
-            print(f"bench: rank {rank} 5 + rest new_bits {[x['new_bits'] for x in w4][:7]}",
-                  file=sys.stderr, flush=True)
+        episode(b)
     event_ms.clear()
 
     # one engine per rank (no vertex parts): the K episodes go back to back through
@@ -602,13 +582,6 @@ def headline(job: Job, args) -> tuple[dict | None, dict]:
         per_ep = local_stats
     deliveries = sum(s["new_bits"] for ep in per_ep for s in ep)
     msgs = sum(s["fwd_sent"] + s["pushes"] + s["acks"] + s["reads"] + s["read_oks"] for s in per_ep[-1])
-    if os.environ.get("GG_BENCH_DEBUG"):
-        print(f"bench: rank {rank} R {R} rounds {[len(ep) for ep in local_stats]} new_bits of episode 0 "
-              f"{[x['new_bits'] for x in local_stats[0]]}", file=sys.stderr, flush=True)
-        print(f"bench: rank {rank} mode {mode}: local round 0 of the episodes "
-              f"{[{f: ep[0][f] for f in ('new_bits', 'fwd_sent', 'pushes')} for ep in local_stats]}; "
-              f"global {[{f: ep[0][f] for f in ('new_bits', 'fwd_sent', 'pushes')} for ep in per_ep]}",
-              file=sys.stderr, flush=True)
 
     dinfo = None
     if runner is not None:
@@ -761,9 +734,6 @@ def validate_ipc(job: Job, args, setup):
         for e in built["engs"]:
             e.reset()
             inject(e, arr)
-        if os.environ.get("GG_BENCH_VAL_ROUNDS"):  # (debug)
-            rounds = int(os.environ["GG_BENCH_VAL_ROUNDS"])
-            gold = None
         n = rounds if job.rank != f_rank else min(rounds, f_round)
         local = built["runner"].step(n, reduce=False) if n else []
         if job.rank == f_rank:
@@ -776,9 +746,6 @@ def validate_ipc(job: Job, args, setup):
            if gold is not None else "completion only (no golden run of this shape)"}
     if job.agree(ok):
         glob = reduce_counts(local, job, COUNT_FIELDS)
-        if os.environ.get("GG_BENCH_DEBUG"):
-            print(f"bench: rank {job.rank} validation local new_bits {[x['new_bits'] for x in local][:6]}",
-                  file=sys.stderr, flush=True)
         diffs = count_diffs(glob, gold["rounds"], COUNT_FIELDS, "ipc", "O2") if gold is not None else []
         if not diffs:
             rec["result"] = "passed"
