@@ -108,9 +108,10 @@ struct BatchKey {
     size_t windows = 0;
     const void* inj_buf = nullptr;
     int db_state = 0;  // double-buffered rounds active at r0, and the current set buffer
+    uint64_t solo_hash = 0;  // the solo schedule of the batch's marking rounds (and the round before r0)
     bool operator==(const BatchKey& o) const {
         return r0 == o.r0 && m == o.m && inj_hash == o.inj_hash && u_hash == o.u_hash && windows == o.windows &&
-               inj_buf == o.inj_buf && db_state == o.db_state;
+               inj_buf == o.inj_buf && db_state == o.db_state && solo_hash == o.solo_hash;
     }
 };
 
@@ -220,6 +221,12 @@ struct gg_engine {
     std::vector<int64_t> dist_round_of;        // round of each pending slot
     std::vector<uint64_t> dist_path;           // its kernel path (GG_PATH_*)
     uint64_t last_path = 0;                    // path of the round enqueue_round enqueued last
+    // solo marking rounds (RoundArgs::solo): per round, the busy flag the stream
+    // kernels reported the last time it ran (-1: not seen), with a strike count
+    // (a hint flips after two runs in a row that disagree with it), and the solo
+    // kind of the last enqueued round
+    std::vector<int8_t> busy_hint, busy_strike;
+    uint32_t last_solo = 0;
     bool last_mark = false;                    // ... and whether it marks round r+1's candidates (mark_cand):
                                                // then the unpack of its exchange marks the owned receivers of
                                                // the ghosts that sent an F row (round r+1 runs no round_prep)
@@ -463,6 +470,8 @@ void gg_engine::free_topology() {
     }
     have_topo = false;
     part_rows = false;
+    busy_hint.clear();
+    busy_strike.clear();
 }
 
 static void rccl_destroy(ncclComm_t c);
@@ -490,6 +499,8 @@ gg_engine::~gg_engine() {
 
 namespace {
 
+int zero_async(gg_engine* e, void* p, size_t bytes);
+
 // Back to round 0, asynchronously: every call that reads results waits on the stream.
 int reset_device_state(gg_engine* e) {
     const size_t rowbytes = e->rows * e->nwp * 8;
@@ -500,11 +511,11 @@ int reset_device_state(gg_engine* e) {
         if (ra.n_seg < gg::kResetSegs) ra.seg[ra.n_seg++] = {reinterpret_cast<uint64_t*>(p), bytes / 8, val};
         else e->err = "internal: reset segment table full";  // caught below
     };
-    seg(e->d_sets[0], rowbytes, 0);
-    if (e->db_ok) seg(e->d_sets[1], rowbytes, 0);
     e->set_cur = 0;
     e->d_base = e->d_sets[0];
     e->db_active = e->db_ok;
+    seg(e->d_sets[0], rowbytes, 0);
+    if (e->db_ok) seg(e->d_sets[1], rowbytes, 0);
     // F rows and flags are already all zero after two rounds without new bits
     // (a stale row is cleared in the round it expires), e.g. after an episode
     // run to quiescence. Single engine only: ghost rows follow remote rounds.
@@ -678,7 +689,9 @@ void launch_stream_m(const gg::RoundArgs& a, bool maskw, hipStream_t s) {
     } else if (a.db) {
         // the marking kernel first: in rounds with block lists it sums round r-1's
         // rings and publishes them for the other one
-        if (a.mark_cand) launch_stream_t<G, false, 2>(a, s);  // the rounds that are not busy
+        // (solo marking rounds: only the kernel the last run of this round needed)
+        if (a.mark_cand && a.solo != gg::SOLO_DB) launch_stream_t<G, false, 2>(a, s);  // the rounds that are not busy
+        if (a.solo == gg::SOLO_MARK) return;
         if (a.n_edges < 4ull * a.n_own) launch_stream_t<G, false, 3>(a, s);  // mean in-degree < 4: 3 rows a batch
         else launch_stream_t<G, false, 1>(a, s);
     } else {
@@ -1000,6 +1013,72 @@ uint64_t path_of(const gg_engine* e, int64_t r, bool db) {
 
 int zero_async(gg_engine* e, void* p, size_t bytes);
 
+// Round r is a marking round with block lists (RoundArgs::block_lists: the
+// marking kernel and expand_stream_db are both launched, each exits when the
+// round is the other's) — enqueue_round's rule, from the host state before
+// db_advance(r). db: db_round(e, r).
+bool bll_round(const gg_engine* e, int64_t r, bool db) {
+    static const bool no_bll = ab_knob("GG_BLOCK_LISTS") && atoi(ab_knob("GG_BLOCK_LISTS")) == 0;  // A/B
+    const int64_t base = (int64_t)e->cfg.sync_base_ticks;
+    const bool sync = e->cfg.enable_sync != 0;
+    return db && mark_ok(e) && !(sync && r >= base) && db_round(e, r + 1) && !(sync && r + 1 >= base) &&
+           e->n_hubs == 0 && !no_bll;
+}
+
+// The solo kind of marking round r (RoundArgs::solo): the kernel the device chose
+// the last time this round ran (busy_hint), or 0 (launch both) when unknown.
+// Test hook GG_SOLO: 0 = never solo; mark / db / alt = that kind in every marking
+// round whatever the hints (every schedule is exact; only the speed differs).
+uint32_t solo_of(const gg_engine* e, int64_t r, bool db) {
+    if (!bll_round(e, r, db)) return 0;
+    const char* force = test_knob("GG_SOLO");
+    if (force) {
+        if (!strcmp(force, "0")) return 0;
+        if (!strcmp(force, "mark")) return gg::SOLO_MARK;
+        if (!strcmp(force, "db")) return gg::SOLO_DB;
+        if (!strcmp(force, "alt")) return (r & 1) ? gg::SOLO_DB : gg::SOLO_MARK;
+    }
+    const int8_t h = r >= 0 && (size_t)r < e->busy_hint.size() ? e->busy_hint[r] : (int8_t)-1;
+    return h < 0 ? 0u : (h ? gg::SOLO_DB : gg::SOLO_MARK);
+}
+
+// A round's busy flag (busy_count of the nodes that became active the round before): the hint
+// for the next run of that round flips only after two runs in a row disagree.
+void learn_busy(gg_engine* e, int64_t r, bool busy) {
+    if (r < 0 || r > (1 << 20)) return;
+    if (e->busy_hint.size() <= (size_t)r) {
+        e->busy_hint.resize(r + 1, -1);
+        e->busy_strike.resize(r + 1, 0);
+    }
+    const int8_t b = busy ? 1 : 0;
+    if (e->busy_hint[r] < 0 || e->busy_hint[r] == b) {
+        e->busy_hint[r] = b;
+        e->busy_strike[r] = 0;
+    } else if (++e->busy_strike[r] >= 2) {
+        e->busy_hint[r] = b;
+        e->busy_strike[r] = 0;
+    }
+}
+
+// The solo schedule of rounds r0..r0+m-1 as enqueue_round will set it (with the
+// solo kind of the round before r0), for the batch key; the host state is
+// simulated and restored.
+uint64_t solo_sched_hash(gg_engine* e, int64_t r0, uint32_t m) {
+    const bool sdb = e->db_active, sfd = e->f_dirty;
+    const int sset = e->set_cur;
+    uint64_t h = gg_mix64(0x501Dull ^ e->last_solo);
+    for (uint32_t k = 0; k < m; ++k) {
+        const bool dbk = db_round(e, r0 + k);
+        h = gg_mix64(h ^ ((uint64_t)solo_of(e, r0 + k, dbk) << 8) ^ k);
+        db_advance(e, r0 + k, dbk);
+    }
+    e->db_active = sdb;
+    e->f_dirty = sfd;
+    e->set_cur = sset;
+    e->d_base = e->d_sets[sset];
+    return h;
+}
+
 // Enqueue round e->round (kernels only). inj: device pairs for this round.
 int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned long long* d_ctr,
                   const uint32_t* d_tab = nullptr) {
@@ -1209,6 +1288,11 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         static const bool no_bll = ab_knob("GG_BLOCK_LISTS") && atoi(ab_knob("GG_BLOCK_LISTS")) == 0;  // A/B
         a.block_lists = (a.prep_in_compact && a.mark_cand && a.db && a.stream_ok && !sync_stream && !maskw &&
                          e->n_hubs == 0 && !no_bll) ? 1u : 0u;
+        // one expand kernel in a marking round when the last run of it says which
+        a.solo = a.block_lists ? solo_of(e, r, db) : 0u;
+        a.prev_mark = e->last_solo == gg::SOLO_MARK ? 1u : e->last_solo == gg::SOLO_DB ? 2u : 0u;
+        e->last_solo = a.solo;
+        if (a.solo) e->last_path |= GG_PATH_SOLO;
         if (!a.block_lists) {
             const uint64_t groups = (a.n_own + 7) / 8;  // >= tile groups
             const uint64_t per_block = (uint64_t)gg::kBlock * gg::kCompactQ;
@@ -1257,7 +1341,8 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
 // Host-side stats of one round from its 64 counter slots; per-kind times from
 // the device clock stamps (first block start .. last block end, 100 MHz).
 // slots: nslots x kCounters (kSlots raw slots, or 1 slot folded by gg::fold_slots)
-void fold_stats(gg_engine* e, const unsigned long long* slots, int64_t round, gg_round_stats* s, int nslots = gg::kSlots) {
+void fold_stats(gg_engine* e, const unsigned long long* slots, int64_t round, gg_round_stats* s, int nslots = gg::kSlots,
+                bool learn = true) {
     unsigned long long c[gg::kCounters] = {0};
     unsigned long long t0[gg::K_NKIND], t1[gg::K_NKIND];
     for (int q = 0; q < gg::K_NKIND; ++q) t0[q] = ~0ull, t1[q] = 0;
@@ -1301,6 +1386,11 @@ void fold_stats(gg_engine* e, const unsigned long long* slots, int64_t round, gg
     s->work_gathers = c[gg::C_GATHERS];
     e->pend_acks = c[gg::C_NEXT_ACKS];
     e->pend_ackdrop = c[gg::C_NEXT_ACKDROP];
+    // round + 1 is busy (the stream kernels' busy_count, from the nodes that became
+    // active in this round): the hint for which expand kernel its next run needs
+    if (learn)
+        learn_busy(e, round + 1, 2.0 * (double)c[gg::C_NACT] * (double)e->n_in_edges >=
+                                     (double)e->n_own * (double)e->n_own);
 }
 
 // Zero `bytes` (a multiple of 8, 16-byte aligned) on the engine stream with a
@@ -1432,6 +1522,7 @@ int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& o
     key.windows = e->windows.size();
     key.inj_buf = e->d_inj;
     key.db_state = (e->db_active ? 2 : 0) | e->set_cur;
+    key.solo_hash = solo_sched_hash(e, r0, m);
     {  // which rounds inject (mark_injections is launched only there), not what
         uint64_t p = gg_mix64(m);
         for (size_t k = 0; k < m; ++k) p = gg_mix64(p ^ (off[k + 1] > off[k] ? 2 * k + 1 : 2 * k));
@@ -2528,10 +2619,12 @@ int enqueue_step_batch(gg_engine* e, uint32_t m, bool wait, std::vector<uint64_t
     const int64_t save_round = e->round;
     const bool save_db = e->db_active, save_fd = e->f_dirty;
     const int save_set = e->set_cur;
+    const uint32_t save_solo = e->last_solo;
     auto enqueue_batch = [&]() -> int {
         e->db_active = save_db;  // (a failed capture may have run it once already)
         e->f_dirty = save_fd;
         e->set_cur = save_set;
+        e->last_solo = save_solo;
         e->d_base = e->d_sets[save_set];
         if (int rz = zero_async(e, e->d_counters, (size_t)m * gg::kSlots * gg::kCounters * 8)) return rz;
         for (uint32_t k = 0; k < m; ++k) {
@@ -2556,10 +2649,12 @@ int enqueue_step_batch(gg_engine* e, uint32_t m, bool wait, std::vector<uint64_t
     e->db_active = save_db;
     e->f_dirty = save_fd;
     e->set_cur = save_set;
+    e->last_solo = save_solo;
     paths.assign(m, 0);
     for (uint32_t k = 0; k < m; ++k) {
         const bool dbk = db_round(e, r0 + k);
-        paths[k] = path_of(e, r0 + k, dbk);
+        e->last_solo = solo_of(e, r0 + k, dbk);
+        paths[k] = path_of(e, r0 + k, dbk) | (e->last_solo ? GG_PATH_SOLO : 0u);
         db_advance(e, r0 + k, dbk);
     }
     return rc;
@@ -2567,10 +2662,10 @@ int enqueue_step_batch(gg_engine* e, uint32_t m, bool wait, std::vector<uint64_t
 
 // The host side of a batch's rounds once their folded counter rows are in `rows`.
 void finish_step_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<uint64_t>& paths,
-                       const unsigned long long* rows, gg_round_stats* out, bool retire) {
+                       const unsigned long long* rows, gg_round_stats* out, bool retire, bool learn = true) {
     for (uint32_t k = 0; k < m; ++k) {
         gg_round_stats s;
-        fold_stats(e, rows + (size_t)k * gg::kCounters, r0 + k, &s, 1);
+        fold_stats(e, rows + (size_t)k * gg::kCounters, r0 + k, &s, 1, learn);
         s.path = paths[k];
         e->quiet = s.new_bits ? 0 : e->quiet + 1;
         if (out) out[k] = s;
@@ -2596,6 +2691,7 @@ void reset_host_state(gg_engine* e, bool keep_schedule) {
     e->dist_open = false;
     e->u_hist.clear();
     e->u_bits.clear();
+    e->last_solo = 0;
 }
 
 }  // namespace
@@ -2677,6 +2773,10 @@ int gg_run_episodes(gg_engine* e, uint32_t n, uint32_t episodes, gg_round_stats*
             int q = 2;  // what a reset leaves
             for (uint32_t j = 0; j < n; ++j) q = e->h_counters[(size_t)j * gg::kCounters + gg::C_NEW] ? 0 : q + 1;
             quiet_end = q;
+            // and which expand kernel each marking round needs (the later episodes: one each)
+            for (uint32_t j = 0; j < n; ++j)
+                learn_busy(e, j + 1, 2.0 * (double)e->h_counters[(size_t)j * gg::kCounters + gg::C_NACT] *
+                                             (double)e->n_in_edges >= (double)e->n_own * (double)e->n_own);
         }
     }
     HIPCHK(hipEventRecord(e->ev[1], e->stream));
@@ -2692,7 +2792,7 @@ int gg_run_episodes(gg_engine* e, uint32_t n, uint32_t episodes, gg_round_stats*
         e->pend_acks = e->pend_ackdrop = 0;
         e->quiet = k ? 2 : quiet0;  // (what a reset leaves)
         finish_step_batch(e, 0, n, paths[k], e->h_ep + (size_t)k * n * gg::kCounters, out ? out + (size_t)k * n : nullptr,
-                          k + 1 == episodes);
+                          k + 1 == episodes, false);
     }
     return GG_OK;
 }
@@ -3579,10 +3679,12 @@ static int dist_step_batched(gg_engine* e, uint32_t n_rounds) {
         e->injtab_dev_hash = ~0ull;  // gg_step's table cache no longer matches d_injtab
         const bool save_db = e->db_active, save_fd = e->f_dirty;
         const int save_set = e->set_cur;
+        const uint32_t save_solo = e->last_solo;
         auto enqueue = [&]() -> int {
             e->db_active = save_db;
             e->f_dirty = save_fd;
             e->set_cur = save_set;
+            e->last_solo = save_solo;
             e->d_base = e->d_sets[save_set];
             if (int rz = zero_async(e, e->d_counters + k0 * slot, (size_t)m * slot * 8)) return rz;
             for (uint32_t k = 0; k < m; ++k) {
@@ -3603,6 +3705,7 @@ static int dist_step_batched(gg_engine* e, uint32_t n_rounds) {
         key.windows = e->windows.size();
         key.inj_buf = e->d_inj;
         key.db_state = (e->db_active ? 2 : 0) | e->set_cur;
+        key.solo_hash = solo_sched_hash(e, r0, m);
         {
             uint64_t p = gg_mix64(m);
             for (size_t k = 0; k < m; ++k) p = gg_mix64(p ^ (off[k + 1] > off[k] ? 2 * k + 1 : 2 * k));
@@ -3640,10 +3743,12 @@ static int dist_step_batched(gg_engine* e, uint32_t n_rounds) {
         e->db_active = save_db;
         e->f_dirty = save_fd;
         e->set_cur = save_set;
+        e->last_solo = save_solo;
         for (uint32_t k = 0; k < m; ++k) {
             const bool dbk = db_round(e, r0 + k);
             e->dist_round_of[k0 + k] = r0 + k;
-            e->dist_path[k0 + k] = path_of(e, r0 + k, dbk);
+            e->last_solo = solo_of(e, r0 + k, dbk);
+            e->dist_path[k0 + k] = path_of(e, r0 + k, dbk) | (e->last_solo ? GG_PATH_SOLO : 0u);
             db_advance(e, r0 + k, dbk);
             retire_round(e, r0 + k);
         }

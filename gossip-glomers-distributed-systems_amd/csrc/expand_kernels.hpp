@@ -158,6 +158,16 @@ struct RoundArgs {
     uint32_t block_lists;       // ... and no compact_round either: the marking kernel sums the
                                 // rings itself and each of its blocks lists the candidates of
                                 // its own granules of the owned nodes in LDS
+    uint32_t solo;              // marking rounds: 0 = both expand kernels are launched and each exits
+                                // when the round is the other's (busy or not, decided on the device);
+                                // SOLO_MARK / SOLO_DB = the host launched only that one (its guess
+                                // from the last run of this round: busy_count of its C_NACT), which
+                                // then takes the round whatever it finds: the marking kernel visits
+                                // every node when the round is busy, expand_stream_db every node
+                                // always; either sums round r-1's rings itself
+    uint32_t prev_mark;         // round r-1 was a solo marking round: 1 = its kernel marked round r's
+                                // candidates, 2 = it marked nothing (expand_stream_db: round r is
+                                // dense); 0 = the device decides from the act ring (busy_prev)
     uint8_t* zmark;             // [rows] F row of this parity is stale (node active 2 rounds ago)
     uint8_t* tile_cand;         // [n_tiles rounded to 8] tile has a candidate (sparse rounds)
     struct TileWork* work;      // live tiles of a sparse round (compact_round; expand_round)
@@ -347,8 +357,11 @@ __device__ __forceinline__ bool busy_round(const RoundArgs& a) {
     const double act = (double)a.act[(a.round - 1) & 3];
     return 2.0 * act * (double)a.n_edges >= (double)a.n_own * (double)a.n_own;
 }
-// Round r-1 was busy (the same test one round earlier, from the act ring).
+// Round r-1's expand marked no candidates for round r: it was busy (the same
+// test one round earlier, from the act ring: expand_stream_db took it), or the
+// host launched only expand_stream_db in it (RoundArgs::solo).
 __device__ __forceinline__ bool busy_prev(const RoundArgs& a) {
+    if (a.prev_mark) return a.prev_mark == 2;
     const double act = (double)a.act[(a.round - 2) & 3];
     return 2.0 * act * (double)a.n_edges >= (double)a.n_own * (double)a.n_own;
 }
@@ -573,6 +586,8 @@ __device__ __forceinline__ bool rings_in(const RoundArgs& a) {
     return dense;
 }
 
+constexpr uint32_t SOLO_MARK = 1, SOLO_DB = 2;
+
 // Round r-1's rings as a kernel of round r sees them. Published (rings_in ran
 // earlier in the round) or, in rounds with block lists, summed from r-1's slots
 // by every wave, with block 0 publishing them for round r+1 and clearing round
@@ -587,7 +602,7 @@ __device__ __forceinline__ RingView ring_view(const RoundArgs& a) {
     RingView v;
     const int pr = (int)((a.round - 1) & 3), p2 = (int)((a.round - 2) & 3);
     v.act_m2 = a.act[p2];
-    if (!SUM || !a.block_lists) {
+    if (!(SUM || a.solo) || !a.block_lists) {
         v.act = a.act[pr];
         v.act_deg = a.act_deg ? a.act_deg[pr] : 0ull;
         v.tot = a.tot ? a.tot[pr] : 0ull;
@@ -1592,13 +1607,17 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
     // marking rounds launch two kernels: expand_stream_db takes the busy ones
     // (every node, nothing marked) and expand_stream_db_mark the others (the
     // candidate list, or every node after a busy round; the next round's
-    // candidates marked)
-    if (!a.stream_ok || (MARK ? busy : (DB && a.mark_cand && !busy))) {
+    // candidates marked) — or only the one the host expects (solo), which then
+    // takes the round whatever it finds
+    if (!a.stream_ok || (!a.solo && (MARK ? busy : (DB && a.mark_cand && !busy)))) {
         noop_exit(a, K_STREAM, t_start);
         return;
     }
-    // dense_round(): a round without round_prep after a busy round is dense too
-    const bool dense = busy || (a.prep_in_compact && busy_count(a, rv.act_m2));
+    // dense_round(): a round without round_prep after a round whose expand marked
+    // nothing (busy, or a solo expand_stream_db) is dense too; a solo
+    // expand_stream_db round is dense (it has no candidate list)
+    const bool prev_unmarked = a.prev_mark ? a.prev_mark == 2 : busy_count(a, rv.act_m2);  // busy_prev()
+    const bool dense = busy || (DB && !MARK && a.solo) || (a.prep_in_compact && prev_unmarked);
     // block lists (sparse rounds without compact_round): thread t of block b
     // takes the 16 nodes of granule t * grid + b (one 16-byte load of candidate
     // bytes; the host sizes the grid so 256 granules a block cover every node),

@@ -123,6 +123,7 @@ DIAG_FIELDS = ("round", "kernel_ms", "work_rows", "work_gathers", "prep_ms", "ex
 # gg_round_stats.path bits (gossip.h GG_PATH_*)
 IPC_BLOB_BYTES = 1024  # gossip.h GG_IPC_BLOB_BYTES
 PATH_STREAM, PATH_DB, PATH_SYNC_STREAM, PATH_TILES, PATH_MASKED, PATH_BATCHED, PATH_NO_PREP = 1, 2, 4, 8, 16, 32, 64
+PATH_SOLO = 128
 COUNT_FIELDS = [f for f in STAT_FIELDS if f not in DIAG_FIELDS]
 
 GG_SYMBOLS = [

@@ -136,6 +136,8 @@ typedef struct {
 #define GG_PATH_BATCHED 32u     /* batched gossip (expand_batched) */
 #define GG_PATH_NO_PREP 64u     /* no round_prep launch: the previous round's expand marked this round's
                                    candidates (double-buffered rounds of a single engine before the timers) */
+#define GG_PATH_SOLO 128u       /* marking round with one expand kernel: the one the last run of this round
+                                   needed (busy or not), instead of both with one exiting at once */
 
 /* Inter-node messages of a round = fwd_sent + pushes + acks + reads + read_oks. */
 

@@ -104,3 +104,59 @@ def test_marking_rounds_equal_oracle(hip_lib, cpu_lib, monkeypatch, no_mark):
             assert (n_np > 3) if no_mark == "0" else (n_np == 0), (k, mode, [s["path"] for s in st])
             g.close()
         c.close()
+
+
+@pytest.mark.parametrize("solo", ["learned", "mark", "db", "alt"])
+def test_solo_marking_rounds_equal_oracle(hip_lib, cpu_lib, monkeypatch, solo):
+    """Solo marking rounds (GG_PATH_SOLO): once a marking round has run, the
+    engine launches only the expand kernel that run needed (the busy flag the
+    kernels report) instead of both with one exiting at once. Any schedule is
+    exact — a marking kernel in a busy round visits every node, a solo
+    expand_stream_db visits every node and the round after it is dense — so the
+    forced schedules (GG_SOLO = mark / db / alt, every marking round) must equal
+    O2 as the learned one does: three episodes per scenario (the first learns,
+    the second recaptures its batch with the schedule, the third replays it and
+    runs through gg_run_episodes), every round against O2."""
+    import random
+
+    import numpy as np
+
+    from ggamd import topology as T
+    from ggamd.engine import PATH_NO_PREP, PATH_SOLO
+    from ggamd.workload import inject, uniform_injections
+    from helpers import Scenario, diff_stats, make_engine
+    monkeypatch.setenv("GG_DB", "1")
+    if solo != "learned":
+        monkeypatch.setenv("GG_SOLO", solo)
+    rnd = random.Random(9)
+    scs = [Scenario(T.tree(6000, 4), 256, 34, uniform_injections(6000, 200, 1), seed=2, sync_base=14, sync_jitter=3),
+           Scenario(T.tree(3000, 4), 128, 30, [(n, v, v % 5) for n, v, _ in uniform_injections(3000, 100, 4)],
+                    seed=3, enable_sync=False),
+           Scenario(T.random_regular(5000, 6, seed=3), 128, 24, [(rnd.randrange(5000), v, rnd.randrange(6))
+                                                                 for v in range(120)], seed=4, sync_base=9),
+           Scenario(T.grid_links(60, seed=5), 512, 26, uniform_injections(3600, 400, 6), seed=7, enable_sync=False)]
+    for k, sc in enumerate(scs):
+        c = make_engine(cpu_lib, sc)
+        want = c.step(sc.rounds)
+        g = make_engine(hip_lib, sc, device=0)
+        runs = [g.step(sc.rounds)]
+        g.reset()
+        inject(g, sc.injections)
+        runs.append(g.step(sc.rounds))
+        g.reset()
+        inject(g, sc.injections)
+        runs += g.run_episodes(sc.rounds, 2)
+        for j, st in enumerate(runs):
+            d = diff_stats(want, st)
+            assert not d, (k, j, d[:6])
+        assert np.array_equal(g.read_bits(), c.read_bits()), k
+        assert np.array_equal(g.delivery_rounds(), c.delivery_rounds()), k
+        n_marking = sum(1 for s in runs[1] if s["path"] & PATH_NO_PREP)
+        n_solo = [sum(1 for s in st if s["path"] & PATH_SOLO) for st in runs]
+        if solo == "learned":
+            assert n_solo[0] == 0 and min(n_solo[1:]) >= 1, (k, n_solo, n_marking)
+        else:
+            assert min(n_solo) >= 1, (k, n_solo)
+        g.close()
+        c.close()
+
