@@ -953,6 +953,7 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
             fails += d
         rounds_local = [s for ep in eps_local for s in ep]
         sent = sum(s["sent_bytes"] for s in rounds_local) / max(1, len(rounds_local))
+        sent_max = max((s["sent_bytes"] for s in rounds_local), default=0)
         dinfo = eng.dist_info() if world > 1 else None
         n_own = dinfo["owned"] if dinfo else V
         nwp = next_pow2(K // 64 // (L * halves))
@@ -1028,6 +1029,7 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
             "deliveries_per_step": deliveries // args.leg_steps,
             "hbm_bytes_per_gpu": hbm, "hbm_bytes_max": max(hbm),
             "exchange_bytes_per_round_rank0": sent if world > 1 else None,
+            "exchange_bytes_densest_round_rank0": sent_max if world > 1 else None,
             "shard": dinfo, "setup_s": setup_s,
             "check": "passed" if ok else "FAILED", "checks": checks,
             "roofline": roof,

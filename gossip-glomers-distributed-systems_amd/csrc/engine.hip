@@ -206,6 +206,7 @@ struct gg_engine {
     uint8_t* d_needmark = nullptr;
     uint32_t* d_stamp = nullptr;
     uint32_t* d_xcnt = nullptr;
+    uint32_t* d_sfirst = nullptr;        // [P+1] first send entry of each peer (tile segments)
     uint32_t* d_xtk = nullptr;           // [4] last-block tickets: pack_ghosts (finish), unpack_ghosts (stale clear)
     unsigned long long* d_segbytes = nullptr;  // [2P]: bytes to each part, bytes from each part
     unsigned long long* h_segbytes = nullptr;  // pinned copy
@@ -449,6 +450,7 @@ void gg_engine::free_topology() {
     dfree(d_needmark);
     dfree(d_stamp);
     dfree(d_xcnt);
+    dfree(d_sfirst);
     dfree(d_xtk);
     dfree(d_segbytes);
     dfree(d_payload);
@@ -564,7 +566,7 @@ int reset_device_state(gg_engine* e) {
     if (e->d_dr) seg(e->d_dr, n_own * e->nw * 64 * 4, ~0ull);
     if (e->d_stamp) seg(e->d_stamp, (e->n_ghost + 1) / 2 * 8, ~0ull);
     if (e->d_needmark) seg(e->d_needmark, (e->send_off[e->P] + 7) / 8 * 8, 0);
-    if (e->d_xcnt) seg(e->d_xcnt, (e->P + 1) / 2 * 8, 0);
+    if (e->d_xcnt) seg(e->d_xcnt, (2 * e->P * 4 + 7) / 8 * 8, 0);
     ra.sync_next = e->d_sync_next;
     ra.sync_k = e->d_sync_k;
     ra.n_own = n_own;
@@ -1909,10 +1911,15 @@ static int setup_exchange(gg_engine* e) {
     e->xsoff.assign(Wd + 1, 0);
     e->xroff.assign(Wd + 1, 0);
     std::vector<gg::XchgTile> tiles;
+    // a segment holds either layout (expand_kernels.hpp: entries with heads, or the
+    // device-driven exchange's tile records + rows)
+    auto cap = [&](uint64_t n) -> uint64_t {
+        return n ? std::max<uint64_t>(16 + 2 * n * e->xstride, gg::tile_rows_off(n) + 2 * n * 8 * e->nwp) : 0;
+    };
     for (uint32_t q = 0; q < Wd; ++q) {
         const uint64_t ns = e->send_off[q + 1] - e->send_off[q], nr = e->recv_off[q + 1] - e->recv_off[q];
-        e->xsoff[q + 1] = e->xsoff[q] + (ns ? 16 + 2 * ns * e->xstride : 0);
-        e->xroff[q + 1] = e->xroff[q] + (nr ? 16 + 2 * nr * e->xstride : 0);
+        e->xsoff[q + 1] = e->xsoff[q] + cap(ns);
+        e->xroff[q + 1] = e->xroff[q] + cap(nr);
         for (uint64_t k0 = e->send_off[q]; k0 < e->send_off[q + 1]; k0 += gg::kBlock)
             tiles.push_back({q, (uint32_t)k0, (uint32_t)std::min<uint64_t>(gg::kBlock, e->send_off[q + 1] - k0),
                              (uint32_t)e->send_off[q]});
@@ -1931,7 +1938,13 @@ static int setup_exchange(gg_engine* e) {
     HIPCHK(hipMemcpy(e->d_xroff, e->xroff.data(), (Wd + 1) * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMalloc(&e->d_needmark, (e->send_off[Wd] + 7) / 8 * 8 + 8));
     HIPCHK(hipMalloc(&e->d_stamp, (e->n_ghost + 1) / 2 * 8 + 8));
-    HIPCHK(hipMalloc(&e->d_xcnt, (Wd + 1) / 2 * 8 + 8));
+    HIPCHK(hipMalloc(&e->d_xcnt, 2 * Wd * 4 + 8));  // rows (entries) per peer, then tile records per peer
+    {
+        std::vector<uint32_t> sf(Wd + 1);
+        for (uint32_t q = 0; q <= Wd; ++q) sf[q] = (uint32_t)e->send_off[q];
+        HIPCHK(hipMalloc(&e->d_sfirst, (Wd + 1) * 4));
+        HIPCHK(hipMemcpy(e->d_sfirst, sf.data(), (Wd + 1) * 4, hipMemcpyHostToDevice));
+    }
     HIPCHK(hipMalloc(&e->d_xtk, 16));
     HIPCHK(hipMemset(e->d_xtk, 0, 16));
     HIPCHK(hipMalloc(&e->d_segbytes, 2 * Wd * 8));
@@ -2912,12 +2925,13 @@ static int enqueue_pack(gg_engine* e, int64_t r, uint32_t slot) {
         pa.self = e->part;
         pa.seg_bytes = e->d_segbytes;
         pa.payload = e->d_payload + slot;
+        pa.sfirst = e->d_sfirst;
         hipLaunchKernelGGL(gg::pack_ghosts, dim3(std::min<uint32_t>(e->n_xtiles, 4096)), dim3(gg::kBlock), 0,
                            e->stream, pa);
         HIPCHK(hipGetLastError());
     } else {
         hipLaunchKernelGGL(gg::finish_pack, dim3(1), dim3(64), 0, e->stream, e->d_xcnt, e->d_xsend, e->d_xsoff, e->P,
-                           e->part, e->xstride, e->d_segbytes, e->d_payload + slot, ipc_args(e));
+                           e->part, e->xstride, e->d_segbytes, e->d_payload + slot, ipc_args(e), (uint32_t)e->nwp);
         HIPCHK(hipGetLastError());
     }
     return GG_OK;

@@ -3896,7 +3896,23 @@ __global__ void build_edge_mask(const int64_t* in_ptr, const uint32_t* in_col, u
 // {entries, payload bytes}, then entries of `stride` bytes: a 16-byte head
 // {position in the send list | XK_SET, 0, row word when nwp == 1} and the row
 // (nwp >= 2). A quiet round sends headers only.
+// The device-driven exchange (below) packs tile segments instead, with no head
+// per entry (round 5: at W = 64 the heads were half of every entry):
+//   header   {records | rows << 32, payload bytes}
+//   records  [ceil(n / 256)] slots of 80 B, one per send tile (256 consecutive
+//            send-list entries) that ships anything, in arrival order:
+//            {tile's first entry - the peer's first | first row << 32, 0,
+//             F bitmap (4 words), S bitmap (4 words)}
+//   rows     [2 n] rows of W/8 bytes (8 at W = 64): a tile's rows in entry
+//            order, F before S for one entry; entry j's F row sits at
+//            first row + (F and S bits below j), its S row one after its F row
+// so a dense round ships 8 bytes a sender row at W = 64 (plus 80 B a tile)
+// instead of 16.
 constexpr uint32_t XK_SET = 0x80000000u;
+constexpr uint32_t kTileRec = 80;  // tile record bytes
+__host__ __device__ inline uint64_t tile_rows_off(uint64_t n_entries) {  // rows area of a tile segment
+    return 16 + kTileRec * ((n_entries + kBlock - 1) / kBlock);
+}
 
 // Device-driven exchange (gg_dist_ipc_*): every engine exports one window of
 // uncached HBM — flags, then two receive buffers by the parity of the exchange
@@ -4009,18 +4025,23 @@ struct PackArgs {
     uint32_t parts, self;
     unsigned long long* seg_bytes;
     unsigned long long* payload;
+    const uint32_t* sfirst;     // [parts + 1] first send entry of each peer (tile segments)
 };
 
 __device__ __forceinline__ void finish_pack_body(uint32_t* cnt, uint8_t* out, const uint64_t* seg_off, uint32_t parts,
                                                  uint32_t self, uint32_t stride, unsigned long long* seg_bytes,
-                                                 unsigned long long* payload, const IpcArgs& ip);
+                                                 unsigned long long* payload, const IpcArgs& ip, uint32_t nwp);
 
 __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
     __shared__ uint32_t s_row[2 * kBlock], s_head[2 * kBlock];
     __shared__ uint32_t s_cnt[kBlock / 64];
-    __shared__ uint32_t s_base, s_tot;
+    __shared__ uint32_t s_base, s_tot, s_rec;
+    __shared__ unsigned long long s_bm[2][kBlock / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t cpe = x.nwp >= 2 ? 1 + x.nwp / 2 : 1;  // 16-byte chunks per entry
+    const bool tf = x.ipc.peer_win != nullptr;  // tile segments (device-driven exchange)
+    // 16-byte chunks per entry (tile segments: per row; W = 64: one 8-byte word)
+    const uint32_t cpe = tf ? (x.nwp >= 2 ? x.nwp / 2 : 1) : (x.nwp >= 2 ? 1 + x.nwp / 2 : 1);
+    const uint64_t rowb = 8ull * x.nwp;
     // a dead exchange (a wait ran out; ipc_wait, the only writer, ran before this
     // launch, so every block reads the same word): store nothing into the peers
     if (x.ipc.peer_win && ipc_failed(x.ipc.err)) return;
@@ -4046,6 +4067,13 @@ __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
             if (lane >= o) incl += y;
         }
         if (lane == 63) s_cnt[wave] = incl;
+        if (tf) {
+            const unsigned long long bf = __ballot(fa), bs = __ballot(sn);
+            if (lane == 0) {
+                s_bm[0][wave] = bf;
+                s_bm[1][wave] = bs;
+            }
+        }
         __syncthreads();
         if (threadIdx.x == 0) {
             uint32_t tot = 0;
@@ -4056,6 +4084,7 @@ __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
             }
             s_tot = tot;
             s_base = tot ? atomicAdd(&x.cnt[t.peer], tot) : 0u;
+            s_rec = (tf && tot) ? atomicAdd(&x.cnt[x.parts + t.peer], 1u) : 0u;
         }
         __syncthreads();
         uint32_t pos = s_cnt[wave] + incl - c;
@@ -4070,6 +4099,55 @@ __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
             s_head[pos] = idx | XK_SET;
         }
         __syncthreads();
+        if (tf) {
+            // the tile's record and its rows (no head per entry)
+            uint8_t* tseg = ipc_segment(x.ipc, t.peer, seq);
+            if (threadIdx.x < 5 && s_tot) {
+                ulonglong2 v;
+                if (threadIdx.x == 0) {
+                    v.x = (unsigned long long)(t.k0 - t.first) | ((unsigned long long)s_base << 32);
+                    v.y = 0;
+                } else {
+                    const int q = threadIdx.x - 1;  // bitmap words F0 F1 | F2 F3 | S0 S1 | S2 S3
+                    v.x = s_bm[q >> 1][(q & 1) * 2];
+                    v.y = s_bm[q >> 1][(q & 1) * 2 + 1];
+                }
+                *reinterpret_cast<ulonglong2*>(tseg + 16 + (uint64_t)s_rec * kTileRec + 16 * threadIdx.x) = v;
+            }
+            uint8_t* rows = tseg + tile_rows_off(x.sfirst[t.peer + 1] - x.sfirst[t.peer]);
+            for (uint32_t e = threadIdx.x; e < s_tot * cpe; e += kBlock) {
+                const uint32_t j = e / cpe, ch = e % cpe;
+                const uint32_t hd = s_head[j], rr = s_row[j];
+                const bool set = (hd & XK_SET) != 0, lag = (rr & XK_SET) != 0;
+                const uint64_t u2 = rr & ~XK_SET;
+                uint8_t* dst = rows + (uint64_t)(s_base + j) * rowb;
+                if (x.nwp == 1) {
+                    *reinterpret_cast<uint64_t*>(dst) = set ? (x.base[u2] | (lag ? x.F_cur[u2] : 0ull))
+                                                            : (x.set_prev ? x.base[u2] & ~x.set_prev[u2] : x.F_cur[u2]);
+                    continue;
+                }
+                const uint64_t o = u2 * x.nwp + 2 * ch;
+                ulonglong2 v;
+                if (set) {
+                    v = *reinterpret_cast<const ulonglong2*>(x.base + o);
+                    if (lag) {
+                        const ulonglong2 f = *reinterpret_cast<const ulonglong2*>(x.F_cur + o);
+                        v.x |= f.x;
+                        v.y |= f.y;
+                    }
+                } else if (x.set_prev) {
+                    v = *reinterpret_cast<const ulonglong2*>(x.base + o);
+                    const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(x.set_prev + o);
+                    v.x &= ~q.x;
+                    v.y &= ~q.y;
+                } else {
+                    v = *reinterpret_cast<const ulonglong2*>(x.F_cur + o);
+                }
+                *reinterpret_cast<ulonglong2*>(dst + 16 * ch) = v;
+            }
+            __syncthreads();  // LDS reuse
+            continue;
+        }
         uint8_t* seg = (x.ipc.peer_win ? ipc_segment(x.ipc, t.peer, seq) : x.out + x.seg_off[t.peer]) + 16 +
                        (uint64_t)s_base * x.stride;
         for (uint32_t e = threadIdx.x; e < s_tot * cpe; e += kBlock) {
@@ -4122,7 +4200,7 @@ __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
     }
     __syncthreads();
     if (s_last && threadIdx.x < 64) finish_pack_body(x.cnt, x.out, x.seg_off, x.parts, x.self, x.stride, x.seg_bytes,
-                                                     x.payload, x.ipc);
+                                                     x.payload, x.ipc, x.nwp);
 }
 
 // After pack_ghosts: each peer's header, its byte count for an exact-size
@@ -4131,7 +4209,7 @@ __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
 // when no tile has entries to pack)
 __device__ __forceinline__ void finish_pack_body(uint32_t* cnt, uint8_t* out, const uint64_t* seg_off, uint32_t parts,
                                                  uint32_t self, uint32_t stride, unsigned long long* seg_bytes,
-                                                 unsigned long long* payload, const IpcArgs& ip) {
+                                                 unsigned long long* payload, const IpcArgs& ip, uint32_t nwp) {
     const uint32_t q = threadIdx.x;
     unsigned long long pay = 0;
     const uint64_t seq = ip.peer_win ? *ip.seq : 0;
@@ -4140,17 +4218,24 @@ __device__ __forceinline__ void finish_pack_body(uint32_t* cnt, uint8_t* out, co
         const bool peer = q != self && seg_off[q + 1] > seg_off[q];  // segments with capacity only
         if (peer) {
             ulonglong2 h;
-            h.x = n;
-            h.y = (unsigned long long)n * stride;
+            if (ip.peer_win) {  // tile segment: records and rows
+                const uint32_t nr = cnt[parts + q];
+                h.x = (unsigned long long)nr | ((unsigned long long)n << 32);
+                h.y = (unsigned long long)nr * kTileRec + (unsigned long long)n * 8ull * nwp;
+                cnt[parts + q] = 0;
+            } else {
+                h.x = n;
+                h.y = (unsigned long long)n * stride;
+            }
             *reinterpret_cast<ulonglong2*>(ip.peer_win ? ipc_segment(ip, q, seq) : out + seg_off[q]) = h;
-            pay = (unsigned long long)n * stride;
+            pay = h.y;
             if (ip.peer_win) {  // the segment is complete at system scope: peer q may read it
                 __threadfence_system();
                 __hip_atomic_store(reinterpret_cast<uint64_t*>(ip.peer_win[q] + kWinReady) + self, seq + 1,
                                    __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
-        seg_bytes[q] = peer ? 16 + (unsigned long long)n * stride : 0ull;
+        seg_bytes[q] = peer ? 16 + pay : 0ull;
         cnt[q] = 0;
     }
     pay = wave_sum(pay);
@@ -4158,9 +4243,10 @@ __device__ __forceinline__ void finish_pack_body(uint32_t* cnt, uint8_t* out, co
 }
 
 __global__ void finish_pack(uint32_t* cnt, uint8_t* out, const uint64_t* seg_off, uint32_t parts, uint32_t self,
-                            uint32_t stride, unsigned long long* seg_bytes, unsigned long long* payload, IpcArgs ip) {
+                            uint32_t stride, unsigned long long* seg_bytes, unsigned long long* payload, IpcArgs ip,
+                            uint32_t nwp) {
     if (ip.peer_win && ipc_failed(ip.err)) return;
-    finish_pack_body(cnt, out, seg_off, parts, self, stride, seg_bytes, payload, ip);
+    finish_pack_body(cnt, out, seg_off, parts, self, stride, seg_bytes, payload, ip, nwp);
 }
 
 // Sync rounds: ghosts that fired in r-1 run their callback in r+1 and read the
@@ -4206,6 +4292,7 @@ __global__ __launch_bounds__(kBlock) void unpack_ghosts(UnpackArgs x) {
     if (x.ipc.peer_win)  // this round's receive buffer
         x.in = reinterpret_cast<const uint8_t*>(x.ipc.my_win) + kWinHdr + (seq & 1) * x.ipc.rbuf;
     // (IPC: ipc_wait ran before — every source's segment of this round has landed)
+    const bool tf = x.ipc.peer_win != nullptr;  // tile segments: s_pref counts records
     if (threadIdx.x == 0) {
         uint32_t tot = 0, m = 0;
         for (uint32_t p = 0; p < x.parts; ++p) {
@@ -4221,8 +4308,63 @@ __global__ __launch_bounds__(kBlock) void unpack_ghosts(UnpackArgs x) {
     }
     __syncthreads();
     const uint32_t m = s_src[63];
-    const uint64_t total = (uint64_t)s_pref[m] * cpe;
     uint32_t nact = 0;
+    if (tf) {
+        // one record (a send tile of 256 entries) per block iteration: item q of the
+        // tile is entry j = q / cpr, chunk q % cpr of its rows (W = 64: the row word)
+        const uint32_t cpr = x.nwp >= 2 ? x.nwp / 2 : 1, lcpr = __ffs(cpr) - 1;
+        const uint64_t rowb = 8ull * x.nwp;
+        __shared__ unsigned long long s_rb[9];  // k0 | first row << 32, F[4], S[4]
+        for (uint32_t rr = blockIdx.x; rr < s_pref[m]; rr += gridDim.x) {
+            uint32_t lo = 0, hi = m - 1;  // the source segment holding record rr
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (s_pref[mid] <= rr) lo = mid;
+                else hi = mid - 1;
+            }
+            const uint32_t p = s_src[lo];
+            const uint8_t* seg = x.in + x.seg_off[p];
+            __syncthreads();  // s_rb reuse
+            if (threadIdx.x < 9)
+                s_rb[threadIdx.x] = *reinterpret_cast<const unsigned long long*>(
+                    seg + 16 + (uint64_t)(rr - s_pref[lo]) * kTileRec + (threadIdx.x ? 8 + 8 * threadIdx.x : 0));
+            __syncthreads();
+            const uint32_t k0 = (uint32_t)s_rb[0], r0 = (uint32_t)(s_rb[0] >> 32);
+            const uint8_t* rows = seg + tile_rows_off(x.gfirst[p + 1] - x.gfirst[p]);
+            for (uint32_t q = threadIdx.x; q < ((uint32_t)kBlock << lcpr); q += kBlock) {
+                const uint32_t j = q >> lcpr, ch = q & (cpr - 1), w = j >> 6;
+                const unsigned long long bit = 1ull << (j & 63), below = bit - 1ull;
+                const bool fb = (s_rb[1 + w] & bit) != 0, sb = (s_rb[5 + w] & bit) != 0;
+                if (!fb && !sb) continue;
+                uint32_t pos = r0 + __popcll(s_rb[1 + w] & below) + __popcll(s_rb[5 + w] & below);
+                for (int ww = 0; ww < 4; ++ww)
+                    if (ww < (int)w) pos += __popcll(s_rb[1 + ww]) + __popcll(s_rb[5 + ww]);
+                const uint64_t g0 = x.gfirst[p] + k0 + j;
+                const uint64_t g = x.grow ? x.grow[g0] : g0;  // locality-ordered shards: the ghost's row
+                const uint64_t row = x.ghost0 + g;
+                if (fb) {
+                    const uint8_t* src = rows + (uint64_t)pos * rowb;
+                    if (x.nwp == 1) x.F_cur[row] = *reinterpret_cast<const uint64_t*>(src);
+                    else *reinterpret_cast<ulonglong2*>(x.F_cur + row * x.nwp + 2 * ch) =
+                             *reinterpret_cast<const ulonglong2*>(src + 16 * ch);
+                    if (ch == 0) {
+                        x.flg_cur[row] = FL_ACT;
+                        x.stamp[g] = x.round;
+                        ++nact;
+                        if (x.cand_mark)
+                            for (int64_t qq = x.gout_ptr[g]; qq < x.gout_ptr[g + 1]; ++qq) x.cand_mark[x.gout_col[qq]] = CA_NODE;
+                    }
+                }
+                if (sb) {
+                    const uint8_t* src = rows + (uint64_t)(pos + (fb ? 1 : 0)) * rowb;
+                    if (x.nwp == 1) x.base[row] = *reinterpret_cast<const uint64_t*>(src);
+                    else *reinterpret_cast<ulonglong2*>(x.base + row * x.nwp + 2 * ch) =
+                             *reinterpret_cast<const ulonglong2*>(src + 16 * ch);
+                }
+            }
+        }
+    }
+    const uint64_t total = tf ? 0ull : (uint64_t)s_pref[m] * cpe;
     for (uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x; e < total; e += (uint64_t)gridDim.x * kBlock) {
         const uint32_t j = (uint32_t)(e / cpe), ch = (uint32_t)(e % cpe);
         uint32_t lo = 0, hi = m - 1;  // the source segment holding entry j
