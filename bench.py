@@ -895,6 +895,8 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
             for j, f in enumerate(COUNT_FIELDS):
                 g[f] = tot[1 + j] & M64
             check.append(g)
+            if len(check) % 5 == 0:
+                log(f"checking episode: round {len(check) - 1}, {g['new_bits']} deliveries")
             if (g["new_bits"] == 0 and len(check) > 1) or len(check) >= 120:
                 break
         R = len(check)
@@ -1164,6 +1166,9 @@ def main():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 "
                     "(nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
     args = ap.parse_args()
+    if os.environ.get("GG_BENCH_WATCHDOG"):  # stacks of every thread every N seconds (hang diagnosis)
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["GG_BENCH_WATCHDOG"]), repeat=True, file=sys.stderr)
 
     job = Job(args.backend, args.gpus)
     out, info = headline(job, args)

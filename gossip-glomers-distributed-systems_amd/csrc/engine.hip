@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <chrono>
 #include <cstring>
 #include <map>
 #include <string>
@@ -3290,12 +3291,21 @@ int gg_dist_ipc_import(gg_engine* e, const uint8_t* blobs) {
     std::vector<uint64_t> off(P, 0), rb(P, 0);
     e->peer_map.assign(P, nullptr);
     e->send_mask = e->recv_mask = 0;
+    const bool dbg = test_knob("GG_IPC_DEBUG") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto note = [&](const char* what, uint32_t q) {
+        if (dbg)
+            std::fprintf(stderr, "gg_dist_ipc_import part %u: %s %u at %.3f s\n", e->part, what, q,
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+    };
     for (uint32_t q = 0; q < P; ++q) {
         const bool snd = q != e->part && e->xsoff[q + 1] > e->xsoff[q];
         const bool rcv = q != e->part && e->xroff[q + 1] > e->xroff[q];
         if (!snd && !rcv) continue;
         void* m = nullptr;
+        note("open", q);
         HIPCHK(hipIpcOpenMemHandle(&m, b[q].handle, hipIpcMemLazyEnablePeerAccess));
+        note("opened", q);
         e->peer_map[q] = m;
         win[q] = static_cast<uint8_t*>(m);
         off[q] = b[q].roff[e->part];
@@ -3309,6 +3319,7 @@ int gg_dist_ipc_import(gg_engine* e, const uint8_t* blobs) {
     HIPCHK(hipMemcpy(e->d_peer_win, win.data(), P * sizeof(uint8_t*), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->d_peer_off, off.data(), P * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->d_peer_rbuf, rb.data(), P * 8, hipMemcpyHostToDevice));
+    note("tables done", P);
     e->ipc = true;
     return GG_OK;
 }

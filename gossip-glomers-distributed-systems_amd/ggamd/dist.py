@@ -310,7 +310,11 @@ def _ipc_connect(engines: list[Engine], group, rank: int, world: int, P: int) ->
     """Every process exports its engines' windows (one blob each, engines in
     lane-group order), one all_gather of the blobs, and each engine imports the
     P blobs of its own lane group in part order."""
+    import time
+
     from .engine import IPC_BLOB_BYTES
+    dbg = os.environ.get("GG_IPC_DEBUG")
+    t0 = time.perf_counter()
     err = None
     try:
         mine = b"".join(e.dist_ipc_export() for e in engines)
@@ -323,6 +327,8 @@ def _ipc_connect(engines: list[Engine], group, rank: int, world: int, P: int) ->
     got = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(got, t, group=group)
     allb = [g.cpu().numpy().tobytes() for g in got]  # allb[r][h * BLOB:]: engine h of rank r
+    if dbg:
+        print(f"_ipc_connect rank {rank}: exported and gathered in {time.perf_counter() - t0:.3f} s", flush=True)
     if err is not None:
         raise err
     B = IPC_BLOB_BYTES
