@@ -75,9 +75,20 @@ TRAFFIC_JSON = {"C2": os.path.join(REPO, "profiles", "traffic.json"),  # committ
 CPU_LIB = os.path.join(REPO, "oracle", "_build", "libgossip_cpu.so")
 GOLD_C2 = os.path.join(REPO, "tests", "golden", "bench_c2.json")
 # the random-row request ceiling (rows of <= 128 B gathered by a per-node index,
-# tools/gather_bench.hip, DESIGN.md §4): what a kernel whose rows are one line
-# each can reach, where the byte roofline cannot be
+# tools/gather_bench.hip, DESIGN.md §7): what a kernel whose rows are one line
+# each can reach, where the byte roofline cannot be. profiles/request_ceiling.json
+# holds the same ceiling in the L2's memory-side requests (TCC_EA0_RDREQ +
+# WRREQ per second of gather_bench under rocprofv3), the unit of line_frac
 ROW_CEILING_PER_S = 47e9
+REQ_CEILING_JSON = os.path.join(REPO, "profiles", "request_ceiling.json")
+
+
+def request_ceiling():
+    try:
+        d = json.load(open(REQ_CEILING_JSON))
+        return float(d["requests_per_s"]), os.path.relpath(REQ_CEILING_JSON, REPO)
+    except (OSError, ValueError, KeyError, TypeError):
+        return ROW_CEILING_PER_S, "tools/gather_bench.hip rows/s (profiles/r2/gather_ceiling.txt)"
 
 
 def pmc_traffic(kind: str, shape: dict):
@@ -92,23 +103,26 @@ def pmc_traffic(kind: str, shape: dict):
     try:
         d = json.load(open(path))
     except (OSError, ValueError, TypeError):
-        return None, None
+        return None, None, None
     if d.get("shape") != shape:
         return None, (f"{os.path.relpath(path, REPO)} profiled {d.get('shape')}, not this run's {shape}: "
-                      "no counter traffic for this shape")
+                      "no counter traffic for this shape"), None
     base = lambda name: name.split("(")[0].split("<")[0].split("::")[-1]  # noqa: E731
     ents = {}
     for name, ent in d.get("kernels", {}).items():
         b = base(name)
         if b in KIND_KERNELS[kind]:
-            e = ents.setdefault(b, [0.0, 0])
+            e = ents.setdefault(b, [0.0, 0, 0.0, "rd_requests_per_dispatch" in ent])
             e[0] += ent["traffic_bytes_per_dispatch"] * ent["dispatches"]
             e[1] += ent["dispatches"]
+            e[2] += (ent.get("rd_requests_per_dispatch", 0.0) + ent.get("wr_requests_per_dispatch", 0.0)) * \
+                ent["dispatches"]
     launches = sum(ents[k][1] for k in MAIN_KERNELS[kind] if k in ents)
     if not launches:
-        return None, None
+        return None, None, None
     per_round = sum(v[0] for v in ents.values()) / launches
-    return per_round, f'{os.path.relpath(path, REPO)} ({d.get("source", "")}; kernels {sorted(ents)})'
+    reqs = sum(v[2] for v in ents.values()) / launches if all(v[3] for v in ents.values()) else None
+    return per_round, f'{os.path.relpath(path, REPO)} ({d.get("source", "")}; kernels {sorted(ents)})', reqs
 
 
 def dense_bytes_per_round(V: int, E: int, nwp: int) -> int:
@@ -134,10 +148,13 @@ def roofline(rounds_local: list[dict], nwp: int, n_own: int, E_own: int, shape: 
     """The dominant kernel kind's roofline over a run's rounds (this rank):
     per-kind device times (first block start to last block end of each launch,
     stamped by the kernels) and the algorithmic bytes each launch had to move
-    (counted by the kernels). line_frac: the same launches priced
-    as random-row requests — every row a node moved or gathered is
-    ceil(row bytes / 128) lines — against the measured random-row ceiling;
-    the byte roofline is out of reach for gathers of rows this small."""
+    (counted by the kernels). line_frac: the kind's memory-side
+    requests per second (TCC_EA0_RDREQ + WRREQ per round from the committed
+    PMC pass of this shape, over the kind's measured time per round) against
+    the same counters' rate at the random-row ceiling (gather_bench): random
+    rows of <= 128 B are request-bound, so the byte roofline is out of reach
+    for them. Without a request pass for this shape: a row model from the
+    kernels' work counters (line_source says which)."""
     kinds = {}
     n = max(1, len(rounds_local))
     for kind, name in KERNELS.items():
@@ -149,7 +166,8 @@ def roofline(rounds_local: list[dict], nwp: int, n_own: int, E_own: int, shape: 
                        "avg_launch_ms": ms / n, "GBps": by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0}
     dom = max(kinds, key=lambda k: kinds[k]["total_ms"])
     D = kinds[dom]
-    traffic, traffic_src = pmc_traffic(dom, shape)
+    traffic, traffic_src, reqs = pmc_traffic(dom, shape)
+    ceiling, ceiling_src = request_ceiling()
     lines_per_row = max(1, (8 * nwp + 127) // 128)
     # rows moved by the round's kernels: gathered sender rows + own row read + row written
     rows = sum(s["work_gathers"] + 2 * s["work_rows"] for s in rounds_local)
@@ -171,7 +189,12 @@ def roofline(rounds_local: list[dict], nwp: int, n_own: int, E_own: int, shape: 
         "avg_launch_ms": D["avg_launch_ms"],
         "launches": D["launches"],
         "dense_bytes_per_round": dense_bytes_per_round(n_own, E_own, nwp),
-        "line_frac": lines_per_s / ROW_CEILING_PER_S,
+        "line_frac": ((reqs / (D["avg_launch_ms"] * 1e-3) / ceiling) if reqs and D["avg_launch_ms"] > 0
+                      else lines_per_s / ROW_CEILING_PER_S),
+        "line_source": (f"PMC: {reqs:.4g} memory-side requests per round of this kind ({traffic_src}) over "
+                        f"{D['avg_launch_ms']:.4g} ms, against {ceiling:.4g} requests/s ({ceiling_src})" if reqs
+                        else "row model (no request pass for this shape): line_model"),
+        "requests_per_launch": reqs,
         "line_model": {"rows_moved": rows, "lines_per_row": lines_per_row, "line_bytes": 128,
                        "lines_per_s": lines_per_s, "ceiling_lines_per_s": ROW_CEILING_PER_S,
                        "over": "every kernel of the timed rounds (round device time)",
@@ -1136,6 +1159,8 @@ def o1_c1_leg():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C2", choices=["C2", "C4"])
+    ap.add_argument("--no-headline", action="store_true",
+                    help="legs only (profiling a leg's kernels alone); the JSON line then carries only the legs")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
@@ -1171,7 +1196,10 @@ def main():
         faulthandler.dump_traceback_later(float(os.environ["GG_BENCH_WATCHDOG"]), repeat=True, file=sys.stderr)
 
     job = Job(args.backend, args.gpus)
-    out, info = headline(job, args)
+    if args.no_headline:
+        out, info = {"note": "--no-headline: legs only"}, {"xchg": args.xchg}
+    else:
+        out, info = headline(job, args)
     legs_arg = args.legs if args.legs is not None else ("C4,C5" if args.config == "C2" else "none")
     names = [x.strip().upper() for x in legs_arg.split(",") if x.strip() and x.strip().lower() != "none"]
     legs = {}

@@ -50,7 +50,8 @@ constexpr int kMaxBlocks = 2048;
 // lean rounds whatever the free memory), GG_SYNC_EAGER / GG_SYNC_ALLOC_ROUND (the
 // streamed-sync buffers with the topology / from a given round), GG_COMPACT_ATOMIC /
 // GG_COMPACT_SPLIT (one-launch or split compaction whatever the size),
-// GG_IPC_SPIN_LIMIT (sleeps before a device-driven exchange wait gives up).
+// GG_IPC_SPIN_LIMIT (sleeps before a device-driven exchange wait gives up), GG_LSAT=0 / 1
+// (lean saturation digest off / on whatever the graph).
 const char* test_knob(const char* name) { return getenv(name); }
 // A/B switches of past measurements (GG_ALL_FULL, GG_NO_GRAPH, GG_SYNC_ALLPUSH,
 // GG_FLAGS_FIRST, GG_FF_FRAC16, GG_PREP_WIDE, GG_XCHG_EXACT_BYTES): read only in a -DGG_AB_KNOBS build.
@@ -295,6 +296,10 @@ struct gg_engine {
     uint8_t* d_pushany = nullptr;    // [rows] a streamed callback pushed to some peer
     uint2* d_nmeta = nullptr;        // [n_own] node list with the nodes' bytes (streamed sync rounds)
     uint64_t* d_sat_new = nullptr;   // [rows/64] its bits found in the current round
+    uint8_t* d_lsat = nullptr;       // [rows] lean-round saturation digest (RoundArgs::lsat)
+    uint32_t* d_llab = nullptr;      // [n_own] component labels (the digest's targets; several components)
+    uint32_t* d_lccnt = nullptr;     // [rows] lanes injected per component label this episode
+    uint32_t* d_lreach = nullptr;    // [rows] per node: lanes injected into its component
     std::vector<uint32_t> u_hist;    // u_hist[r]: lanes of this engine injected in rounds <= r
     std::vector<uint64_t> u_bits;    // those lanes (nw words)
     bool sync_tiles = false;         // GG_SYNC_TILES=1: sync rounds on the tile path (A/B)
@@ -410,6 +415,10 @@ void gg_engine::free_topology() {
     dfree(d_ibits);
     dfree(d_sat);
     dfree(d_sat_new);
+    dfree(d_lsat);
+    dfree(d_llab);
+    dfree(d_lccnt);
+    dfree(d_lreach);
     dfree(d_pushany);
     dfree(d_nmeta);
     dfree(d_pend);
@@ -558,6 +567,8 @@ int reset_device_state(gg_engine* e) {
         seg(e->d_sat, e->rows / 8, 0);
         seg(e->d_sat_new, e->rows / 8, 0);
     }
+    if (e->d_lsat) seg(e->d_lsat, e->rows, 0);
+    if (e->d_lccnt) seg(e->d_lccnt, e->rows * 4, 0);
     if (e->d_hlive) seg(e->d_hlive, (e->n_hubs + 7) / 8 * 8, 0);
     if (e->d_pend) {
         seg(e->d_pend, e->rows * e->nwp * 8, 0);
@@ -1160,6 +1171,20 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         a.usat = lanes_through(e, r);
         a.sat_reset = (r == 0 || a.usat != lanes_through(e, r - 1)) ? 1u : 0u;
     }
+    a.lsat = nullptr;
+    a.lusat = 0;
+    a.lreach = e->d_lreach;
+    a.llab = e->d_llab;
+    a.lccnt = e->d_lccnt;
+    if (e->d_lsat) {
+        // lean saturation digest: a bit is set when the node's set holds every
+        // lane injected through the round that set it; lanes injected in r-1 >= 1
+        // void the older bits (those of r-1 too: it only costs their skips)
+        a.lsat = e->d_lsat;
+        a.lusat = lanes_through(e, r);
+        if (r >= 2 && lanes_through(e, r - 1) != lanes_through(e, r - 2))
+            if (int rz = zero_async(e, e->d_lsat, e->rows)) return rz;
+    }
     a.n_mchunks = e->n_mchunks;
     a.fired_m1 = e->d_fired[(r - 1) & 3];
     a.fired_m2 = e->d_fired[(r - 2) & 3];
@@ -1284,6 +1309,11 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         if (n_inj) {
             hipLaunchKernelGGL(gg::mark_injections, dim3(gg::kMarkInjBlocks), dim3(256), 0, e->stream, a);
             HIPCHK(hipGetLastError());
+            if (e->d_lreach) {  // the lean digest's per-node targets after this round's injections
+                hipLaunchKernelGGL(gg::lreach_fill, dim3((unsigned)std::min<uint64_t>((a.n_own + 255) / 256, 8192)),
+                                   dim3(256), 0, e->stream, e->d_llab, e->d_lccnt, e->d_lreach, a.n_own);
+                HIPCHK(hipGetLastError());
+            }
         }
         // block lists (RoundArgs::block_lists): a marking round needs
         // no compact_round — its two double-buffered expand kernels list their
@@ -1750,6 +1780,64 @@ static uint32_t hub_threshold() {
     return 512;
 }
 
+// Component labels of a symmetric single engine (gg::cc_*): passes until one
+// changes nothing. With one component the digest's target stays lusat (no
+// arrays); with several, lccnt / lreach hold the per-component targets.
+static int lsat_components(gg_engine* e) {
+    const uint64_t n = e->n_own;
+    HIPCHK(hipMalloc(&e->d_llab, n * 4));
+    uint32_t* d_ch = nullptr;
+    HIPCHK(hipMalloc(&d_ch, 16));
+    const unsigned blocks = (unsigned)std::min<uint64_t>((n + 255) / 256, 16384);
+    hipLaunchKernelGGL(gg::cc_init, dim3(blocks), dim3(256), 0, e->stream, e->d_llab, n);
+    const uint32_t hub_deg = e->n_hubs ? e->hub_deg : 0u;
+    int rc = GG_OK;
+    for (int pass = 0;; ++pass) {
+        uint32_t h = 0;
+        if (hipMemsetAsync(d_ch, 0, 4, e->stream) != hipSuccess) { rc = GG_EIO; break; }
+        hipLaunchKernelGGL(gg::cc_pass, dim3(blocks), dim3(256), 0, e->stream, e->d_in_ptr, e->d_in_col, e->d_llab, n,
+                           hub_deg, d_ch);
+        if (e->n_hubs)
+            hipLaunchKernelGGL(gg::cc_hubs, dim3((unsigned)std::min<uint64_t>(e->n_hchunks, 16384)), dim3(gg::kBlock),
+                               0, e->stream, e->d_hchunks, e->n_hchunks, e->d_in_col, e->d_llab, d_ch);
+        for (int j = 0; j < 2; ++j)
+            hipLaunchKernelGGL(gg::cc_jump, dim3(blocks), dim3(256), 0, e->stream, e->d_llab, n, d_ch);
+        if (hipGetLastError() != hipSuccess || hipMemcpyAsync(&h, d_ch, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+            hipStreamSynchronize(e->stream) != hipSuccess) {
+            rc = GG_EIO;
+            break;
+        }
+        if (!h) break;
+        if (pass > 100000) {
+            rc = GG_EIO;
+            break;
+        }
+    }
+    unsigned long long roots = 0;
+    if (rc == GG_OK) {
+        unsigned long long* d_r = reinterpret_cast<unsigned long long*>(d_ch + 2);
+        if (hipMemsetAsync(d_r, 0, 8, e->stream) != hipSuccess) rc = GG_EIO;
+        hipLaunchKernelGGL(gg::cc_roots, dim3(blocks), dim3(256), 0, e->stream, e->d_llab, n, d_r);
+        if (rc || hipMemcpyAsync(&roots, d_r, 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+            hipStreamSynchronize(e->stream) != hipSuccess)
+            rc = GG_EIO;
+    }
+    (void)hipFree(d_ch);
+    if (rc) {
+        e->err = "lean digest: component labels failed";
+        return rc;
+    }
+    if (roots <= 1) {
+        dfree(e->d_llab);
+        return GG_OK;
+    }
+    HIPCHK(hipMalloc(&e->d_lccnt, e->rows * 4));
+    HIPCHK(hipMemsetAsync(e->d_lccnt, 0, e->rows * 4, e->stream));
+    HIPCHK(hipMalloc(&e->d_lreach, e->rows * 4));
+    HIPCHK(hipMemsetAsync(e->d_lreach, 0, e->rows * 4, e->stream));
+    return GG_OK;
+}
+
 // Hubs, per-node state and the episode reset after the in-lists are on the
 // device. iptr/optr: host copies of the in-/out-list pointers (optr null:
 // symmetric, out-lists = in-lists); iptr null: the caller has checked that no
@@ -1812,6 +1900,10 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     dfree(e->d_ibits);
     dfree(e->d_sat);
     dfree(e->d_sat_new);
+    dfree(e->d_lsat);
+    dfree(e->d_llab);
+    dfree(e->d_lccnt);
+    dfree(e->d_lreach);
     dfree(e->d_pushany);
     dfree(e->d_nmeta);
     dfree(e->d_pend);
@@ -1864,6 +1956,21 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
         const char* q = ab_knob("GG_FF_FRAC16");
         e->ff_frac16 = q ? (uint32_t)std::max(1, atoi(q)) : 8u;
         if (e->ff_ok) HIPCHK(hipMalloc(&e->d_abits, e->rows / 8));
+    }
+    // lean-round saturation digest (RoundArgs::lsat; W >= 128) on graphs with hubs:
+    // there the hubs — most of the in-edges — saturate rounds before the last
+    // delivery round (C4 1190 -> 840 ms/step); on a tree nodes saturate only in
+    // the last delivery rounds and the marking costs more than the skips save
+    // (C2 +5-8 %, profiles/r5/INDEX.md). GG_LSAT=1 / 0 forces it on / off.
+    const char* lk = test_knob("GG_LSAT");
+    if (e->nwp >= 2 && (lk ? atoi(lk) != 0 : e->n_hubs > 0)) {
+        HIPCHK(hipMalloc(&e->d_lsat, e->rows));
+        HIPCHK(hipMemsetAsync(e->d_lsat, 0, e->rows, e->stream));
+        // targets per component when there are several (a node never holds a lane
+        // injected outside its component: R-MAT's isolated nodes and small
+        // components keep every node of the giant one below "every lane")
+        if (e->symmetric && e->P <= 1 && e->n_ghost == 0 && n_own > 1)
+            if (int rc = lsat_components(e)) return rc;
     }
     HIPCHK(hipMalloc(&e->d_base, rowbytes));
     e->d_sets[0] = e->d_base;
@@ -4089,7 +4196,7 @@ int gg_device_bytes(const gg_engine* e, uint64_t* total, uint64_t* sync_part) {
         e->d_out_col == e->d_in_col ? nullptr : e->d_out_col, e->d_sets[0] ? e->d_sets[0] : e->d_base,
         e->d_sets[1], e->d_F[0], e->d_F[1], e->d_flg[0], e->d_flg[1], e->d_cand, e->d_zmark, e->d_tile_cand,
         e->d_work, e->d_n_work, e->d_bcount, e->d_nodes, e->d_act, e->d_act_deg, e->d_tot, e->d_act_s,
-        e->d_act_deg_s, e->d_tot_s, e->d_abits, e->d_hubs, e->d_hub_c0, e->d_hchunks, e->d_mchunks, e->d_pend,
+        e->d_act_deg_s, e->d_tot_s, e->d_abits, e->d_lsat, e->d_llab, e->d_lccnt, e->d_lreach, e->d_hubs, e->d_hub_c0, e->d_hchunks, e->d_mchunks, e->d_pend,
         e->d_pend_src, e->d_bset[0], e->d_bset[1], e->d_hscratch, e->d_hflag, e->d_hlive, e->d_fired[0],
         e->d_fired[1], e->d_fired[2], e->d_fired[3], e->d_sync_next, e->d_sync_k, e->d_dr, e->d_counters,
         e->d_inj, e->d_injtab};

@@ -240,6 +240,18 @@ struct RoundArgs {
                                 // and hold injected lanes only, so it stays true until a new
                                 // lane is injected (sat_reset). Owned rows; ghosts stay 0.
     uint64_t* sat_new;          // [rows/64] bits found this round (merged by the next round_prep)
+    uint8_t* lsat;              // [rows] lean rounds (W >= 128), or nullptr: 1 = the owned node's set
+                                // held every lane injected through the round that set it (lusat then).
+                                // Sets only grow and hold injected lanes only, and the host clears the
+                                // digest after any later injection, so a set bit means the node's set
+                                // of r-1 holds every lane any sender row of r-1 can carry: it gathers
+                                // nothing (expand_stream, hub_chunks, hub_finish skip its in-edges)
+    uint32_t lusat;             // lanes of this engine's range injected in rounds <= r
+    const uint32_t* lreach;     // [n_own] the lanes injected through r whose source lies in the node's
+                                // component (symmetric single engines with several components), or
+                                // nullptr: lusat for every node. A set never holds more (§4.2)
+    const uint32_t* llab;       // [n_own] component label (a node id), with lreach
+    uint32_t* lccnt;            // [n_own] by label: lanes injected into the component so far
     uint32_t usat;              // lanes of this engine's range injected in rounds <= r
     uint32_t sat_reset;         // usat grew this round: every digest bit is void
     const uint64_t* fired_m1;   // sync-fired bitmaps of rounds r-1, r-2, r-3
@@ -461,6 +473,113 @@ __device__ __forceinline__ void sat_mark(const RoundArgs& a, const Row<WPL>& S, 
 #pragma unroll
     for (int o = G / 2; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
     if (lg == 0 && c == a.usat) atomicOr(a.sat_new + (rep >> 6), 1ull << (rep & 63));
+}
+
+// Lean saturation digest: a node group whose node's set changed this round
+// counts it and sets the node's bit when it holds every lane injected so far.
+// Group-uniform call.
+// Sum over a node group of G lanes (G-aligned), every lane gets it: DPP moves
+// inside 16-lane rows (quad swaps, half-row and row mirrors: VALU only), a
+// cross-lane permute only past 16 lanes (ds_bpermute goes through the LDS unit
+// and its counter; five of them per changed node cost C2's dense rounds ~10 %).
+#ifndef GG_LSAT_DPP
+#define GG_LSAT_DPP 1
+#endif
+template <int G>
+__device__ __forceinline__ uint32_t group_sum(uint32_t x) {
+#if GG_LSAT_DPP
+    if constexpr (G >= 2) x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+    if constexpr (G >= 4) x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
+    if constexpr (G >= 8) x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    if constexpr (G >= 16) x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false); // row_mirror
+    if constexpr (G >= 32) x += (uint32_t)__shfl_xor((int)x, 16, 64);
+    if constexpr (G >= 64) x += (uint32_t)__shfl_xor((int)x, 32, 64);
+#else
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o, 64);
+#endif
+    return x;
+}
+
+template <int G, int WPL>
+__device__ __forceinline__ void lsat_mark(const RoundArgs& a, const Row<WPL>& S, uint64_t rep, int lg, uint32_t tgt) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int w = 0; w < WPL; ++w) c += (uint32_t)__popcll(S.w[w]);
+    c = group_sum<G>(c);
+    // a plain byte store: a bitmap word took 64 same-address atomics when a run of
+    // consecutive nodes saturated in one round (C2 +11 %)
+    if (lg == 0 && c == tgt) a.lsat[rep] = 1;
+}
+
+// Component labels for the lean digest's targets (symmetric single engines, at
+// topology install): min-label propagation pulled over the in-lists (= out-lists)
+// with pointer jumping, until a pass changes nothing. Labels only decrease and
+// stay inside the component, so in-place updates (and atomicMin for hubs) are safe.
+__global__ void cc_init(uint32_t* lab, uint64_t n) {
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
+        lab[v] = (uint32_t)v;
+}
+// one thread per node of in-degree <= hub_deg (hubs: cc_hubs)
+__global__ void cc_pass(const int64_t* in_ptr, const uint32_t* in_col, uint32_t* lab, uint64_t n, uint32_t hub_deg,
+                        uint32_t* changed) {
+    bool ch = false;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
+        const int64_t p0 = in_ptr[v], p1 = in_ptr[v + 1];
+        if (hub_deg && p1 - p0 > (int64_t)hub_deg) continue;
+        const uint32_t l0 = lab[v];
+        uint32_t m = l0;
+        for (int64_t e = p0; e < p1; ++e) m = min(m, lab[in_col[e] & kColMask]);
+        if (m < l0) {
+            lab[v] = m;
+            ch = true;
+        }
+    }
+    if (ch) *changed = 1u;
+}
+// a block per hub in-edge chunk: the chunk's smallest label, atomicMin into the hub
+__global__ __launch_bounds__(kBlock) void cc_hubs(const HubChunk* ch, uint64_t n_ch, const uint32_t* in_col,
+                                                  uint32_t* lab, uint32_t* changed) {
+    __shared__ uint32_t s_m[kBlock / 64];
+    for (uint64_t c = blockIdx.x; c < n_ch; c += gridDim.x) {
+        const HubChunk hc = ch[c];
+        uint32_t m = ~0u;
+        for (uint32_t k = threadIdx.x; k < hc.n; k += kBlock) m = min(m, lab[in_col[hc.e0 + k] & kColMask]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o, 64));
+        if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < kBlock / 64; ++w) m = min(m, s_m[w]);
+            if (m < atomicMin(lab + hc.node, m)) *changed = 1u;
+        }
+        __syncthreads();
+    }
+}
+__global__ void cc_jump(uint32_t* lab, uint64_t n, uint32_t* changed) {
+    bool ch = false;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t l = lab[v], ll = lab[l];
+        if (ll < l) {
+            lab[v] = ll;
+            ch = true;
+        }
+    }
+    if (ch) *changed = 1u;
+}
+// components = nodes that are their own label
+__global__ void cc_roots(const uint32_t* lab, uint64_t n, unsigned long long* roots) {
+    unsigned long long c = 0;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
+        c += lab[v] == (uint32_t)v ? 1u : 0u;
+    c = wave_sum(c);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(roots, c);
+}
+
+// A node of the lean digest gathers nothing this round: saturated and no client
+// broadcast to it (one would change its set: forwards and marks need its degree)
+__device__ __forceinline__ bool lsat_skip(const RoundArgs& a, uint64_t rep, uint8_t ca) {
+    return a.lsat && !(ca & CA_INJ) && a.lsat[rep];
 }
 
 // The digest's first bits: one pass over every owned row at the start of the
@@ -971,7 +1090,17 @@ __global__ void mark_injections(RoundArgs a) {
         const uint64_t i = p[2 * k];
         a.cand[a.own0 + i] |= CA_NODE | CA_INJ;  // same value from every thread of a node
         if (!a.stream_ok) a.tile_cand[i / a.tile_nodes] = 1;  // lean rounds use the node list
+        // the lean digest's component targets: one per pair (a value broadcast twice
+        // into one component counts twice, so that target is never reached: no skip)
+        if (a.lccnt) atomicAdd(a.lccnt + a.llab[i], 1u);
     }
+}
+
+// The lean digest's per-node targets after a round's injections: lreach[v] =
+// lanes injected so far into v's component (lccnt by label).
+__global__ void lreach_fill(const uint32_t* lab, const uint32_t* ccnt, uint32_t* lreach, uint64_t n) {
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
+        lreach[v] = ccnt[lab[v]];
 }
 constexpr unsigned kMarkInjBlocks = 16;
 
@@ -1774,6 +1903,8 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
     auto fetch_meta = [&](uint32_t n, Meta& m) {
         m.node = n;
         if (n < a.n_own) {
+            // the digest byte is loaded with the rest (no load waits on another here)
+            const uint8_t sb = (!MASKW && a.lsat) ? a.lsat[a.own0 + n] : (uint8_t)0;
             m.p0 = a.in_ptr[n];
             m.deg = (uint32_t)(a.in_ptr[n + 1] - m.p0);
             m.ca = a.cand[a.own0 + n];      // CA_INJ: client broadcasts this round
@@ -1784,6 +1915,8 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             if (a.hub_deg && m.deg > a.hub_deg) {  // a hub: hub_chunks/hub_finish take it
                 m.node |= kHubBit;
                 m.deg = 0;
+            } else if (sb && !(m.ca & CA_INJ)) {
+                m.deg = 0;  // saturated (lsat_skip): no gathers, no forwards, marks nobody
             }
         } else {
             m.p0 = 0;
@@ -1823,6 +1956,8 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         // and the words of the window bitmaps covering its first D in-edges)
         // (an all-full double-buffered round: every owned set is the same, row 0's)
         if (!hub && !full) dma16((const void*)((db ? a.base_prev : a.base) + rep * a.nwp + off), my + D * 1024);
+        // the lean digest's target, loaded with the DMAs (waited for with them)
+        const uint32_t tgt = (!MASKW && a.lreach && !hub) ? a.lreach[rep] : a.lusat;
         uint64_t mw[3][2];
         if constexpr (MASKW) {
 #pragma unroll
@@ -1981,6 +2116,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             }
         }
         const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
+        if (!MASKW && any && a.lsat) lsat_mark<G, WPL>(a, S, rep, lg, tgt);
         const bool zm = !db && (m0.fl & FL_ACT) != 0;  // F row of round r-2 in this buffer
         // rows written this round are read next round from HBM anyway (F by
         // other nodes' gathers, base by this node): streamed past the caches,
@@ -3174,7 +3310,9 @@ __global__ __launch_bounds__(kBlock) void hub_chunks(RoundArgs a) {
     unsigned long long c_bytes = 0;
     for (uint64_t c = blockIdx.x; c < a.n_hchunks; c += gridDim.x) {
         const HubChunk hc = a.hchunks[c];
-        if (!dense && !a.cand[hc.node]) continue;  // block-uniform
+        const uint8_t hca = a.cand[a.own0 + hc.node];
+        if (!dense && !hca) continue;  // block-uniform
+        if (lsat_skip(a, a.own0 + hc.node, hca)) continue;  // saturated hub (hub_finish skips its chunks)
         const uint32_t per = (hc.n + NGB - 1) / NGB;
         const int64_t e0 = hc.e0 + (int64_t)j * per;
         const int64_t e1 = min(hc.e0 + (int64_t)hc.n, e0 + (int64_t)per);
@@ -3250,7 +3388,8 @@ __global__ __launch_bounds__(kBlock) void hub_finish(RoundArgs a) {
         const uint32_t i = a.hubs[h];
         const uint8_t ca = a.cand[i];
         if (!dense && !ca) continue;  // block-uniform
-        const uint32_t c0 = a.hub_c0[h], c1 = a.hub_c0[h + 1];
+        const bool hsat = lsat_skip(a, a.own0 + i, ca);  // hub_chunks skipped its chunks (stale hscratch)
+        const uint32_t c0 = a.hub_c0[h], c1 = hsat ? c0 : a.hub_c0[h + 1];
         const uint32_t per = (c1 - c0 + NGB - 1) / NGB;
         const uint32_t q0 = c0 + j * per, q1 = min(c1, q0 + per);
         Row<WPL> O, R;
@@ -3295,6 +3434,7 @@ __global__ __launch_bounds__(kBlock) void hub_finish(RoundArgs a) {
                 }
             }
             const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
+            if (any && a.lsat) lsat_mark<G, WPL>(a, S, rep, lg, a.lreach ? a.lreach[rep] : a.lusat);
             const uint8_t fl = a.db ? a.flg_prev[rep] : a.flg_cur[rep];  // (db: r-1, else r-2)
             const bool zm = !a.db && (fl & FL_ACT) != 0;
             const bool lane_new = [&] {
@@ -3317,10 +3457,10 @@ __global__ __launch_bounds__(kBlock) void hub_finish(RoundArgs a) {
                 if (any || fl || a.db) a.flg_cur[rep] = any ? FL_ACT : 0;
                 if (ca) a.cand[rep] = 0;
                 c_active += 1;
-                c_gathers += nin;
+                c_gathers += hsat ? 0 : nin;
                 c_nact += any ? 1 : 0;
                 c_nactdeg += any ? deg : 0;
-                c_bytes += 16 + 2 + (uint64_t)(c1 - c0) * 16 * a.nwp + 8 * a.nwp +
+                c_bytes += 16 + 2 + (hsat ? 1 : 0) + (uint64_t)(c1 - c0) * 16 * a.nwp + 8 * a.nwp +
                            ((any || zm) ? 8 * a.nwp : 0) + (any ? 8 * a.nwp + 1 : 0);
             }
         }

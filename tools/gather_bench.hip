@@ -8,6 +8,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                    \
@@ -69,6 +70,26 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&idx, n * 4));
     CK(hipMalloc(&out, 8192ull * 256 * 16));
     std::vector<uint32_t> h(n);
+    if (argc > 1 && std::string(argv[1]) == "--calibrate") {
+        // the request ceiling for bench.py's line_frac: uniformly random rows of an
+        // 8 GiB table (HBM), 64 / 128 / 512 B, K = 8; run under rocprofv3 --pmc
+        // TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum for the requests a row costs
+        // (tools/request_ceiling.py multiplies them with the rows/s printed here)
+        const uint64_t tb = 8ull << 30;
+        for (int rb : {64, 128, 512}) {
+            const uint64_t rows = tb / rb;
+            uint64_t s = 88172645463325252ull + rb;
+            auto rnd = [&]() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; };
+            for (uint64_t i = 0; i < n; ++i) h[i] = (uint32_t)(rnd() % rows);
+            CK(hipMemcpy(idx, h.data(), n * 4, hipMemcpyHostToDevice));
+            const double ms = rb == 64 ? run<4, 8>(table, idx, n, out, 4096)
+                              : rb == 128 ? run<8, 8>(table, idx, n, out, 4096) : run<32, 8>(table, idx, n, out, 4096);
+            printf("calibrate rows %3d B G=%2d rows_per_dispatch %llu rows_per_s %.4e\n", rb, rb / 16,
+                   (unsigned long long)n, n / (ms * 1e-3));
+            fflush(stdout);
+        }
+        return 0;
+    }
     // where does the row-request ceiling sit? table in L2 (2 MB), in the
     // Infinity Cache (64 MB) or in HBM (8 GB); rows in flight per lane K
     for (uint64_t tb : {2ull << 20, 64ull << 20, 8ull << 30}) {
