@@ -38,3 +38,15 @@ def cpu_lib():
 def hip_lib():
     assert os.path.exists(HIP_LIB), "libgossip_hip.so missing: run make in the package dir"
     return HIP_LIB
+
+
+@pytest.fixture(autouse=True)
+def _no_orphan_ranks():
+    """Rank processes a failed multi-process test left behind (one rank died
+    in its rendezvous, the others wait in theirs) are killed when the test
+    ends, so the run reports the failure instead of hanging at exit."""
+    yield
+    import multiprocessing
+    for p in multiprocessing.active_children():
+        p.kill()
+        p.join(10)

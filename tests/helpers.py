@@ -1,7 +1,10 @@
 """Shared drivers for the parity tests: run one scenario on any engine."""
 from __future__ import annotations
 
+import itertools
+import os
 import random
+import socket
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -167,3 +170,26 @@ def symmetric_random_scenario(rnd: random.Random, max_v=60, W=None, rounds=50, e
         ok.append(w)
     sc.windows = ok
     return sc
+
+
+_ports = itertools.count()
+
+
+def free_port() -> int:
+    """A rendezvous port below Linux's ephemeral range (32768-60999): a port the
+    OS handed out and this process closed again can be handed to one of gloo's
+    own outgoing connections before the store binds it (EADDRINUSE, seen once
+    in the GPU suite). Ports step per call and per process, and each is checked
+    by a bind first."""
+    for _ in range(4000):
+        p = 20000 + (os.getpid() * 61 + next(_ports) * 7) % 12000
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
+    raise RuntimeError("no free rendezvous port")
+

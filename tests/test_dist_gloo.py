@@ -17,11 +17,8 @@ from helpers import c1_scenario, diff_stats, make_engine, random_scenario
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from helpers import free_port
+    return free_port()
 
 
 def _worker(rank, world, port, lib, sc, q, lane_groups=1):

@@ -23,11 +23,8 @@ pytestmark = pytest.mark.gpu
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from helpers import free_port
+    return free_port()
 
 
 def _worker(rank, world, port, lib, scenarios, q, lane_groups=1, env=None, generate=False, transport=None,
