@@ -92,11 +92,14 @@ def request_ceiling():
 
 
 def pmc_traffic(kind: str, shape: dict):
-    """HBM bytes per round of a kernel kind from the committed rocprofv3 PMC
-    passes (tools/traffic.py: FETCH_SIZE and WRITE_SIZE in separate passes over
-    this same bench command, FETCH_SIZE doubled for gfx950): the sum over the
-    kind's kernels of bytes x dispatches, per dispatch of its main kernel (one
-    per round). None unless the passes profiled a run of exactly this shape
+    """HBM bytes and memory-side requests per EPISODE of a kernel kind from the
+    committed rocprofv3 PMC passes (tools/traffic.py: FETCH_SIZE, WRITE_SIZE and
+    TCC_EA0_RDREQ/WRREQ in separate passes over this same bench command,
+    FETCH_SIZE doubled for gfx950): the sum over the kind's kernels of value x
+    dispatches, over the profiled run's episodes — its reset_state dispatches
+    less the one of the topology install (one per episode; a round can launch
+    one or both of the marking-round kernels, so rounds are not countable from
+    the dispatches). None unless the passes profiled a run of exactly this shape
     (config, nodes, lanes, world, parts, halves): another run's traffic is not
     this run's."""
     path = TRAFFIC_JSON.get(shape["config"])
@@ -109,6 +112,7 @@ def pmc_traffic(kind: str, shape: dict):
                       "no counter traffic for this shape"), None
     base = lambda name: name.split("(")[0].split("<")[0].split("::")[-1]  # noqa: E731
     ents = {}
+    resets = sum(ent["dispatches"] for name, ent in d.get("kernels", {}).items() if base(name) == "reset_state")
     for name, ent in d.get("kernels", {}).items():
         b = base(name)
         if b in KIND_KERNELS[kind]:
@@ -117,12 +121,13 @@ def pmc_traffic(kind: str, shape: dict):
             e[1] += ent["dispatches"]
             e[2] += (ent.get("rd_requests_per_dispatch", 0.0) + ent.get("wr_requests_per_dispatch", 0.0)) * \
                 ent["dispatches"]
-    launches = sum(ents[k][1] for k in MAIN_KERNELS[kind] if k in ents)
-    if not launches:
+    episodes = resets - 1
+    if episodes < 1 or not ents:
         return None, None, None
-    per_round = sum(v[0] for v in ents.values()) / launches
-    reqs = sum(v[2] for v in ents.values()) / launches if all(v[3] for v in ents.values()) else None
-    return per_round, f'{os.path.relpath(path, REPO)} ({d.get("source", "")}; kernels {sorted(ents)})', reqs
+    per_ep = sum(v[0] for v in ents.values()) / episodes
+    reqs = sum(v[2] for v in ents.values()) / episodes if all(v[3] for v in ents.values()) else None
+    return per_ep, (f'{os.path.relpath(path, REPO)} ({d.get("source", "")}; kernels {sorted(ents)}; '
+                    f'{episodes} episodes)'), reqs
 
 
 def dense_bytes_per_round(V: int, E: int, nwp: int) -> int:
@@ -144,7 +149,7 @@ def cpu_counts():
     return os.cpu_count() or 1, aff or 1
 
 
-def roofline(rounds_local: list[dict], nwp: int, n_own: int, E_own: int, shape: dict) -> dict:
+def roofline(rounds_local: list[dict], nwp: int, n_own: int, E_own: int, shape: dict, episodes: int) -> dict:
     """The dominant kernel kind's roofline over a run's rounds (this rank):
     per-kind device times (first block start to last block end of each launch,
     stamped by the kernels) and the algorithmic bytes each launch had to move
@@ -166,7 +171,10 @@ def roofline(rounds_local: list[dict], nwp: int, n_own: int, E_own: int, shape: 
                        "avg_launch_ms": ms / n, "GBps": by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0}
     dom = max(kinds, key=lambda k: kinds[k]["total_ms"])
     D = kinds[dom]
-    traffic, traffic_src, reqs = pmc_traffic(dom, shape)
+    traffic_ep, traffic_src, reqs_ep = pmc_traffic(dom, shape)
+    R = n / max(1, episodes)  # rounds per episode: one launch of the kind per round
+    traffic = traffic_ep / R if traffic_ep else None
+    kind_s_ep = D["total_ms"] / max(1, episodes) * 1e-3  # the kind's device time per episode
     ceiling, ceiling_src = request_ceiling()
     lines_per_row = max(1, (8 * nwp + 127) // 128)
     # rows moved by the round's kernels: gathered sender rows + own row read + row written
@@ -189,12 +197,13 @@ def roofline(rounds_local: list[dict], nwp: int, n_own: int, E_own: int, shape: 
         "avg_launch_ms": D["avg_launch_ms"],
         "launches": D["launches"],
         "dense_bytes_per_round": dense_bytes_per_round(n_own, E_own, nwp),
-        "line_frac": ((reqs / (D["avg_launch_ms"] * 1e-3) / ceiling) if reqs and D["avg_launch_ms"] > 0
+        "line_frac": ((reqs_ep / kind_s_ep / ceiling) if reqs_ep and kind_s_ep > 0
                       else lines_per_s / ROW_CEILING_PER_S),
-        "line_source": (f"PMC: {reqs:.4g} memory-side requests per round of this kind ({traffic_src}) over "
-                        f"{D['avg_launch_ms']:.4g} ms, against {ceiling:.4g} requests/s ({ceiling_src})" if reqs
+        "line_source": (f"PMC: {reqs_ep:.4g} memory-side requests per episode of this kind ({traffic_src}) over "
+                        f"its {kind_s_ep * 1e3:.4g} ms per episode, against {ceiling:.4g} requests/s at the random-row "
+                        f"ceiling ({ceiling_src})" if reqs_ep
                         else "row model (no request pass for this shape): line_model"),
-        "requests_per_launch": reqs,
+        "requests_per_launch": reqs_ep / R if reqs_ep else None,
         "line_model": {"rows_moved": rows, "lines_per_row": lines_per_row, "line_bytes": 128,
                        "lines_per_s": lines_per_s, "ceiling_lines_per_s": ROW_CEILING_PER_S,
                        "over": "every kernel of the timed rounds (round device time)",
@@ -622,7 +631,7 @@ def headline(job: Job, args) -> tuple[dict | None, dict]:
     rounds_local = [s for ep in local_stats for s in ep]
     shape = {"config": cfg, "nodes": V // world if cfg == "C2" else V, "lanes": K, "world": world,
              "parts": args.parts if cfg == "C4" else world, "halves": len(engs)}
-    roof = roofline(rounds_local, nwp, n_own, E_own, shape)
+    roof = roofline(rounds_local, nwp, n_own, E_own, shape, args.steps)
     roof["event_ms_per_step"] = (sum(event_ms) / len(event_ms)) if event_ms else None
     roof["per_call_ms_per_step"] = per_call_ms
     roof["stamp_ms_per_step"] = sum(s["kernel_ms"] for s in rounds_local) / args.steps
@@ -983,7 +992,7 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
         n_own = dinfo["owned"] if dinfo else V
         nwp = next_pow2(K // 64 // (L * halves))
         shape = {"config": name, "nodes": V, "lanes": K, "world": world, "parts": P, "halves": halves}
-        roof = roofline(rounds_local, nwp, n_own, E_local, shape) if rank == 0 else None
+        roof = roofline(rounds_local, nwp, n_own, E_local, shape, args.leg_steps) if rank == 0 else None
         if roof is not None:
             roof["event_ms_per_step"] = event_ms
             roof["stamp_ms_per_step"] = sum(s["kernel_ms"] for s in rounds_local) / args.leg_steps

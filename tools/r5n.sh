@@ -31,5 +31,5 @@ for cfg in $1; do
   pass ${cfg}_req TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum -- "${cmd[@]}"
   out=$O/traffic_$cfg.json
   python3 tools/traffic.py $(ls $O/${cfg}_fetch/*counter_collection.csv) $(ls $O/${cfg}_write/*counter_collection.csv) \
-    "rocprofv3 --pmc passes over: ${cmd[*]:1} (r5n)" $out $cfg --req $(ls $O/${cfg}_req/*counter_collection.csv) | head -12
+    "rocprofv3 --pmc passes over: ${cmd[*]:1} (r5n)" $out $cfg --req $(ls $O/${cfg}_req/*counter_collection.csv) > $O/traffic_$cfg.txt; head -12 $O/traffic_$cfg.txt
 done
