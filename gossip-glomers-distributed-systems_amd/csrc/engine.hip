@@ -297,9 +297,14 @@ struct gg_engine {
     uint2* d_nmeta = nullptr;        // [n_own] node list with the nodes' bytes (streamed sync rounds)
     uint64_t* d_sat_new = nullptr;   // [rows/64] its bits found in the current round
     uint8_t* d_lsat = nullptr;       // [rows] lean-round saturation digest (RoundArgs::lsat)
-    uint32_t* d_llab = nullptr;      // [n_own] component labels (the digest's targets; several components)
-    uint32_t* d_lccnt = nullptr;     // [rows] lanes injected per component label this episode
-    uint32_t* d_lreach = nullptr;    // [rows] per node: lanes injected into its component
+    uint32_t* d_llab = nullptr;      // [n_own] component labels of the owned rows (several components)
+    uint32_t* d_lreach = nullptr;    // [rows] per owned row: lanes broadcast into its component
+    uint32_t* d_ltab = nullptr;      // [1 + 2 ltab_cap] (label, count) table behind d_lreach
+    uint32_t ltab_cap = 0;
+    uint64_t ltab_hash = 0;          // the table d_lreach was filled from (0: none yet)
+    std::vector<uint32_t> h_lab;     // labels on the host: by local row (single engine) or by node id
+    bool lab_global = false;         // (vertex parts: labels of the whole graph)
+    std::vector<uint64_t> lret;      // label << 32 | lane of the retired rounds' broadcasts (lane in range)
     std::vector<uint32_t> u_hist;    // u_hist[r]: lanes of this engine injected in rounds <= r
     std::vector<uint64_t> u_bits;    // those lanes (nw words)
     bool sync_tiles = false;         // GG_SYNC_TILES=1: sync rounds on the tile path (A/B)
@@ -417,8 +422,8 @@ void gg_engine::free_topology() {
     dfree(d_sat_new);
     dfree(d_lsat);
     dfree(d_llab);
-    dfree(d_lccnt);
     dfree(d_lreach);
+    dfree(d_ltab);
     dfree(d_pushany);
     dfree(d_nmeta);
     dfree(d_pend);
@@ -568,7 +573,6 @@ int reset_device_state(gg_engine* e) {
         seg(e->d_sat_new, e->rows / 8, 0);
     }
     if (e->d_lsat) seg(e->d_lsat, e->rows, 0);
-    if (e->d_lccnt) seg(e->d_lccnt, e->rows * 4, 0);
     if (e->d_hlive) seg(e->d_hlive, (e->n_hubs + 7) / 8 * 8, 0);
     if (e->d_pend) {
         seg(e->d_pend, e->rows * e->nwp * 8, 0);
@@ -850,8 +854,20 @@ uint32_t lanes_through(gg_engine* e, int64_t r) {
 
 // Round r has run: its client broadcasts are no longer needed, once the lane
 // history covers it.
+uint32_t lab_of(const gg_engine* e, uint64_t node);
+
 void retire_round(gg_engine* e, int64_t r) {
     (void)lanes_through(e, r);
+    if (e->d_ltab) {  // the digest's component counts keep the round's broadcasts
+        auto it = e->inj.find(r);
+        if (it != e->inj.end())
+            for (const auto& x : it->second) {
+                const uint64_t wd = x.lane >> 6;
+                if (wd < e->w0 || wd >= e->w0 + e->nw) continue;
+                const uint32_t l = lab_of(e, x.node);
+                if (l != ~0u) e->lret.push_back((uint64_t)l << 32 | x.lane);
+            }
+    }
     e->inj.erase(r);
 }
 
@@ -1174,15 +1190,15 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
     a.lsat = nullptr;
     a.lusat = 0;
     a.lreach = e->d_lreach;
-    a.llab = e->d_llab;
-    a.lccnt = e->d_lccnt;
     if (e->d_lsat) {
         // lean saturation digest: a bit is set when the node's set holds every
         // lane injected through the round that set it; lanes injected in r-1 >= 1
         // void the older bits (those of r-1 too: it only costs their skips)
         a.lsat = e->d_lsat;
         a.lusat = lanes_through(e, r);
-        if (r >= 2 && lanes_through(e, r - 1) != lanes_through(e, r - 2))
+        // (component targets cover the whole known schedule: ltab_sync clears the
+        // digest when they change)
+        if (!e->d_lreach && r >= 2 && lanes_through(e, r - 1) != lanes_through(e, r - 2))
             if (int rz = zero_async(e, e->d_lsat, e->rows)) return rz;
     }
     a.n_mchunks = e->n_mchunks;
@@ -1309,11 +1325,6 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         if (n_inj) {
             hipLaunchKernelGGL(gg::mark_injections, dim3(gg::kMarkInjBlocks), dim3(256), 0, e->stream, a);
             HIPCHK(hipGetLastError());
-            if (e->d_lreach) {  // the lean digest's per-node targets after this round's injections
-                hipLaunchKernelGGL(gg::lreach_fill, dim3((unsigned)std::min<uint64_t>((a.n_own + 255) / 256, 8192)),
-                                   dim3(256), 0, e->stream, e->d_llab, e->d_lccnt, e->d_lreach, a.n_own);
-                HIPCHK(hipGetLastError());
-            }
         }
         // block lists (RoundArgs::block_lists): a marking round needs
         // no compact_round — its two double-buffered expand kernels list their
@@ -1471,8 +1482,63 @@ uint32_t local_row(const gg_engine* e, uint64_t node) {
     return e->loc_of[node];
 }
 
+// A node's component label (lean digest targets), ~0u if unknown.
+uint32_t lab_of(const gg_engine* e, uint64_t node) {
+    if (e->h_lab.empty() || node >= e->V) return ~0u;
+    if (e->lab_global) return e->h_lab[node];
+    const uint32_t l = local_row(e, node);
+    return l < e->h_lab.size() ? e->h_lab[l] : ~0u;
+}
+
+// The lean digest's component targets: per label, the distinct lanes (of this
+// engine's range) broadcast into the component over the whole known schedule —
+// retired rounds and every round still listed — so a target is never below
+// what the component will receive, and equals it once every listed round has
+// run (a value sent twice into one component counts once). When the table changes (new
+// broadcasts, another episode's set) it is uploaded, every owned row's target
+// refilled and the digest cleared (its bits were judged against the old
+// targets). Called before a batch is enqueued (never while capturing).
+int ltab_sync(gg_engine* e) {
+    if (!e->d_ltab) return GG_OK;
+    std::vector<uint64_t> keys = e->lret;
+    for (const auto& kv : e->inj)
+        for (const auto& x : kv.second) {
+            const uint64_t wd = x.lane >> 6;
+            if (wd < e->w0 || wd >= e->w0 + e->nw) continue;
+            const uint32_t l = lab_of(e, x.node);
+            if (l != ~0u) keys.push_back((uint64_t)l << 32 | x.lane);
+        }
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    std::vector<std::pair<uint32_t, uint32_t>> t;
+    for (const uint64_t k : keys) {
+        const uint32_t l = (uint32_t)(k >> 32);
+        if (t.empty() || t.back().first != l) t.push_back({l, 0u});
+        ++t.back().second;
+    }
+    uint64_t h = gg_mix64(0x6c7361747461626cull ^ t.size());
+    for (const auto& p : t) h = gg_mix64(h ^ ((uint64_t)p.first << 32 | p.second));
+    h |= 1;  // (0: none yet)
+    if (h == e->ltab_hash) return GG_OK;
+    std::vector<uint32_t> buf(1, t.size() > e->ltab_cap ? gg::kTabOverflow : (uint32_t)t.size());
+    if (buf[0] != gg::kTabOverflow)
+        for (const auto& p : t) {
+            buf.push_back(p.first);
+            buf.push_back(p.second);
+        }
+    // (pageable source: the copy is staged before the call returns)
+    HIPCHK(hipMemcpyAsync(e->d_ltab, buf.data(), buf.size() * 4, hipMemcpyHostToDevice, e->stream));
+    hipLaunchKernelGGL(gg::lreach_fill_tab, dim3((unsigned)std::min<uint64_t>((e->n_own + 255) / 256, 8192)), dim3(256),
+                       0, e->stream, e->d_llab, e->d_ltab, e->d_lreach, e->n_own);
+    HIPCHK(hipGetLastError());
+    if (int rc = zero_async(e, e->d_lsat, e->rows)) return rc;
+    e->ltab_hash = h;
+    return GG_OK;
+}
+
 // Pack the owned injections of rounds [r0, r0+n) into h_inj; off[k] = first pair of round r0+k.
 size_t pack_injections(gg_engine* e, int64_t r0, uint32_t n, std::vector<size_t>& off, size_t base = 0) {
+    if (ltab_sync(e) != GG_OK) return (size_t)-1;
     off.assign(n + 1, 0);
     std::vector<std::pair<uint32_t, uint32_t>> tmp;
     for (uint32_t k = 0; k < n; ++k) {
@@ -1780,28 +1846,30 @@ static uint32_t hub_threshold() {
     return 512;
 }
 
-// Component labels of a symmetric single engine (gg::cc_*): passes until one
-// changes nothing. With one component the digest's target stays lusat (no
-// arrays); with several, lccnt / lreach hold the per-component targets.
-static int lsat_components(gg_engine* e) {
-    const uint64_t n = e->n_own;
-    HIPCHK(hipMalloc(&e->d_llab, n * 4));
+// Component labels (gg::cc_*) of a symmetric CSR of n rows into d_lab: passes
+// of pull-min (nodes of in-degree <= 256 one thread each; above, a hub chunk
+// list when there is one, else a wave per node) and pointer jumping, until one
+// changes nothing; *roots = the number of components.
+static int cc_labels(gg_engine* e, const int64_t* d_ptr, const uint32_t* d_col, uint64_t n, uint32_t* d_lab,
+                     unsigned long long* roots, const gg::HubChunk* chunks, uint64_t n_ch, uint32_t hub_deg) {
     uint32_t* d_ch = nullptr;
     HIPCHK(hipMalloc(&d_ch, 16));
     const unsigned blocks = (unsigned)std::min<uint64_t>((n + 255) / 256, 16384);
-    hipLaunchKernelGGL(gg::cc_init, dim3(blocks), dim3(256), 0, e->stream, e->d_llab, n);
-    const uint32_t hub_deg = e->n_hubs ? e->hub_deg : 0u;
+    const uint32_t split = chunks ? hub_deg : 256u;
+    hipLaunchKernelGGL(gg::cc_init, dim3(blocks), dim3(256), 0, e->stream, d_lab, n);
     int rc = GG_OK;
     for (int pass = 0;; ++pass) {
         uint32_t h = 0;
         if (hipMemsetAsync(d_ch, 0, 4, e->stream) != hipSuccess) { rc = GG_EIO; break; }
-        hipLaunchKernelGGL(gg::cc_pass, dim3(blocks), dim3(256), 0, e->stream, e->d_in_ptr, e->d_in_col, e->d_llab, n,
-                           hub_deg, d_ch);
-        if (e->n_hubs)
-            hipLaunchKernelGGL(gg::cc_hubs, dim3((unsigned)std::min<uint64_t>(e->n_hchunks, 16384)), dim3(gg::kBlock),
-                               0, e->stream, e->d_hchunks, e->n_hchunks, e->d_in_col, e->d_llab, d_ch);
+        hipLaunchKernelGGL(gg::cc_pass, dim3(blocks), dim3(256), 0, e->stream, d_ptr, d_col, d_lab, n, split, d_ch);
+        if (chunks)
+            hipLaunchKernelGGL(gg::cc_hubs, dim3((unsigned)std::min<uint64_t>(n_ch, 16384)), dim3(gg::kBlock), 0,
+                               e->stream, chunks, n_ch, d_col, d_lab, d_ch);
+        else
+            hipLaunchKernelGGL(gg::cc_pass_wide, dim3(blocks), dim3(256), 0, e->stream, d_ptr, d_col, d_lab, n, split,
+                               d_ch);
         for (int j = 0; j < 2; ++j)
-            hipLaunchKernelGGL(gg::cc_jump, dim3(blocks), dim3(256), 0, e->stream, e->d_llab, n, d_ch);
+            hipLaunchKernelGGL(gg::cc_jump, dim3(blocks), dim3(256), 0, e->stream, d_lab, n, d_ch);
         if (hipGetLastError() != hipSuccess || hipMemcpyAsync(&h, d_ch, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
             hipStreamSynchronize(e->stream) != hipSuccess) {
             rc = GG_EIO;
@@ -1813,29 +1881,49 @@ static int lsat_components(gg_engine* e) {
             break;
         }
     }
-    unsigned long long roots = 0;
     if (rc == GG_OK) {
         unsigned long long* d_r = reinterpret_cast<unsigned long long*>(d_ch + 2);
         if (hipMemsetAsync(d_r, 0, 8, e->stream) != hipSuccess) rc = GG_EIO;
-        hipLaunchKernelGGL(gg::cc_roots, dim3(blocks), dim3(256), 0, e->stream, e->d_llab, n, d_r);
-        if (rc || hipMemcpyAsync(&roots, d_r, 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+        hipLaunchKernelGGL(gg::cc_roots, dim3(blocks), dim3(256), 0, e->stream, d_lab, n, d_r);
+        if (rc || hipMemcpyAsync(roots, d_r, 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
             hipStreamSynchronize(e->stream) != hipSuccess)
             rc = GG_EIO;
     }
     (void)hipFree(d_ch);
-    if (rc) {
-        e->err = "lean digest: component labels failed";
+    if (rc) e->err = "lean digest: component labels failed";
+    return rc;
+}
+
+// The digest's per-component targets once labels are known (h_lab, d_llab set):
+// the per-row targets and their table; ltab_sync fills them.
+static int lsat_targets_alloc(gg_engine* e) {
+    e->ltab_cap = std::max<uint32_t>(64, (uint32_t)std::min<uint64_t>(4ull * e->cfg.n_lanes, 1u << 20));
+    HIPCHK(hipMalloc(&e->d_lreach, e->rows * 4));
+    HIPCHK(hipMemsetAsync(e->d_lreach, 0, e->rows * 4, e->stream));
+    HIPCHK(hipMalloc(&e->d_ltab, (1 + 2 * (size_t)e->ltab_cap) * 4));
+    HIPCHK(hipMemsetAsync(e->d_ltab, 0, 4, e->stream));
+    e->ltab_hash = 0;
+    e->lret.clear();
+    return GG_OK;
+}
+
+// Symmetric single engine: labels of its rows (its hub chunk list for the hubs).
+// One component: no targets (lusat is every node's).
+static int lsat_components(gg_engine* e) {
+    const uint64_t n = e->n_own;
+    HIPCHK(hipMalloc(&e->d_llab, n * 4));
+    unsigned long long roots = 0;
+    if (int rc = cc_labels(e, e->d_in_ptr, e->d_in_col, n, e->d_llab, &roots, e->n_hubs ? e->d_hchunks : nullptr,
+                           e->n_hchunks, e->hub_deg))
         return rc;
-    }
     if (roots <= 1) {
         dfree(e->d_llab);
         return GG_OK;
     }
-    HIPCHK(hipMalloc(&e->d_lccnt, e->rows * 4));
-    HIPCHK(hipMemsetAsync(e->d_lccnt, 0, e->rows * 4, e->stream));
-    HIPCHK(hipMalloc(&e->d_lreach, e->rows * 4));
-    HIPCHK(hipMemsetAsync(e->d_lreach, 0, e->rows * 4, e->stream));
-    return GG_OK;
+    e->h_lab.resize(n);
+    HIPCHK(hipMemcpy(e->h_lab.data(), e->d_llab, n * 4, hipMemcpyDeviceToHost));
+    e->lab_global = false;
+    return lsat_targets_alloc(e);
 }
 
 // Hubs, per-node state and the episode reset after the in-lists are on the
@@ -1902,8 +1990,12 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     dfree(e->d_sat_new);
     dfree(e->d_lsat);
     dfree(e->d_llab);
-    dfree(e->d_lccnt);
     dfree(e->d_lreach);
+    dfree(e->d_ltab);
+    e->h_lab.clear();
+    e->h_lab.shrink_to_fit();
+    e->lret.clear();
+    e->ltab_hash = 0;
     dfree(e->d_pushany);
     dfree(e->d_nmeta);
     dfree(e->d_pend);
@@ -1961,15 +2053,18 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     // there the hubs — most of the in-edges — saturate rounds before the last
     // delivery round (C4 1190 -> 840 ms/step); on a tree nodes saturate only in
     // the last delivery rounds and the marking costs more than the skips save
-    // (C2 +5-8 %, profiles/r5/INDEX.md). GG_LSAT=1 / 0 forces it on / off.
+    // (C2 +5-8 %, profiles/r5/INDEX.md). Vertex parts hold no whole component, so
+    // their targets would be every lane, which a disconnected graph never reaches:
+    // off there too. GG_LSAT=1 / 0 forces it on / off.
     const char* lk = test_knob("GG_LSAT");
-    if (e->nwp >= 2 && (lk ? atoi(lk) != 0 : e->n_hubs > 0)) {
+    const bool whole = e->symmetric && e->P <= 1 && e->n_ghost == 0;
+    if (e->nwp >= 2 && (lk ? atoi(lk) != 0 : (e->n_hubs > 0 && whole))) {
         HIPCHK(hipMalloc(&e->d_lsat, e->rows));
         HIPCHK(hipMemsetAsync(e->d_lsat, 0, e->rows, e->stream));
         // targets per component when there are several (a node never holds a lane
         // injected outside its component: R-MAT's isolated nodes and small
         // components keep every node of the giant one below "every lane")
-        if (e->symmetric && e->P <= 1 && e->n_ghost == 0 && n_own > 1)
+        if (whole && n_own > 1)
             if (int rc = lsat_components(e)) return rc;
     }
     HIPCHK(hipMalloc(&e->d_base, rowbytes));
@@ -2002,6 +2097,7 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     e->dist_open = false;
     e->u_hist.clear();
     e->u_bits.clear();
+    e->lret.clear();
     if (test_knob("GG_SYNC_EAGER") && atoi(test_knob("GG_SYNC_EAGER"))) {
         const int rc = alloc_sync(e);
         if (rc) return rc;
@@ -2332,6 +2428,45 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
 // memory (host memory: the rank's ghost ids and per-part offsets only).
 static int install_shard(gg_engine* e, gg_gen::Csr g, const std::vector<uint64_t>& plo, uint64_t* nnz_out);
 
+// The lean digest on the vertex parts of a generated graph (hub graphs by
+// default, GG_LSAT as for single engines): a component spans parts, so its
+// labels come from the whole graph, built once on this device in original ids
+// and dropped after labelling; the labels stay on the host (the broadcasts'
+// counts per component, ltab_sync) and the owned rows' on the device.
+static int lsat_parts(gg_engine* e, const gg_gen_spec* spec) {
+    const char* lk = test_knob("GG_LSAT");
+    if (!(e->nwp >= 2 && e->symmetric && e->d_gid && e->n_own && (lk ? atoi(lk) != 0 : e->n_hubs > 0))) return GG_OK;
+    gg_gen::Csr g{};
+    std::string err;
+    int rc = gg_gen::build_csr(*spec, e->stream, 0u, &g, &err);
+    if (rc) return e->fail(rc, err);
+    uint32_t* d_lab = nullptr;
+    unsigned long long roots = 0;
+    if (hipMalloc(&d_lab, e->V * 4) != hipSuccess) rc = e->fail(GG_EIO, "lean digest: label buffer");
+    if (!rc) rc = cc_labels(e, g.row_ptr, g.col, e->V, d_lab, &roots, nullptr, 0, 0);
+    (void)hipFree(g.row_ptr);
+    (void)hipFree(g.col);
+    if (!rc && !e->d_lsat) {
+        if (hipMalloc(&e->d_lsat, e->rows) != hipSuccess || hipMemsetAsync(e->d_lsat, 0, e->rows, e->stream) != hipSuccess)
+            rc = e->fail(GG_EIO, "lean digest: allocation");
+    }
+    if (!rc && roots > 1) {
+        e->h_lab.resize(e->V);
+        if (hipMemcpy(e->h_lab.data(), d_lab, e->V * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMalloc(&e->d_llab, e->n_own * 4) != hipSuccess) {
+            rc = e->fail(GG_EIO, "lean digest: labels");
+        } else {
+            e->lab_global = true;
+            hipLaunchKernelGGL(gg::llab_gather, dim3((unsigned)std::min<uint64_t>((e->n_own + 255) / 256, 8192)),
+                               dim3(256), 0, e->stream, d_lab, e->d_gid, e->d_llab, e->n_own);
+            rc = hipGetLastError() == hipSuccess ? lsat_targets_alloc(e) : GG_EIO;
+            if (rc == GG_OK) rc = hipStreamSynchronize(e->stream) == hipSuccess ? GG_OK : GG_EIO;
+        }
+    }
+    (void)hipFree(d_lab);
+    return rc;
+}
+
 static int generate_sharded(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_out) {
     const uint64_t V = e->V;
     const uint32_t P = e->P;
@@ -2343,7 +2478,8 @@ static int generate_sharded(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz
     std::string err;
     int rc = gg_gen::build_csr_rows(*spec, e->stream, 0u, lo, hi, &g, &err);
     if (rc) return e->fail(rc, err);
-    return install_shard(e, g, plo, nnz_out);
+    if ((rc = install_shard(e, g, plo, nnz_out))) return rc;
+    return lsat_parts(e, spec);
 }
 
 // A rank's own rows [plo[part], plo[part+1]) of a symmetric graph (g: row_ptr
@@ -2812,6 +2948,7 @@ void reset_host_state(gg_engine* e, bool keep_schedule) {
     e->dist_open = false;
     e->u_hist.clear();
     e->u_bits.clear();
+    e->lret.clear();
     e->last_solo = 0;
 }
 
@@ -4196,7 +4333,7 @@ int gg_device_bytes(const gg_engine* e, uint64_t* total, uint64_t* sync_part) {
         e->d_out_col == e->d_in_col ? nullptr : e->d_out_col, e->d_sets[0] ? e->d_sets[0] : e->d_base,
         e->d_sets[1], e->d_F[0], e->d_F[1], e->d_flg[0], e->d_flg[1], e->d_cand, e->d_zmark, e->d_tile_cand,
         e->d_work, e->d_n_work, e->d_bcount, e->d_nodes, e->d_act, e->d_act_deg, e->d_tot, e->d_act_s,
-        e->d_act_deg_s, e->d_tot_s, e->d_abits, e->d_lsat, e->d_llab, e->d_lccnt, e->d_lreach, e->d_hubs, e->d_hub_c0, e->d_hchunks, e->d_mchunks, e->d_pend,
+        e->d_act_deg_s, e->d_tot_s, e->d_abits, e->d_lsat, e->d_llab, e->d_lreach, e->d_ltab, e->d_hubs, e->d_hub_c0, e->d_hchunks, e->d_mchunks, e->d_pend,
         e->d_pend_src, e->d_bset[0], e->d_bset[1], e->d_hscratch, e->d_hflag, e->d_hlive, e->d_fired[0],
         e->d_fired[1], e->d_fired[2], e->d_fired[3], e->d_sync_next, e->d_sync_k, e->d_dr, e->d_counters,
         e->d_inj, e->d_injtab};

@@ -247,11 +247,9 @@ struct RoundArgs {
                                 // of r-1 holds every lane any sender row of r-1 can carry: it gathers
                                 // nothing (expand_stream, hub_chunks, hub_finish skip its in-edges)
     uint32_t lusat;             // lanes of this engine's range injected in rounds <= r
-    const uint32_t* lreach;     // [n_own] the lanes injected through r whose source lies in the node's
-                                // component (symmetric single engines with several components), or
-                                // nullptr: lusat for every node. A set never holds more (§4.2)
-    const uint32_t* llab;       // [n_own] component label (a node id), with lreach
-    uint32_t* lccnt;            // [n_own] by label: lanes injected into the component so far
+    const uint32_t* lreach;     // [n_own] lanes broadcast into the node's component over the whole known
+                                // schedule (symmetric graphs with several components: lreach_fill_tab),
+                                // or nullptr: lusat for every node. A set never holds more (§4.2)
     uint32_t usat;              // lanes of this engine's range injected in rounds <= r
     uint32_t sat_reset;         // usat grew this round: every digest bit is void
     const uint64_t* fired_m1;   // sync-fired bitmaps of rounds r-1, r-2, r-3
@@ -534,6 +532,24 @@ __global__ void cc_pass(const int64_t* in_ptr, const uint32_t* in_col, uint32_t*
             lab[v] = m;
             ch = true;
         }
+    }
+    if (ch) *changed = 1u;
+}
+// one wave per node of in-degree > deg_min (the whole graph of a vertex-part
+// engine has no hub chunk list): lanes stride the in-list, a wave minimum
+__global__ void cc_pass_wide(const int64_t* in_ptr, const uint32_t* in_col, uint32_t* lab, uint64_t n, uint32_t deg_min,
+                             uint32_t* changed) {
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
+    const int ln = threadIdx.x & 63;
+    bool ch = false;
+    for (uint64_t v = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; v < n; v += waves) {
+        const int64_t p0 = in_ptr[v], p1 = in_ptr[v + 1];
+        if (p1 - p0 <= (int64_t)deg_min) continue;  // wave-uniform
+        uint32_t m = ~0u;
+        for (int64_t e = p0 + ln; e < p1; e += 64) m = min(m, lab[in_col[e] & kColMask]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o, 64));
+        if (ln == 0 && m < atomicMin(lab + v, m)) ch = true;
     }
     if (ch) *changed = 1u;
 }
@@ -1090,17 +1106,35 @@ __global__ void mark_injections(RoundArgs a) {
         const uint64_t i = p[2 * k];
         a.cand[a.own0 + i] |= CA_NODE | CA_INJ;  // same value from every thread of a node
         if (!a.stream_ok) a.tile_cand[i / a.tile_nodes] = 1;  // lean rounds use the node list
-        // the lean digest's component targets: one per pair (a value broadcast twice
-        // into one component counts twice, so that target is never reached: no skip)
-        if (a.lccnt) atomicAdd(a.lccnt + a.llab[i], 1u);
     }
 }
 
-// The lean digest's per-node targets after a round's injections: lreach[v] =
-// lanes injected so far into v's component (lccnt by label).
-__global__ void lreach_fill(const uint32_t* lab, const uint32_t* ccnt, uint32_t* lreach, uint64_t n) {
+// The lean digest's per-node targets: lreach[v] = the count of v's component
+// label in tab = {n, then n (label, count) pairs by ascending label; n =
+// kTabOverflow: too many labels, no target is reachable}. Labels absent from
+// the table have no broadcast: target 0, which no changed set equals.
+constexpr uint32_t kTabOverflow = ~0u;
+__global__ void lreach_fill_tab(const uint32_t* lab, const uint32_t* tab, uint32_t* lreach, uint64_t n) {
+    const uint32_t m = tab[0];
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t c = ~0u;
+        if (m != kTabOverflow) {
+            const uint32_t l = lab[v];
+            uint32_t lo = 0, hi = m;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (tab[1 + 2 * mid] < l) lo = mid + 1;
+                else hi = mid;
+            }
+            c = (lo < m && tab[1 + 2 * lo] == l) ? tab[2 + 2 * lo] : 0u;
+        }
+        lreach[v] = c;
+    }
+}
+// owned rows' labels from the global label array (vertex parts: row -> id map)
+__global__ void llab_gather(const uint32_t* glab, const uint32_t* gid, uint32_t* llab, uint64_t n) {
     for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x)
-        lreach[v] = ccnt[lab[v]];
+        llab[v] = glab[gid[v]];
 }
 constexpr unsigned kMarkInjBlocks = 16;
 

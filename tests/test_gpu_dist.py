@@ -509,6 +509,33 @@ def test_world8_c4_shape_full_width_equals_oracle(hip_lib, cpu_lib):
     _check_against_oracle(cpu_lib, scs, res, 8)
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_parts_lean_digest_equals_oracle(hip_lib, cpu_lib, world):
+    """The lean saturation digest on vertex parts (device-built R-MAT with hubs):
+    component labels of the whole generated graph, per-component targets from
+    every rank's broadcasts (a later batch of values, two of them re-sent into
+    other components) — against O2, and with fewer sender-row gathers than the
+    same run without the digest (GG_LSAT=0)."""
+    import random as _r
+
+    from ggamd import topology as T
+    rnd = _r.Random(71)
+    inj = [(rnd.randrange(4096), v, 0) for v in range(200)] + [(rnd.randrange(4096), 200 + v, 9) for v in range(56)]
+    inj += [(11, 5, 3), (3000, 201, 10)]
+    gen = dict(kind="rmat", n=4096, k=16, seed=72, a=0.57, b=0.19, c=0.19)
+    scs = [Scenario(T.rmat(4096, 16, seed=72), 256, 24, inj, seed=73, enable_sync=False, gen=gen),
+           Scenario(T.rmat(4096, 16, seed=72), 1024, 20, inj, seed=74, sync_base=11, sync_jitter=2, gen=gen)]
+    gathers = {}
+    for lsat in ("1", "0"):
+        env = {"GG_HUB_DEG": "16", "GG_HUB_CHUNK": "7"}
+        if lsat == "0":
+            env["GG_LSAT"] = "0"
+        res = _run(hip_lib, scs, world, env=env, generate=True, transport="ipc", timeout=240)
+        _check_against_oracle(cpu_lib, scs, res, world)
+        gathers[lsat] = sum(st["work_gathers"] for r in res for st in r[0][0])
+    assert gathers["1"] < gathers["0"], gathers
+
+
 def test_world8_lane_groups_by_parts_equals_oracle(hip_lib, cpu_lib):
     """2 lane groups x 4 vertex parts (world 8), device-built partitions, the
     engine's exchange sequencing, against O2."""
