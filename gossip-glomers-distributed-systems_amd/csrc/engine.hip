@@ -111,9 +111,10 @@ struct BatchKey {
     const void* inj_buf = nullptr;
     int db_state = 0;  // double-buffered rounds active at r0, and the current set buffer
     uint64_t solo_hash = 0;  // the solo schedule of the batch's marking rounds (and the round before r0)
+    uint32_t zr = 0;         // rounds of counter slots zeroed before the batch (0: fold_slots left them zero)
     bool operator==(const BatchKey& o) const {
         return r0 == o.r0 && m == o.m && inj_hash == o.inj_hash && u_hash == o.u_hash && windows == o.windows &&
-               inj_buf == o.inj_buf && db_state == o.db_state && solo_hash == o.solo_hash;
+               inj_buf == o.inj_buf && db_state == o.db_state && solo_hash == o.solo_hash && zr == o.zr;
     }
 };
 
@@ -221,6 +222,7 @@ struct gg_engine {
     std::vector<uint64_t> xsend_bytes, xrecv_bytes, xsend_off, xrecv_off;  // [world]
     uint32_t dist_k = 0;                       // pending rounds (counter slots in use)
     uint32_t ctr_dirty = kMaxBatch;            // counter slots [0, ctr_dirty) may be non-zero
+    uint32_t batch_zr = 0;                     // enqueue_step_batch: rounds of slots it zeroes first (BatchKey::zr)
     std::vector<int64_t> dist_round_of;        // round of each pending slot
     std::vector<uint64_t> dist_path;           // its kernel path (GG_PATH_*)
     uint64_t last_path = 0;                    // path of the round enqueue_round enqueued last
@@ -1062,6 +1064,7 @@ bool bll_round(const gg_engine* e, int64_t r, bool db) {
 uint32_t solo_of(const gg_engine* e, int64_t r, bool db) {
     if (!bll_round(e, r, db)) return 0;
     const char* force = test_knob("GG_SOLO");
+    if (r == 0 && !force) return gg::SOLO_MARK;  // nothing became active before round 0: never busy
     if (force) {
         if (!strcmp(force, "0")) return 0;
         if (!strcmp(force, "mark")) return gg::SOLO_MARK;
@@ -1093,13 +1096,22 @@ void learn_busy(gg_engine* e, int64_t r, bool busy) {
 // The solo schedule of rounds r0..r0+m-1 as enqueue_round will set it (with the
 // solo kind of the round before r0), for the batch key; the host state is
 // simulated and restored.
+// Lean streaming rounds whose last run was busy skip compact_round and run
+// dense (RoundArgs::no_list; exact either way: a dense round visits every
+// node). GG_NO_LIST = 0: never; 1: in every such round whatever the hints.
+bool list_skip_hint(const gg_engine* e, int64_t r) {
+    const char* k = test_knob("GG_NO_LIST");
+    if (k) return atoi(k) != 0;
+    return r >= 0 && (size_t)r < e->busy_hint.size() && e->busy_hint[r] == 1;
+}
+
 uint64_t solo_sched_hash(gg_engine* e, int64_t r0, uint32_t m) {
     const bool sdb = e->db_active, sfd = e->f_dirty;
     const int sset = e->set_cur;
     uint64_t h = gg_mix64(0x501Dull ^ e->last_solo);
     for (uint32_t k = 0; k < m; ++k) {
         const bool dbk = db_round(e, r0 + k);
-        h = gg_mix64(h ^ ((uint64_t)solo_of(e, r0 + k, dbk) << 8) ^ k);
+        h = gg_mix64(h ^ ((uint64_t)solo_of(e, r0 + k, dbk) << 8) ^ ((uint64_t)list_skip_hint(e, r0 + k) << 16) ^ k);
         db_advance(e, r0 + k, dbk);
     }
     e->db_active = sdb;
@@ -1337,7 +1349,11 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         a.prev_mark = e->last_solo == gg::SOLO_MARK ? 1u : e->last_solo == gg::SOLO_DB ? 2u : 0u;
         e->last_solo = a.solo;
         if (a.solo) e->last_path |= GG_PATH_SOLO;
-        if (!a.block_lists) {
+        // a lean streaming round the last run found busy: no list, dense (exact either
+        // way). Not when compact_round sums the rings (prep_in_compact)
+        a.no_list = (!a.block_lists && a.stream_ok && !sync_stream && !a.prep_in_compact && !e->cfg.batch_ticks &&
+                     list_skip_hint(e, r)) ? 1u : 0u;
+        if (!a.block_lists && !a.no_list) {
             const uint64_t groups = (a.n_own + 7) / 8;  // >= tile groups
             const uint64_t per_block = (uint64_t)gg::kBlock * gg::kCompactQ;
             const uint64_t nb = (groups + per_block - 1) / per_block;
@@ -1622,6 +1638,7 @@ int run_batch(gg_engine* e, int64_t r0, uint32_t m, const std::vector<size_t>& o
     key.inj_buf = e->d_inj;
     key.db_state = (e->db_active ? 2 : 0) | e->set_cur;
     key.solo_hash = solo_sched_hash(e, r0, m);
+    key.zr = e->batch_zr;
     {  // which rounds inject (mark_injections is launched only there), not what
         uint64_t p = gg_mix64(m);
         for (size_t k = 0; k < m; ++k) p = gg_mix64(p ^ (off[k + 1] > off[k] ? 2 * k + 1 : 2 * k));
@@ -2883,7 +2900,10 @@ int enqueue_step_batch(gg_engine* e, uint32_t m, bool wait, std::vector<uint64_t
         e->set_cur = save_set;
         e->last_solo = save_solo;
         e->d_base = e->d_sets[save_set];
-        if (int rz = zero_async(e, e->d_counters, (size_t)m * gg::kSlots * gg::kCounters * 8)) return rz;
+        // the slots are zero after a fold (fold_slots clears what it read): only a
+        // batch after other users of the slots (sharded rounds, setup) zeroes them
+        if (e->batch_zr)
+            if (int rz = zero_async(e, e->d_counters, (size_t)e->batch_zr * gg::kSlots * gg::kCounters * 8)) return rz;
         for (uint32_t k = 0; k < m; ++k) {
             const uint32_t ni = (uint32_t)(off[k + 1] - off[k]);
             e->round = r0 + k;
@@ -2893,14 +2913,16 @@ int enqueue_step_batch(gg_engine* e, uint32_t m, bool wait, std::vector<uint64_t
         }
         // fold the 64 slots of each round on the device: one 256-byte row per round to the host
         unsigned long long* folded = e->d_counters + (size_t)kMaxBatch * gg::kSlots * gg::kCounters;
-        hipLaunchKernelGGL(gg::fold_slots, dim3(m), dim3(gg::kCounters), 0, e->stream, e->d_counters, folded);
+        hipLaunchKernelGGL(gg::fold_slots, dim3(m), dim3(gg::kCounters), 0, e->stream, e->d_counters, folded, 1u);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(e->h_counters, folded, (size_t)m * gg::kCounters * 8, hipMemcpyDeviceToHost,
                               e->stream));
         return GG_OK;
     };
+    e->batch_zr = e->ctr_dirty ? std::max(e->ctr_dirty, m) : 0u;
     rc = run_batch(e, r0, m, off, total, enqueue_batch, wait);
-    e->ctr_dirty = std::max(e->ctr_dirty, m);
+    e->batch_zr = 0;
+    e->ctr_dirty = rc ? kMaxBatch : 0u;  // (fold_slots zeroed the m rounds it read, the rest was zero)
     e->round = save_round + m;
     // the double-buffer state after the batch (a replayed graph enqueued nothing)
     e->db_active = save_db;

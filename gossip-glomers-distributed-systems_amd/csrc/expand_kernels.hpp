@@ -168,6 +168,8 @@ struct RoundArgs {
     uint32_t prev_mark;         // round r-1 was a solo marking round: 1 = its kernel marked round r's
                                 // candidates, 2 = it marked nothing (expand_stream_db: round r is
                                 // dense); 0 = the device decides from the act ring (busy_prev)
+    uint32_t no_list;           // lean streaming round without compact_round (the host expects it busy,
+                                // from the last run of this round): dense whatever the act ring says
     uint8_t* zmark;             // [rows] F row of this parity is stale (node active 2 rounds ago)
     uint8_t* tile_cand;         // [n_tiles rounded to 8] tile has a candidate (sparse rounds)
     struct TileWork* work;      // live tiles of a sparse round (compact_round; expand_round)
@@ -381,7 +383,7 @@ __device__ __forceinline__ bool busy_prev(const RoundArgs& a) {
 // candidates (expand_stream_db takes it, not the marking kernel), so the round
 // after it visits every node and marks for the next one.
 __device__ __forceinline__ bool dense_round(const RoundArgs& a) {
-    return a.stream_ok && (busy_round(a) || (a.prep_in_compact && busy_prev(a)));
+    return a.stream_ok && (a.no_list || busy_round(a) || (a.prep_in_compact && busy_prev(a)));
 }
 
 // Flags-first streaming round: fewer than half of the in-edges name a sender
@@ -1780,7 +1782,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
     // nothing (busy, or a solo expand_stream_db) is dense too; a solo
     // expand_stream_db round is dense (it has no candidate list)
     const bool prev_unmarked = a.prev_mark ? a.prev_mark == 2 : busy_count(a, rv.act_m2);  // busy_prev()
-    const bool dense = busy || (DB && !MARK && a.solo) || (a.prep_in_compact && prev_unmarked);
+    const bool dense = busy || a.no_list || (DB && !MARK && a.solo) || (a.prep_in_compact && prev_unmarked);
     // block lists (sparse rounds without compact_round): thread t of block b
     // takes the 16 nodes of granule t * grid + b (one 16-byte load of candidate
     // bytes; the host sizes the grid so 256 granules a block cover every node),
@@ -3944,9 +3946,10 @@ __global__ void zero_words(uint64_t* p, uint64_t n) {
     if (i == 0 && (n & 1)) p[n - 1] = 0;
 }
 
-__global__ void fold_slots(const unsigned long long* ctr, unsigned long long* out) {
+// (clear: zero the slots read, so the next batch needs no zeroing launch)
+__global__ void fold_slots(unsigned long long* ctr, unsigned long long* out, uint32_t clear) {
     const int j = threadIdx.x;
-    const unsigned long long* c = ctr + (size_t)blockIdx.x * kSlots * kCounters;
+    unsigned long long* c = ctr + (size_t)blockIdx.x * kSlots * kCounters;
     const bool stampj = j >= kStamp0 && j < kStamp0 + 2 * K_NKIND;
     unsigned long long v = 0;
     for (int k = 0; k < kSlots; ++k) {
@@ -3954,6 +3957,8 @@ __global__ void fold_slots(const unsigned long long* ctr, unsigned long long* ou
         v = stampj ? (x > v ? x : v) : v + x;
     }
     out[(size_t)blockIdx.x * kCounters + j] = v;
+    if (clear)
+        for (int k = 0; k < kSlots; ++k) c[k * kCounters + j] = 0;
 }
 
 // Episode reset: fill up to kResetSegs arrays (8-byte words) and start the
