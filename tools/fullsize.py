@@ -201,6 +201,14 @@ def main():
            "engine_device_bytes": held["total"], "engine_sync_buffer_bytes": held["sync"],
            "topology_source": "device generator" if args.device_gen else "host CSR", "engine_ready_s": ready_s, "inter_node_msgs": msgs, "msgs_per_op": msgs / K,
            "kernels": kinds, "oracle": bool(ref), "properties_failed": fails}
+    # the byte roofline and the request-ceiling fraction (line_frac), as bench.py
+    # reports them (PMC requests when profiles/ holds a pass of this shape)
+    sys.path.insert(0, REPO)
+    import bench as B
+    shape = {"config": wl.name, "nodes": V, "lanes": wl.n_lanes, "world": 1, "parts": 1, "halves": 1}
+    roof = B.roofline(st, B.next_pow2(max(1, wl.n_lanes // 64)), V, int(topo.nnz), shape, 1)
+    out["roofline"] = {k: roof[k] for k in ("kernel", "achieved", "frac", "line_frac", "line_source", "traffic",
+                                            "avg_launch_ms")}
     log(json.dumps(out))
     if args.json:
         json.dump(out, open(args.json, "w"), indent=1)
