@@ -197,14 +197,15 @@ def roofline(rounds_local: list[dict], nwp: int, n_own: int, E_own: int, shape: 
         "avg_launch_ms": D["avg_launch_ms"],
         "launches": D["launches"],
         "dense_bytes_per_round": dense_bytes_per_round(n_own, E_own, nwp),
-        "line_frac": ((reqs_ep / kind_s_ep / ceiling) if reqs_ep and kind_s_ep > 0
-                      else lines_per_s / ROW_CEILING_PER_S),
+        "line_frac": (reqs_ep / kind_s_ep / ceiling) if reqs_ep and kind_s_ep > 0 else None,
         "line_source": (f"PMC: {reqs_ep:.4g} memory-side requests per episode of this kind ({traffic_src}) over "
                         f"its {kind_s_ep * 1e3:.4g} ms per episode, against {ceiling:.4g} requests/s at the random-row "
                         f"ceiling ({ceiling_src})" if reqs_ep
-                        else "row model (no request pass for this shape): line_model"),
+                        else "null: no request pass of this shape in profiles/ (line_model.frac is a row model "
+                             "that overcounts rows sharing a line, e.g. grid neighbours at W = 64)"),
         "requests_per_launch": reqs_ep / R if reqs_ep else None,
-        "line_model": {"rows_moved": rows, "lines_per_row": lines_per_row, "line_bytes": 128,
+        "line_model": {"frac": lines_per_s / ROW_CEILING_PER_S, "rows_moved": rows, "lines_per_row": lines_per_row,
+                       "line_bytes": 128,
                        "lines_per_s": lines_per_s, "ceiling_lines_per_s": ROW_CEILING_PER_S,
                        "over": "every kernel of the timed rounds (round device time)",
                        "note": "rows = sender rows gathered + 2 x nodes visited (own row read, and "
