@@ -1208,6 +1208,8 @@ int enqueue_round(gg_engine* e, const uint32_t* d_inj, uint32_t n_inj, unsigned 
         // void the older bits (those of r-1 too: it only costs their skips)
         a.lsat = e->d_lsat;
         a.lusat = lanes_through(e, r);
+        static const bool nomark = ab_knob("GG_LSAT_NOMARK") != nullptr;  // A/B: read only
+        a.lmark = nomark ? 0u : 1u;
         // (component targets cover the whole known schedule: ltab_sync clears the
         // digest when they change)
         if (!e->d_lreach && r >= 2 && lanes_through(e, r - 1) != lanes_through(e, r - 2))

@@ -249,6 +249,7 @@ struct RoundArgs {
                                 // of r-1 holds every lane any sender row of r-1 can carry: it gathers
                                 // nothing (expand_stream, hub_chunks, hub_finish skip its in-edges)
     uint32_t lusat;             // lanes of this engine's range injected in rounds <= r
+    uint32_t lmark;             // the digest's writers mark this round (0: read only)
     const uint32_t* lreach;     // [n_own] lanes broadcast into the node's component over the whole known
                                 // schedule (symmetric graphs with several components: lreach_fill_tab),
                                 // or nullptr: lusat for every node. A set never holds more (§4.2)
@@ -1939,8 +1940,6 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
     auto fetch_meta = [&](uint32_t n, Meta& m) {
         m.node = n;
         if (n < a.n_own) {
-            // the digest byte is loaded with the rest (no load waits on another here)
-            const uint8_t sb = (!MASKW && a.lsat) ? a.lsat[a.own0 + n] : (uint8_t)0;
             m.p0 = a.in_ptr[n];
             m.deg = (uint32_t)(a.in_ptr[n + 1] - m.p0);
             m.ca = a.cand[a.own0 + n];      // CA_INJ: client broadcasts this round
@@ -1951,8 +1950,6 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             if (a.hub_deg && m.deg > a.hub_deg) {  // a hub: hub_chunks/hub_finish take it
                 m.node |= kHubBit;
                 m.deg = 0;
-            } else if (sb && !(m.ca & CA_INJ)) {
-                m.deg = 0;  // saturated (lsat_skip): no gathers, no forwards, marks nobody
             }
         } else {
             m.p0 = 0;
@@ -1964,6 +1961,13 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
 #pragma unroll
         for (int b = 0; b < D; ++b)
             c[b] = ((uint32_t)b < m.deg) ? a.in_col[m.p0 + b] : 0u;
+    };
+    // the lean digest's byte of an item, loaded with its columns one stage
+    // ahead (a load in fetch_meta made it wait for the candidate byte early: +5 %
+    // on C4's dense rounds); applied before the item's row DMAs
+    auto fetch_sat = [&](const Meta& m) -> uint32_t {
+        if constexpr (MASKW) return 0u;
+        return (a.lsat && !(m.node & kHubBit) && m.node < a.n_own) ? (uint32_t)a.lsat[a.own0 + m.node] : 0u;
     };
 
     uint32_t k = (bl ? 0u : blockIdx.x * NGB) + threadIdx.x / G;
@@ -1983,8 +1987,11 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
     fetch_meta(n1, m1);
     vm_drain();
     fetch_cols(m0, c0);
+    uint32_t s0 = fetch_sat(m0), s1 = 0;
     vm_drain();  // nothing pending at the loop head: no compiler drains inside
     for (; k < n_items; k += stride) {
+        // saturated (lsat_skip) and no client broadcast: no gathers, no forwards, marks nobody
+        if (s0 && !(m0.ca & CA_INJ)) m0.deg = 0;
         const bool hub = (m0.node & kHubBit) != 0;
         const uint64_t i = m0.node & ~kHubBit;
         const uint64_t rep = a.own0 + i;
@@ -1993,7 +2000,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         // (an all-full double-buffered round: every owned set is the same, row 0's)
         if (!hub && !full) dma16((const void*)((db ? a.base_prev : a.base) + rep * a.nwp + off), my + D * 1024);
         // the lean digest's target, loaded with the DMAs (waited for with them)
-        const uint32_t tgt = (!MASKW && a.lreach && !hub) ? a.lreach[rep] : a.lusat;
+        const uint32_t tgt = (!MASKW && a.lreach && a.lmark && !hub) ? a.lreach[rep] : a.lusat;
         uint64_t mw[3][2];
         if constexpr (MASKW) {
 #pragma unroll
@@ -2013,6 +2020,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         // list entry of item k+3*stride
         Meta m2;
         fetch_cols(m1, c1);
+        s1 = fetch_sat(m1);
         fetch_meta(n2, m2);
         const uint32_t n3 = node_of(k + 3 * stride);
         vm_drain();
@@ -2152,7 +2160,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             }
         }
         const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
-        if (!MASKW && any && a.lsat) lsat_mark<G, WPL>(a, S, rep, lg, tgt);
+        if (!MASKW && any && a.lsat && a.lmark) lsat_mark<G, WPL>(a, S, rep, lg, tgt);
         const bool zm = !db && (m0.fl & FL_ACT) != 0;  // F row of round r-2 in this buffer
         // rows written this round are read next round from HBM anyway (F by
         // other nodes' gathers, base by this node): streamed past the caches,
@@ -2213,6 +2221,7 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
         c_bytes += db ? ((lane_new || cp) ? 16 : 0) : ((lane_new || zm) ? 16 : 0) + (lane_new ? 16 : 0);
         }  // !hub
         m0 = m1;
+        s0 = s1;
         m1 = m2;
         n2 = n3;
 #pragma unroll
@@ -3470,7 +3479,7 @@ __global__ __launch_bounds__(kBlock) void hub_finish(RoundArgs a) {
                 }
             }
             const bool any = ((__ballot(T != 0) >> gshift) & gmask) != 0;
-            if (any && a.lsat) lsat_mark<G, WPL>(a, S, rep, lg, a.lreach ? a.lreach[rep] : a.lusat);
+            if (any && a.lsat && a.lmark) lsat_mark<G, WPL>(a, S, rep, lg, a.lreach ? a.lreach[rep] : a.lusat);
             const uint8_t fl = a.db ? a.flg_prev[rep] : a.flg_cur[rep];  // (db: r-1, else r-2)
             const bool zm = !a.db && (fl & FL_ACT) != 0;
             const bool lane_new = [&] {
