@@ -2072,7 +2072,7 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     // there the hubs — most of the in-edges — saturate rounds before the last
     // delivery round (C4 1190 -> 840 ms/step); on a tree nodes saturate only in
     // the last delivery rounds and the marking costs more than the skips save
-    // (C2 +5-8 %, profiles/r5/INDEX.md). Vertex parts hold no whole component, so
+    // (C2 +1 %, profiles/r5/INDEX.md). Vertex parts hold no whole component, so
     // their targets would be every lane, which a disconnected graph never reaches:
     // off there too. GG_LSAT=1 / 0 forces it on / off.
     const char* lk = test_knob("GG_LSAT");
