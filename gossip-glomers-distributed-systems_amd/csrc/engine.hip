@@ -977,12 +977,14 @@ int ensure_db(gg_engine* e) {
     size_t free_b = 0, total_b = 0;
     (void)hipMemGetInfo(&free_b, &total_b);
     // (graphs with hubs are bound by their gathers: C4 at 10^8 nodes ran 1.154 s per
-    // episode either way, profiles/r3/bench_c4_db.json, so they keep their HBM)
+    // episode either way, profiles/r3/bench_c4_db.json, and with the lean digest
+    // 823 vs 826 ms for 48 GiB more HBM, profiles/r5/INDEX.md, so they keep their HBM;
+    // GG_DB=1 forces the double-buffered rounds on them too)
     // GG_NO_DB=1 / GG_DB=1 (test hooks): never / whenever the graph allows it,
     // whatever the free memory (the tests pin both paths; gg_round_stats.path says
     // which one a round took)
     const bool force = test_knob("GG_DB") && atoi(test_knob("GG_DB"));
-    const bool ok = e->round == 0 && e->nwp >= 2 && e->nwp <= 128 && !e->cfg.batch_ticks && e->n_hubs == 0 &&
+    const bool ok = e->round == 0 && e->nwp >= 2 && e->nwp <= 128 && !e->cfg.batch_ticks && (e->n_hubs == 0 || force) &&
                     (force || free_b > rowbytes + (16ull << 30)) && !test_knob("GG_NO_DB");
     if (!ok) return GG_OK;
     HIPCHK(hipMalloc(&e->d_sets[1], rowbytes));
