@@ -1280,8 +1280,24 @@ __global__ __launch_bounds__(1024) void compact_scan(RoundArgs a, uint32_t nb) {
         return;
     }
     const uint32_t per = (nb + 1023) / 1024, b0 = threadIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
+    // 16-byte loads, four in flight, when a thread's run is 16-byte aligned (C5 at
+    // 2^30 nodes: 128 counts a thread; one count per load made the pass latency-bound, ~200 us)
+    const bool vec = (per & 3u) == 0;
     uint32_t sum = 0;
-    for (uint32_t b = b0; b < b1; ++b) sum += a.bcount[b];
+    uint32_t b = b0;
+    if (vec) {
+        const uint4* v4 = reinterpret_cast<const uint4*>(a.bcount);
+        for (; b + 16 <= b1; b += 16) {
+            const uint4 x0 = v4[b / 4], x1 = v4[b / 4 + 1], x2 = v4[b / 4 + 2], x3 = v4[b / 4 + 3];
+            sum += x0.x + x0.y + x0.z + x0.w + x1.x + x1.y + x1.z + x1.w + x2.x + x2.y + x2.z + x2.w + x3.x + x3.y +
+                   x3.z + x3.w;
+        }
+        for (; b + 4 <= b1; b += 4) {
+            const uint4 x = v4[b / 4];
+            sum += x.x + x.y + x.z + x.w;
+        }
+    }
+    for (; b < b1; ++b) sum += a.bcount[b];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t incl = sum;
 #pragma unroll
@@ -1303,7 +1319,29 @@ __global__ __launch_bounds__(1024) void compact_scan(RoundArgs a, uint32_t nb) {
     }
     __syncthreads();
     uint32_t off = s_w[wave] + incl - sum;
-    for (uint32_t b = b0; b < b1; ++b) {
+    b = b0;
+    if (vec) {
+        uint4* v4 = reinterpret_cast<uint4*>(a.bcount);
+        for (; b + 16 <= b1; b += 16) {
+            uint4 x[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) x[q] = v4[b / 4 + q];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 v = x[q];
+                x[q] = make_uint4(off, off + v.x, off + v.x + v.y, off + v.x + v.y + v.z);
+                off += v.x + v.y + v.z + v.w;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v4[b / 4 + q] = x[q];
+        }
+        for (; b + 4 <= b1; b += 4) {
+            const uint4 v = v4[b / 4];
+            v4[b / 4] = make_uint4(off, off + v.x, off + v.x + v.y, off + v.x + v.y + v.z);
+            off += v.x + v.y + v.z + v.w;
+        }
+    }
+    for (; b < b1; ++b) {
         const uint32_t v = a.bcount[b];
         a.bcount[b] = off;
         off += v;
