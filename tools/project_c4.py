@@ -23,7 +23,13 @@ waits for each round's segment sizes before it enqueues the payload, round 3:
 none — its whole episode is enqueued ahead in one graph, 17 us per C4 round
 measured, profiles/r4/ipc/).
 
+Payload format (--row-bytes R --head-bytes H): the rehearsals measured the
+engine exchange's 16-byte head per entry; the device-driven exchange's tile
+segments (round 5) ship one 80-byte record per 256 entries instead, so each
+payload is scaled by (R + 80/256) / (R + H), R = the F row's bytes.
+
 Usage: python tools/project_c4.py profiles/r3/r3_c4_rehearsal_2p22_p8_ordered.json [--halves H.json] [--scale S] [--host-us U]
+       [--row-bytes R --head-bytes 16]
 """
 import argparse
 import json
@@ -40,19 +46,23 @@ def main():
     ap.add_argument("--links", default="64,76.5,153", help="GB/s per link and direction")
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--host-us", type=float, default=0.0, help="host time per round on the critical path")
+    ap.add_argument("--row-bytes", type=float, default=0.0, help="F row bytes: rescale payloads to tile segments")
+    ap.add_argument("--head-bytes", type=float, default=16.0, help="per-entry head bytes the rehearsal measured")
     args = ap.parse_args()
+    xs = (args.row_bytes + 80.0 / 256.0) / (args.row_bytes + args.head_bytes) if args.row_bytes else 1.0
     d = json.load(open(args.rehearsal))
     P = d["config"]["parts"]
     h = json.load(open(args.halves)) if args.halves else None
     out = {"rehearsal": args.rehearsal, "halves": args.halves, "parts": P, "lane_groups": d["config"]["lane_groups"],
-           "nodes": d["config"]["nodes"], "scale": args.scale, "host_us_per_round": args.host_us, "projections": []}
+           "nodes": d["config"]["nodes"], "scale": args.scale, "host_us_per_round": args.host_us,
+           "payload_scale": xs, "projections": []}
     single = sum(r["single_ms"] for r in rounds_of(d)) * args.scale
     for link in [float(x) for x in args.links.split(",")]:
         B = link * 1e9 * min(7, max(1, P - 1))
         t_after = t_ovl = t_half = 0.0
         for i, r in enumerate(rounds_of(d)):
             c = r["rank_ms_max"] * args.scale
-            x = r["payload_bytes_max"] * args.scale / B * 1e3
+            x = r["payload_bytes_max"] * xs * args.scale / B * 1e3
             hst = args.host_us * 1e-3
             t_after += c + x + hst
             t_ovl += max(c, x) + hst
@@ -61,7 +71,7 @@ def main():
                 # a GPU holds two lane-half ranks: both halves' kernels and payloads
                 c2 = 2 * hr["rank_ms_mean"] * args.scale if hr["rank_ms_max"] < 1.2 * hr["rank_ms_mean"] else \
                     (hr["rank_ms_max"] + hr["rank_ms_mean"]) * args.scale
-                x2 = 2 * hr["payload_bytes_max"] * args.scale / B * 1e3
+                x2 = 2 * hr["payload_bytes_max"] * xs * args.scale / B * 1e3
                 t_half += max(c2, x2) + hst
         p = {"link_GBps": link, "single_ms": single, "exchange_after_ms": t_after,
              "speedup_exchange_after": single / t_after, "overlap_bound_ms": t_ovl,
