@@ -304,6 +304,9 @@ struct gg_engine {
     uint32_t* d_ltab = nullptr;      // [1 + 2 ltab_cap] (label, count) table behind d_lreach
     uint32_t ltab_cap = 0;
     uint64_t ltab_hash = 0;          // the table d_lreach was filled from (0: none yet)
+    std::vector<uint32_t> h_ltab;    // its host copy (the source of the last upload)
+    hipEvent_t ltab_ev = nullptr;    // recorded after that upload: h_ltab is reused only past it
+    bool ltab_ev_live = false;
     std::vector<uint32_t> h_lab;     // labels on the host: by local row (single engine) or by node id
     bool lab_global = false;         // (vertex parts: labels of the whole graph)
     std::vector<uint64_t> lret;      // label << 32 | lane of the retired rounds' broadcasts (lane in range)
@@ -511,6 +514,7 @@ gg_engine::~gg_engine() {
     dfree(d_injtab);
     for (auto& x : ev) (void)hipEventDestroy(x);
     if (inj_ev) (void)hipEventDestroy(inj_ev);
+    if (ltab_ev) (void)hipEventDestroy(ltab_ev);
     if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -1540,14 +1544,21 @@ int ltab_sync(gg_engine* e) {
     for (const auto& p : t) h = gg_mix64(h ^ ((uint64_t)p.first << 32 | p.second));
     h |= 1;  // (0: none yet)
     if (h == e->ltab_hash) return GG_OK;
-    std::vector<uint32_t> buf(1, t.size() > e->ltab_cap ? gg::kTabOverflow : (uint32_t)t.size());
+    if (e->ltab_ev_live) {  // the previous upload has read h_ltab
+        HIPCHK(hipEventSynchronize(e->ltab_ev));
+        e->ltab_ev_live = false;
+    }
+    std::vector<uint32_t>& buf = e->h_ltab;
+    buf.assign(1, t.size() > e->ltab_cap ? gg::kTabOverflow : (uint32_t)t.size());
     if (buf[0] != gg::kTabOverflow)
         for (const auto& p : t) {
             buf.push_back(p.first);
             buf.push_back(p.second);
         }
-    // (pageable source: the copy is staged before the call returns)
     HIPCHK(hipMemcpyAsync(e->d_ltab, buf.data(), buf.size() * 4, hipMemcpyHostToDevice, e->stream));
+    if (!e->ltab_ev) HIPCHK(hipEventCreateWithFlags(&e->ltab_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(e->ltab_ev, e->stream));
+    e->ltab_ev_live = true;
     hipLaunchKernelGGL(gg::lreach_fill_tab, dim3((unsigned)std::min<uint64_t>((e->n_own + 255) / 256, 8192)), dim3(256),
                        0, e->stream, e->d_llab, e->d_ltab, e->d_lreach, e->n_own);
     HIPCHK(hipGetLastError());
