@@ -25,6 +25,8 @@
 #include <chrono>
 #include <cstring>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <type_traits>
@@ -2464,37 +2466,76 @@ static int install_shard(gg_engine* e, gg_gen::Csr g, const std::vector<uint64_t
 // default, GG_LSAT as for single engines): a component spans parts, so its
 // labels come from the whole graph, built once on this device in original ids
 // and dropped after labelling; the labels stay on the host (the broadcasts'
-// counts per component, ltab_sync) and the owned rows' on the device.
+// counts per component, ltab_sync) and the owned rows' on the device. The host
+// labels are kept per generator spec for the process, so a second engine of the
+// same graph (lane halves) uploads them instead of building the graph again; a
+// build that fails (e.g. no HBM left beside the parts) leaves the part without
+// component targets (lusat: exact, no skips on a disconnected graph) instead of
+// failing the install.
+static std::mutex g_lab_mu;
+static std::map<std::vector<uint64_t>, std::shared_ptr<const std::vector<uint32_t>>> g_lab_cache;
+
 static int lsat_parts(gg_engine* e, const gg_gen_spec* spec) {
     const char* lk = test_knob("GG_LSAT");
     if (!(e->nwp >= 2 && e->symmetric && e->d_gid && e->n_own && (lk ? atoi(lk) != 0 : e->n_hubs > 0))) return GG_OK;
-    gg_gen::Csr g{};
-    std::string err;
-    int rc = gg_gen::build_csr(*spec, e->stream, 0u, &g, &err);
-    if (rc) return e->fail(rc, err);
-    uint32_t* d_lab = nullptr;
-    unsigned long long roots = 0;
-    if (hipMalloc(&d_lab, e->V * 4) != hipSuccess) rc = e->fail(GG_EIO, "lean digest: label buffer");
-    if (!rc) rc = cc_labels(e, g.row_ptr, g.col, e->V, d_lab, &roots, nullptr, 0, 0);
-    (void)hipFree(g.row_ptr);
-    (void)hipFree(g.col);
-    if (!rc && !e->d_lsat) {
-        if (hipMalloc(&e->d_lsat, e->rows) != hipSuccess || hipMemsetAsync(e->d_lsat, 0, e->rows, e->stream) != hipSuccess)
-            rc = e->fail(GG_EIO, "lean digest: allocation");
+    if (!e->d_lsat) {
+        HIPCHK(hipMalloc(&e->d_lsat, e->rows));
+        HIPCHK(hipMemsetAsync(e->d_lsat, 0, e->rows, e->stream));
     }
-    if (!rc && roots > 1) {
-        e->h_lab.resize(e->V);
-        if (hipMemcpy(e->h_lab.data(), d_lab, e->V * 4, hipMemcpyDeviceToHost) != hipSuccess ||
-            hipMalloc(&e->d_llab, e->n_own * 4) != hipSuccess) {
+    uint64_t ab[3];
+    std::memcpy(ab, &spec->a, 8);
+    std::memcpy(ab + 1, &spec->b, 8);
+    std::memcpy(ab + 2, &spec->c, 8);
+    const std::vector<uint64_t> key = {spec->kind, spec->k, spec->n, spec->seed, ab[0], ab[1], ab[2]};
+    std::shared_ptr<const std::vector<uint32_t>> labs;
+    {
+        std::lock_guard<std::mutex> lk2(g_lab_mu);
+        auto it = g_lab_cache.find(key);
+        if (it != g_lab_cache.end()) labs = it->second;
+    }
+    uint32_t* d_lab = nullptr;
+    if (!labs) {
+        gg_gen::Csr g{};
+        std::string err;
+        unsigned long long roots = 0;
+        int rc = gg_gen::build_csr(*spec, e->stream, 0u, &g, &err);
+        if (rc == GG_OK && hipMalloc(&d_lab, e->V * 4) != hipSuccess) rc = GG_EIO;
+        if (rc == GG_OK) rc = cc_labels(e, g.row_ptr, g.col, e->V, d_lab, &roots, nullptr, 0, 0);
+        (void)hipFree(g.row_ptr);
+        (void)hipFree(g.col);
+        auto h = std::make_shared<std::vector<uint32_t>>();
+        if (rc == GG_OK && roots > 1) {
+            h->resize(e->V);
+            if (hipMemcpy(h->data(), d_lab, e->V * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = GG_EIO;
+        }
+        if (rc != GG_OK) {  // no component targets for this part (see above)
+            (void)hipGetLastError();
+            (void)hipFree(d_lab);
+            e->err.clear();
+            return hipStreamSynchronize(e->stream) == hipSuccess ? GG_OK : GG_EIO;
+        }
+        labs = h;  // (empty: one component, lusat serves)
+        std::lock_guard<std::mutex> lk2(g_lab_mu);
+        if (g_lab_cache.size() > 4) g_lab_cache.clear();
+        g_lab_cache[key] = labs;
+    }
+    int rc = GG_OK;
+    if (!labs->empty()) {
+        e->h_lab = *labs;
+        e->lab_global = true;
+        if (!d_lab) {
+            HIPCHK(hipMalloc(&d_lab, e->V * 4));
+            HIPCHK(hipMemcpy(d_lab, e->h_lab.data(), e->V * 4, hipMemcpyHostToDevice));
+        }
+        if (hipMalloc(&e->d_llab, e->n_own * 4) != hipSuccess) {
             rc = e->fail(GG_EIO, "lean digest: labels");
         } else {
-            e->lab_global = true;
             hipLaunchKernelGGL(gg::llab_gather, dim3((unsigned)std::min<uint64_t>((e->n_own + 255) / 256, 8192)),
                                dim3(256), 0, e->stream, d_lab, e->d_gid, e->d_llab, e->n_own);
             rc = hipGetLastError() == hipSuccess ? lsat_targets_alloc(e) : GG_EIO;
-            if (rc == GG_OK) rc = hipStreamSynchronize(e->stream) == hipSuccess ? GG_OK : GG_EIO;
         }
     }
+    if (rc == GG_OK) rc = hipStreamSynchronize(e->stream) == hipSuccess ? GG_OK : GG_EIO;
     (void)hipFree(d_lab);
     return rc;
 }
