@@ -14,17 +14,23 @@ Headline (--config C2, default; BASELINE.json configs[1]): a 4-ary tree
 --config C4 (configs[3]) as the headline: R-MAT (.57,.19,.19,.05), edge factor
   16, 10^8 nodes, K = 4096, strong scaling over N = L x P ranks (--parts P).
 
-Legs (--legs, default C4,C5 after a C2 headline; in the same JSON line under
-"legs", every N including 1): the two configs the north-star targets are
-quoted on, each built in HBM by the on-device generators and self-checked —
+Legs (--legs, default C3,C4,C5 after a C2 headline; in the same JSON line
+under "legs", every N including 1): BASELINE.json's other scale configs, each
+built in HBM by the on-device generators and self-checked —
+  C3  10^7-node random 8-regular, W = 1024, a seeded bisection in rounds
+      [2, 12) healed by the sync timers (the partition-window and sync-heal
+      kernels), N vertex parts;
   C4  10^8-node R-MAT, W = 4096, STRONG scaling: N vertex parts (two lane
       halves per GPU, one half's exchange under the other half's kernels);
       ms/step, deliveries/s, HBM per GPU, the dominant kernel's roofline;
   C5  2^30-node grid + one long link per node, W = 64, N vertex parts: HBM per
       GPU, rounds to full delivery, episode time.
   Checks: every timed episode equals the checking episode counter by counter;
-  P1 / KAT-3 / ACK (ggamd.checks; C4's components from the exported graph);
-  N > 1: every round's global counters equal one unsharded engine on rank 0.
+  the checking episode's every round (all counters and the delivery hash)
+  equals O2's run of the workload on the host-built graph
+  (tests/golden/fullsize_*.json); P1 / KAT-3 / ACK (ggamd.checks; C4's
+  components from the exported graph); N > 1: every round's global counters
+  equal one unsharded engine on rank 0.
 
 N > 1 exchange (--xchg auto): the device-driven IPC exchange when every rank
 maps its peers and one whole C2 episode through it equals O2's run of the
@@ -70,6 +76,7 @@ KIND_KERNELS = {
                "expand_batched"],
 }
 TRAFFIC_JSON = {"C2": os.path.join(REPO, "profiles", "traffic.json"),  # committed PMC passes per config
+                "C3": os.path.join(REPO, "profiles", "traffic_C3.json"),
                 "C4": os.path.join(REPO, "profiles", "traffic_C4.json"),
                 "C5": os.path.join(REPO, "profiles", "traffic_C5.json")}
 CPU_LIB = os.path.join(REPO, "oracle", "_build", "libgossip_cpu.so")
@@ -319,6 +326,16 @@ def gold_c2(nodes: int, lanes: int):
                 None)
 
 
+def gold_full(name: str, V: int, K: int, seed: int):
+    """O2's full-size record of a leg's workload (tests/golden/make_fullsize_golden.py),
+    or None when there is none of exactly this shape."""
+    path = os.path.join(REPO, "tests", "golden", f"fullsize_{name.lower()}.json")
+    if not os.path.exists(path):
+        return None
+    g = json.load(open(path))
+    return g if (g["nodes"], g["lanes"], g["seed"]) == (V, K, seed) else None
+
+
 def peer_info(job: Job) -> dict:
     """Where the ranks' GPUs are: distinct devices or not, and peer access from this one."""
     torch = job.torch
@@ -420,6 +437,7 @@ def headline(job: Job, args) -> tuple[dict | None, dict]:
                     parallelism=parallelism, scaling=scaling, workload=workload)
 
     def close_all(b):
+        ipc_release(job, b["engs"] if b is not None else [])
         if b is not None:
             for e in b["engs"]:
                 e.close()
@@ -739,6 +757,21 @@ def headline(job: Job, args) -> tuple[dict | None, dict]:
     return out, info
 
 
+def ipc_release(job: Job, engs) -> None:
+    """Collective (every rank, at the same point): unmap the peers' windows of this
+    rank's engines (gg_dist_ipc_close; a no-op without the device-driven exchange),
+    then a barrier — only then may any rank close an engine, which frees its own
+    window. Closing engines without it freed windows that peers still mapped, and
+    the next leg's imports hung in hipIpcOpenMemHandle (8 ranks, C5 2^28 after the
+    C2 headline: profiles/r6/INDEX.md)."""
+    for e in engs:
+        try:
+            e.dist_ipc_close()
+        except Exception as exc:  # noqa: BLE001 — the barrier below still runs on every rank
+            print(f"bench: rank {job.rank}: gg_dist_ipc_close failed ({exc!r})", file=sys.stderr, flush=True)
+    job.barrier()
+
+
 def validate_ipc(job: Job, args, setup):
     """Build the job on the device-driven exchange and run one whole episode
     through it (C2: every round — at least 4, so the consumed-flag waits and the
@@ -788,6 +821,7 @@ def validate_ipc(job: Job, args, setup):
             print(f"bench: device-driven validation episode differs from O2: {diffs}", file=sys.stderr)
     else:
         rec["result"] = f"failed on some rank (rank {job.rank}: {err})" if err else "failed on some rank"
+    ipc_release(job, built["engs"] if built is not None else [])
     if built is not None:
         for e in built["engs"]:
             e.close()
@@ -820,6 +854,7 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
     from ggamd.engine import COUNT_FIELDS, Engine, stats_dict
     from ggamd.workload import BASE_SEED, inject, injection_arrays, uniform_injections
 
+    windows = []  # seeded partition windows (a, b, epoch seed): kept across resets (gossip.h gg_reset)
     if name == "C4":
         V = args.c4_nodes or 100_000_000
         K = 4096
@@ -828,6 +863,17 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
         workload = (f"C4: R-MAT (.57,.19,.19,.05) edge factor 16, symmetrized, {V} nodes, {K} messages broadcast "
                     "in round 0 at seeded uniform nodes, sync on, no partitions; graph built in HBM by the "
                     "on-device generator; strong scaling (the same graph at every N)")
+    elif name == "C3":
+        V = args.c3_nodes or 10_000_000
+        K = 1024
+        seed = BASE_SEED + 3
+        gen = dict(kind="random_regular", n=V, k=8, seed=seed)
+        windows = [(2, 12, seed ^ 0x5EED)]
+        workload = (f"C3: random 8-regular graph, {V} nodes, {K} messages broadcast in round 0 at seeded uniform "
+                    "nodes; a seeded bisection of the nodes drops every message across it in rounds [2, 12) "
+                    "(Maelstrom --nemesis partition), the sync timers (rounds >= 20) heal it; one step = one "
+                    "episode until every node holds every value and a round delivers nothing; graph built in "
+                    "HBM by the on-device generator; strong scaling (the same graph at every N)")
     else:
         side = args.c5_side or 32768
         V = side * side
@@ -873,9 +919,12 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
         E = 0
         for e in engs:
             E = e.generate(**gen)  # this rank's rows (gossip_gen.h); halves: the same rows twice
+            for a, b, ep in windows:
+                e.partition_seeded(a, b, ep)
         return E
 
     def close_engs():
+        ipc_release(job, engs)
         for e in engs:
             e.close()
         engs.clear()
@@ -894,7 +943,19 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
     try:
         E_local = phase(build_engines, "engine build")
         xchg = xchg_pref if P > 1 else "none"
-        runner = phase(lambda: build_runner(xchg), f"exchange setup ({xchg})")
+        note = None
+        try:
+            runner = phase(lambda: build_runner(xchg), f"exchange setup ({xchg})")
+        except LegAbort as exc:
+            if xchg != "ipc":
+                raise
+            # a window mapping failed or ran out its bound (GG_IPC_OPEN_TIMEOUT_S) on some
+            # rank: every rank rebuilds its engines on the engine exchange
+            close_engs()
+            E_local = phase(build_engines, "engine rebuild")
+            xchg = "engine"
+            note = f"device-driven exchange setup failed ({exc}): rebuilt on the engine exchange"
+            runner = phase(lambda: build_runner(xchg), "exchange setup (engine)")
         setup_s = time.perf_counter() - tb
         log(f"built in {setup_s:.1f} s: {len(engs)} engine(s) per GPU, P={P} L={L}, exchange {xchg}")
         eng = engs[0]
@@ -912,6 +973,7 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
 
         reset_all()
         check = []
+        delivered = 0
         while True:
             ok, st = True, None
             try:
@@ -928,9 +990,11 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
             for j, f in enumerate(COUNT_FIELDS):
                 g[f] = tot[1 + j] & M64
             check.append(g)
+            delivered += g["new_bits"]
             if len(check) % 5 == 0:
                 log(f"checking episode: round {len(check) - 1}, {g['new_bits']} deliveries")
-            if (g["new_bits"] == 0 and len(check) > 1) or len(check) >= 120:
+            # quiescence; a healed partition (C3): only after every node holds every value
+            if (g["new_bits"] == 0 and len(check) > 1 and (not windows or delivered == V * K)) or len(check) >= 120:
                 break
         R = len(check)
         if check[-1]["new_bits"]:
@@ -966,7 +1030,6 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
             res = timed()
         except Exception as exc:  # noqa: BLE001
             print(f"bench[{name}]: rank {rank}: timed episodes failed ({exc!r})", file=sys.stderr, flush=True)
-        note = None
         if not job.agree(res is not None):
             if xchg != "ipc":
                 raise LegAbort("timed episodes failed on some rank")
@@ -987,6 +1050,12 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
             d = count_diffs(ep, check, COUNT_FIELDS, f"timed episode {k}", "checking episode", 3)
             fails += d
         rounds_local = [s for ep in eps_local for s in ep]
+        # the lean saturation digest on each rank (gossip.h GG_PATH_LSAT / _COMP bits)
+        lpath = 0
+        for s in rounds_local:
+            lpath |= int(s.get("path", 0))
+        lsat = [("off", "universe", "component targets")[m]
+                for m in job.gather_i64(2 if lpath & 512 else (1 if lpath & 256 else 0))]
         sent = sum(s["sent_bytes"] for s in rounds_local) / max(1, len(rounds_local))
         sent_max = max((s["sent_bytes"] for s in rounds_local), default=0)
         dinfo = eng.dist_info() if world > 1 else None
@@ -1021,6 +1090,8 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
                 ref = Engine(V, K, seed=seed, enable_sync=True, device=local)
                 try:
                     ref.generate(**gen)
+                    for a, b, ep in windows:
+                        ref.partition_seeded(a, b, ep)
                     inject(ref, inj_arr)
                     single = ref.step(R)
                     topo = ref.export_topology() if name == "C4" else None
@@ -1039,13 +1110,30 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
                 del topo
                 exp_d, exp_f = expected_from_components(lab, size, vol, srcs)
                 checks["components_s"] = time.perf_counter() - t
+                ncomp = int((size > 0).sum())
+                checks["components"] = ncomp
+                if ncomp > 1 and any(m != "component targets" for m in lsat):
+                    checks["lsat_note"] = ("a disconnected graph, but some rank ran the lean digest without "
+                                           "component targets (slower, still exact): " + ", ".join(lsat))
+            elif name == "C3":  # connected; the timers fire, so KAT-3 does not apply
+                exp_d, exp_f = V * K, None
             else:  # the grid spans every node: one component
                 exp_d, exp_f = V * K, K * (nnz - (V - 1))
             bad += episode_failures(check, exp_d, exp_f)
-            checks["properties"] = ("P1 (deliveries = sum of source component sizes), KAT-3 (forwards = sum of "
-                                    "vol(comp) - |comp| + 1: no timer fired before quiescence) and ACK "
-                                    "(acks(r+1) = broadcasts delivered in r) hold on the checking episode")
+            checks["properties"] = ("P1 (deliveries = sum of source component sizes), " +
+                                    ("" if exp_f is None else "KAT-3 (forwards = sum of vol(comp) - |comp| + 1: no "
+                                     "timer fired before quiescence), ") +
+                                    "ACK (acks(r+1) = broadcasts delivered in r) hold on the checking episode")
             checks["expected"] = {"deliveries": exp_d, "forwards": exp_f}
+            gold = gold_full(name, V, K, seed)
+            if gold is not None:  # O2 on the host-built graph, every round (tests/golden/fullsize_*.json)
+                d = count_diffs(check, gold["rounds"], COUNT_FIELDS, "checking episode", "O2")
+                bad += d
+                checks["oracle"] = (f"every round's global counters and delivery hash equal O2's run of this "
+                                    f"workload on the host-built graph (tests/golden/fullsize_{name.lower()}.json, "
+                                    f"{len(gold['rounds'])} rounds)" if not d else "FAILED: " + "; ".join(d[:4]))
+            else:
+                checks["oracle"] = "no O2 record of this shape (tests/golden/fullsize_*.json)"
             return bad
 
         fails += phase(verify, "checks") or []
@@ -1063,6 +1151,7 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
             "ms_per_step": elapsed / args.leg_steps * 1e3,
             "deliveries_per_step": deliveries // args.leg_steps,
             "hbm_bytes_per_gpu": hbm, "hbm_bytes_max": max(hbm),
+            "lsat": lsat,
             "exchange_bytes_per_round_rank0": sent if world > 1 else None,
             "exchange_bytes_densest_round_rank0": sent_max if world > 1 else None,
             "shard": dinfo, "setup_s": setup_s,
@@ -1181,10 +1270,11 @@ def main():
                     help="--config C4 with --parts > 1: 2 = two engines per GPU over the two halves of its lanes, "
                          "one half's exchange overlapping the other half's kernels (ggamd.dist.HalvesRunner)")
     ap.add_argument("--legs", default=None,
-                    help="comma list of C4,C5 (default after a C2 headline: C4,C5; 'none' to skip)")
+                    help="comma list of C3,C4,C5 (default after a C2 headline: C3,C4,C5; 'none' to skip)")
     ap.add_argument("--leg-steps", type=int, default=3, help="timed episodes per leg")
     ap.add_argument("--leg-parts", type=int, default=0, help="legs: vertex parts P (default N)")
     ap.add_argument("--leg-halves", type=int, default=0, choices=[0, 1], help="legs: 1 = no lane halves for C4")
+    ap.add_argument("--c3-nodes", type=int, help="C3 leg nodes (10^7; smaller for rehearsals)")
     ap.add_argument("--c4-nodes", type=int, help="C4 leg nodes (10^8; smaller for rehearsals)")
     ap.add_argument("--c5-side", type=int, help="C5 leg grid side (32768 = 2^30 nodes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -1210,11 +1300,11 @@ def main():
         out, info = {"note": "--no-headline: legs only"}, {"xchg": args.xchg}
     else:
         out, info = headline(job, args)
-    legs_arg = args.legs if args.legs is not None else ("C4,C5" if args.config == "C2" else "none")
+    legs_arg = args.legs if args.legs is not None else ("C3,C4,C5" if args.config == "C2" else "none")
     names = [x.strip().upper() for x in legs_arg.split(",") if x.strip() and x.strip().lower() != "none"]
     legs = {}
     for name in names:
-        if name not in ("C4", "C5"):
+        if name not in ("C3", "C4", "C5"):
             raise SystemExit(f"--legs: unknown leg {name}")
         pref = info["xchg"] if info["xchg"] in ("ipc", "engine") else "engine"
         if args.backend != "nccl" and pref == "engine":

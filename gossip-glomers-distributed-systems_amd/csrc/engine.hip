@@ -23,6 +23,7 @@
 #include <atomic>
 #include <cstdio>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -1044,6 +1045,7 @@ uint64_t path_of(const gg_engine* e, int64_t r, bool db) {
     for (int k = 0; k < 5; ++k) maskw |= window_at(e, r - 3 + k) != nullptr;
     const bool syncw = e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks + 2;
     uint64_t p = maskw ? GG_PATH_MASKED : 0;
+    if (e->d_lsat) p |= GG_PATH_LSAT | (e->d_lreach ? GG_PATH_LSAT_COMP : 0u);
     if (db && mark_ok(e) && !(e->cfg.enable_sync && r >= (int64_t)e->cfg.sync_base_ticks)) p |= GG_PATH_NO_PREP;
     if (db) return p | GG_PATH_DB;
     if (syncw && !maskw && e->d_srec) return p | GG_PATH_SYNC_STREAM;
@@ -2464,69 +2466,108 @@ static int install_shard(gg_engine* e, gg_gen::Csr g, const std::vector<uint64_t
 
 // The lean digest on the vertex parts of a generated graph (hub graphs by
 // default, GG_LSAT as for single engines): a component spans parts, so its
-// labels come from the whole graph, built once on this device in original ids
-// and dropped after labelling; the labels stay on the host (the broadcasts'
-// counts per component, ltab_sync) and the owned rows' on the device. The host
-// labels are kept per generator spec for the process, so a second engine of the
-// same graph (lane halves) uploads them instead of building the graph again; a
-// build that fails (e.g. no HBM left beside the parts) leaves the part without
-// component targets (lusat: exact, no skips on a disconnected graph) instead of
-// failing the install.
+// labels come from the whole graph, built on this device in original ids and
+// dropped after labelling; the labels stay on the host (the broadcasts'
+// counts per component, ltab_sync) and the owned rows' on the device. They are
+// built BEFORE the part allocates anything (lab_prepare, at the start of
+// generate_sharded), so the whole-graph build meets the same free HBM at every
+// N — two C4 lane halves at N = 2 once found none beside their parts — and
+// kept per generator spec for the process: a second engine of the same graph
+// (lane halves) takes them from the cache. A build that fails anyway is cached
+// as a failure with its reason: the part then runs the digest against "every
+// lane" (exact, no skips on a disconnected graph), its rounds report
+// GG_PATH_LSAT without GG_PATH_LSAT_COMP, and the reason goes to stderr.
+// GG_LSAT_LABELS_FAIL=1 forces that failure (test hook).
+struct LabEntry {
+    std::shared_ptr<const std::vector<uint32_t>> labs;  // empty vector: one component
+    std::string fail;                                    // non-empty: the build failed
+};
 static std::mutex g_lab_mu;
-static std::map<std::vector<uint64_t>, std::shared_ptr<const std::vector<uint32_t>>> g_lab_cache;
+static std::map<std::vector<uint64_t>, LabEntry> g_lab_cache;
 
-static int lsat_parts(gg_engine* e, const gg_gen_spec* spec) {
-    const char* lk = test_knob("GG_LSAT");
-    if (!(e->nwp >= 2 && e->symmetric && e->d_gid && e->n_own && (lk ? atoi(lk) != 0 : e->n_hubs > 0))) return GG_OK;
-    if (!e->d_lsat) {
-        HIPCHK(hipMalloc(&e->d_lsat, e->rows));
-        HIPCHK(hipMemsetAsync(e->d_lsat, 0, e->rows, e->stream));
-    }
+static std::vector<uint64_t> lab_key(const gg_gen_spec* spec) {
     uint64_t ab[3];
     std::memcpy(ab, &spec->a, 8);
     std::memcpy(ab + 1, &spec->b, 8);
     std::memcpy(ab + 2, &spec->c, 8);
-    const std::vector<uint64_t> key = {spec->kind, spec->k, spec->n, spec->seed, ab[0], ab[1], ab[2]};
-    std::shared_ptr<const std::vector<uint32_t>> labs;
+    return {spec->kind, spec->k, spec->n, spec->seed, ab[0], ab[1], ab[2]};
+}
+
+static bool lsat_wanted(const gg_engine* e, bool hubs_known) {
+    const char* lk = test_knob("GG_LSAT");
+    if (lk) return atoi(lk) != 0 && e->nwp >= 2;
+    return e->nwp >= 2 && (!hubs_known || e->n_hubs > 0);  // before the install: hubs unknown, prepare anyway
+}
+
+// The whole graph's component labels into the cache (once per spec and process).
+static void lab_prepare(gg_engine* e, const gg_gen_spec* spec) {
+    if (!lsat_wanted(e, false) || spec->kind == GG_GEN_TREE) return;  // (a tree is connected)
+    const auto key = lab_key(spec);
     {
-        std::lock_guard<std::mutex> lk2(g_lab_mu);
-        auto it = g_lab_cache.find(key);
-        if (it != g_lab_cache.end()) labs = it->second;
+        std::lock_guard<std::mutex> lk(g_lab_mu);
+        if (g_lab_cache.count(key)) return;
     }
+    LabEntry ent;
+    gg_gen::Csr g{};
+    std::string err;
+    unsigned long long roots = 0;
     uint32_t* d_lab = nullptr;
-    if (!labs) {
-        gg_gen::Csr g{};
-        std::string err;
-        unsigned long long roots = 0;
-        int rc = gg_gen::build_csr(*spec, e->stream, 0u, &g, &err);
-        if (rc == GG_OK && hipMalloc(&d_lab, e->V * 4) != hipSuccess) rc = GG_EIO;
-        if (rc == GG_OK) rc = cc_labels(e, g.row_ptr, g.col, e->V, d_lab, &roots, nullptr, 0, 0);
-        (void)hipFree(g.row_ptr);
-        (void)hipFree(g.col);
-        auto h = std::make_shared<std::vector<uint32_t>>();
-        if (rc == GG_OK && roots > 1) {
-            h->resize(e->V);
-            if (hipMemcpy(h->data(), d_lab, e->V * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = GG_EIO;
-        }
-        if (rc != GG_OK) {  // no component targets for this part (see above)
-            (void)hipGetLastError();
-            (void)hipFree(d_lab);
-            e->err.clear();
-            return hipStreamSynchronize(e->stream) == hipSuccess ? GG_OK : GG_EIO;
-        }
-        labs = h;  // (empty: one component, lusat serves)
-        std::lock_guard<std::mutex> lk2(g_lab_mu);
-        if (g_lab_cache.size() > 4) g_lab_cache.clear();
-        g_lab_cache[key] = labs;
+    int rc = test_knob("GG_LSAT_LABELS_FAIL") ? GG_EIO : GG_OK;
+    if (rc) err = "GG_LSAT_LABELS_FAIL";
+    if (rc == GG_OK) rc = gg_gen::build_csr(*spec, e->stream, 0u, &g, &err);
+    if (rc == GG_OK && hipMalloc(&d_lab, e->V * 4) != hipSuccess) rc = GG_EIO, err = "labels: hipMalloc";
+    if (rc == GG_OK) {
+        rc = cc_labels(e, g.row_ptr, g.col, e->V, d_lab, &roots, nullptr, 0, 0);
+        if (rc) err = "cc_labels: " + e->err;
+    }
+    (void)hipFree(g.row_ptr);
+    (void)hipFree(g.col);
+    auto h = std::make_shared<std::vector<uint32_t>>();
+    if (rc == GG_OK && roots > 1) {
+        h->resize(e->V);
+        if (hipMemcpy(h->data(), d_lab, e->V * 4, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = GG_EIO, err = "labels: copy to host";
+    }
+    (void)hipFree(d_lab);
+    (void)hipGetLastError();
+    (void)hipStreamSynchronize(e->stream);
+    e->err.clear();
+    if (rc == GG_OK) {
+        ent.labs = h;
+    } else {
+        ent.fail = err.empty() ? "whole-graph build failed" : err;
+    }
+    std::lock_guard<std::mutex> lk(g_lab_mu);
+    if (g_lab_cache.size() > 4) g_lab_cache.clear();
+    g_lab_cache[key] = ent;
+}
+
+static int lsat_parts(gg_engine* e, const gg_gen_spec* spec) {
+    if (!(e->symmetric && e->d_gid && e->n_own && lsat_wanted(e, true))) return GG_OK;
+    if (!e->d_lsat) {
+        HIPCHK(hipMalloc(&e->d_lsat, e->rows));
+        HIPCHK(hipMemsetAsync(e->d_lsat, 0, e->rows, e->stream));
+    }
+    LabEntry ent;
+    if (spec->kind != GG_GEN_TREE) {
+        lab_prepare(e, spec);  // (a no-op after generate_sharded's call)
+        std::lock_guard<std::mutex> lk(g_lab_mu);
+        auto it = g_lab_cache.find(lab_key(spec));
+        if (it != g_lab_cache.end()) ent = it->second;
+        else ent.fail = "labels evicted from the cache";
+    }
+    if (!ent.fail.empty()) {
+        std::fprintf(stderr, "gg engine part %u: lean digest without component targets (every lane is the "
+                             "target): %s\n", e->part, ent.fail.c_str());
+        return hipStreamSynchronize(e->stream) == hipSuccess ? GG_OK : GG_EIO;
     }
     int rc = GG_OK;
-    if (!labs->empty()) {
-        e->h_lab = *labs;
+    uint32_t* d_lab = nullptr;
+    if (ent.labs && !ent.labs->empty()) {
+        e->h_lab = *ent.labs;
         e->lab_global = true;
-        if (!d_lab) {
-            HIPCHK(hipMalloc(&d_lab, e->V * 4));
-            HIPCHK(hipMemcpy(d_lab, e->h_lab.data(), e->V * 4, hipMemcpyHostToDevice));
-        }
+        HIPCHK(hipMalloc(&d_lab, e->V * 4));
+        HIPCHK(hipMemcpy(d_lab, e->h_lab.data(), e->V * 4, hipMemcpyHostToDevice));
         if (hipMalloc(&e->d_llab, e->n_own * 4) != hipSuccess) {
             rc = e->fail(GG_EIO, "lean digest: labels");
         } else {
@@ -2547,6 +2588,7 @@ static int generate_sharded(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz
     for (uint32_t p = 0; p < P; ++p) plo[p] = std::min<uint64_t>(V, (V * p / P) / 64 * 64);
     plo[P] = V;
     const uint64_t lo = plo[e->part], hi = plo[e->part + 1];
+    lab_prepare(e, spec);  // the whole graph's labels while this part holds no HBM yet
     gg_gen::Csr g{};
     std::string err;
     int rc = gg_gen::build_csr_rows(*spec, e->stream, 0u, lo, hi, &g, &err);
@@ -3620,13 +3662,58 @@ int gg_dist_ipc_import(gg_engine* e, const uint8_t* blobs) {
             std::fprintf(stderr, "gg_dist_ipc_import part %u: %s %u at %.3f s\n", e->part, what, q,
                          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     };
+    if (dbg) {
+        size_t fr = 0, tot = 0;
+        (void)hipMemGetInfo(&fr, &tot);
+        std::fprintf(stderr, "gg_dist_ipc_import part %u: HBM free %.2f of %.2f GiB, own window %.3f GiB\n",
+                     e->part, fr / 1073741824.0, tot / 1073741824.0,
+                     (gg::kWinHdr + 2.0 * std::max<uint64_t>(e->win_rbuf, 256)) / 1073741824.0);
+    }
+    double limit_s = 120.0;
+    if (const char* s = test_knob("GG_IPC_OPEN_TIMEOUT_S")) limit_s = std::max(1.0, atof(s));
     for (uint32_t q = 0; q < P; ++q) {
         const bool snd = q != e->part && e->xsoff[q + 1] > e->xsoff[q];
         const bool rcv = q != e->part && e->xroff[q + 1] > e->xroff[q];
         if (!snd && !rcv) continue;
         void* m = nullptr;
         note("open", q);
-        HIPCHK(hipIpcOpenMemHandle(&m, b[q].handle, hipIpcMemLazyEnablePeerAccess));
+        {  // bounded: a mapping that never returns fails this rank instead of hanging it
+            struct Open {
+                std::mutex mu;
+                std::condition_variable cv;
+                bool done = false;
+                hipError_t rc = hipSuccess;
+                void* m = nullptr;
+            };
+            auto st = std::make_shared<Open>();
+            const int dev = e->device;
+            const hipIpcMemHandle_t h = b[q].handle;
+            std::thread([st, h, dev] {
+                (void)hipSetDevice(dev);
+                void* mm = nullptr;
+                const hipError_t rc = hipIpcOpenMemHandle(&mm, h, hipIpcMemLazyEnablePeerAccess);
+                std::lock_guard<std::mutex> lk(st->mu);
+                st->rc = rc;
+                st->m = mm;
+                st->done = true;
+                st->cv.notify_all();
+            }).detach();
+            std::unique_lock<std::mutex> lk(st->mu);
+            if (!st->cv.wait_for(lk, std::chrono::duration<double>(limit_s), [&] { return st->done; })) {
+                for (void*& pm : e->peer_map)
+                    if (pm) (void)hipIpcCloseMemHandle(pm), pm = nullptr;
+                return e->fail(GG_EIO, "gg_dist_ipc_import: hipIpcOpenMemHandle of part " + std::to_string(q) +
+                                           "'s window did not return within " + std::to_string((int)limit_s) +
+                                           " s (GG_IPC_OPEN_TIMEOUT_S)");
+            }
+            if (st->rc != hipSuccess) {
+                for (void*& pm : e->peer_map)
+                    if (pm) (void)hipIpcCloseMemHandle(pm), pm = nullptr;
+                return e->fail(GG_EIO, std::string("gg_dist_ipc_import: hipIpcOpenMemHandle: ") +
+                                           hipGetErrorString(st->rc));
+            }
+            m = st->m;
+        }
         note("opened", q);
         e->peer_map[q] = m;
         win[q] = static_cast<uint8_t*>(m);
@@ -3643,6 +3730,24 @@ int gg_dist_ipc_import(gg_engine* e, const uint8_t* blobs) {
     HIPCHK(hipMemcpy(e->d_peer_rbuf, rb.data(), P * 8, hipMemcpyHostToDevice));
     note("tables done", P);
     e->ipc = true;
+    return GG_OK;
+}
+
+int gg_dist_ipc_close(gg_engine* e) {
+    if (!e) return GG_EINVAL;
+    if (!e->ipc && e->peer_map.empty()) return GG_OK;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));  // (waits are bounded: a dead exchange drains)
+    if (e->dist_exec) (void)hipGraphExecDestroy(e->dist_exec);  // its kernels name the peer windows
+    e->dist_exec = nullptr;
+    for (void*& m : e->peer_map)
+        if (m) (void)hipIpcCloseMemHandle(m);
+    e->peer_map.clear();
+    dfree(e->d_peer_win);
+    dfree(e->d_peer_off);
+    dfree(e->d_peer_rbuf);
+    e->send_mask = e->recv_mask = 0;
+    e->ipc = false;
     return GG_OK;
 }
 

@@ -157,6 +157,13 @@ class ShardedRunner:
         else:
             self.transport = "torch all_to_all_single" if self.nccl else "gloo via host"
 
+    def close(self) -> None:
+        """Collective: drop the device-driven exchange's peer mappings on every rank
+        before any rank closes its engine (see _ipc_teardown)."""
+        if self.transport.startswith("device-driven"):
+            _ipc_teardown([self.eng], self.group)
+            self.transport = "closed"
+
     def _init_engine_comm(self) -> bool:
         """Open the engine's own RCCL communicator (over its lane group's parts)
         if every rank can (agreed by an all_reduce first, so no rank waits in a
@@ -338,6 +345,23 @@ def _ipc_connect(engines: list[Engine], group, rank: int, world: int, P: int) ->
         e.dist_ipc_import(blobs)
 
 
+def _ipc_teardown(engines: list[Engine], group) -> None:
+    """Collective: every rank unmaps its peers' windows (gg_dist_ipc_close), then
+    one all_reduce, so that no window is freed (engine close) while a peer still
+    maps it. A rank whose unmapping failed still joins the collective."""
+    err = None
+    for e in engines:
+        try:
+            e.dist_ipc_close()
+        except Exception as exc:  # noqa: BLE001
+            err = err or exc
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, group=group)
+    if err is not None:
+        raise err
+
+
 def _sum_rounds(a: list[dict], b: list[dict]) -> list[dict]:
     """Per-round counters of two engines over disjoint lanes, summed (seen_hash mod 2^64)."""
     out = []
@@ -405,6 +429,13 @@ class HalvesRunner:
             for e in engines:
                 self.xports.append(HostTransport(e, device, group, rank_of=[glob(g * P + x) for x in range(P)]))
             self.transport = "engine sequencing, gloo host transport, two lane halves per GPU"
+
+    def close(self) -> None:
+        """Collective: drop both halves' peer mappings on every rank before any
+        rank closes its engines (see _ipc_teardown)."""
+        if self.transport.startswith("device-driven"):
+            _ipc_teardown(self.engs, self.group)
+            self.transport = "closed"
 
     def step(self, n_rounds: int, reduce: bool = True) -> list[dict]:
         if self.transport.startswith("device-driven"):

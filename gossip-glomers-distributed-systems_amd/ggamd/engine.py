@@ -135,7 +135,7 @@ GG_SYMBOLS = [
     "gg_read_bits_nodes", "gg_delivery_rounds_nodes",
     "gg_dist_round_begin", "gg_dist_round_end", "gg_dist_flush", "gg_dist_owned", "gg_dist_info",
     "gg_dist_comm_available", "gg_dist_comm_id", "gg_dist_comm_init", "gg_dist_transport_init", "gg_dist_step",
-    "gg_dist_ipc_export", "gg_dist_ipc_import", "gg_dist_run_episodes",
+    "gg_dist_ipc_export", "gg_dist_ipc_import", "gg_dist_ipc_close", "gg_dist_run_episodes",
 ]
 
 _LIBS: dict[str, C.CDLL] = {}
@@ -187,6 +187,7 @@ def load_library(path: str) -> C.CDLL:
     lib.gg_dist_run_episodes.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, P(GGRoundStats)]
     lib.gg_dist_ipc_export.argtypes = [C.c_void_p, C.c_void_p]
     lib.gg_dist_ipc_import.argtypes = [C.c_void_p, C.c_void_p]
+    lib.gg_dist_ipc_close.argtypes = [C.c_void_p]
     lib.gg_dist_transport_init.argtypes = [C.c_void_p, P(GGTransport)]
     lib.gg_delivery_rounds_nodes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
     if hasattr(lib, "gg_topology_generate"):
@@ -463,6 +464,12 @@ class Engine:
         assert len(blobs) == self.parts * IPC_BLOB_BYTES
         buf = (C.c_uint8 * len(blobs)).from_buffer_copy(blobs)
         self._ok(self.lib.gg_dist_ipc_import(self.h, buf))
+
+    def dist_ipc_close(self) -> None:
+        """Unmap the peers' windows (collective teardown, first half: every part
+        calls it, the caller barriers, then the engines are closed)."""
+        if getattr(self, "h", None):
+            self._ok(self.lib.gg_dist_ipc_close(self.h))
 
     def dist_comm_init(self, uid: bytes) -> None:
         assert len(uid) == 128

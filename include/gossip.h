@@ -138,6 +138,8 @@ typedef struct {
                                    candidates (double-buffered rounds of a single engine before the timers) */
 #define GG_PATH_SOLO 128u       /* marking round with one expand kernel: the one the last run of this round
                                    needed (busy or not), instead of both with one exiting at once */
+#define GG_PATH_LSAT 256u       /* the engine holds the lean saturation digest */
+#define GG_PATH_LSAT_COMP 512u  /* ... with per-component targets (else every injected lane is the target) */
 
 /* Inter-node messages of a round = fwd_sent + pushes + acks + reads + read_oks. */
 
@@ -352,7 +354,17 @@ int gg_dist_run_episodes(gg_engine* e, uint32_t n_rounds, uint32_t episodes, gg_
  * and import again). gg_dist_round_begin reports zero bytes to move. */
 #define GG_IPC_BLOB_BYTES 1024
 int gg_dist_ipc_export(gg_engine* e, uint8_t* blob /* GG_IPC_BLOB_BYTES */);
+/* A mapping that does not return within GG_IPC_OPEN_TIMEOUT_S seconds (env, default
+ * 120) fails the import with GG_EIO instead of hanging the rank. */
 int gg_dist_ipc_import(gg_engine* e, const uint8_t* blobs /* P x GG_IPC_BLOB_BYTES, part order */);
+/* Collective teardown, first half: wait for the engine's stream, unmap every peer
+ * window (hipIpcCloseMemHandle) and drop the exchange; the engine's own window
+ * stays allocated. Every part calls it, then the caller barriers, and only then
+ * does any part destroy its engine (which frees its window): no window is freed
+ * while a peer still maps it. (The reference's nodes hold no shared memory; this
+ * is the device-driven exchange's lifecycle, broadcast.go:50-57's fan-out across
+ * processes.) */
+int gg_dist_ipc_close(gg_engine* e);
 
 /* gg_read_bits / gg_delivery_rounds for a list of owned nodes (any engine). */
 int gg_read_bits_nodes(gg_engine* e, const uint32_t* nodes, uint64_t n, uint64_t* out);

@@ -23,6 +23,8 @@
 // Message counts use per-claimer popcounts (forward exclusion, :52) and the
 // partition masks at the send round. Acks of round r are the broadcasts
 // delivered in round r; they are counted by the sender in round r-1.
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
@@ -69,6 +71,63 @@ struct Acc {  // per-thread counters
 
 inline int popc(uint64_t x) { return __builtin_popcountll(x); }
 
+// Storage that is not zeroed at allocation: the full-size configs (C5: 2^30
+// nodes, 6.4e9 adjacency entries) fill their buffers once, with every thread
+// (reset_state), instead of twice on one.
+template <class T>
+struct NoInit : std::allocator<T> {
+    template <class U>
+    struct rebind { using other = NoInit<U>; };
+    NoInit() = default;
+    template <class U>
+    NoInit(const NoInit<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept { ::new ((void*)p) U; }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+};
+using Words = std::vector<uint64_t, NoInit<uint64_t>>;
+
+// A read-only window on CSR storage held elsewhere in the engine: a symmetric
+// topology on one vertex part keeps ONE copy of the caller's rows and reads it
+// as in-lists, out-lists and (per-edge windows) the caller's CSR alike.
+template <class T>
+struct View {
+    const T* p = nullptr;
+    uint64_t n = 0;
+    const T& operator[](uint64_t i) const { return p[i]; }
+    const T* data() const { return p; }
+    uint64_t size() const { return n; }
+    template <class V>
+    void of(const V& v) { p = reinterpret_cast<const T*>(v.data()); n = v.size(); }
+};
+
+// n items over T threads, contiguous ranges: f(t, begin, end)
+template <class Fn>
+void pfor(int T, uint64_t n, Fn&& f) {
+    if (T <= 1 || n < 65536) {
+        f(0, 0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) th.emplace_back([&, t] { f(t, n * t / T, n * (t + 1) / T); });
+    for (auto& x : th) x.join();
+}
+
+// Host threads: the CPUs this process may run on, capped by the runtime's
+// declared share (OMP_NUM_THREADS: the GPU box's per-GPU share of its host
+// cores); GG_CPU_THREADS overrides both.
+int default_threads() {
+    int n = 0;
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = CPU_COUNT(&cs);
+    if (n <= 0) n = (int)std::max(1u, std::thread::hardware_concurrency());
+    if (const char* s = getenv("OMP_NUM_THREADS"))
+        if (atoi(s) > 0) n = std::min(n, atoi(s));
+    if (const char* s = getenv("GG_CPU_THREADS")) n = std::max(1, atoi(s));
+    return n;
+}
+
 }  // namespace
 
 struct gg_engine {
@@ -85,16 +144,25 @@ struct gg_engine {
     std::vector<uint64_t> rank_lo;         // [world+1]
     bool have_topo = false, symmetric = true;
     // owned rows; columns are replica indices (rank * slice + offset)
-    std::vector<int64_t> crp;              // the caller's CSR (per-edge windows)
-    std::vector<int32_t> ccol;
-    std::vector<int64_t> in_ptr, out_ptr;
-    std::vector<uint32_t> in_col, out_col;
-    std::vector<uint8_t> in_recip;
+    View<int64_t> crp;                     // the caller's CSR (per-edge windows)
+    View<int32_t> ccol;
+    View<int64_t> in_ptr, out_ptr;
+    View<uint32_t> in_col, out_col;
+    std::vector<uint8_t> in_recip;         // empty: every in-edge is reciprocal (symmetric topology)
+    bool recip(int64_t e) const { return in_recip.empty() || in_recip[e]; }
+    // the storage behind the views (a symmetric topology on one part: only s_ptr, s_col)
+    std::vector<int64_t, NoInit<int64_t>> s_ptr, s_optr, s_crp;
+    std::vector<uint32_t, NoInit<uint32_t>> s_col, s_ocol;
+    std::vector<int32_t, NoInit<int32_t>> s_ccol;
     // replicas [world*slice][nw]
-    std::vector<uint64_t> seen[2], F[2];
+    Words seen[2], F[2];
+    // act[b][rep] = 1 iff F[b]'s row is not zero (a sender with nothing new is skipped)
+    std::vector<uint8_t, NoInit<uint8_t>> act[2];
     std::vector<uint64_t> fired[4];        // [world*slice/64]
-    std::vector<int64_t> sync_next;        // owned
-    std::vector<uint32_t> sync_k;
+    bool fired_nz[4] = {false, false, false, false};  // slot holds some fired bit
+    bool fired_any(int64_t r) const { return r >= 0 && fired_nz[r & 3]; }
+    std::vector<int64_t, NoInit<int64_t>> sync_next;  // owned (filled by reset_state)
+    std::vector<uint32_t, NoInit<uint32_t>> sync_k;
     std::vector<int32_t> dr;               // owned rows * W
     // batched gossip (cfg.batch_ticks): pending values, and who delivered them
     std::vector<uint64_t> pend;            // owned rows * nw
@@ -137,8 +205,9 @@ struct gg_engine {
         return w->seeded ? (int)gg_part_group(cfg.seed, w->epoch_seed, g) : (int)w->group[g];
     }
     // message from global a to global b sent in round r dropped?
-    bool masked(int64_t r, uint64_t a, uint64_t b) const {
-        const Window* w = window_at(r);
+    bool masked(int64_t r, uint64_t a, uint64_t b) const { return masked_in(window_at(r), a, b); }
+    // the same under the window of its round (window_at, hoisted out of a round's loops)
+    bool masked_in(const Window* w, uint64_t a, uint64_t b) const {
         if (!w) return false;
         if (w->edges) {  // the link a -> b (symmetric topology: it exists both ways)
             const int32_t* r0 = ccol.data() + crp[a];
@@ -154,14 +223,22 @@ struct gg_engine {
     }
     void reset_state() {
         for (int b = 0; b < 2; ++b) {
-            std::fill(seen[b].begin(), seen[b].end(), 0ull);
-            std::fill(F[b].begin(), F[b].end(), 0ull);
+            pfor(threads, seen[b].size(), [&](int, uint64_t i0, uint64_t i1) {
+                std::fill(seen[b].begin() + i0, seen[b].begin() + i1, 0ull);
+                std::fill(F[b].begin() + i0, F[b].begin() + i1, 0ull);
+            });
+            std::fill(act[b].begin(), act[b].end(), (uint8_t)0);
         }
-        for (int b = 0; b < 4; ++b) std::fill(fired[b].begin(), fired[b].end(), 0ull);
-        for (uint64_t i = 0; i < hi - lo; ++i) {
-            sync_k[i] = 0;
-            sync_next[i] = gg_sync_interval(cfg.seed, lo + i, 0, cfg.sync_base_ticks, cfg.sync_jitter_ticks);
+        for (int b = 0; b < 4; ++b) {
+            std::fill(fired[b].begin(), fired[b].end(), 0ull);
+            fired_nz[b] = false;
         }
+        pfor(threads, hi - lo, [&](int, uint64_t i0, uint64_t i1) {
+            for (uint64_t i = i0; i < i1; ++i) {
+                sync_k[i] = 0;
+                sync_next[i] = gg_sync_interval(cfg.seed, lo + i, 0, cfg.sync_base_ticks, cfg.sync_jitter_ticks);
+            }
+        });
         std::fill(dr.begin(), dr.end(), -1);
         std::fill(pend.begin(), pend.end(), 0ull);
         std::fill(pend_src.begin(), pend_src.end(), ~0u);
@@ -199,10 +276,10 @@ void gg_engine::compute_round_batched(Acc& a) {
     const uint64_t n_own = hi - lo;
     const bool sync = cfg.enable_sync != 0;
     const uint32_t W = (uint32_t)(nw * 64);
-    std::vector<uint64_t>& sp_all = seen[(r + 1) & 1];
-    std::vector<uint64_t>& sc_all = seen[r & 1];
-    std::vector<uint64_t>& Fp_all = F[(r + 1) & 1];
-    std::vector<uint64_t>& Fc_all = F[r & 1];
+    auto& sp_all = seen[(r + 1) & 1];
+    auto& sc_all = seen[r & 1];
+    auto& Fp_all = F[(r + 1) & 1];
+    auto& Fc_all = F[r & 1];
     std::fill(fired[r & 3].begin(), fired[r & 3].end(), 0ull);
     std::unordered_map<uint32_t, std::vector<uint32_t>> inj_by_node;
     {
@@ -212,6 +289,7 @@ void gg_engine::compute_round_batched(Acc& a) {
             inj.erase(it);
         }
     }
+    fired_nz[r & 3] = false;
     const bool tick = (r + 1) % (int64_t)cfg.batch_ticks == 0;
     std::vector<uint64_t> S(nw), sp(nw);
     std::vector<uint64_t> firedw;
@@ -329,6 +407,7 @@ void gg_engine::compute_round_batched(Acc& a) {
     a.dropped += a.node_dropped;
     a.node_dropped = 0;
     for (uint64_t g : firedw) fired[r & 3][g >> 6] |= 1ull << (g & 63);
+    fired_nz[r & 3] = !firedw.empty();
 }
 
 void gg_engine::compute_round(Acc& total) {
@@ -337,10 +416,12 @@ void gg_engine::compute_round(Acc& total) {
     const uint64_t own0 = (uint64_t)part * slice;
     const bool sync = cfg.enable_sync != 0;
     const uint32_t W = (uint32_t)(nw * 64);  // this engine's lanes
-    std::vector<uint64_t>& sp_all = seen[(r + 1) & 1];  // seen_prev (round r-1)
-    std::vector<uint64_t>& sc_all = seen[r & 1];        // seen_cur
-    std::vector<uint64_t>& Fp_all = F[(r + 1) & 1];
-    std::vector<uint64_t>& Fc_all = F[r & 1];
+    auto& sp_all = seen[(r + 1) & 1];  // seen_prev (round r-1)
+    auto& sc_all = seen[r & 1];        // seen_cur
+    auto& Fp_all = F[(r + 1) & 1];
+    auto& Fc_all = F[r & 1];
+    const uint8_t* act_p = act[(r + 1) & 1].data();
+    uint8_t* act_c = act[r & 1].data();
     // fired slot of round r: owned words cleared here (world slices are refreshed by the exchange)
     {
         auto& fr = fired[r & 3];
@@ -360,30 +441,48 @@ void gg_engine::compute_round(Acc& total) {
     const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads, n_own / 256 + 1));
     std::vector<Acc> accs(T);
     std::vector<std::vector<uint64_t>> firedw(T);
+    // the windows of the rounds this one reads, and whether any timer fired in
+    // r-1 (reads arriving now) and r-3 (pushes arriving now): hoisted out of the
+    // per-edge loop, which is then one sender row per edge in lean rounds
+    const Window *wm3 = window_at(r - 3), *wm2 = window_at(r - 2), *wm1 = window_at(r - 1);
+    const Window *w00 = window_at(r), *wp1 = window_at(r + 1);
+    const bool any_w = wm3 || wm2 || wm1 || w00 || wp1;
+    const bool f1 = sync && fired_any(r - 1), f2 = sync && fired_any(r - 2), f3 = sync && fired_any(r - 3);
+    const bool any_inj = !inj_by_node.empty();
     auto work = [&](int t) {
         Acc& a = accs[t];
         std::vector<uint64_t> S(nw), sp(nw);
         const uint64_t b0 = n_own * t / T, b1 = n_own * (t + 1) / T;
+        constexpr uint64_t kAhead = 8;  // sender rows prefetched this many nodes ahead
         for (uint64_t i = b0; i < b1; ++i) {
             const uint64_t g = lo + i, rep = own0 + i;
+            if (i + kAhead < b1)
+                for (int64_t e = in_ptr[i + kAhead]; e < in_ptr[i + kAhead + 1]; ++e) {
+                    const uint64_t u = in_col[e];
+                    if (act_p[u])
+                        for (uint64_t j = 0; j < nw; j += 8) __builtin_prefetch(&Fp_all[u * nw + j]);
+                }
             const uint64_t* spv = &sp_all[rep * nw];
             for (uint64_t j = 0; j < nw; ++j) sp[j] = S[j] = spv[j];
             // (1) client broadcasts
-            auto ij = inj_by_node.find((uint32_t)g);
-            if (ij != inj_by_node.end())
-                for (uint32_t lane : ij->second) S[lane >> 6] |= 1ull << (lane & 63);
+            if (any_inj) {
+                auto ij = inj_by_node.find((uint32_t)g);
+                if (ij != inj_by_node.end())
+                    for (uint32_t lane : ij->second) S[lane >> 6] |= 1ull << (lane & 63);
+            }
             // (2) node broadcasts, ascending sender
             uint64_t cl_recip = 0, cl_deliv = 0, cl_ackdrop = 0;
             for (int64_t e = in_ptr[i]; e < in_ptr[i + 1]; ++e) {
                 const uint64_t urep = in_col[e];
-                const uint64_t u = global_of(urep);
-                if (sync && fired_at(r - 1, urep) && !masked(r - 1, u, g)) {  // read arrives
-                    a.read_oks++;                                             // HandleRead :131
-                    if (masked(r, g, u)) a.node_dropped++;
+                const uint64_t u = any_w ? global_of(urep) : urep;  // (only the masks read it)
+                if (f1 && fired_at(r - 1, urep) && !masked_in(wm1, u, g)) {  // read arrives
+                    a.read_oks++;                                          // HandleRead :131
+                    if (masked_in(w00, g, u)) a.node_dropped++;
                 }
-                if (masked(r - 1, u, g)) continue;                            // dropped in flight
-                const bool push = sync && fired_at(r - 3, urep) && !masked(r - 3, u, g) &&
-                                  !masked(r - 2, g, u);
+                if (masked_in(wm1, u, g)) continue;                        // dropped in flight
+                const bool push = f3 && fired_at(r - 3, urep) && !masked_in(wm3, u, g) &&
+                                  !masked_in(wm2, g, u);
+                if (!push && !act_p[urep]) continue;  // its F row is zero: nothing to claim
                 const uint64_t* src = push ? &sp_all[urep * nw] : &Fp_all[urep * nw];
                 uint64_t pc = 0;
                 for (uint64_t j = 0; j < nw; ++j) {
@@ -391,22 +490,22 @@ void gg_engine::compute_round(Acc& total) {
                     S[j] |= c;
                     pc += popc(c);
                 }
-                if (pc && in_recip[e]) {
+                if (pc && recip(e)) {
                     cl_recip += pc;
-                    if (!masked(r, g, u)) {
+                    if (!masked_in(w00, g, u)) {
                         cl_deliv += pc;
-                        if (masked(r + 1, u, g)) cl_ackdrop += pc;
+                        if (masked_in(wp1, u, g)) cl_ackdrop += pc;
                     }
                 }
             }
             // (3) sync callback: fired in r-2, peers ascending
             uint64_t cb_new = 0, cb_new_deliv = 0, cb_new_ackdrop = 0;
             uint64_t push_sent = 0, push_deliv = 0, push_ackdrop = 0;
-            if (sync && fired_at(r - 2, rep)) {
+            if (f2 && fired_at(r - 2, rep)) {
                 for (int64_t e = out_ptr[i]; e < out_ptr[i + 1]; ++e) {
                     const uint64_t wrep = out_col[e];
                     const uint64_t w = global_of(wrep);
-                    if (masked(r - 2, g, w) || masked(r - 1, w, g)) continue;
+                    if (masked_in(wm2, g, w) || masked_in(wm1, w, g)) continue;
                     const uint64_t* R = &sp_all[wrep * nw];
                     uint64_t pn = 0, pp = 0;
                     for (uint64_t j = 0; j < nw; ++j) {
@@ -416,10 +515,10 @@ void gg_engine::compute_round(Acc& total) {
                     }
                     cb_new += pn;
                     push_sent += pp;
-                    if (!masked(r, g, w)) {
+                    if (!masked_in(w00, g, w)) {
                         cb_new_deliv += pn;
                         push_deliv += pp;
-                        if (masked(r + 1, w, g)) {
+                        if (masked_in(wp1, w, g)) {
                             cb_new_ackdrop += pn;
                             push_ackdrop += pp;
                         }
@@ -445,18 +544,18 @@ void gg_engine::compute_round(Acc& total) {
                     }
                 }
             }
+            act_c[rep] = Tn != 0;
             a.new_bits += Tn;
             // counts of what v sends in round r
             const uint64_t deg = (uint64_t)(out_ptr[i + 1] - out_ptr[i]);
             uint64_t U = deg, AD = 0, mdrop = 0;
-            const bool mr = window_at(r) != nullptr, mr1 = window_at(r + 1) != nullptr;
-            if (mr || mr1) {
+            if (w00 || wp1) {
                 U = 0;
                 for (int64_t e = out_ptr[i]; e < out_ptr[i + 1]; ++e) {
                     const uint64_t w = global_of(out_col[e]);
-                    if (!masked(r, g, w)) {
+                    if (!masked_in(w00, g, w)) {
                         U++;
-                        if (masked(r + 1, w, g)) AD++;
+                        if (masked_in(wp1, w, g)) AD++;
                     } else {
                         mdrop++;
                     }
@@ -499,6 +598,9 @@ void gg_engine::compute_round(Acc& total) {
         total.add(accs[t]);
         for (uint64_t rep : firedw[t]) fired[r & 3][rep >> 6] |= 1ull << (rep & 63);
     }
+    // the slot's own words; a vertex part ORs its peers' in at gg_dist_round_end
+    fired_nz[r & 3] = false;
+    for (int t = 0; t < T; ++t) fired_nz[r & 3] |= !firedw[t].empty();
 }
 
 // --------------------------------------------------------------------------
@@ -530,9 +632,7 @@ int gg_create(const gg_config* cfg, gg_engine** out) {
     e->nw_g = cfg->n_lanes / 64;
     e->w0 = e->nw_g * e->lgrp / L;
     e->nw = e->nw_g * (e->lgrp + 1) / L - e->w0;
-    unsigned hc = std::thread::hardware_concurrency();
-    e->threads = hc ? (int)hc : 1;
-    if (const char* s = getenv("GG_CPU_THREADS")) e->threads = std::max(1, atoi(s));
+    e->threads = default_threads();
     *out = e;
     return GG_OK;
 }
@@ -544,37 +644,70 @@ const char* gg_last_error(const gg_engine* e) { return e ? e->err.c_str() : "nul
 int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64_t nnz) {
     if (!e || !row_ptr || (nnz && !col)) return GG_EINVAL;
     const uint64_t V = e->V;
+    const int T = e->threads;
     if (row_ptr[0] != 0 || (uint64_t)row_ptr[V] != nnz) return e->fail(GG_EINVAL, "row_ptr[0]/row_ptr[V] mismatch");
-    for (uint64_t v = 0; v < V; ++v) {
-        if (row_ptr[v + 1] < row_ptr[v]) return e->fail(GG_EINVAL, "row_ptr not monotone");
-        for (int64_t k = row_ptr[v]; k < row_ptr[v + 1]; ++k) {
-            if (col[k] < 0 || (uint64_t)col[k] >= V) return e->fail(GG_EINVAL, "neighbour id out of range");
-            if (k > row_ptr[v] && col[k] <= col[k - 1])
-                return e->fail(GG_EINVAL, "neighbour list not ascending/unique");
-        }
+    {  // rows monotone, ids in range, each row ascending and unique (the first bad row reports)
+        std::vector<uint64_t> bad_v(std::max(T, 1), V);
+        std::vector<const char*> bad_m(std::max(T, 1), nullptr);
+        pfor(T, V, [&](int t, uint64_t v0, uint64_t v1) {
+            for (uint64_t v = v0; v < v1; ++v) {
+                const char* m = nullptr;
+                if (row_ptr[v + 1] < row_ptr[v]) {
+                    m = "row_ptr not monotone";
+                } else {
+                    for (int64_t k = row_ptr[v]; k < row_ptr[v + 1] && !m; ++k) {
+                        if (col[k] < 0 || (uint64_t)col[k] >= V) m = "neighbour id out of range";
+                        else if (k > row_ptr[v] && col[k] <= col[k - 1]) m = "neighbour list not ascending/unique";
+                    }
+                }
+                if (m) {
+                    bad_v[t] = v;
+                    bad_m[t] = m;
+                    return;
+                }
+            }
+        });
+        uint64_t bv = V;
+        const char* bm = nullptr;
+        for (size_t t = 0; t < bad_v.size(); ++t)
+            if (bad_m[t] && bad_v[t] < bv) bv = bad_v[t], bm = bad_m[t];
+        if (bm) return e->fail(GG_EINVAL, bm);
     }
-    // transpose: in-lists ascending by sender
-    std::vector<int64_t> tin(V + 1, 0);
-    for (uint64_t k = 0; k < nnz; ++k) tin[col[k] + 1]++;
-    for (uint64_t v = 0; v < V; ++v) tin[v + 1] += tin[v];
-    std::vector<uint32_t> tcol(nnz);
-    {
-        std::vector<int64_t> pos(tin.begin(), tin.end() - 1);
-        for (uint64_t u = 0; u < V; ++u)
-            for (int64_t k = row_ptr[u]; k < row_ptr[u + 1]; ++k) tcol[pos[col[k]]++] = (uint32_t)u;
-    }
+    // symmetric iff every link u -> v has its v -> u (rows are ascending and unique)
     bool sym = true;
-    for (uint64_t v = 0; v < V && sym; ++v) {
-        if (tin[v + 1] - tin[v] != row_ptr[v + 1] - row_ptr[v]) sym = false;
-        else
-            for (int64_t k = 0; k < tin[v + 1] - tin[v]; ++k)
-                if ((int64_t)tcol[tin[v] + k] != col[row_ptr[v] + k]) { sym = false; break; }
+    {
+        std::atomic<bool> asym{false};
+        pfor(T, V, [&](int, uint64_t u0, uint64_t u1) {
+            for (uint64_t u = u0; u < u1 && !asym.load(std::memory_order_relaxed); ++u)
+                for (int64_t k = row_ptr[u]; k < row_ptr[u + 1]; ++k) {
+                    const int32_t v = col[k];
+                    if (!std::binary_search(col + row_ptr[v], col + row_ptr[v + 1], (int32_t)u)) {
+                        asym = true;
+                        break;
+                    }
+                }
+        });
+        sym = !asym;
     }
     e->symmetric = sym;
-    e->crp.assign(row_ptr, row_ptr + V + 1);
-    e->ccol.assign(col, col + nnz);
     e->windows.erase(std::remove_if(e->windows.begin(), e->windows.end(), [](const Window& w) { return w.edges; }),
                      e->windows.end());
+    // in-lists ascending by sender: the rows themselves when symmetric, else the transpose
+    std::vector<int64_t> tin_s;
+    std::vector<uint32_t> tcol_s;
+    const int64_t* tin = row_ptr;
+    const uint32_t* tcol = reinterpret_cast<const uint32_t*>(col);
+    if (!sym) {
+        tin_s.assign(V + 1, 0);
+        for (uint64_t k = 0; k < nnz; ++k) tin_s[col[k] + 1]++;
+        for (uint64_t v = 0; v < V; ++v) tin_s[v + 1] += tin_s[v];
+        tcol_s.resize(nnz);
+        std::vector<int64_t> pos(tin_s.begin(), tin_s.end() - 1);
+        for (uint64_t u = 0; u < V; ++u)
+            for (int64_t k = row_ptr[u]; k < row_ptr[u + 1]; ++k) tcol_s[pos[col[k]]++] = (uint32_t)u;
+        tin = tin_s.data();
+        tcol = tcol_s.data();
+    }
     // edge-balanced vertex ranges over the in-lists (pull work)
     const uint32_t Wd = e->P;  // vertex parts of this lane group
     e->rank_lo.assign(Wd + 1, V);
@@ -594,36 +727,68 @@ int gg_topology(gg_engine* e, const int64_t* row_ptr, const int32_t* col, uint64
     e->lo = e->rank_lo[e->part];
     e->hi = e->rank_lo[e->part + 1];
     const uint64_t n_own = e->hi - e->lo;
-    // owned rows with replica column ids
-    e->in_ptr.assign(n_own + 1, 0);
-    e->out_ptr.assign(n_own + 1, 0);
-    for (uint64_t i = 0; i < n_own; ++i) {
-        e->in_ptr[i + 1] = e->in_ptr[i] + (tin[e->lo + i + 1] - tin[e->lo + i]);
-        e->out_ptr[i + 1] = e->out_ptr[i] + (row_ptr[e->lo + i + 1] - row_ptr[e->lo + i]);
-    }
-    e->in_col.resize(e->in_ptr[n_own]);
-    e->in_recip.resize(e->in_ptr[n_own]);
-    e->out_col.resize(e->out_ptr[n_own]);
-    for (uint64_t i = 0; i < n_own; ++i) {
-        const uint64_t v = e->lo + i;
-        const int32_t* ob = col + row_ptr[v];
-        const int32_t* oe = col + row_ptr[v + 1];
-        for (int64_t k = 0; k < tin[v + 1] - tin[v]; ++k) {
-            uint32_t u = tcol[tin[v] + k];
-            e->in_col[e->in_ptr[i] + k] = (uint32_t)e->rep_of(u);
-            e->in_recip[e->in_ptr[i] + k] = std::binary_search(ob, oe, (int32_t)u) ? 1 : 0;
+    // copy helpers (every thread: the full-size configs hold 6.4e9 entries)
+    auto copy_ptr = [&](auto& dst, const int64_t* src, uint64_t n) {
+        dst.resize(n);
+        pfor(T, n, [&](int, uint64_t i0, uint64_t i1) { std::copy(src + i0, src + i1, dst.begin() + i0); });
+    };
+    e->s_optr.clear(); e->s_ocol.clear(); e->s_crp.clear(); e->s_ccol.clear();
+    e->in_recip.clear();
+    if (Wd == 1 && sym) {
+        // one part (replica index = global id) of a symmetric graph: ONE copy of the
+        // caller's rows serves as in-lists, out-lists and the per-edge window CSR
+        copy_ptr(e->s_ptr, row_ptr, V + 1);
+        e->s_col.resize(nnz);
+        pfor(T, nnz, [&](int, uint64_t i0, uint64_t i1) {
+            for (uint64_t k = i0; k < i1; ++k) e->s_col[k] = (uint32_t)col[k];
+        });
+        e->in_ptr.of(e->s_ptr);
+        e->in_col.of(e->s_col);
+        e->out_ptr = e->in_ptr;
+        e->out_col = e->in_col;
+        e->crp.of(e->s_ptr);
+        e->ccol.of(e->s_col);
+    } else {
+        copy_ptr(e->s_crp, row_ptr, V + 1);
+        e->s_ccol.assign(col, col + nnz);
+        e->crp.of(e->s_crp);
+        e->ccol.of(e->s_ccol);
+        // owned rows with replica column ids
+        e->s_ptr.assign(n_own + 1, 0);
+        e->s_optr.assign(n_own + 1, 0);
+        for (uint64_t i = 0; i < n_own; ++i) {
+            e->s_ptr[i + 1] = e->s_ptr[i] + (tin[e->lo + i + 1] - tin[e->lo + i]);
+            e->s_optr[i + 1] = e->s_optr[i] + (row_ptr[e->lo + i + 1] - row_ptr[e->lo + i]);
         }
-        for (int64_t k = 0; k < row_ptr[v + 1] - row_ptr[v]; ++k)
-            e->out_col[e->out_ptr[i] + k] = (uint32_t)e->rep_of((uint64_t)ob[k]);
+        e->s_col.resize(e->s_ptr[n_own]);
+        if (!sym) e->in_recip.resize(e->s_ptr[n_own]);  // symmetric: every in-edge is reciprocal
+        e->s_ocol.resize(e->s_optr[n_own]);
+        for (uint64_t i = 0; i < n_own; ++i) {
+            const uint64_t v = e->lo + i;
+            const int32_t* ob = col + row_ptr[v];
+            const int32_t* oe = col + row_ptr[v + 1];
+            for (int64_t k = 0; k < tin[v + 1] - tin[v]; ++k) {
+                uint32_t u = tcol[tin[v] + k];
+                e->s_col[e->s_ptr[i] + k] = (uint32_t)e->rep_of(u);
+                if (!sym) e->in_recip[e->s_ptr[i] + k] = std::binary_search(ob, oe, (int32_t)u) ? 1 : 0;
+            }
+            for (int64_t k = 0; k < row_ptr[v + 1] - row_ptr[v]; ++k)
+                e->s_ocol[e->s_optr[i] + k] = (uint32_t)e->rep_of((uint64_t)ob[k]);
+        }
+        e->in_ptr.of(e->s_ptr);
+        e->in_col.of(e->s_col);
+        e->out_ptr.of(e->s_optr);
+        e->out_col.of(e->s_ocol);
     }
     const uint64_t rows = (uint64_t)Wd * e->slice;
-    for (int b = 0; b < 2; ++b) {
-        e->seen[b].assign(rows * e->nw, 0);
-        e->F[b].assign(rows * e->nw, 0);
+    for (int b = 0; b < 2; ++b) {  // zeroed by reset_state below
+        e->seen[b].resize(rows * e->nw);
+        e->F[b].resize(rows * e->nw);
+        e->act[b].resize(rows);
     }
     for (int b = 0; b < 4; ++b) e->fired[b].assign(rows / 64, 0);
-    e->sync_next.assign(n_own, 0);
-    e->sync_k.assign(n_own, 0);
+    e->sync_next.resize(n_own);
+    e->sync_k.resize(n_own);
     if (e->cfg.flags & GG_TRACK_DELIVERY) e->dr.assign(n_own * e->nw * 64, -1);
     else e->dr.clear();
     e->pend.assign(e->cfg.batch_ticks ? n_own * e->nw : 0, 0ull);
@@ -873,9 +1038,15 @@ int gg_dist_round_end(gg_engine* e, gg_round_stats* out) {
             const uint64_t rep = (uint64_t)q * e->slice + (g - e->rank_lo[q]);
             std::memcpy(&e->seen[r & 1][rep * e->nw], p, e->nw * 8);
             std::memcpy(&e->F[r & 1][rep * e->nw], p + e->nw * 8, e->nw * 8);
+            e->act[r & 1][rep] = 0;
+            for (uint64_t j = 0; j < e->nw; ++j) e->act[r & 1][rep] |= e->F[r & 1][rep * e->nw + j] != 0;
             uint64_t& w = e->fired[r & 3][rep >> 6];
-            if (p[2 * e->nw * 8]) w |= 1ull << (rep & 63);
-            else w &= ~(1ull << (rep & 63));
+            if (p[2 * e->nw * 8]) {
+                w |= 1ull << (rep & 63);
+                e->fired_nz[r & 3] = true;
+            } else {
+                w &= ~(1ull << (rep & 63));
+            }
         }
     }
     gg_round_stats s;
@@ -909,6 +1080,7 @@ int gg_dist_comm_available(char* why, uint64_t cap) {
 int gg_dist_comm_id(const gg_engine*, uint8_t*) { return GG_EIO; }
 int gg_dist_ipc_export(gg_engine*, uint8_t*) { return GG_EIO; }  // no device memory to map
 int gg_dist_ipc_import(gg_engine*, const uint8_t*) { return GG_EIO; }
+int gg_dist_ipc_close(gg_engine* e) { return e ? GG_OK : GG_EINVAL; }  // nothing mapped
 int gg_dist_comm_init(gg_engine* e, const uint8_t*) { return e ? e->fail(GG_EIO, "CPU oracle: no RCCL") : GG_EINVAL; }
 int gg_dist_step(gg_engine* e, uint32_t) { return e ? e->fail(GG_EIO, "CPU oracle: no RCCL") : GG_EINVAL; }
 int gg_dist_run_episodes(gg_engine* e, uint32_t, uint32_t, gg_round_stats*) {

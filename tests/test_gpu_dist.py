@@ -772,6 +772,7 @@ def _ipc_worker(rank, world, port, lib, scenarios, q, lane_groups, env):
                 e.broadcast(int(n), int(v), int(rr))
             again = r.step(sc.rounds)
             out.append(res + (again,))
+            r.close()  # collective: every rank unmaps its peers' windows before any window is freed
             e.close()
         q.put((rank, out))
     except BaseException as exc:  # report instead of leaving the parent waiting
@@ -1012,7 +1013,19 @@ def _episodes_worker(rank, world, port, lib, scenarios, q, lane_groups, episodes
             for n, v, rr in sc.injections:
                 e.broadcast(int(n), int(v), int(rr))
             again = r.step(sc.rounds)
+            # collective teardown (gg_dist_ipc_close on every rank, then a barrier), and
+            # the same engines map each other's windows again: the same episode once more
+            r.close()
+            r = ShardedRunner(e, dev, transport="ipc")
+            e.reset()
+            for n, v, rr in sc.injections:
+                e.broadcast(int(n), int(v), int(rr))
+            reimported = r.step(sc.rounds)
+            from ggamd.engine import COUNT_FIELDS
+            key = lambda st: [[x[f] for f in COUNT_FIELDS] for x in st]  # noqa: E731
+            assert key(reimported) == key(again), "an episode after re-import differs"
             out.append((eps, owned, bits, again))
+            r.close()
             e.close()
         q.put((rank, out))
     except BaseException as exc:  # report instead of leaving the parent waiting

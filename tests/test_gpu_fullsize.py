@@ -1,6 +1,10 @@
 """BASELINE.json's two largest configs at their full size, in the GPU suite
 (graphs built in HBM by the on-device generators, gossip_gen.h).
 
+* C5 and C4 against the CPU oracle O2 at full size, round by round: every
+  counter and the delivery hash (tests/golden/fullsize_c5.json, fullsize_c4.json,
+  made by tests/golden/make_fullsize_golden.py from the host builders' graphs:
+  O2 needs minutes of the host's cores there, beyond this suite's budget).
 * C5, 2^30 nodes (grid + one long link per node, W = 64): the grid spans
   every node, so each message must reach all V nodes (P1), and before any
   sync timer fires every node forwards each value to all neighbours but its
@@ -16,10 +20,13 @@
   this GPU (gg_config.lane_groups: 2048 lanes each, another kernel
   instantiation over another row width): every round's counters and delivery
   hash, summed over the ranks, equal the single engine's.
-The reference has no full-size fixtures; these are size-independent
-properties of broadcast.go's algorithm, the CPU oracle O2 is
-pinned against it at 4K nodes (tests/test_golden.py).
+The reference has no fixtures at all; the properties are size-independent
+consequences of broadcast.go's algorithm, and O2 is pinned
+against the message-level restatement O1 and the KATs (tests/test_o2_vs_o1.py).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -42,16 +49,42 @@ def _to_quiescence(e, inj, cap=60):
             return out
 
 
-def test_c5_full_size_properties(hip_lib):
+def _golden(name):
+    """O2's full-size record of a config (tests/golden/make_fullsize_golden.py:
+    the host-built graph, every round's counters and delivery hash)."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"fullsize_{name}.json")
+    with open(path) as f:
+        return json.load(f)
+
+
+def _diff_golden(st, gold):
+    """Every round's counters and seen_hash (the fingerprint of every (node, value)
+    first-delivery round so far) against O2's record."""
+    want = gold["rounds"]
+    assert len(st) == len(want), f"quiescence after {len(st)} rounds, O2 after {len(want)}"
+    for a, w in zip(st, want):
+        bad = [(f, a[f] & M64, w[f]) for f in COUNT_FIELDS if (a[f] & M64) != w[f]]
+        assert not bad, f"round {w['round']}: HIP != O2 {bad}"
+
+
+def test_c5_full_size_equals_o2(hip_lib):
+    """C5 at 2^30 nodes against O2 round by round: the device-generated graph
+    has the host builder's adjacency count, and every round's counters and
+    delivery hash to quiescence equal O2's run on the host-built graph
+    (tests/golden/fullsize_c5.json); then P1 / KAT-3 / ACK."""
+    gold = _golden("c5")
     side, K = 32768, 64
     V = side * side
     seed = BASE_SEED + 5
+    assert (gold["nodes"], gold["lanes"], gold["seed"]) == (V, K, seed)
     e = Engine(V, K, seed=seed, enable_sync=True, library=hip_lib)
     try:
         nnz = e.generate("grid_links", side, seed=seed)
         st = _to_quiescence(e, injection_arrays(uniform_injections(V, K, seed)))
     finally:
         e.close()
+    assert nnz == gold["nnz"]
+    _diff_golden(st, gold)
     assert st[-1]["new_bits"] == 0, "no quiescence within 60 rounds"
     assert all(s["syncs_fired"] == 0 for s in st), "a sync timer fired before quiescence"
     assert sum(s["new_bits"] for s in st) == V * K  # P1: every message reached every node
@@ -118,8 +151,11 @@ def test_c3_full_size_equals_o2(hip_lib, cpu_lib):
         c.close()
 
 
-def test_c4_full_size_lane_groups_equal_single(hip_lib):
-    """Also, on the single engine: P1 (every message reaches exactly its
+def test_c4_full_size_equals_o2_and_lane_groups(hip_lib):
+    """C4 at 10^8 nodes, W = 4096: the single engine's every round (counters and
+    delivery hash) against O2's run on the host-built graph
+    (tests/golden/fullsize_c4.json: O2 as 4 lane-group engines of 1024 lanes,
+    summed); then, on the same engine: P1 (every message reaches exactly its
     source's connected component) and KAT-3 (no timer fires before
     quiescence, so forwards = Σ_m [vol(comp) - (|comp| - 1)]), with the
     components computed from the exported graph."""
@@ -129,13 +165,17 @@ def test_c4_full_size_lane_groups_equal_single(hip_lib):
     inj_l = uniform_injections(V, K, seed)
     inj = injection_arrays(inj_l)
     e = Engine(V, K, seed=seed, enable_sync=True, library=hip_lib)
+    gold = _golden("c4")
+    assert (gold["nodes"], gold["lanes"], gold["seed"]) == (V, K, seed)
     try:
-        e.generate(**gen)
+        nnz = e.generate(**gen)
         want = _to_quiescence(e, inj)
         print("C4: episode done, exporting the graph", flush=True)
         topo = e.export_topology()
     finally:
         e.close()
+    assert nnz == gold["nnz"]
+    _diff_golden(want, gold)  # O2 on the host-built graph, every round
     assert want[-1]["new_bits"] == 0
     assert all(s["syncs_fired"] == 0 for s in want), "a sync timer fired before quiescence"
     lab, size, vol = components(topo.row_ptr, topo.col)
