@@ -84,18 +84,25 @@ GOLD_C2 = os.path.join(REPO, "tests", "golden", "bench_c2.json")
 # the random-row request ceiling (rows of <= 128 B gathered by a per-node index,
 # tools/gather_bench.hip): what a kernel whose rows are one line
 # each can reach, where the byte roofline cannot be. profiles/request_ceiling.json
-# holds the same ceiling in the L2's memory-side requests (TCC_EA0_RDREQ +
-# WRREQ per second of gather_bench under rocprofv3), the unit of line_frac
+# holds it in the L2's memory-side requests (TCC_EA0_RDREQ per second of
+# gather_bench under rocprofv3), the unit of line_frac, and the write side
+# (TCC_EA0_WRREQ of its random-row stores and coalesced sweep); this constant
+# is only the fallback without that file
 ROW_CEILING_PER_S = 47e9
 REQ_CEILING_JSON = os.path.join(REPO, "profiles", "request_ceiling.json")
 
 
 def request_ceiling():
+    """(read, write) memory-side request ceilings per second and their source: the
+    random-row gathers, and the highest of the random-row stores and the coalesced
+    store sweep (tools/gather_bench.hip --calibrate, profiles/request_ceiling.json).
+    Write requests run far faster than reads (reset_state's sweep: ~86 G/s), so
+    counting a kernel's writes against the read ceiling overstated line_frac."""
     try:
         d = json.load(open(REQ_CEILING_JSON))
-        return float(d["requests_per_s"]), os.path.relpath(REQ_CEILING_JSON, REPO)
+        return float(d["requests_per_s"]), d.get("write_requests_per_s"), os.path.relpath(REQ_CEILING_JSON, REPO)
     except (OSError, ValueError, KeyError, TypeError):
-        return ROW_CEILING_PER_S, "tools/gather_bench.hip rows/s (profiles/r2/gather_ceiling.txt)"
+        return ROW_CEILING_PER_S, None, "tools/gather_bench.hip rows/s (profiles/r2/gather_ceiling.txt)"
 
 
 def pmc_traffic(kind: str, shape: dict):
@@ -123,16 +130,17 @@ def pmc_traffic(kind: str, shape: dict):
     for name, ent in d.get("kernels", {}).items():
         b = base(name)
         if b in KIND_KERNELS[kind]:
-            e = ents.setdefault(b, [0.0, 0, 0.0, "rd_requests_per_dispatch" in ent])
+            e = ents.setdefault(b, [0.0, 0, 0.0, 0.0, "rd_requests_per_dispatch" in ent])
             e[0] += ent["traffic_bytes_per_dispatch"] * ent["dispatches"]
             e[1] += ent["dispatches"]
-            e[2] += (ent.get("rd_requests_per_dispatch", 0.0) + ent.get("wr_requests_per_dispatch", 0.0)) * \
-                ent["dispatches"]
+            e[2] += ent.get("rd_requests_per_dispatch", 0.0) * ent["dispatches"]
+            e[3] += ent.get("wr_requests_per_dispatch", 0.0) * ent["dispatches"]
     episodes = resets - 1
     if episodes < 1 or not ents:
         return None, None, None
     per_ep = sum(v[0] for v in ents.values()) / episodes
-    reqs = sum(v[2] for v in ents.values()) / episodes if all(v[3] for v in ents.values()) else None
+    reqs = ((sum(v[2] for v in ents.values()) / episodes, sum(v[3] for v in ents.values()) / episodes)
+            if all(v[4] for v in ents.values()) else None)
     return per_ep, (f'{os.path.relpath(path, REPO)} ({d.get("source", "")}; kernels {sorted(ents)}; '
                     f'{episodes} episodes)'), reqs
 
@@ -160,13 +168,13 @@ def roofline(rounds_local: list[dict], nwp: int, n_own: int, E_own: int, shape: 
     """The dominant kernel kind's roofline over a run's rounds (this rank):
     per-kind device times (first block start to last block end of each launch,
     stamped by the kernels) and the algorithmic bytes each launch had to move
-    (counted by the kernels). line_frac: the kind's memory-side
-    requests per second (TCC_EA0_RDREQ + WRREQ per round from the committed
-    PMC pass of this shape, over the kind's measured time per round) against
-    the same counters' rate at the random-row ceiling (gather_bench): random
-    rows of <= 128 B are request-bound, so the byte roofline is out of reach
-    for them. Without a request pass for this shape: a row model from the
-    kernels' work counters (line_source says which)."""
+    (counted by the kernels). line_frac: the time the kind's
+    memory-side requests of an episode (TCC_EA0_RDREQ and WRREQ from the
+    committed PMC pass of this shape) need at the measured ceilings — reads at
+    the random-row gather rate, writes at the fastest store rate
+    (tools/gather_bench.hip --calibrate) — over the kind's measured time per
+    episode: random rows of <= 128 B are request-bound, so the byte roofline
+    is out of reach for them. null without a request pass of this shape."""
     kinds = {}
     n = max(1, len(rounds_local))
     for kind, name in KERNELS.items():
@@ -182,12 +190,19 @@ def roofline(rounds_local: list[dict], nwp: int, n_own: int, E_own: int, shape: 
     R = n / max(1, episodes)  # rounds per episode: one launch of the kind per round
     traffic = traffic_ep / R if traffic_ep else None
     kind_s_ep = D["total_ms"] / max(1, episodes) * 1e-3  # the kind's device time per episode
-    ceiling, ceiling_src = request_ceiling()
-    lines_per_row = max(1, (8 * nwp + 127) // 128)
-    # rows moved by the round's kernels: gathered sender rows + own row read + row written
-    rows = sum(s["work_gathers"] + 2 * s["work_rows"] for s in rounds_local)
+    rd_ceil, wr_ceil, ceiling_src = request_ceiling()
+    line_frac = line_src = None
+    if reqs_ep and kind_s_ep > 0:
+        rd, wr = reqs_ep
+        # the time the kind's requests need at the ceilings, reads and writes each at its
+        # own rate (no write ceiling measured: writes at the read rate, an upper bound)
+        need = rd / rd_ceil + wr / (wr_ceil or rd_ceil)
+        line_frac = need / kind_s_ep
+        line_src = (f"PMC: {rd:.4g} read + {wr:.4g} write memory-side requests per episode of this kind "
+                    f"({traffic_src}) need {need * 1e3:.4g} ms at {rd_ceil:.4g} read / "
+                    f"{(wr_ceil or rd_ceil):.4g} write requests/s (the random-row gather and the fastest store "
+                    f"ceilings, {ceiling_src}); the kind ran {kind_s_ep * 1e3:.4g} ms per episode")
     round_ms = sum(s["kernel_ms"] for s in rounds_local)
-    lines_per_s = rows * lines_per_row / (round_ms * 1e-3) if round_ms > 0 else 0.0
     round_bytes = sum(s["prep_bytes"] + s["expand_bytes"] + s["stream_bytes"] for s in rounds_local)
     return {
         "bound": "hbm",
@@ -204,21 +219,10 @@ def roofline(rounds_local: list[dict], nwp: int, n_own: int, E_own: int, shape: 
         "avg_launch_ms": D["avg_launch_ms"],
         "launches": D["launches"],
         "dense_bytes_per_round": dense_bytes_per_round(n_own, E_own, nwp),
-        "line_frac": (reqs_ep / kind_s_ep / ceiling) if reqs_ep and kind_s_ep > 0 else None,
-        "line_source": (f"PMC: {reqs_ep:.4g} memory-side requests per episode of this kind ({traffic_src}) over "
-                        f"its {kind_s_ep * 1e3:.4g} ms per episode, against {ceiling:.4g} requests/s at the random-row "
-                        f"ceiling ({ceiling_src})" if reqs_ep
-                        else "null: no request pass of this shape in profiles/ (line_model.frac is a row model "
-                             "that overcounts rows sharing a line, e.g. grid neighbours at W = 64)"),
-        "requests_per_launch": reqs_ep / R if reqs_ep else None,
-        "line_model": {"frac": lines_per_s / ROW_CEILING_PER_S, "rows_moved": rows, "lines_per_row": lines_per_row,
-                       "line_bytes": 128,
-                       "lines_per_s": lines_per_s, "ceiling_lines_per_s": ROW_CEILING_PER_S,
-                       "over": "every kernel of the timed rounds (round device time)",
-                       "note": "rows = sender rows gathered + 2 x nodes visited (own row read, and "
-                               "written: counted for every visited node, an upper bound), from the "
-                               "kernels' work counters; columns and flag bytes stream and are not "
-                               "counted"},
+        "line_frac": line_frac,
+        "line_source": line_src or "null: no request pass of this shape in profiles/",
+        "read_requests_per_launch": reqs_ep[0] / R if reqs_ep else None,
+        "write_requests_per_launch": reqs_ep[1] / R if reqs_ep else None,
         "timing": "per launch: device clock (s_memrealtime) from the first block start to the last "
                   "block end of that kernel, stamped by every block (no-op launches included, as in "
                   "rocprofv3's average)",
@@ -654,7 +658,7 @@ def headline(job: Job, args) -> tuple[dict | None, dict]:
     roof["event_ms_per_step"] = (sum(event_ms) / len(event_ms)) if event_ms else None
     roof["per_call_ms_per_step"] = per_call_ms
     roof["stamp_ms_per_step"] = sum(s["kernel_ms"] for s in rounds_local) / args.steps
-    roof["timing"] += ("; cross-check: HIP events on the engine stream around episodes 1..K-1 of the "
+    roof["timing"] += ("; cross-check: HIP events on the engine stream around episodes 2..K-1 (episode 1 may recapture the batch) of the "
                        "pipelined run (event_ms_per_step)")
     xbytes = None
     if runner is not None:  # payload bytes this rank sent per round (mean over the timed rounds)
@@ -1209,11 +1213,19 @@ def cpu_baseline(cfg, topo, inj, V, K, seed, R):
         e.close()
         return dl / dt, eps, rounds, dt
 
+    scaling = None
     if cfg == "C2":
         v_all, n_all, r_all, _ = o2_episodes(topo, inj, V, K, seed, threads, 8.0, R)
         sample_all = f"{n_all} full C2 episodes ({r_all} rounds each)"
         v_one, n_one, r_one, _ = o2_episodes(topo, inj, V, K, seed, 1, 6.0, R)
         sample_one = f"{n_one} full C2 episode(s) on one thread"
+        # thread scaling inside the share (the whole box is not this process's to take)
+        scaling = {"1": v_one, str(threads): v_all}
+        t = 2
+        while t < threads:
+            scaling[str(t)] = o2_episodes(topo, inj, V, K, seed, t, 2.0, R)[0]
+            t *= 2
+        scaling = dict(sorted(scaling.items(), key=lambda kv: int(kv[0])))
     else:  # C4: R-MAT samples of the same generator (the 10^8-node graph needs ~150 GB of host state)
         Va = 1 << 20
         ta = T.rmat(Va, 16, seed=seed)
@@ -1225,10 +1237,15 @@ def cpu_baseline(cfg, topo, inj, V, K, seed, R):
         sample_one = f"{n_one} episode(s) ({r_one} rounds) of the R-MAT generator at 2^17 nodes on one thread"
     o1 = o1_c1_leg()
     return {"value": v_all, "unit": "deliveries/s", "cores": threads, "kind": "port",
-            "sample": f"O2 bitset oracle (oracle/o2_bitset.cpp, -O3, AVX-512 host) on {threads} threads: "
-                      f"{sample_all}",
+            "sample": f"O2 bitset oracle (oracle/o2_bitset.cpp, -O3) on {threads} threads: {sample_all}",
             "host_cpus": host_cpus, "affinity_cpus": affinity, "cores_basis": basis,
             "single_thread": {"value": v_one, "unit": "deliveries/s", "cores": 1, "sample": sample_one},
+            "thread_scaling": scaling,
+            "whole_box": {"value": None, "cores": affinity,
+                          "note": (f"not measured: this process's CPU share is {threads} of the host's {host_cpus} "
+                                   "CPUs (OMP_NUM_THREADS on the GPU box; the other GPUs' jobs own the rest), so "
+                                   "O2 runs on that share; thread_scaling gives its curve inside the share"
+                                   if threads < affinity else "= value (every CPU this process may use)")},
             "o1_per_message": o1}
 
 

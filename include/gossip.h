@@ -215,8 +215,9 @@ int gg_step_device_ms(const gg_engine* e, double* ms);
  * episode (its trailing quiet rounds tell the later resets which buffers an
  * episode leaves dirty) and at the end.
  * Single engine (not vertex-sharded), 1 <= n_rounds <= 256. gg_step_device_ms
- * then gives the device time per episode of episodes 1..K-1, the ones queued
- * after the host wait (episode 0 alone when episodes == 1). (Host side of a Maelstrom run that
+ * then gives the device time per episode of episodes 2..K-1 (episode 1 can hold
+ * a graph capture: the hints learned from episode 0 change the batch; with two
+ * episodes it is episode 1, with one episode 0). (Host side of a Maelstrom run that
  * replays one broadcast workload many times; the reference has no counterpart.) */
 int gg_run_episodes(gg_engine* e, uint32_t n_rounds, uint32_t episodes, gg_round_stats* out);
 

@@ -66,33 +66,42 @@ def test_traffic_json_and_bench_normalisation(tmp_path, monkeypatch):
     # 3 episodes (4 resets less the install's), 4 rounds each, both kernels every round
     want_bytes = 12 * ((2 * 1000.0 + 500.0) + (2 * 10.0 + 5.0)) * 1024 / 3
     assert per_ep == pytest.approx(want_bytes) and "3 episodes" in src
-    assert reqs == pytest.approx(12 * (16000 + 8000 + 160 + 80) / 3)
+    assert reqs[0] == pytest.approx(12 * (16000 + 160) / 3) and reqs[1] == pytest.approx(12 * (8000 + 80) / 3)
     # another shape: no traffic, and no line_frac
     other = dict(d["shape"], nodes=1 << 21)
     assert bench.pmc_traffic("stream", other)[0] is None
 
-    # roofline over synthetic rounds: line_frac = requests per episode / kind time per episode / ceiling
+    # roofline over synthetic rounds: line_frac = (reads at the read ceiling + writes at the
+    # write ceiling) per episode / the kind's time per episode
     rounds = [{"round": i % 4, "kernel_ms": 0.5, "prep_ms": 0.0, "expand_ms": 0.0, "stream_ms": 0.4,
                "prep_bytes": 0, "expand_bytes": 0, "stream_bytes": 10 ** 8, "work_gathers": 10, "work_rows": 10}
               for i in range(12)]
+    ceil = tmp_path / "ceiling.json"
+    ceil.write_text(json.dumps({"requests_per_s": 5e10, "write_requests_per_s": 8e10}))
+    monkeypatch.setattr(bench, "REQ_CEILING_JSON", str(ceil))
     roof = bench.roofline(rounds, 16, 1 << 20, 2 * (1 << 20), d["shape"], 3)
-    ceiling, _ = bench.request_ceiling()
-    assert roof["line_frac"] == pytest.approx(reqs / (4 * 0.4e-3) / ceiling)
+    assert roof["line_frac"] == pytest.approx((reqs[0] / 5e10 + reqs[1] / 8e10) / (4 * 0.4e-3))
     assert roof["traffic"] == pytest.approx(per_ep / 4)
     roof2 = bench.roofline(rounds, 16, 1 << 20, 2 * (1 << 20), other, 3)
-    assert roof2["line_frac"] is None and roof2["line_model"]["frac"] > 0
+    assert roof2["line_frac"] is None and "line_model" not in roof2
 
 
 def test_request_ceiling(tmp_path):
     stdout = tmp_path / "gather.txt"
     stdout.write_text("calibrate rows  64 B G= 4 rows_per_dispatch 1000 rows_per_s 4.0e+10\n"
-                      "calibrate rows 512 B G=32 rows_per_dispatch 1000 rows_per_s 1.0e+10\n")
+                      "calibrate rows 512 B G=32 rows_per_dispatch 1000 rows_per_s 1.0e+10\n"
+                      "calibrate writes  64 B G= 4 rows_per_dispatch 1000 rows_per_s 5.0e+10\n"
+                      "calibrate seqwrite bytes_per_dispatch 2000000 bytes_per_s 5.0e+12\n")
     rows = []
     for d, (name, rd) in enumerate((("void gather<4, 8>(uint4 const*, unsigned int const*, unsigned long, uint4*)", 1050),
                                     ("void gather<32, 8>(uint4 const*, unsigned int const*, unsigned long, uint4*)",
                                      4050))):
         rows += [dict(Dispatch_Id=d, Kernel_Name=name, Counter_Name="TCC_EA0_RDREQ_sum", Counter_Value=rd),
                  dict(Dispatch_Id=d, Kernel_Name=name, Counter_Name="TCC_EA0_WRREQ_sum", Counter_Value=0)]
+    for d, (name, wr) in enumerate((("void scatter<4, 8>(uint4*, unsigned int const*, unsigned long)", 1100),
+                                    ("seqwrite(uint4*, unsigned long)", 32000)), start=2):
+        rows += [dict(Dispatch_Id=d, Kernel_Name=name, Counter_Name="TCC_EA0_RDREQ_sum", Counter_Value=0),
+                 dict(Dispatch_Id=d, Kernel_Name=name, Counter_Name="TCC_EA0_WRREQ_sum", Counter_Value=wr)]
     _csv(tmp_path / "req.csv", rows)
     out = tmp_path / "ceiling.json"
     subprocess.check_call([sys.executable, os.path.join(REPO, "tools", "request_ceiling.py"), str(stdout),
@@ -101,3 +110,7 @@ def test_request_ceiling(tmp_path):
     by = {r["row_bytes"]: r for r in d["rows"]}
     assert by[64]["requests_per_row"] == pytest.approx(1.05) and by[512]["requests_per_row"] == pytest.approx(4.05)
     assert d["requests_per_s"] == pytest.approx(max(4.0e10 * 1.05, 1.0e10 * 4.05))
+    # writes: the random-row stores (5e10 rows/s x 1.1) and the sweep (32000 requests in 0.4 us)
+    assert d["write_rows"][0]["requests_per_row"] == pytest.approx(1.1)
+    assert d["write_sweep"]["requests_per_s"] == pytest.approx(32000 / (2e6 / 5e12))
+    assert d["write_requests_per_s"] == pytest.approx(max(5e10 * 1.1, 32000 / (2e6 / 5e12)))

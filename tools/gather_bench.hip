@@ -1,5 +1,6 @@
 // gather_bench.hip — random whole-row gathers from a large table on MI355X
-// (tools only): rows/s and GB/s for row sizes 32..512 B, uniformly random or
+// (tools only; --calibrate also times random-row and coalesced stores, the
+// write side of bench.py's line_frac): rows/s and GB/s for row sizes 32..512 B, uniformly random or
 // power-law (row index = the top bits of a product of uniforms, hubs first),
 // into registers (G lanes x 16 B per row, K rows in flight per lane) — the
 // access shape of expand_stream's sender-row gathers at 8..64 lanes per node.
@@ -44,6 +45,42 @@ __global__ __launch_bounds__(256) void gather(const uint4* table, const uint32_t
     out[(uint64_t)blockIdx.x * 256 + threadIdx.x] = acc;
 }
 
+// the write side of the calibration: K random rows per lane group stored (G
+// lanes x 16 B each), and a coalesced sweep (reset_state's pattern)
+template <int G, int K>
+__global__ __launch_bounds__(256) void scatter(uint4* table, const uint32_t* idx, uint64_t n_rows_idx) {
+    const int lg = threadIdx.x % G;
+    const uint64_t groups = (uint64_t)gridDim.x * (256 / G);
+    for (uint64_t r0 = ((uint64_t)blockIdx.x * (256 / G) + threadIdx.x / G) * K; r0 < n_rows_idx; r0 += groups * K) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (r0 + k < n_rows_idx) {
+                const uint32_t ix = idx[r0 + k];
+                table[(uint64_t)ix * G + lg] = make_uint4(ix, (uint32_t)lg, (uint32_t)k, 1u);
+            }
+    }
+}
+
+__global__ __launch_bounds__(256) void seqwrite(uint4* table, uint64_t n16) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256)
+        table[i] = make_uint4((uint32_t)i, 0u, 0u, 1u);
+}
+
+template <int G, int K>
+double run_scatter(uint4* table, const uint32_t* idx, uint64_t n, int blocks) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    hipLaunchKernelGGL((scatter<G, K>), dim3(blocks), dim3(256), 0, 0, table, idx, n);
+    CK(hipEventRecord(a, 0));
+    for (int r = 0; r < 3; ++r) hipLaunchKernelGGL((scatter<G, K>), dim3(blocks), dim3(256), 0, 0, table, idx, n);
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / 3;
+}
+
 template <int G, int K>
 double run(const uint4* table, const uint32_t* idx, uint64_t n, uint4* out, int blocks) {
     hipEvent_t a, b;
@@ -86,6 +123,36 @@ int main(int argc, char** argv) {
                               : rb == 128 ? run<8, 8>(table, idx, n, out, 4096) : run<32, 8>(table, idx, n, out, 4096);
             printf("calibrate rows %3d B G=%2d rows_per_dispatch %llu rows_per_s %.4e\n", rb, rb / 16,
                    (unsigned long long)n, n / (ms * 1e-3));
+            fflush(stdout);
+        }
+        // writes: random rows of 16 / 64 / 128 B (scatter<G, 8>), then a coalesced
+        // sweep of 2 GiB (seqwrite); the write-request ceiling is the highest rate
+        for (int rb : {16, 64, 128}) {
+            const uint64_t rows = tb / rb;
+            uint64_t s = 0x9E3779B97F4A7C15ull + rb;
+            auto rnd = [&]() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; };
+            for (uint64_t i = 0; i < n; ++i) h[i] = (uint32_t)(rnd() % rows);
+            CK(hipMemcpy(idx, h.data(), n * 4, hipMemcpyHostToDevice));
+            const double ms = rb == 16 ? run_scatter<1, 8>(table, idx, n, 4096)
+                              : rb == 64 ? run_scatter<4, 8>(table, idx, n, 4096) : run_scatter<8, 8>(table, idx, n, 4096);
+            printf("calibrate writes %3d B G=%2d rows_per_dispatch %llu rows_per_s %.4e\n", rb, rb / 16,
+                   (unsigned long long)n, n / (ms * 1e-3));
+            fflush(stdout);
+        }
+        {
+            const uint64_t n16 = (2ull << 30) / 16;
+            hipEvent_t a, b;
+            CK(hipEventCreate(&a));
+            CK(hipEventCreate(&b));
+            hipLaunchKernelGGL(seqwrite, dim3(8192), dim3(256), 0, 0, table, n16);
+            CK(hipEventRecord(a, 0));
+            for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(seqwrite, dim3(8192), dim3(256), 0, 0, table, n16);
+            CK(hipEventRecord(b, 0));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            printf("calibrate seqwrite bytes_per_dispatch %llu bytes_per_s %.4e\n", (unsigned long long)(n16 * 16),
+                   n16 * 16 / (ms / 3 * 1e-3));
             fflush(stdout);
         }
         return 0;

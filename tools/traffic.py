@@ -57,7 +57,8 @@ def main():
             ker[k]["rd_requests_per_dispatch"] = mean(rd.get(k, []))
             ker[k]["wr_requests_per_dispatch"] = mean(wr.get(k, []))
     cfg = argv[4] if len(argv) > 4 else "C2"
-    default = {"C2": {"nodes": 1 << 20, "lanes": 1024}, "C4": {"nodes": 100_000_000, "lanes": 4096},
+    default = {"C2": {"nodes": 1 << 20, "lanes": 1024}, "C3": {"nodes": 10_000_000, "lanes": 1024},
+               "C4": {"nodes": 100_000_000, "lanes": 4096},
                "C5": {"nodes": 1 << 30, "lanes": 64}}.get(cfg, {})
     shape = dict(config=cfg, world=1, parts=1, halves=1, **default)
     if len(argv) > 5:
