@@ -29,6 +29,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <type_traits>
@@ -55,7 +56,9 @@ constexpr int kMaxBlocks = 2048;
 // streamed-sync buffers with the topology / from a given round), GG_COMPACT_ATOMIC /
 // GG_COMPACT_SPLIT (one-launch or split compaction whatever the size),
 // GG_IPC_SPIN_LIMIT (sleeps before a device-driven exchange wait gives up), GG_LSAT=0 / 1
-// (lean saturation digest off / on whatever the graph).
+// (lean saturation digest off / on whatever the graph), GG_NEED_BITS=0 (the device-driven
+// exchange ships every active F row), GG_LSAT_LABELS_FAIL=1 (vertex parts: the component
+// labels' build fails; the digest falls back to "every lane"), GG_IPC_OPEN_TIMEOUT_S.
 const char* test_knob(const char* name) { return getenv(name); }
 // A/B switches of past measurements (GG_ALL_FULL, GG_NO_GRAPH, GG_SYNC_ALLPUSH,
 // GG_FLAGS_FIRST, GG_FF_FRAC16, GG_PREP_WIDE, GG_XCHG_EXACT_BYTES): read only in a -DGG_AB_KNOBS build.
@@ -219,6 +222,17 @@ struct gg_engine {
     unsigned long long* h_segbytes = nullptr;  // pinned copy
     unsigned long long* d_payload = nullptr;   // [kMaxBatch] payload bytes of each pending round
     uint32_t xstride = 16;
+    // need bits (device-driven exchange): per source part, where its
+    // need slots sit in this engine's receive region and their size, and for each
+    // destination where ours sit in its window; which peers produce them
+    uint64_t* d_need_in = nullptr;             // [P] window offset of source q's need slot 0 (receiver side)
+    uint64_t* d_need_out = nullptr;            // [P] offset of our need slot 0 in part q's receive region
+    uint64_t* d_need_bytes = nullptr;          // [2P] need slot bytes: [q] we write to q, [P + q] q writes to us
+    gg::NeedWord* d_need_words = nullptr;      // the words our need_bits kernel writes (per source, 64 ghosts)
+    uint32_t n_need_words = 0;
+    uint64_t need_peers = 0;                   // parts whose need bits we may use (they hold the digest)
+    std::set<int64_t> inj_rounds;              // rounds with a client broadcast (the need bits' condition)
+    bool need_produce = false;                 // we write need bits (we hold the digest)
     // exact-size directions (their sizes travel first, one host wait per round),
     // decided per direction from its capacity, which both ends compute alike
     std::vector<uint8_t> xexact_s, xexact_r;   // [P] to / from each part
@@ -476,6 +490,13 @@ void gg_engine::free_topology() {
     dfree(d_xcnt);
     dfree(d_sfirst);
     dfree(d_xtk);
+    dfree(d_need_in);
+    dfree(d_need_out);
+    dfree(d_need_bytes);
+    dfree(d_need_words);
+    n_need_words = 0;
+    need_peers = 0;
+    need_produce = false;
     dfree(d_segbytes);
     dfree(d_payload);
     for (void*& m : peer_map)
@@ -2139,6 +2160,7 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
     e->lanes.clear();
     e->lane_value.clear();
     e->inj.clear();
+    e->inj_rounds.clear();
     e->round = 0;
     e->pend_acks = e->pend_ackdrop = 0;
     e->hash_total = 0;
@@ -2168,14 +2190,41 @@ static int setup_exchange(gg_engine* e) {
     auto cap = [&](uint64_t n) -> uint64_t {
         return n ? std::max<uint64_t>(16 + 2 * n * e->xstride, gg::tile_rows_off(n) + 2 * n * 8 * e->nwp) : 0;
     };
+    // a region also holds three need slots (IPC exchange: one bit per entry of the
+    // opposite direction, rotating by seq % 3) when both directions carry entries
+    auto need = [&](uint64_t n_this, uint64_t n_back) -> uint64_t {
+        return (n_this && n_back) ? 3 * gg::need_slot_bytes(n_back) : 0;
+    };
+    std::vector<uint64_t> need_in(Wd, 0), need_out(Wd, 0), need_bytes(2 * Wd, 0);
+    std::vector<gg::NeedWord> words;
     for (uint32_t q = 0; q < Wd; ++q) {
         const uint64_t ns = e->send_off[q + 1] - e->send_off[q], nr = e->recv_off[q + 1] - e->recv_off[q];
-        e->xsoff[q + 1] = e->xsoff[q] + cap(ns);
-        e->xroff[q + 1] = e->xroff[q] + cap(nr);
+        if (ns && nr) {
+            // our region in q's window (we send ns entries, q sends us nr: our bits cover q's nr)
+            need_out[q] = cap(ns);
+            need_bytes[q] = gg::need_slot_bytes(nr);
+            // q's region in ours (q sends nr, we send ns: q's bits cover our ns entries to q)
+            need_in[q] = gg::kWinHdr + e->xroff[q] + cap(nr);
+            need_bytes[Wd + q] = gg::need_slot_bytes(ns);
+            for (uint64_t j = 0; j < nr; j += 64)
+                words.push_back({q, (uint32_t)j, (uint32_t)std::min<uint64_t>(64, nr - j)});
+        }
+        e->xsoff[q + 1] = e->xsoff[q] + cap(ns) + need(ns, nr);
+        e->xroff[q + 1] = e->xroff[q] + cap(nr) + need(nr, ns);
         for (uint64_t k0 = e->send_off[q]; k0 < e->send_off[q + 1]; k0 += gg::kBlock)
             tiles.push_back({q, (uint32_t)k0, (uint32_t)std::min<uint64_t>(gg::kBlock, e->send_off[q + 1] - k0),
                              (uint32_t)e->send_off[q]});
     }
+    HIPCHK(hipMalloc(&e->d_need_in, Wd * 8));
+    HIPCHK(hipMemcpy(e->d_need_in, need_in.data(), Wd * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&e->d_need_out, Wd * 8));
+    HIPCHK(hipMemcpy(e->d_need_out, need_out.data(), Wd * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&e->d_need_bytes, 2 * Wd * 8));
+    HIPCHK(hipMemcpy(e->d_need_bytes, need_bytes.data(), 2 * Wd * 8, hipMemcpyHostToDevice));
+    e->n_need_words = (uint32_t)words.size();
+    HIPCHK(hipMalloc(&e->d_need_words, std::max<size_t>(1, words.size()) * sizeof(gg::NeedWord)));
+    if (!words.empty())
+        HIPCHK(hipMemcpy(e->d_need_words, words.data(), words.size() * sizeof(gg::NeedWord), hipMemcpyHostToDevice));
     e->n_xtiles = (uint32_t)tiles.size();
     HIPCHK(hipMalloc(&e->d_xtiles, std::max<size_t>(1, tiles.size()) * sizeof(gg::XchgTile)));
     if (!tiles.empty())
@@ -2947,6 +2996,7 @@ static int add_broadcast(gg_engine* e, uint32_t node, int64_t message, int64_t r
         e->lane_value.push_back(message);
     }
     dst.push_back({node, lane});
+    if (e->inj_rounds.empty() || *e->inj_rounds.rbegin() != round) e->inj_rounds.insert(round);
     return GG_OK;
 }
 
@@ -3072,6 +3122,7 @@ void reset_host_state(gg_engine* e, bool keep_schedule) {
         e->lanes.clear();
         e->lane_value.clear();
         e->inj.clear();
+        e->inj_rounds.clear();
     }
     e->dirty_parity = (int)(e->round & 1);
     e->round = 0;
@@ -3283,8 +3334,31 @@ static int enqueue_pack(gg_engine* e, int64_t r, uint32_t slot) {
         hipLaunchKernelGGL(gg::ipc_wait, dim3(1), dim3(64), 0, e->stream, ipc_args(e), 0);
         HIPCHK(hipGetLastError());
     }
+    if (e->ipc && e->need_produce && e->n_need_words) {  // our need bits of round r, for the peers' pack of r+1
+        gg::NeedArgs na{};
+        na.words = e->d_need_words;
+        na.n_words = e->n_need_words;
+        na.gfirst = e->d_gfirst;
+        na.grow = e->d_grow;
+        na.gout_ptr = e->d_gout_ptr;
+        na.gout_col = e->d_gout_col;
+        na.lsat = e->d_lsat;
+        na.need_out = e->d_need_out;
+        na.need_bytes = e->d_need_bytes;
+        na.ipc = ipc_args(e);
+        hipLaunchKernelGGL(gg::need_bits, dim3(std::min<uint32_t>((e->n_need_words + 3) / 4, 4096)), dim3(gg::kBlock), 0,
+                           e->stream, na);
+        HIPCHK(hipGetLastError());
+    }
     if (e->n_xtiles) {
         gg::PackArgs pa{};
+        // the peers' need bits of round r-1 (exact when no lane is injected in r-1 and r:
+        // expand_kernels.hpp NeedWord)
+        if (e->ipc && e->need_peers && r >= 1 && !e->inj_rounds.count(r) && !e->inj_rounds.count(r - 1)) {
+            pa.need_in = e->d_need_in;
+            pa.need_bytes_in = e->d_need_bytes + e->P;
+            pa.need_peers = e->need_peers;
+        }
         pa.F_cur = e->d_F[r & 1];
         pa.base = e->d_base;
         // a double-buffered round wrote no F rows: the payload's are set(r) & ~set(r-1)
@@ -3618,6 +3692,7 @@ int gg_dist_comm_init(gg_engine* e, const uint8_t* id_in) {
 namespace {
 struct IpcBlob {
     uint32_t magic, part, parts, lgrp;
+    uint32_t need, pad;     // the exporting engine writes need bits (it holds the lean digest)
     uint64_t rbuf;          // receive buffer bytes of the exporting engine
     uint64_t roff[64];      // where source part q's segment lands in its receive buffer (xroff[q])
     hipIpcMemHandle_t handle;
@@ -3648,6 +3723,12 @@ int gg_dist_ipc_export(gg_engine* e, uint8_t* blob) {
     b.parts = e->P;
     b.lgrp = e->lgrp;
     b.rbuf = std::max<uint64_t>(e->win_rbuf, 256);
+    // need bits: with the lean digest, unless GG_NEED_BITS=0 (A/B)
+    {
+        const char* nk = test_knob("GG_NEED_BITS");
+        e->need_produce = e->d_lsat != nullptr && e->symmetric && e->n_need_words && !(nk && atoi(nk) == 0);
+    }
+    b.need = e->need_produce ? 1u : 0u;
     for (uint32_t q = 0; q < e->P; ++q) b.roff[q] = e->xroff[q];
     HIPCHK(hipIpcGetMemHandle(&b.handle, e->d_win));
     std::memset(blob, 0, GG_IPC_BLOB_BYTES);
@@ -3672,6 +3753,7 @@ int gg_dist_ipc_import(gg_engine* e, const uint8_t* blobs) {
     std::vector<uint64_t> off(P, 0), rb(P, 0);
     e->peer_map.assign(P, nullptr);
     e->send_mask = e->recv_mask = 0;
+    e->need_peers = 0;
     const bool dbg = test_knob("GG_IPC_DEBUG") != nullptr;
     auto t0 = std::chrono::steady_clock::now();
     auto note = [&](const char* what, uint32_t q) {
@@ -3738,6 +3820,7 @@ int gg_dist_ipc_import(gg_engine* e, const uint8_t* blobs) {
         rb[q] = b[q].rbuf;
         if (snd) e->send_mask |= 1ull << q;
         if (rcv) e->recv_mask |= 1ull << q;
+        if (snd && rcv && b[q].need) e->need_peers |= 1ull << q;  // q's bits cover our sends to q
     }
     HIPCHK(hipMalloc(&e->d_peer_win, P * sizeof(uint8_t*)));
     HIPCHK(hipMalloc(&e->d_peer_off, P * 8));
@@ -3764,6 +3847,7 @@ int gg_dist_ipc_close(gg_engine* e) {
     dfree(e->d_peer_off);
     dfree(e->d_peer_rbuf);
     e->send_mask = e->recv_mask = 0;
+    e->need_peers = 0;
     e->ipc = false;
     return GG_OK;
 }

@@ -4223,6 +4223,29 @@ __device__ __forceinline__ uint8_t* ipc_segment(const IpcArgs& ip, uint32_t q, u
     return ip.peer_win[q] + kWinHdr + (seq & 1) * ip.peer_rbuf[q] + ip.peer_off[q];
 }
 
+// Need bits (device-driven exchange, round 6): after its round r, part p writes
+// into each peer q's window one bit per ghost it holds from q — "some owned
+// receiver of this ghost is not saturated" (the lean digest, lsat == 0) — and q
+// packs round r+1 without the F rows whose bit is clear. Exact when no client
+// broadcasts anything in rounds r and r+1 (the host's condition; every part
+// sees every broadcast): a saturated receiver holds every lane that can reach
+// it among those broadcast through r — the digest is judged against targets
+// that already count them (can't schedule into the past), and a clear by a
+// later target change only forgets bits — and an F row of round r+1 carries
+// only such lanes then; a row that is not sent is a ghost that sent nothing
+// (its stale row is cleared as for any quiet ghost).
+// Three slots rotate by seq % 3: q reads slot (seq - 1) % 3 in its pack of round
+// seq while p may already write slot seq % 3; p writes a slot again three rounds
+// later, after ipc_wait(0) saw q's unpack of round seq + 1, i.e. after q's pack
+// of round seq + 1 read it. The slots sit in the sender's region of the parity-0
+// receive buffer, after its rows area.
+struct NeedWord {
+    uint32_t peer;  // source part of the ghosts (the part we write to)
+    uint32_t j0;    // first ghost of the word, relative to that source's first (a multiple of 64)
+    uint32_t n;     // ghosts in the word (<= 64)
+};
+__host__ __device__ inline uint64_t need_slot_bytes(uint64_t n) { return (n + 127) / 128 * 16; }
+
 struct XchgTile {
     uint32_t peer;   // part index of the destination
     uint32_t k0;     // first send entry of the tile (global send-list index)
@@ -4252,6 +4275,11 @@ struct PackArgs {
     unsigned long long* seg_bytes;
     unsigned long long* payload;
     const uint32_t* sfirst;     // [parts + 1] first send entry of each peer (tile segments)
+    // need bits of the round before (nullptr: every F row ships): window offset of
+    // each source's slot 0 and slot bytes, and the sources that write them
+    const uint64_t* need_in;
+    const uint64_t* need_bytes_in;
+    uint64_t need_peers;
 };
 
 __device__ __forceinline__ void finish_pack_body(uint32_t* cnt, uint8_t* out, const uint64_t* seg_off, uint32_t parts,
@@ -4278,7 +4306,13 @@ __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
         const bool valid = threadIdx.x < t.n;
         const uint32_t u = valid ? x.send_idx[k] : 0u;
         const uint8_t fl = valid ? x.flg_cur[u] : (uint8_t)0;
-        const bool fa = (fl & FL_ACT) != 0;
+        bool fa = (fl & FL_ACT) != 0;
+        if (fa && x.need_in && ((x.need_peers >> t.peer) & 1ull)) {  // the peer's need bit of this entry
+            const uint32_t j = k - t.first;
+            const uint8_t* nb = reinterpret_cast<const uint8_t*>(x.ipc.my_win) + x.need_in[t.peer] +
+                                ((seq + 2) % 3) * x.need_bytes_in[t.peer];
+            fa = ((*reinterpret_cast<const unsigned long long*>(nb + (j >> 6) * 8) >> (j & 63)) & 1ull) != 0;
+        }
         bool sn = false;
         if (valid && x.sync) {
             const bool nm = x.needmark[k] != 0;
@@ -4427,6 +4461,43 @@ __global__ __launch_bounds__(kBlock) void pack_ghosts(PackArgs x) {
     __syncthreads();
     if (s_last && threadIdx.x < 64) finish_pack_body(x.cnt, x.out, x.seg_off, x.parts, x.self, x.stride, x.seg_bytes,
                                                      x.payload, x.ipc, x.nwp);
+}
+
+struct NeedArgs {
+    const NeedWord* words;
+    uint32_t n_words;
+    const uint32_t* gfirst;     // [parts + 1] first ghost (exchange order) from each source
+    const uint32_t* grow;       // ghost row of the g-th ghost, or nullptr (the same)
+    const int64_t* gout_ptr;    // ghost -> owned receivers
+    const uint32_t* gout_col;
+    const uint8_t* lsat;        // the lean digest of the owned rows (after this round)
+    const uint64_t* need_out;   // [parts] our slot 0 in part q's region (after its rows area)
+    const uint64_t* need_bytes; // [parts] slot bytes
+    IpcArgs ipc;
+};
+
+// One wave per word of 64 ghosts: the ghost's bit = some owned receiver of it is
+// not saturated; the word goes into the source part's window (slot seq % 3).
+__global__ __launch_bounds__(kBlock) void need_bits(NeedArgs a) {
+    if (ipc_failed(a.ipc.err)) return;
+    const uint64_t seq = *a.ipc.seq;
+    const int lane = threadIdx.x & 63;
+    for (uint32_t w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); w < a.n_words; w += gridDim.x * (kBlock / 64)) {
+        const NeedWord nw = a.words[w];
+        bool need = false;
+        if ((uint32_t)lane < nw.n) {
+            const uint64_t g0 = (uint64_t)a.gfirst[nw.peer] + nw.j0 + lane;
+            const uint64_t g = a.grow ? a.grow[g0] : g0;
+            for (int64_t e = a.gout_ptr[g]; e < a.gout_ptr[g + 1] && !need; ++e) need = a.lsat[a.gout_col[e]] == 0;
+        }
+        const unsigned long long bits = __ballot(need);
+        if (lane == 0) {
+            uint8_t* dst = a.ipc.peer_win[nw.peer] + kWinHdr + a.ipc.peer_off[nw.peer] + a.need_out[nw.peer] +
+                           (seq % 3) * a.need_bytes[nw.peer] + (nw.j0 >> 6) * 8;
+            *reinterpret_cast<unsigned long long*>(dst) = bits;
+        }
+    }
+    __threadfence_system();  // before pack_ghosts' ready flags (a later kernel of this stream)
 }
 
 // After pack_ghosts: each peer's header, its byte count for an exact-size

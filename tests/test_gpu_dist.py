@@ -515,7 +515,9 @@ def test_parts_lean_digest_equals_oracle(hip_lib, cpu_lib, world):
     component labels of the whole generated graph, per-component targets from
     every rank's broadcasts (a later batch of values, two of them re-sent into
     other components) — against O2, and with fewer sender-row gathers than the
-    same run without the digest (GG_LSAT=0)."""
+    same run without the digest (GG_LSAT=0); and the exchange's need bits
+    (expand_kernels.hpp NeedWord) ship fewer payload bytes than the same run
+    without them (GG_NEED_BITS=0), against O2 as well."""
     import random as _r
 
     from ggamd import topology as T
@@ -525,15 +527,21 @@ def test_parts_lean_digest_equals_oracle(hip_lib, cpu_lib, world):
     gen = dict(kind="rmat", n=4096, k=16, seed=72, a=0.57, b=0.19, c=0.19)
     scs = [Scenario(T.rmat(4096, 16, seed=72), 256, 24, inj, seed=73, enable_sync=False, gen=gen),
            Scenario(T.rmat(4096, 16, seed=72), 1024, 20, inj, seed=74, sync_base=11, sync_jitter=2, gen=gen)]
-    gathers = {}
-    for lsat in ("1", "0"):
+    gathers, sent = {}, {}
+    for lsat in ("1", "0", "1-no-need"):
         env = {"GG_HUB_DEG": "16", "GG_HUB_CHUNK": "7"}
         if lsat == "0":
             env["GG_LSAT"] = "0"
+        if lsat == "1-no-need":
+            env["GG_NEED_BITS"] = "0"
         res = _run(hip_lib, scs, world, env=env, generate=True, transport="ipc", timeout=240)
         _check_against_oracle(cpu_lib, scs, res, world)
         gathers[lsat] = sum(st["work_gathers"] for r in res for st in r[0][0])
+        sent[lsat] = sum(st["sent_bytes"] for r in res for k in range(len(scs)) for st in r[k][0])
     assert gathers["1"] < gathers["0"], gathers
+    # need bits (the peers skip the F rows of ghosts whose receivers here are all
+    # saturated; rounds with client broadcasts in them or the round before keep every row)
+    assert sent["1"] < sent["1-no-need"], sent
 
 
 def test_world8_lane_groups_by_parts_equals_oracle(hip_lib, cpu_lib):

@@ -28,8 +28,12 @@ engine exchange's 16-byte head per entry; the device-driven exchange's tile
 segments (round 5) ship one 80-byte record per 256 entries instead, so each
 payload is scaled by (R + 80/256) / (R + H), R = the F row's bytes.
 
+Payloads measured over the device-driven exchange (--payload-json, from
+tools/c4_ipc_payload.py: tile segments, with or without need bits) replace the
+rehearsal's per-round payloads as they are.
+
 Usage: python tools/project_c4.py profiles/r3/r3_c4_rehearsal_2p22_p8_ordered.json [--halves H.json] [--scale S] [--host-us U]
-       [--row-bytes R --head-bytes 16]
+       [--row-bytes R --head-bytes 16] [--payload-json P.json --payload-key need|all]
 """
 import argparse
 import json
@@ -48,14 +52,24 @@ def main():
     ap.add_argument("--host-us", type=float, default=0.0, help="host time per round on the critical path")
     ap.add_argument("--row-bytes", type=float, default=0.0, help="F row bytes: rescale payloads to tile segments")
     ap.add_argument("--head-bytes", type=float, default=16.0, help="per-entry head bytes the rehearsal measured")
+    ap.add_argument("--payload-json", help="tools/c4_ipc_payload.py output: its per-round largest per-rank payload "
+                                           "(device-driven exchange, tile segments) replaces the rehearsal's")
+    ap.add_argument("--payload-key", default="need", help="need | all (with or without need bits)")
     args = ap.parse_args()
     xs = (args.row_bytes + 80.0 / 256.0) / (args.row_bytes + args.head_bytes) if args.row_bytes else 1.0
     d = json.load(open(args.rehearsal))
+    if args.payload_json:  # measured tile-segment payloads: no rescaling
+        pj = json.load(open(args.payload_json))
+        assert pj["config"]["nodes"] == d["config"]["nodes"] and pj["config"]["parts"] == d["config"]["parts"]
+        for r, q in zip(rounds_of(d), pj["per_round"]):
+            r["payload_bytes_max"] = q[f"payload_bytes_max_{args.payload_key}"]
+        xs = 1.0
     P = d["config"]["parts"]
     h = json.load(open(args.halves)) if args.halves else None
     out = {"rehearsal": args.rehearsal, "halves": args.halves, "parts": P, "lane_groups": d["config"]["lane_groups"],
            "nodes": d["config"]["nodes"], "scale": args.scale, "host_us_per_round": args.host_us,
-           "payload_scale": xs, "projections": []}
+           "payload_scale": xs, "payload_json": args.payload_json, "payload_key": args.payload_key,
+           "projections": []}
     single = sum(r["single_ms"] for r in rounds_of(d)) * args.scale
     for link in [float(x) for x in args.links.split(",")]:
         B = link * 1e9 * min(7, max(1, P - 1))
