@@ -762,12 +762,12 @@ def headline(job: Job, args) -> tuple[dict | None, dict]:
 
 
 def ipc_release(job: Job, engs) -> None:
-    """Collective (every rank, at the same point): unmap the peers' windows of this
-    rank's engines (gg_dist_ipc_close; a no-op without the device-driven exchange),
-    then a barrier — only then may any rank close an engine, which frees its own
-    window. Closing engines without it freed windows that peers still mapped, and
-    the next leg's imports hung in hipIpcOpenMemHandle (8 ranks, C5 2^28 after the
-    C2 headline: profiles/r6/INDEX.md)."""
+    """Collective (every rank, at the same point): every engine of this rank leaves
+    the device-driven exchange (gg_dist_ipc_close; a no-op without it), then a
+    barrier — only then may any rank close an engine, whose window goes back to the
+    process's pool for a later leg (gossip.h: windows are never freed while the
+    process lives; freeing and reallocating them between legs is what stalled the
+    8-rank rehearsal)."""
     for e in engs:
         try:
             e.dist_ipc_close()

@@ -408,6 +408,10 @@ static void dfree(T*& p) {
     p = nullptr;
 }
 
+namespace {
+void win_release(uint8_t* p);  // the IPC window pool (below, gg_dist_ipc_export)
+}
+
 void gg_engine::free_topology() {
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
     graph_exec = nullptr;
@@ -499,14 +503,13 @@ void gg_engine::free_topology() {
     need_produce = false;
     dfree(d_segbytes);
     dfree(d_payload);
-    for (void*& m : peer_map)
-        if (m) (void)hipIpcCloseMemHandle(m);
-    peer_map.clear();
+    peer_map.clear();  // mappings: the process's cache keeps them (see win_acquire)
     dfree(d_peer_win);
     dfree(d_peer_off);
     dfree(d_peer_rbuf);
     dfree(d_xticket);
-    dfree(d_win);
+    if (d_win) win_release(d_win);  // back to the pool, not freed (see win_acquire)
+    d_win = nullptr;
     ipc = false;
     if (h_segbytes) (void)hipHostFree(h_segbytes);
     h_segbytes = nullptr;
@@ -3701,6 +3704,74 @@ static_assert(sizeof(IpcBlob) <= GG_IPC_BLOB_BYTES, "IPC blob size");
 constexpr uint32_t kIpcMagic = 0x43504947u;  // "GIPC"
 }  // namespace
 
+// Window pool and mapping cache (round 6). On this ROCm (dmabuf IPC), a window
+// freed after its peers had mapped and unmapped it, followed by a new window
+// allocated and exported, sometimes failed: hipIpcGetMemHandle returned
+// "invalid argument" on the new window and the peer process blocked in the
+// runtime — the new allocation can take the address range of a mapping just
+// closed (tools/ipc_reopen_repro.hip, scenario 5; intermittent: one run in two).
+// That is what stalled the 8-rank rehearsal between the C2 headline and the C5
+// leg (every engine freed its window, the next leg exported new ones). So no
+// window is freed and no mapping is closed while the process lives: an engine
+// takes the smallest free pooled window of its device that is large enough
+// (else allocates and exports a new one, once), returns it when it is destroyed,
+// and a peer window already mapped by this process is mapped again from the
+// cache (keyed by its handle), never reopened. A reused window's flag area is
+// zeroed before it is exported again (the new exchange's sequence numbers start
+// at 0; every peer has left the old exchange: gg_dist_ipc_close + barrier).
+namespace {
+struct PooledWin {
+    uint8_t* ptr;
+    uint64_t bytes;
+    int device;
+    bool busy;
+    hipIpcMemHandle_t handle;
+};
+std::mutex g_ipc_mu;
+std::vector<PooledWin> g_win_pool;
+std::map<std::string, void*> g_peer_maps;  // handle bytes -> this process's mapping
+
+int win_acquire(gg_engine* e, uint64_t bytes) {
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    PooledWin* best = nullptr;
+    for (auto& w : g_win_pool)
+        if (!w.busy && w.device == e->device && w.bytes >= bytes && (!best || w.bytes < best->bytes)) best = &w;
+    if (best) {
+        best->busy = true;
+        e->d_win = best->ptr;
+        HIPCHK(hipMemset(e->d_win, 0, gg::kWinHdr));  // the flags of its last exchange
+        return GG_OK;
+    }
+    PooledWin w{};
+    // uncached: stores from the peers' pack kernels and this engine's reads meet in HBM
+    HIPCHK(hipExtMallocWithFlags(reinterpret_cast<void**>(&w.ptr), bytes, hipDeviceMallocUncached));
+    HIPCHK(hipMemset(w.ptr, 0, bytes));
+    HIPCHK(hipIpcGetMemHandle(&w.handle, w.ptr));
+    w.bytes = bytes;
+    w.device = e->device;
+    w.busy = true;
+    g_win_pool.push_back(w);
+    e->d_win = w.ptr;
+    return GG_OK;
+}
+
+void win_release(uint8_t* p) {
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    for (auto& w : g_win_pool)
+        if (w.ptr == p) w.busy = false;
+}
+
+bool win_handle(const uint8_t* p, hipIpcMemHandle_t* h) {
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    for (auto& w : g_win_pool)
+        if (w.ptr == p) {
+            *h = w.handle;
+            return true;
+        }
+    return false;
+}
+}  // namespace
+
 int gg_dist_ipc_export(gg_engine* e, uint8_t* blob) {
     if (!e || !blob) return GG_EINVAL;
     if (!e->have_topo) return e->fail(GG_EINVAL, "no topology");
@@ -3711,9 +3782,7 @@ int gg_dist_ipc_export(gg_engine* e, uint8_t* blob) {
     if (!e->d_win) {
         e->win_rbuf = (e->xroff[e->P] + 255) / 256 * 256;
         const uint64_t bytes = gg::kWinHdr + 2 * std::max<uint64_t>(e->win_rbuf, 256);
-        // uncached: stores from the peers' pack kernels and this engine's reads meet in HBM
-        HIPCHK(hipExtMallocWithFlags(reinterpret_cast<void**>(&e->d_win), bytes, hipDeviceMallocUncached));
-        HIPCHK(hipMemset(e->d_win, 0, bytes));
+        if (int rc = win_acquire(e, bytes)) return rc;  // (a pooled window, or a new one exported once)
         HIPCHK(hipMalloc(&e->d_xticket, 16));
         HIPCHK(hipMemset(e->d_xticket, 0, 16));
     }
@@ -3730,7 +3799,7 @@ int gg_dist_ipc_export(gg_engine* e, uint8_t* blob) {
     }
     b.need = e->need_produce ? 1u : 0u;
     for (uint32_t q = 0; q < e->P; ++q) b.roff[q] = e->xroff[q];
-    HIPCHK(hipIpcGetMemHandle(&b.handle, e->d_win));
+    if (!win_handle(e->d_win, &b.handle)) return e->fail(GG_EIO, "gg_dist_ipc_export: window not in the pool");
     std::memset(blob, 0, GG_IPC_BLOB_BYTES);
     std::memcpy(blob, &b, sizeof(b));
     return GG_OK;
@@ -3775,8 +3844,15 @@ int gg_dist_ipc_import(gg_engine* e, const uint8_t* blobs) {
         const bool rcv = q != e->part && e->xroff[q + 1] > e->xroff[q];
         if (!snd && !rcv) continue;
         void* m = nullptr;
-        note("open", q);
-        {  // bounded: a mapping that never returns fails this rank instead of hanging it
+        const std::string key(reinterpret_cast<const char*>(&b[q].handle), sizeof(hipIpcMemHandle_t));
+        {
+            std::lock_guard<std::mutex> lk(g_ipc_mu);
+            auto it = g_peer_maps.find(key);
+            if (it != g_peer_maps.end()) m = it->second;
+        }
+        if (m) note("mapped already (cache)", q);
+        else note("open", q);
+        if (!m) {  // bounded: a mapping that never returns fails this rank instead of hanging it
             struct Open {
                 std::mutex mu;
                 std::condition_variable cv;
@@ -3799,19 +3875,19 @@ int gg_dist_ipc_import(gg_engine* e, const uint8_t* blobs) {
             }).detach();
             std::unique_lock<std::mutex> lk(st->mu);
             if (!st->cv.wait_for(lk, std::chrono::duration<double>(limit_s), [&] { return st->done; })) {
-                for (void*& pm : e->peer_map)
-                    if (pm) (void)hipIpcCloseMemHandle(pm), pm = nullptr;
+                e->peer_map.assign(P, nullptr);  // (the mappings made so far stay in the cache)
                 return e->fail(GG_EIO, "gg_dist_ipc_import: hipIpcOpenMemHandle of part " + std::to_string(q) +
                                            "'s window did not return within " + std::to_string((int)limit_s) +
                                            " s (GG_IPC_OPEN_TIMEOUT_S)");
             }
             if (st->rc != hipSuccess) {
-                for (void*& pm : e->peer_map)
-                    if (pm) (void)hipIpcCloseMemHandle(pm), pm = nullptr;
+                e->peer_map.assign(P, nullptr);
                 return e->fail(GG_EIO, std::string("gg_dist_ipc_import: hipIpcOpenMemHandle: ") +
                                            hipGetErrorString(st->rc));
             }
             m = st->m;
+            std::lock_guard<std::mutex> lk2(g_ipc_mu);
+            g_peer_maps[key] = m;
         }
         note("opened", q);
         e->peer_map[q] = m;
@@ -3840,9 +3916,7 @@ int gg_dist_ipc_close(gg_engine* e) {
     HIPCHK(hipStreamSynchronize(e->stream));  // (waits are bounded: a dead exchange drains)
     if (e->dist_exec) (void)hipGraphExecDestroy(e->dist_exec);  // its kernels name the peer windows
     e->dist_exec = nullptr;
-    for (void*& m : e->peer_map)
-        if (m) (void)hipIpcCloseMemHandle(m);
-    e->peer_map.clear();
+    e->peer_map.clear();  // (the mappings stay in the process's cache: never reopened, never closed)
     dfree(e->d_peer_win);
     dfree(e->d_peer_off);
     dfree(e->d_peer_rbuf);

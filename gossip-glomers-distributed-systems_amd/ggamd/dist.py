@@ -346,9 +346,11 @@ def _ipc_connect(engines: list[Engine], group, rank: int, world: int, P: int) ->
 
 
 def _ipc_teardown(engines: list[Engine], group) -> None:
-    """Collective: every rank unmaps its peers' windows (gg_dist_ipc_close), then
-    one all_reduce, so that no window is freed (engine close) while a peer still
-    maps it. A rank whose unmapping failed still joins the collective."""
+    """Collective: every rank leaves the exchange (gg_dist_ipc_close: its stream
+    drained, its peers' windows no longer used), then one all_reduce, so that no
+    engine is destroyed — its window going back to the process's pool, to be
+    zeroed and exported by a later engine — while a peer may still write into it.
+    A rank whose call failed still joins the collective."""
     err = None
     for e in engines:
         try:

@@ -358,13 +358,17 @@ int gg_dist_ipc_export(gg_engine* e, uint8_t* blob /* GG_IPC_BLOB_BYTES */);
 /* A mapping that does not return within GG_IPC_OPEN_TIMEOUT_S seconds (env, default
  * 120) fails the import with GG_EIO instead of hanging the rank. */
 int gg_dist_ipc_import(gg_engine* e, const uint8_t* blobs /* P x GG_IPC_BLOB_BYTES, part order */);
-/* Collective teardown, first half: wait for the engine's stream, unmap every peer
- * window (hipIpcCloseMemHandle) and drop the exchange; the engine's own window
- * stays allocated. Every part calls it, then the caller barriers, and only then
- * does any part destroy its engine (which frees its window): no window is freed
- * while a peer still maps it. (The reference's nodes hold no shared memory; this
- * is the device-driven exchange's lifecycle, broadcast.go:50-57's fan-out across
- * processes.) */
+/* Collective teardown, first half: wait for the engine's stream and leave the
+ * exchange (the engine no longer touches its peers' windows; it can export and
+ * import again). Every part calls it, then the caller barriers, and only then does
+ * any part destroy its engine: the engine's window goes back to the process's
+ * window pool and is handed, flags zeroed, to a later engine, so no peer may still
+ * be writing into it. Windows are never freed and peer mappings never closed while
+ * the process lives (a freed-and-reallocated window could take the address range
+ * of a mapping just closed, and the runtime then failed its export or blocked the
+ * peer's open: DESIGN.md §5.4); a peer window mapped before is mapped again from
+ * the process's cache. (The reference's nodes share no memory; this is the
+ * device-driven exchange's lifecycle for broadcast.go:50-57's fan-out.) */
 int gg_dist_ipc_close(gg_engine* e);
 
 /* gg_read_bits / gg_delivery_rounds for a list of owned nodes (any engine). */

@@ -50,6 +50,7 @@ def _worker(rank, world, port, lib, scenarios, q, lane_groups=1, env=None, gener
                 assert r.host_xport.groups >= sc.rounds, r.host_xport.groups  # one group per round at least
             owned = e.dist_owned()
             out.append((stats, owned, e.read_bits_nodes(owned), e.delivery_rounds_nodes(owned)))
+            r.close()  # collective (IPC): every rank leaves the exchange before any engine is destroyed
             e.close()
         q.put((rank, out))
     except BaseException as exc:  # report instead of leaving the parent waiting
@@ -576,6 +577,7 @@ def _halves_worker(rank, world, port, lib, scenarios, q, parts, env):
             bits = engs[0].read_bits_nodes(owned) | engs[1].read_bits_nodes(owned)
             dr = np.maximum(engs[0].delivery_rounds_nodes(owned), engs[1].delivery_rounds_nodes(owned))
             out.append((stats, owned, bits, dr))
+            r.close()
             for e in engs:
                 e.close()
         q.put((rank, out))
@@ -644,6 +646,7 @@ def _part_worker(rank, world, port, lib, scenarios, bounds, q, transport):
             owned = e.dist_owned()
             assert np.array_equal(np.sort(owned), np.arange(lo, hi))  # rows in locality order
             out.append((stats, owned, e.read_bits_nodes(owned), e.delivery_rounds_nodes(owned)))
+            r.close()
             e.close()
         q.put((rank, out))
     except BaseException as exc:

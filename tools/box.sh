@@ -11,6 +11,7 @@
 #   tools/box.sh c4half2 [NODES]    2 ranks on this one GPU: the C4 leg with lane halves (digest mode per rank)
 #   tools/box.sh memset             tools/graph_memset_repro: a captured hipMemsetAsync node against our
 #                                   zero kernel, one process and two at once
+#   tools/box.sh ipcrepro [SCN...]  tools/ipc_reopen_repro: hipIpcOpenMemHandle after close / free / realloc
 #   tools/box.sh pmc "CFGS"         tools/pmc_passes.sh (request ceilings, traffic passes)
 # Output under gpurun_out/box/ (merged back by gpurun).
 set -o pipefail
@@ -89,6 +90,15 @@ memset)
      timeout -k 10 180 tools/graph_memset_repro 300 kernel > $O/kernel_2p_b.txt 2>&1 &
      wait)
     tail -n 3 $O/memset_*.txt $O/kernel_*.txt ;;
+ipcrepro)
+    # each scenario a fresh pair of processes; a step stuck in the runtime is caught by the
+    # repro's own watchdog (exit 1) or a failed call (exit 2); a time limit ends the chain
+    for sc in ${@:-2 4 3 1}; do
+        cached=; [ "${sc%c}" != "$sc" ] && cached=1  # N c: the same with hipMalloc windows
+        REPRO_CACHED=$cached timeout -k 10 90 tools/ipc_reopen_repro ${sc%c} > $O/ipc_reopen_$sc.txt 2>&1 \
+            || { rc=$?; [ $rc -ge 124 ] && { cat $O/ipc_reopen_$sc.txt; exit $rc; }; }
+        echo "== scenario $sc"; cat $O/ipc_reopen_$sc.txt
+    done ;;
 pmc)
     O=gpurun_out/box/pmc bash tools/pmc_passes.sh "$1" ;;
 *)
