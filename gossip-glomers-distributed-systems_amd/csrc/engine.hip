@@ -4470,14 +4470,8 @@ int gg_dist_run_episodes(gg_engine* e, uint32_t n, uint32_t episodes, gg_round_s
     const std::vector<int64_t> lv0 = e->lane_value;
     int rc = ensure_events(e, 2);
     if (rc) return rc;
-    // the timed span (gg_step_device_ms): episodes t0k..K-1. Episode 1 can hold a
-    // graph capture (the hints learned from episode 0 change the batch key), so
-    // with three or more episodes the span starts at episode 2, whose batch
-    // replays episode 1's graph; with two it is episode 1 (capture included)
-    const uint32_t t0k = episodes > 2 ? 2 : (episodes > 1 ? 1 : 0);
     HIPCHK(hipEventRecord(e->ev[0], e->stream));
     for (uint32_t k = 0; k < episodes; ++k) {
-        if (k == 2 && t0k == 2) HIPCHK(hipEventRecord(e->ev[2], e->stream));
         if (k) {  // gg_reset + the same broadcasts, without gg_reset's wait
             reset_host_state(e, true);
             e->inj = inj0;

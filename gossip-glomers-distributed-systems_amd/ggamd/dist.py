@@ -323,6 +323,8 @@ def _ipc_connect(engines: list[Engine], group, rank: int, world: int, P: int) ->
     dbg = os.environ.get("GG_IPC_DEBUG")
     t0 = time.perf_counter()
     err = None
+    if dbg:
+        print(f"_ipc_connect rank {rank}: exporting", flush=True)
     try:
         mine = b"".join(e.dist_ipc_export() for e in engines)
     except Exception as exc:  # still join the all_gather (zero blobs: every importer refuses them)
@@ -352,14 +354,19 @@ def _ipc_teardown(engines: list[Engine], group) -> None:
     zeroed and exported by a later engine — while a peer may still write into it.
     A rank whose call failed still joins the collective."""
     err = None
+    dbg = os.environ.get("GG_IPC_DEBUG")
     for e in engines:
         try:
             e.dist_ipc_close()
         except Exception as exc:  # noqa: BLE001
             err = err or exc
+    if dbg:
+        print(f"_ipc_teardown rank {dist.get_rank(group)}: left the exchange ({err!r})", flush=True)
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
     flag = torch.zeros(1, dtype=torch.int32, device=dev)
     dist.all_reduce(flag, group=group)
+    if dbg:
+        print(f"_ipc_teardown rank {dist.get_rank(group)}: barrier passed", flush=True)
     if err is not None:
         raise err
 

@@ -1024,6 +1024,8 @@ def _episodes_worker(rank, world, port, lib, scenarios, q, lane_groups, episodes
             for n, v, rr in sc.injections:
                 e.broadcast(int(n), int(v), int(rr))
             again = r.step(sc.rounds)
+            if os.environ.get("GG_IPC_DEBUG"):
+                print(f"episodes worker rank {rank}: synchronous episode done", flush=True)
             # collective teardown (gg_dist_ipc_close on every rank, then a barrier), and
             # the same engines map each other's windows again: the same episode once more
             r.close()
