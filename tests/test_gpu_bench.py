@@ -7,8 +7,9 @@ C5 legs the driver's N-GPU runs take, at reduced leg sizes.
   and one unsharded engine (round 5: replays of a batch captured in the
   validation episode read back garbage counters — the memset node — until the
   engine's own zeroing kernel replaced it);
-* the legs: strong-scaling C4 (2 vertex parts x 2 lane halves) and C5, each
-  checked against one unsharded engine, P1 / KAT-3 / ACK;
+* the legs: C3 (partition window healed by the timers), strong-scaling C4
+  (2 vertex parts x 2 lane halves) and C5, each checked against one unsharded
+  engine, P1 / KAT-3 / ACK;
 * GG_BENCH_IPC_FAIL: a rank stops exchanging after 3 validation rounds; its
   peer's waits run out (lowered bound) and every rank rebuilds on the engine
   exchange, whose timed episodes still equal O2;
@@ -45,7 +46,7 @@ def _bench(extra, env=None, timeout=240):
 
 
 def test_bench_two_ranks_with_legs():
-    d, _ = _bench(["--c4-nodes", str(1 << 18), "--c5-side", "512", "--leg-steps", "2"])
+    d, _ = _bench(["--c3-nodes", str(1 << 17), "--c4-nodes", str(1 << 18), "--c5-side", "512", "--leg-steps", "2"])
     c = d["config"]
     assert d["n_gpus"] == 2
     assert c["exchange"].startswith("device-driven"), c["exchange"]
@@ -53,7 +54,7 @@ def test_bench_two_ranks_with_legs():
     assert c["check"] == "every round's global counters equal one unsharded engine"
     assert c["oracle_check"] and c["oracle_check"].startswith("all 2 timed episodes")
     assert c["shard"]["devices"] == 1 and c["shard"]["distinct_devices"] is False
-    for name in ("C4", "C5"):
+    for name in ("C3", "C4", "C5"):
         leg = d["legs"][name]
         assert leg.get("error") is None, leg
         assert leg["check"] == "passed", leg["checks"]
@@ -62,6 +63,10 @@ def test_bench_two_ranks_with_legs():
         assert leg["rounds_to_full_delivery"] >= 1
     assert d["legs"]["C4"]["lane_halves_per_gpu"] == 2
     assert d["legs"]["C5"]["checks"]["expected"]["deliveries"] == 512 * 512 * 64
+    # C3: the partition window cut messages and the timers healed it (P1 after the heal)
+    c3 = d["legs"]["C3"]
+    assert c3["checks"]["expected"]["deliveries"] == (1 << 17) * 1024
+    assert c3["rounds_to_full_delivery"] > 20
 
 
 @pytest.mark.parametrize("hook", ["ipc_fail_round3", "episodes_fail"])
