@@ -58,7 +58,10 @@ constexpr int kMaxBlocks = 2048;
 // GG_IPC_SPIN_LIMIT (sleeps before a device-driven exchange wait gives up), GG_LSAT=0 / 1
 // (lean saturation digest off / on whatever the graph), GG_NEED_BITS=0 (the device-driven
 // exchange ships every active F row), GG_LSAT_LABELS_FAIL=1 (vertex parts: the component
-// labels' build fails; the digest falls back to "every lane"), GG_IPC_OPEN_TIMEOUT_S.
+// labels' build fails; the digest falls back to "every lane"), GG_IPC_OPEN_TIMEOUT_S,
+// GG_IPC_PREALLOC_GB (a pooled window of that size allocated before a generated part
+// is built), GG_IPC_WINDOW_EARLY=1 (the window allocated at exchange planning, before
+// the part's per-node state).
 const char* test_knob(const char* name) { return getenv(name); }
 // A/B switches of past measurements (GG_ALL_FULL, GG_NO_GRAPH, GG_SYNC_ALLPUSH,
 // GG_FLAGS_FIRST, GG_FF_FRAC16, GG_PREP_WIDE, GG_XCHG_EXACT_BYTES): read only in a -DGG_AB_KNOBS build.
@@ -2182,6 +2185,10 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
 // (send_off, recv_off, n_ghost; d_send_idx, d_gout_* already on the device):
 // segment capacities (header + an F and an S entry per send-list node), pack
 // tiles, the size mode of every direction.
+namespace {
+int win_acquire(gg_engine* e, uint64_t bytes);  // the IPC window pool (below, gg_dist_ipc_export)
+}
+
 static int setup_exchange(gg_engine* e) {
     const uint32_t Wd = e->P;
     e->xstride = (uint32_t)(e->nwp >= 2 ? 16 + 8 * e->nwp : 16);
@@ -2271,6 +2278,14 @@ static int setup_exchange(gg_engine* e) {
         e->xexact_s[q] = cs && !never && (force || cs > lim);
         e->xexact_r[q] = cr && !never && (force || cr > lim);
         e->xexact |= e->xexact_s[q] || e->xexact_r[q];
+    }
+    // the device-driven exchange's window, allocated now — before the part's
+    // per-node state — when the caller will take that exchange (see win_acquire)
+    if (test_knob("GG_IPC_WINDOW_EARLY") && Wd > 1 && !e->d_win) {
+        e->win_rbuf = (e->xroff[Wd] + 255) / 256 * 256;
+        if (int rc = win_acquire(e, gg::kWinHdr + 2 * std::max<uint64_t>(e->win_rbuf, 256))) return rc;
+        HIPCHK(hipMalloc(&e->d_xticket, 16));
+        HIPCHK(hipMemset(e->d_xticket, 0, 16));
     }
     return GG_OK;
 }
@@ -2645,7 +2660,13 @@ static int lsat_parts(gg_engine* e, const gg_gen_spec* spec) {
     return rc;
 }
 
+namespace {
+int win_prealloc(gg_engine* e, uint64_t bytes);  // the IPC window pool (below, gg_dist_ipc_export)
+}
+
 static int generate_sharded(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_out) {
+    if (const char* pg = test_knob("GG_IPC_PREALLOC_GB"))  // a window allocated before anything else of the part
+        if (int rc = win_prealloc(e, (uint64_t)(atof(pg) * 1073741824.0))) return rc;
     const uint64_t V = e->V;
     const uint32_t P = e->P;
     std::vector<uint64_t> plo(P + 1);
@@ -3752,6 +3773,24 @@ int win_acquire(gg_engine* e, uint64_t bytes) {
     w.busy = true;
     g_win_pool.push_back(w);
     e->d_win = w.ptr;
+    return GG_OK;
+}
+
+int win_prealloc(gg_engine* e, uint64_t bytes) {  // (one more pooled window per call)
+    PooledWin w{};
+    HIPCHK(hipExtMallocWithFlags(reinterpret_cast<void**>(&w.ptr), bytes, hipDeviceMallocUncached));
+    HIPCHK(hipMemset(w.ptr, 0, bytes));
+    HIPCHK(hipIpcGetMemHandle(&w.handle, w.ptr));
+    w.bytes = bytes;
+    w.device = e->device;
+    w.busy = true;
+    {
+        std::lock_guard<std::mutex> lk(g_ipc_mu);
+        g_win_pool.push_back(w);
+    }
+    e->d_win = w.ptr;
+    win_release(e->d_win);
+    e->d_win = nullptr;
     return GG_OK;
 }
 

@@ -341,10 +341,28 @@ def _ipc_connect(engines: list[Engine], group, rank: int, world: int, P: int) ->
     if err is not None:
         raise err
     B = IPC_BLOB_BYTES
-    for h, e in enumerate(engines):
-        g = rank // P  # the process's lane group index (rank = group * P + part)
-        blobs = b"".join(allb[g * P + q][h * B:(h + 1) * B] for q in range(P))
-        e.dist_ipc_import(blobs)
+    # the ranks map their peers' windows one rank at a time (a barrier between
+    # turns): with every rank opening at once, large windows (C4 2^24 on 2 ranks:
+    # 3.7 GiB) left both ranks blocked in hipIpcOpenMemHandle
+    serial = os.environ.get("GG_IPC_SERIAL_IMPORT", "1") != "0"
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    ierr = None
+    for turn in range(world if serial else 1):
+        if not serial or turn == rank:
+            try:
+                for h, e in enumerate(engines):
+                    g = rank // P  # the process's lane group index (rank = group * P + part)
+                    blobs = b"".join(allb[g * P + q][h * B:(h + 1) * B] for q in range(P))
+                    e.dist_ipc_import(blobs)
+            except Exception as exc:  # noqa: BLE001 — every rank still takes part in every turn
+                ierr = exc
+        if serial:
+            dist.all_reduce(torch.zeros(1, dtype=torch.int32, device=dev), group=group)
+    if dbg:
+        print(f"_ipc_connect rank {rank}: imported ({'in turn' if serial else 'at once'}) in "
+              f"{time.perf_counter() - t0:.3f} s", flush=True)
+    if ierr is not None:
+        raise ierr
 
 
 def _ipc_teardown(engines: list[Engine], group) -> None:

@@ -63,9 +63,10 @@ ipc8)
     bash tools/r5h.sh ;;
 c4half2)
     n=${1:-16777216}
-    GG_BENCH_WATCHDOG=120 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    GG_BENCH_WATCHDOG=${WD:-120} timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29813 bench.py --gpus 2 --backend gloo --steps 2 --warmup 1 \
-        --nodes 65536 --legs C4 --c4-nodes "$n" --leg-steps 2 --no-cpu-baseline > $O/c4half2.json 2> $O/c4half2.err &
+        --nodes 65536 --legs C4 --c4-nodes "$n" --leg-steps 2 --no-cpu-baseline $C4HALF2_ARGS \
+        > $O/c4half2.json 2> $O/c4half2.err &
     tick $! c4half2 $O/c4half2.err
     rc=$?
     tail -20 $O/c4half2.err

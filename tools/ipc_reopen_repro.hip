@@ -62,6 +62,18 @@ struct Msg {
 };
 
 static int g_scn = 1;
+
+// scenario 13: kernels store into the peer's mapped window (and read their own)
+// before the second window is exported and mapped
+__global__ void touch(unsigned long long* peer, const unsigned long long* own, size_t n, unsigned long long v) {
+    unsigned long long acc = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        peer[i] = v + i;
+        acc += own[i];
+    }
+    __threadfence_system();
+    if (acc == 0x5a5a5a5a5a5a5a5aull) peer[0] = acc;  // (keeps the loads)
+}
 static std::atomic<int> g_step{0};
 
 static void watchdog(int who) {
@@ -158,6 +170,11 @@ static void parent() {
 //      export, map (a window pool that only grows)
 //   9  export the same window again while the peer still maps it; the peer maps
 //      the new handle too
+//   10 a second window of REPRO_GB GiB (default 8) beside the first: export, both map at once
+//   11 as 10, the two processes mapping in turn (process 0, then 1)
+//   12 one window of REPRO_GB GiB, nothing before it: export, both map at once
+//   13 kernels store into the first mapped window (50 launches), then as 10
+//   14 REPRO_FILL_GB (default 80) of other device allocations first, then as 12
 // REPRO_CACHED=1: windows from hipMalloc instead of hipExtMallocWithFlags(uncached).
 static void both(int who) {
     const int tx = who ? c2p[1] : p2c[1], rx = who ? p2c[0] : c2p[0];
@@ -191,9 +208,81 @@ static void both(int who) {
         else CK(hipMalloc(q, n));
         CK(hipMemset(*q, 0, n));
     };
+    if (g_scn == 14) {  // REPRO_FILL_GB of other allocations (2 GiB chunks) first, then as 12
+        const double fill = getenv("REPRO_FILL_GB") ? atof(getenv("REPRO_FILL_GB")) : 80.0;
+        const double chunk = getenv("REPRO_CHUNK_MB") ? atof(getenv("REPRO_CHUNK_MB")) : 2048.0;
+        const size_t cb = (size_t)(chunk * (1 << 20));
+        for (double got = 0; got < fill; got += chunk / 1024.0) {
+            void* x = nullptr;
+            CK(hipMalloc(&x, cb));
+            CK(hipMemset(x, 1, cb));
+        }
+        printf("[%d] scenario 14: %.0f GiB allocated\n", who, fill);
+        fflush(stdout);
+        g_scn = 12;
+    }
+    if (g_scn == 12) {
+        const size_t big = (size_t)(getenv("REPRO_GB") ? atof(getenv("REPRO_GB")) : 8.0) * (1ull << 30);
+        alloc(&w, big);
+        const auto t0 = std::chrono::steady_clock::now();
+        exchange_and_open(1);
+        printf("[%d] scenario 12: %.3f s\n", who,
+               std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+        barrier();
+        CK(hipIpcCloseMemHandle(peer));
+        barrier();
+        CK(hipFree(w));
+        g_step = -1;
+        printf("[%d] scenario %d: every open returned\n", who, g_scn);
+        return;
+    }
     alloc(&w, a);
     exchange_and_open(1);
     barrier();
+    if (g_scn == 13) {  // kernels use the first mapping, then a second window (REPRO_GB GiB)
+        for (int k = 0; k < 50; ++k)
+            hipLaunchKernelGGL(touch, dim3(256), dim3(256), 0, 0, (unsigned long long*)peer,
+                               (const unsigned long long*)w, a / 8, (unsigned long long)k);
+        CK(hipDeviceSynchronize());
+        barrier();
+        g_scn = 10;  // then as scenario 10
+    }
+    if (g_scn == 10 || g_scn == 11) {  // a second window of REPRO_GB GiB beside the first (11: opens in turn)
+        const size_t big = (size_t)(getenv("REPRO_GB") ? atof(getenv("REPRO_GB")) : 8.0) * (1ull << 30);
+        void* w1 = w;
+        void* p1 = peer;
+        alloc(&w, big);
+        CK(hipIpcGetMemHandle(&mine.h, w));
+        mine.addr = (unsigned long long)w;
+        send_all(tx, &mine, sizeof mine);
+        recv_all(rx, &theirs, sizeof theirs);
+        for (int turn = 0; turn < 2; ++turn) {
+            if (g_scn == 11 && turn != who) {
+                barrier();
+                continue;
+            }
+            if (g_scn == 10 && turn == 1) break;
+            g_step = 2;
+            printf("[%d] scenario %d step 2: open the peer's %.1f GiB window %#llx ...\n", who, g_scn,
+                   big / 1073741824.0, theirs.addr);
+            fflush(stdout);
+            const auto t0 = std::chrono::steady_clock::now();
+            CK(hipIpcOpenMemHandle(&peer, theirs.h, hipIpcMemLazyEnablePeerAccess));
+            printf("[%d] scenario %d step 2: opened at %p in %.3f s\n", who, g_scn, peer,
+                   std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+            fflush(stdout);
+            if (g_scn == 11) barrier();
+        }
+        barrier();
+        CK(hipIpcCloseMemHandle(peer));
+        CK(hipIpcCloseMemHandle(p1));
+        barrier();
+        CK(hipFree(w));
+        CK(hipFree(w1));
+        g_step = -1;
+        printf("[%d] scenario %d: every open returned\n", who, g_scn);
+        return;
+    }
     if (g_scn == 8) {  // a second window beside the first (nothing unmapped or freed): export, map
         void* w1 = w;
         void* p1 = peer;
