@@ -912,14 +912,15 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
     engs = []
 
     def build_engines():
+        wf = xchg_pref == "ipc" and P > 1  # the exchange window allocated before the part (gossip.h)
         if halves == 2:
             g, q = divmod(rank, P)
             for h in range(2):
                 engs.append(Engine(V, K, seed=seed, enable_sync=True, device=local, rank=(2 * g + h) * P + q,
-                                   world=2 * world, lane_groups=2 * L))
+                                   world=2 * world, lane_groups=2 * L, ipc_window_first=wf))
         else:
             engs.append(Engine(V, K, seed=seed, enable_sync=True, device=local, rank=rank, world=world,
-                               lane_groups=L))
+                               lane_groups=L, ipc_window_first=wf))
         E = 0
         for e in engs:
             E = e.generate(**gen)  # this rank's rows (gossip_gen.h); halves: the same rows twice
@@ -1191,6 +1192,10 @@ def cpu_baseline(cfg, topo, inj, V, K, seed, R):
         os.environ["GG_CPU_THREADS"] = str(thr)
         e = Engine(V_, K_, seed=seed_, enable_sync=True, library=CPU_LIB)
         e.topology(topo_)
+        if rounds is not None:  # one untimed episode: first-touch page faults, thread start-up
+            e.reset()
+            inject(e, inj_)
+            e.step(rounds)
         dl, eps, t0 = 0, 0, time.perf_counter()
         while True:
             e.reset()
@@ -1223,7 +1228,7 @@ def cpu_baseline(cfg, topo, inj, V, K, seed, R):
         scaling = {"1": v_one, str(threads): v_all}
         t = 2
         while t < threads:
-            scaling[str(t)] = o2_episodes(topo, inj, V, K, seed, t, 2.0, R)[0]
+            scaling[str(t)] = o2_episodes(topo, inj, V, K, seed, t, 3.0, R)[0]
             t *= 2
         scaling = dict(sorted(scaling.items(), key=lambda kv: int(kv[0])))
     else:  # C4: R-MAT samples of the same generator (the 10^8-node graph needs ~150 GB of host state)

@@ -58,10 +58,7 @@ constexpr int kMaxBlocks = 2048;
 // GG_IPC_SPIN_LIMIT (sleeps before a device-driven exchange wait gives up), GG_LSAT=0 / 1
 // (lean saturation digest off / on whatever the graph), GG_NEED_BITS=0 (the device-driven
 // exchange ships every active F row), GG_LSAT_LABELS_FAIL=1 (vertex parts: the component
-// labels' build fails; the digest falls back to "every lane"), GG_IPC_OPEN_TIMEOUT_S,
-// GG_IPC_PREALLOC_GB (a pooled window of that size allocated before a generated part
-// is built), GG_IPC_WINDOW_EARLY=1 (the window allocated at exchange planning, before
-// the part's per-node state).
+// labels' build fails; the digest falls back to "every lane"), GG_IPC_OPEN_TIMEOUT_S.
 const char* test_knob(const char* name) { return getenv(name); }
 // A/B switches of past measurements (GG_ALL_FULL, GG_NO_GRAPH, GG_SYNC_ALLPUSH,
 // GG_FLAGS_FIRST, GG_FF_FRAC16, GG_PREP_WIDE, GG_XCHG_EXACT_BYTES): read only in a -DGG_AB_KNOBS build.
@@ -236,6 +233,7 @@ struct gg_engine {
     uint64_t need_peers = 0;                   // parts whose need bits we may use (they hold the digest)
     std::set<int64_t> inj_rounds;              // rounds with a client broadcast (the need bits' condition)
     bool need_produce = false;                 // we write need bits (we hold the digest)
+    bool plan_only = false;                    // install_shard stops after the exchange plan
     // exact-size directions (their sizes travel first, one host wait per round),
     // decided per direction from its capacity, which both ends compute alike
     std::vector<uint8_t> xexact_s, xexact_r;   // [P] to / from each part
@@ -2185,10 +2183,6 @@ static int finish_topology(gg_engine* e, const int64_t* iptr, const int64_t* opt
 // (send_off, recv_off, n_ghost; d_send_idx, d_gout_* already on the device):
 // segment capacities (header + an F and an S entry per send-list node), pack
 // tiles, the size mode of every direction.
-namespace {
-int win_acquire(gg_engine* e, uint64_t bytes);  // the IPC window pool (below, gg_dist_ipc_export)
-}
-
 static int setup_exchange(gg_engine* e) {
     const uint32_t Wd = e->P;
     e->xstride = (uint32_t)(e->nwp >= 2 ? 16 + 8 * e->nwp : 16);
@@ -2278,14 +2272,6 @@ static int setup_exchange(gg_engine* e) {
         e->xexact_s[q] = cs && !never && (force || cs > lim);
         e->xexact_r[q] = cr && !never && (force || cr > lim);
         e->xexact |= e->xexact_s[q] || e->xexact_r[q];
-    }
-    // the device-driven exchange's window, allocated now — before the part's
-    // per-node state — when the caller will take that exchange (see win_acquire)
-    if (test_knob("GG_IPC_WINDOW_EARLY") && Wd > 1 && !e->d_win) {
-        e->win_rbuf = (e->xroff[Wd] + 255) / 256 * 256;
-        if (int rc = win_acquire(e, gg::kWinHdr + 2 * std::max<uint64_t>(e->win_rbuf, 256))) return rc;
-        HIPCHK(hipMalloc(&e->d_xticket, 16));
-        HIPCHK(hipMemset(e->d_xticket, 0, 16));
     }
     return GG_OK;
 }
@@ -2664,9 +2650,11 @@ namespace {
 int win_prealloc(gg_engine* e, uint64_t bytes);  // the IPC window pool (below, gg_dist_ipc_export)
 }
 
+static uint64_t window_bytes(const gg_engine* e) {
+    return gg::kWinHdr + 2 * std::max<uint64_t>((e->xroff[e->P] + 255) / 256 * 256, 256);
+}
+
 static int generate_sharded(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz_out) {
-    if (const char* pg = test_knob("GG_IPC_PREALLOC_GB"))  // a window allocated before anything else of the part
-        if (int rc = win_prealloc(e, (uint64_t)(atof(pg) * 1073741824.0))) return rc;
     const uint64_t V = e->V;
     const uint32_t P = e->P;
     std::vector<uint64_t> plo(P + 1);
@@ -2676,8 +2664,22 @@ static int generate_sharded(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz
     lab_prepare(e, spec);  // the whole graph's labels while this part holds no HBM yet
     gg_gen::Csr g{};
     std::string err;
-    int rc = gg_gen::build_csr_rows(*spec, e->stream, 0u, lo, hi, &g, &err);
-    if (rc) return e->fail(rc, err);
+    int rc = GG_OK;
+    if ((e->cfg.flags & GG_IPC_WINDOW_FIRST) && P > 1) {
+        // planning pass: the part's exchange (its window's size), then everything
+        // dropped, the window allocated, and the part built for good (gossip.h)
+        if ((rc = gg_gen::build_csr_rows(*spec, e->stream, 0u, lo, hi, &g, &err))) return e->fail(rc, err);
+        e->plan_only = true;
+        rc = install_shard(e, g, plo, nullptr);
+        e->plan_only = false;
+        if (rc) return rc;
+        const uint64_t bytes = window_bytes(e);
+        HIPCHK(hipStreamSynchronize(e->stream));
+        e->free_topology();
+        if ((rc = win_prealloc(e, bytes))) return rc;
+        g = gg_gen::Csr{};
+    }
+    if ((rc = gg_gen::build_csr_rows(*spec, e->stream, 0u, lo, hi, &g, &err))) return e->fail(rc, err);
     if ((rc = install_shard(e, g, plo, nnz_out))) return rc;
     return lsat_parts(e, spec);
 }
@@ -2752,6 +2754,7 @@ static int install_shard(gg_engine* e, gg_gen::Csr g, const std::vector<uint64_t
     e->d_gout_col = sh.gout_col;
     e->d_gout_sidx = sh.gout_sidx;
     if ((rc = setup_exchange(e))) return rc;
+    if (e->plan_only) return GG_OK;  // (GG_IPC_WINDOW_FIRST's planning pass: the sizes are known)
     uint64_t dmax = 0;
     if ((rc = gg_gen::max_degree(g.row_ptr, n_own, e->stream, &dmax, &err))) return e->fail(rc, err);
     std::vector<int64_t> iptr;
@@ -3800,6 +3803,13 @@ void win_release(uint8_t* p) {
         if (w.ptr == p) w.busy = false;
 }
 
+uint64_t win_size(const uint8_t* p) {
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    for (auto& w : g_win_pool)
+        if (w.ptr == p) return w.bytes;
+    return 0;
+}
+
 bool win_handle(const uint8_t* p, hipIpcMemHandle_t* h) {
     std::lock_guard<std::mutex> lk(g_ipc_mu);
     for (auto& w : g_win_pool)
@@ -3818,10 +3828,14 @@ int gg_dist_ipc_export(gg_engine* e, uint8_t* blob) {
     if (e->ipc) return e->fail(GG_EINVAL, "exchange transport already set");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
-    if (!e->d_win) {
-        e->win_rbuf = (e->xroff[e->P] + 255) / 256 * 256;
-        const uint64_t bytes = gg::kWinHdr + 2 * std::max<uint64_t>(e->win_rbuf, 256);
-        if (int rc = win_acquire(e, bytes)) return rc;  // (a pooled window, or a new one exported once)
+    e->win_rbuf = (e->xroff[e->P] + 255) / 256 * 256;
+    if (e->d_win && win_size(e->d_win) < window_bytes(e)) {  // (a preallocated window too small)
+        win_release(e->d_win);
+        e->d_win = nullptr;
+    }
+    if (!e->d_win)  // a pooled window, or a new one exported once
+        if (int rc = win_acquire(e, window_bytes(e))) return rc;
+    if (!e->d_xticket) {
         HIPCHK(hipMalloc(&e->d_xticket, 16));
         HIPCHK(hipMemset(e->d_xticket, 0, 16));
     }

@@ -65,13 +65,19 @@ extern "C" {
 
 /* gg_config.flags */
 #define GG_TRACK_DELIVERY 1u /* keep the first-seen round of every (node,lane) */
+/* a vertex-sharded engine that will take the device-driven exchange: gg_topology_generate
+ * first plans the part (its exchange window's size), allocates the window, then builds
+ * the part. On this ROCm a window allocated after its engine's part was built could not be
+ * mapped by the peers (hipIpcOpenMemHandle never returned); one allocated
+ * first could. Costs one more part build (setup only). */
+#define GG_IPC_WINDOW_FIRST 2u
 
 typedef struct gg_engine gg_engine; /* opaque; owns all device memory */
 
 typedef struct {
     uint64_t n_nodes;           /* V: node ids 0..V-1 ("n0".."n<V-1>") */
     uint32_t n_lanes;           /* W: message lanes, multiple of 64, 64..8192 */
-    uint32_t flags;             /* GG_TRACK_DELIVERY */
+    uint32_t flags;             /* GG_TRACK_DELIVERY | GG_IPC_WINDOW_FIRST */
     uint64_t seed;              /* sync schedule + seeded partitions */
     uint32_t sync_base_ticks;   /* 20  (= 2 s,  `main.go:47`) */
     uint32_t sync_jitter_ticks; /* 10  (= rand.Intn(1000) ms, `main.go:46`) */

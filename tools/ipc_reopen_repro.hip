@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <thread>
+#include <vector>
 
 #define CK(x)                                                                    \
     do {                                                                         \
@@ -175,6 +176,7 @@ static void parent() {
 //   12 one window of REPRO_GB GiB, nothing before it: export, both map at once
 //   13 kernels store into the first mapped window (50 launches), then as 10
 //   14 REPRO_FILL_GB (default 80) of other device allocations first, then as 12
+//   15 REPRO_TEMP_GB (default 24) of temporaries allocated, written and freed first, then as 12
 // REPRO_CACHED=1: windows from hipMalloc instead of hipExtMallocWithFlags(uncached).
 static void both(int who) {
     const int tx = who ? c2p[1] : p2c[1], rx = who ? p2c[0] : c2p[0];
@@ -208,6 +210,21 @@ static void both(int who) {
         else CK(hipMalloc(q, n));
         CK(hipMemset(*q, 0, n));
     };
+    if (g_scn == 15) {  // REPRO_TEMP_GB of temporaries allocated, written, freed first (then as 12)
+        const double tg = getenv("REPRO_TEMP_GB") ? atof(getenv("REPRO_TEMP_GB")) : 24.0;
+        std::vector<void*> tmp;
+        for (double got = 0; got < tg; got += 4.0) {
+            void* x = nullptr;
+            CK(hipMalloc(&x, 4ull << 30));
+            CK(hipMemset(x, 7, 4ull << 30));
+            tmp.push_back(x);
+        }
+        CK(hipDeviceSynchronize());
+        for (void* x : tmp) CK(hipFree(x));
+        printf("[%d] scenario 15: %.0f GiB of temporaries allocated and freed\n", who, tg);
+        fflush(stdout);
+        g_scn = 12;
+    }
     if (g_scn == 14) {  // REPRO_FILL_GB of other allocations (2 GiB chunks) first, then as 12
         const double fill = getenv("REPRO_FILL_GB") ? atof(getenv("REPRO_FILL_GB")) : 80.0;
         const double chunk = getenv("REPRO_CHUNK_MB") ? atof(getenv("REPRO_CHUNK_MB")) : 2048.0;
