@@ -912,15 +912,14 @@ def leg(job: Job, args, name: str, xchg_pref: str) -> dict:
     engs = []
 
     def build_engines():
-        wf = xchg_pref == "ipc" and P > 1  # the exchange window allocated before the part (gossip.h)
         if halves == 2:
             g, q = divmod(rank, P)
             for h in range(2):
                 engs.append(Engine(V, K, seed=seed, enable_sync=True, device=local, rank=(2 * g + h) * P + q,
-                                   world=2 * world, lane_groups=2 * L, ipc_window_first=wf))
+                                   world=2 * world, lane_groups=2 * L))
         else:
             engs.append(Engine(V, K, seed=seed, enable_sync=True, device=local, rank=rank, world=world,
-                               lane_groups=L, ipc_window_first=wf))
+                               lane_groups=L))
         E = 0
         for e in engs:
             E = e.generate(**gen)  # this rank's rows (gossip_gen.h); halves: the same rows twice

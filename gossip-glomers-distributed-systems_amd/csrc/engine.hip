@@ -58,7 +58,8 @@ constexpr int kMaxBlocks = 2048;
 // GG_IPC_SPIN_LIMIT (sleeps before a device-driven exchange wait gives up), GG_LSAT=0 / 1
 // (lean saturation digest off / on whatever the graph), GG_NEED_BITS=0 (the device-driven
 // exchange ships every active F row), GG_LSAT_LABELS_FAIL=1 (vertex parts: the component
-// labels' build fails; the digest falls back to "every lane"), GG_IPC_OPEN_TIMEOUT_S.
+// labels' build fails; the digest falls back to "every lane"), GG_IPC_OPEN_TIMEOUT_S (default 30 s),
+// GG_IPC_WINDOW_ALIGN_MB (granularity of new IPC windows; win_round).
 const char* test_knob(const char* name) { return getenv(name); }
 // A/B switches of past measurements (GG_ALL_FULL, GG_NO_GRAPH, GG_SYNC_ALLPUSH,
 // GG_FLAGS_FIRST, GG_FF_FRAC16, GG_PREP_WIDE, GG_XCHG_EXACT_BYTES): read only in a -DGG_AB_KNOBS build.
@@ -233,7 +234,6 @@ struct gg_engine {
     uint64_t need_peers = 0;                   // parts whose need bits we may use (they hold the digest)
     std::set<int64_t> inj_rounds;              // rounds with a client broadcast (the need bits' condition)
     bool need_produce = false;                 // we write need bits (we hold the digest)
-    bool plan_only = false;                    // install_shard stops after the exchange plan
     // exact-size directions (their sizes travel first, one host wait per round),
     // decided per direction from its capacity, which both ends compute alike
     std::vector<uint8_t> xexact_s, xexact_r;   // [P] to / from each part
@@ -2646,10 +2646,6 @@ static int lsat_parts(gg_engine* e, const gg_gen_spec* spec) {
     return rc;
 }
 
-namespace {
-int win_prealloc(gg_engine* e, uint64_t bytes);  // the IPC window pool (below, gg_dist_ipc_export)
-}
-
 static uint64_t window_bytes(const gg_engine* e) {
     return gg::kWinHdr + 2 * std::max<uint64_t>((e->xroff[e->P] + 255) / 256 * 256, 256);
 }
@@ -2664,22 +2660,8 @@ static int generate_sharded(gg_engine* e, const gg_gen_spec* spec, uint64_t* nnz
     lab_prepare(e, spec);  // the whole graph's labels while this part holds no HBM yet
     gg_gen::Csr g{};
     std::string err;
-    int rc = GG_OK;
-    if ((e->cfg.flags & GG_IPC_WINDOW_FIRST) && P > 1) {
-        // planning pass: the part's exchange (its window's size), then everything
-        // dropped, the window allocated, and the part built for good (gossip.h)
-        if ((rc = gg_gen::build_csr_rows(*spec, e->stream, 0u, lo, hi, &g, &err))) return e->fail(rc, err);
-        e->plan_only = true;
-        rc = install_shard(e, g, plo, nullptr);
-        e->plan_only = false;
-        if (rc) return rc;
-        const uint64_t bytes = window_bytes(e);
-        HIPCHK(hipStreamSynchronize(e->stream));
-        e->free_topology();
-        if ((rc = win_prealloc(e, bytes))) return rc;
-        g = gg_gen::Csr{};
-    }
-    if ((rc = gg_gen::build_csr_rows(*spec, e->stream, 0u, lo, hi, &g, &err))) return e->fail(rc, err);
+    int rc = gg_gen::build_csr_rows(*spec, e->stream, 0u, lo, hi, &g, &err);
+    if (rc) return e->fail(rc, err);
     if ((rc = install_shard(e, g, plo, nnz_out))) return rc;
     return lsat_parts(e, spec);
 }
@@ -2754,7 +2736,6 @@ static int install_shard(gg_engine* e, gg_gen::Csr g, const std::vector<uint64_t
     e->d_gout_col = sh.gout_col;
     e->d_gout_sidx = sh.gout_sidx;
     if ((rc = setup_exchange(e))) return rc;
-    if (e->plan_only) return GG_OK;  // (GG_IPC_WINDOW_FIRST's planning pass: the sizes are known)
     uint64_t dmax = 0;
     if ((rc = gg_gen::max_degree(g.row_ptr, n_own, e->stream, &dmax, &err))) return e->fail(rc, err);
     std::vector<int64_t> iptr;
@@ -3755,6 +3736,19 @@ std::mutex g_ipc_mu;
 std::vector<PooledWin> g_win_pool;
 std::map<std::string, void*> g_peer_maps;  // handle bytes -> this process's mapping
 
+// A new window above 1 GiB is allocated in whole GiB. Measured on the 2-rank C4 leg
+// at 2^24 nodes (two lane halves per rank, windows of 3.741 GiB): a window of that
+// exact size, or rounded up to 2 MiB or 256 MiB, could not be mapped by the peer
+// (hipIpcOpenMemHandle never returned, in every allocation order tried); rounded up
+// to 4 GiB it mapped in milliseconds, every time. Windows up to
+// 1 GiB (2^22 nodes) always mapped and keep their exact size.
+// GG_IPC_WINDOW_ALIGN_MB overrides the granularity (0: exact sizes; the A/B).
+uint64_t win_round(uint64_t bytes) {
+    const char* s = test_knob("GG_IPC_WINDOW_ALIGN_MB");
+    const uint64_t a = s ? (uint64_t)(atof(s) * 1048576.0) : (bytes > (1ull << 30) ? 1ull << 30 : 0);
+    return a ? (bytes + a - 1) / a * a : bytes;
+}
+
 int win_acquire(gg_engine* e, uint64_t bytes) {
     std::lock_guard<std::mutex> lk(g_ipc_mu);
     PooledWin* best = nullptr;
@@ -3767,6 +3761,7 @@ int win_acquire(gg_engine* e, uint64_t bytes) {
         return GG_OK;
     }
     PooledWin w{};
+    bytes = win_round(bytes);
     // uncached: stores from the peers' pack kernels and this engine's reads meet in HBM
     HIPCHK(hipExtMallocWithFlags(reinterpret_cast<void**>(&w.ptr), bytes, hipDeviceMallocUncached));
     HIPCHK(hipMemset(w.ptr, 0, bytes));
@@ -3776,24 +3771,6 @@ int win_acquire(gg_engine* e, uint64_t bytes) {
     w.busy = true;
     g_win_pool.push_back(w);
     e->d_win = w.ptr;
-    return GG_OK;
-}
-
-int win_prealloc(gg_engine* e, uint64_t bytes) {  // (one more pooled window per call)
-    PooledWin w{};
-    HIPCHK(hipExtMallocWithFlags(reinterpret_cast<void**>(&w.ptr), bytes, hipDeviceMallocUncached));
-    HIPCHK(hipMemset(w.ptr, 0, bytes));
-    HIPCHK(hipIpcGetMemHandle(&w.handle, w.ptr));
-    w.bytes = bytes;
-    w.device = e->device;
-    w.busy = true;
-    {
-        std::lock_guard<std::mutex> lk(g_ipc_mu);
-        g_win_pool.push_back(w);
-    }
-    e->d_win = w.ptr;
-    win_release(e->d_win);
-    e->d_win = nullptr;
     return GG_OK;
 }
 
@@ -3890,7 +3867,7 @@ int gg_dist_ipc_import(gg_engine* e, const uint8_t* blobs) {
                      e->part, fr / 1073741824.0, tot / 1073741824.0,
                      (gg::kWinHdr + 2.0 * std::max<uint64_t>(e->win_rbuf, 256)) / 1073741824.0);
     }
-    double limit_s = 120.0;
+    double limit_s = 30.0;
     if (const char* s = test_knob("GG_IPC_OPEN_TIMEOUT_S")) limit_s = std::max(1.0, atof(s));
     for (uint32_t q = 0; q < P; ++q) {
         const bool snd = q != e->part && e->xsoff[q + 1] > e->xsoff[q];

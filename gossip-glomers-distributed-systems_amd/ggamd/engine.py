@@ -24,7 +24,6 @@ HIP_LIB = os.environ.get("GG_HIP_LIB") or os.path.join(PKG_DIR, "libgossip_hip.s
 HOST_LIB = os.path.join(PKG_DIR, "libgossip_host.so")
 
 GG_TRACK_DELIVERY = 1
-GG_IPC_WINDOW_FIRST = 2  # gossip.h: size, allocate the IPC window, then build the part
 ERRNO = {-5: "EIO", -12: "ENOMEM", -22: "EINVAL", -28: "ENOSPC", -38: "ENOSYS"}
 
 
@@ -236,11 +235,10 @@ class Engine:
     def __init__(self, n_nodes: int, n_lanes: int, *, seed: int = 0, sync_base: int = 20,
                  sync_jitter: int = 10, enable_sync: bool = True, track_delivery: bool = False,
                  device: int = -1, rank: int = 0, world: int = 1, lane_groups: int = 1,
-                 batch_ticks: int = 0, library: str | None = None, ipc_window_first: bool = False):
+                 batch_ticks: int = 0, library: str | None = None):
         self.lib = load_library(library or HIP_LIB)
         self.library = os.path.abspath(library or HIP_LIB)
-        flags = (GG_TRACK_DELIVERY if track_delivery else 0) | (GG_IPC_WINDOW_FIRST if ipc_window_first else 0)
-        cfg = GGConfig(n_nodes, n_lanes, flags, seed,
+        cfg = GGConfig(n_nodes, n_lanes, GG_TRACK_DELIVERY if track_delivery else 0, seed,
                        sync_base, sync_jitter, 1 if enable_sync else 0, device, rank, world, lane_groups,
                        batch_ticks)
         h = C.c_void_p()

@@ -65,19 +65,13 @@ extern "C" {
 
 /* gg_config.flags */
 #define GG_TRACK_DELIVERY 1u /* keep the first-seen round of every (node,lane) */
-/* a vertex-sharded engine that will take the device-driven exchange: gg_topology_generate
- * first plans the part (its exchange window's size), allocates the window, then builds
- * the part. On this ROCm a window allocated after its engine's part was built could not be
- * mapped by the peers (hipIpcOpenMemHandle never returned); one allocated
- * first could. Costs one more part build (setup only). */
-#define GG_IPC_WINDOW_FIRST 2u
 
 typedef struct gg_engine gg_engine; /* opaque; owns all device memory */
 
 typedef struct {
     uint64_t n_nodes;           /* V: node ids 0..V-1 ("n0".."n<V-1>") */
     uint32_t n_lanes;           /* W: message lanes, multiple of 64, 64..8192 */
-    uint32_t flags;             /* GG_TRACK_DELIVERY | GG_IPC_WINDOW_FIRST */
+    uint32_t flags;             /* GG_TRACK_DELIVERY */
     uint64_t seed;              /* sync schedule + seeded partitions */
     uint32_t sync_base_ticks;   /* 20  (= 2 s,  `main.go:47`) */
     uint32_t sync_jitter_ticks; /* 10  (= rand.Intn(1000) ms, `main.go:46`) */
@@ -362,7 +356,8 @@ int gg_dist_run_episodes(gg_engine* e, uint32_t n_rounds, uint32_t episodes, gg_
 #define GG_IPC_BLOB_BYTES 1024
 int gg_dist_ipc_export(gg_engine* e, uint8_t* blob /* GG_IPC_BLOB_BYTES */);
 /* A mapping that does not return within GG_IPC_OPEN_TIMEOUT_S seconds (env, default
- * 120) fails the import with GG_EIO instead of hanging the rank. */
+ * 30) fails the import with GG_EIO instead of hanging the rank. Windows above 1 GiB are
+ * allocated in whole GiB (the size that maps on this ROCm). */
 int gg_dist_ipc_import(gg_engine* e, const uint8_t* blobs /* P x GG_IPC_BLOB_BYTES, part order */);
 /* Collective teardown, first half: wait for the engine's stream and leave the
  * exchange (the engine no longer touches its peers' windows; it can export and

@@ -173,7 +173,7 @@ static void parent() {
 //      the new handle too
 //   10 a second window of REPRO_GB GiB (default 8) beside the first: export, both map at once
 //   11 as 10, the two processes mapping in turn (process 0, then 1)
-//   12 one window of REPRO_GB GiB, nothing before it: export, both map at once
+//   12 one window of REPRO_GB GiB (or REPRO_BYTES bytes), nothing before it: export, both map at once
 //   13 kernels store into the first mapped window (50 launches), then as 10
 //   14 REPRO_FILL_GB (default 80) of other device allocations first, then as 12
 //   15 REPRO_TEMP_GB (default 24) of temporaries allocated, written and freed first, then as 12
@@ -239,7 +239,9 @@ static void both(int who) {
         g_scn = 12;
     }
     if (g_scn == 12) {
-        const size_t big = (size_t)(getenv("REPRO_GB") ? atof(getenv("REPRO_GB")) : 8.0) * (1ull << 30);
+        size_t big = (size_t)((getenv("REPRO_GB") ? atof(getenv("REPRO_GB")) : 8.0) * (1ull << 30));
+        if (getenv("REPRO_BYTES")) big = strtoull(getenv("REPRO_BYTES"), nullptr, 10);  // an exact size
+        printf("[%d] scenario 12: window of %zu bytes\n", who, big);
         alloc(&w, big);
         const auto t0 = std::chrono::steady_clock::now();
         exchange_and_open(1);
