@@ -91,15 +91,20 @@ def test_request_ceiling(tmp_path):
     stdout.write_text("calibrate rows  64 B G= 4 rows_per_dispatch 1000 rows_per_s 4.0e+10\n"
                       "calibrate rows 512 B G=32 rows_per_dispatch 1000 rows_per_s 1.0e+10\n"
                       "calibrate writes  64 B G= 4 rows_per_dispatch 1000 rows_per_s 5.0e+10\n"
-                      "calibrate seqwrite bytes_per_dispatch 2000000 bytes_per_s 5.0e+12\n")
+                      "calibrate seqwrite bytes_per_dispatch 2000000 bytes_per_s 5.0e+12\n"
+                      "calibrate rows_mall  64 B G= 4 rows_per_dispatch 1000 rows_per_s 6.0e+10\n"
+                      "calibrate writes_mall  64 B G= 4 rows_per_dispatch 1000 rows_per_s 5.5e+10\n"
+                      "calibrate seqwrite_mall bytes_per_dispatch 1000000 bytes_per_s 6.0e+12\n")
     rows = []
-    for d, (name, rd) in enumerate((("void gather<4, 8>(uint4 const*, unsigned int const*, unsigned long, uint4*)", 1050),
-                                    ("void gather<32, 8>(uint4 const*, unsigned int const*, unsigned long, uint4*)",
-                                     4050))):
+    g = "(uint4 const*, unsigned int const*, unsigned long, uint4*)"
+    for d, (name, rd) in enumerate((("void gather<4, 8, 0>" + g, 1050), ("void gather<32, 8, 0>" + g, 4050),
+                                    ("void gather<4, 8, 1>" + g, 1020))):
         rows += [dict(Dispatch_Id=d, Kernel_Name=name, Counter_Name="TCC_EA0_RDREQ_sum", Counter_Value=rd),
                  dict(Dispatch_Id=d, Kernel_Name=name, Counter_Name="TCC_EA0_WRREQ_sum", Counter_Value=0)]
-    for d, (name, wr) in enumerate((("void scatter<4, 8>(uint4*, unsigned int const*, unsigned long)", 1100),
-                                    ("seqwrite(uint4*, unsigned long)", 32000)), start=2):
+    sc = "(uint4*, unsigned int const*, unsigned long)"
+    for d, (name, wr) in enumerate((("void scatter<4, 8, 0>" + sc, 1100), ("void seqwrite<0>(uint4*, unsigned long)", 32000),
+                                    ("void scatter<4, 8, 1>" + sc, 1000), ("void seqwrite<1>(uint4*, unsigned long)", 16000)),
+                                   start=3):
         rows += [dict(Dispatch_Id=d, Kernel_Name=name, Counter_Name="TCC_EA0_RDREQ_sum", Counter_Value=0),
                  dict(Dispatch_Id=d, Kernel_Name=name, Counter_Name="TCC_EA0_WRREQ_sum", Counter_Value=wr)]
     _csv(tmp_path / "req.csv", rows)
@@ -107,10 +112,15 @@ def test_request_ceiling(tmp_path):
     subprocess.check_call([sys.executable, os.path.join(REPO, "tools", "request_ceiling.py"), str(stdout),
                            str(tmp_path / "req.csv"), str(out)], stdout=subprocess.DEVNULL)
     d = json.load(open(out))
-    by = {r["row_bytes"]: r for r in d["rows"]}
-    assert by[64]["requests_per_row"] == pytest.approx(1.05) and by[512]["requests_per_row"] == pytest.approx(4.05)
-    assert d["requests_per_s"] == pytest.approx(max(4.0e10 * 1.05, 1.0e10 * 4.05))
-    # writes: the random-row stores (5e10 rows/s x 1.1) and the sweep (32000 requests in 0.4 us)
-    assert d["write_rows"][0]["requests_per_row"] == pytest.approx(1.1)
-    assert d["write_sweep"]["requests_per_s"] == pytest.approx(32000 / (2e6 / 5e12))
-    assert d["write_requests_per_s"] == pytest.approx(max(5e10 * 1.1, 32000 / (2e6 / 5e12)))
+    by = {(r["row_bytes"], "HBM" in r["table"]): r for r in d["rows"]}
+    assert by[64, True]["requests_per_row"] == pytest.approx(1.05)
+    assert by[512, True]["requests_per_row"] == pytest.approx(4.05)
+    assert by[64, False]["requests_per_row"] == pytest.approx(1.02)
+    # each direction's ceiling: the highest rate over both tables
+    assert d["requests_per_s"] == pytest.approx(max(4.0e10 * 1.05, 1.0e10 * 4.05, 6.0e10 * 1.02))
+    wby = {"HBM" in r["table"]: r for r in d["write_rows"]}
+    assert wby[True]["requests_per_row"] == pytest.approx(1.1) and wby[False]["requests_per_row"] == pytest.approx(1.0)
+    sw = {"HBM" in r["table"]: r for r in d["write_sweeps"]}
+    assert sw[True]["requests_per_s"] == pytest.approx(32000 / (2e6 / 5e12))
+    assert sw[False]["requests_per_s"] == pytest.approx(16000 / (1e6 / 6e12))
+    assert d["write_requests_per_s"] == pytest.approx(max(5e10 * 1.1, 5.5e10, 32000 / (2e6 / 5e12), 16000 / (1e6 / 6e12)))

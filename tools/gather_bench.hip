@@ -21,7 +21,10 @@
         }                                                                        \
     } while (0)
 
-template <int G, int K>
+// T tags the instantiation of a calibration regime (0: an 8 GiB table in HBM; 1: a
+// 256 MiB table the 256 MB Infinity Cache can hold, the regime of C2's state
+// arrays) so rocprofv3 tells their dispatches apart
+template <int G, int K, int T = 0>
 __global__ __launch_bounds__(256) void gather(const uint4* table, const uint32_t* idx, uint64_t n_rows_idx,
                                               uint4* out) {
     const int lg = threadIdx.x % G;
@@ -47,7 +50,7 @@ __global__ __launch_bounds__(256) void gather(const uint4* table, const uint32_t
 
 // the write side of the calibration: K random rows per lane group stored (G
 // lanes x 16 B each), and a coalesced sweep (reset_state's pattern)
-template <int G, int K>
+template <int G, int K, int T = 0>
 __global__ __launch_bounds__(256) void scatter(uint4* table, const uint32_t* idx, uint64_t n_rows_idx) {
     const int lg = threadIdx.x % G;
     const uint64_t groups = (uint64_t)gridDim.x * (256 / G);
@@ -61,19 +64,20 @@ __global__ __launch_bounds__(256) void scatter(uint4* table, const uint32_t* idx
     }
 }
 
+template <int T = 0>
 __global__ __launch_bounds__(256) void seqwrite(uint4* table, uint64_t n16) {
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256)
         table[i] = make_uint4((uint32_t)i, 0u, 0u, 1u);
 }
 
-template <int G, int K>
+template <int G, int K, int T = 0>
 double run_scatter(uint4* table, const uint32_t* idx, uint64_t n, int blocks) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    hipLaunchKernelGGL((scatter<G, K>), dim3(blocks), dim3(256), 0, 0, table, idx, n);
+    hipLaunchKernelGGL((scatter<G, K, T>), dim3(blocks), dim3(256), 0, 0, table, idx, n);
     CK(hipEventRecord(a, 0));
-    for (int r = 0; r < 3; ++r) hipLaunchKernelGGL((scatter<G, K>), dim3(blocks), dim3(256), 0, 0, table, idx, n);
+    for (int r = 0; r < 3; ++r) hipLaunchKernelGGL((scatter<G, K, T>), dim3(blocks), dim3(256), 0, 0, table, idx, n);
     CK(hipEventRecord(b, 0));
     CK(hipEventSynchronize(b));
     float ms;
@@ -81,14 +85,14 @@ double run_scatter(uint4* table, const uint32_t* idx, uint64_t n, int blocks) {
     return ms / 3;
 }
 
-template <int G, int K>
+template <int G, int K, int T = 0>
 double run(const uint4* table, const uint32_t* idx, uint64_t n, uint4* out, int blocks) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    hipLaunchKernelGGL((gather<G, K>), dim3(blocks), dim3(256), 0, 0, table, idx, n, out);
+    hipLaunchKernelGGL((gather<G, K, T>), dim3(blocks), dim3(256), 0, 0, table, idx, n, out);
     CK(hipEventRecord(a, 0));
-    for (int r = 0; r < 3; ++r) hipLaunchKernelGGL((gather<G, K>), dim3(blocks), dim3(256), 0, 0, table, idx, n, out);
+    for (int r = 0; r < 3; ++r) hipLaunchKernelGGL((gather<G, K, T>), dim3(blocks), dim3(256), 0, 0, table, idx, n, out);
     CK(hipEventRecord(b, 0));
     CK(hipEventSynchronize(b));
     float ms;
@@ -144,15 +148,57 @@ int main(int argc, char** argv) {
             hipEvent_t a, b;
             CK(hipEventCreate(&a));
             CK(hipEventCreate(&b));
-            hipLaunchKernelGGL(seqwrite, dim3(8192), dim3(256), 0, 0, table, n16);
+            hipLaunchKernelGGL(seqwrite<0>, dim3(8192), dim3(256), 0, 0, table, n16);
             CK(hipEventRecord(a, 0));
-            for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(seqwrite, dim3(8192), dim3(256), 0, 0, table, n16);
+            for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(seqwrite<0>, dim3(8192), dim3(256), 0, 0, table, n16);
             CK(hipEventRecord(b, 0));
             CK(hipEventSynchronize(b));
             float ms;
             CK(hipEventElapsedTime(&ms, a, b));
             printf("calibrate seqwrite bytes_per_dispatch %llu bytes_per_s %.4e\n", (unsigned long long)(n16 * 16),
                    n16 * 16 / (ms / 3 * 1e-3));
+            fflush(stdout);
+        }
+        // the same shapes on a 256 MiB table (regime T = 1: the Infinity Cache can hold it)
+        const uint64_t tm = 256ull << 20;
+        for (int rb : {64, 128}) {
+            const uint64_t rows = tm / rb;
+            uint64_t s = 0x2545F4914F6CDD1Dull + rb;
+            auto rnd = [&]() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; };
+            for (uint64_t i = 0; i < n; ++i) h[i] = (uint32_t)(rnd() % rows);
+            CK(hipMemcpy(idx, h.data(), n * 4, hipMemcpyHostToDevice));
+            const double ms = rb == 64 ? run<4, 8, 1>(table, idx, n, out, 4096) : run<8, 8, 1>(table, idx, n, out, 4096);
+            printf("calibrate rows_mall %3d B G=%2d rows_per_dispatch %llu rows_per_s %.4e\n", rb, rb / 16,
+                   (unsigned long long)n, n / (ms * 1e-3));
+            fflush(stdout);
+        }
+        for (int rb : {16, 64, 128}) {
+            const uint64_t rows = tm / rb;
+            uint64_t s = 0x5851F42D4C957F2Dull + rb;
+            auto rnd = [&]() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; };
+            for (uint64_t i = 0; i < n; ++i) h[i] = (uint32_t)(rnd() % rows);
+            CK(hipMemcpy(idx, h.data(), n * 4, hipMemcpyHostToDevice));
+            const double ms = rb == 16 ? run_scatter<1, 8, 1>(table, idx, n, 4096)
+                              : rb == 64 ? run_scatter<4, 8, 1>(table, idx, n, 4096)
+                                         : run_scatter<8, 8, 1>(table, idx, n, 4096);
+            printf("calibrate writes_mall %3d B G=%2d rows_per_dispatch %llu rows_per_s %.4e\n", rb, rb / 16,
+                   (unsigned long long)n, n / (ms * 1e-3));
+            fflush(stdout);
+        }
+        {
+            const uint64_t n16 = tm / 16;
+            hipEvent_t a, b;
+            CK(hipEventCreate(&a));
+            CK(hipEventCreate(&b));
+            hipLaunchKernelGGL(seqwrite<1>, dim3(8192), dim3(256), 0, 0, table, n16);
+            CK(hipEventRecord(a, 0));
+            for (int r = 0; r < 10; ++r) hipLaunchKernelGGL(seqwrite<1>, dim3(8192), dim3(256), 0, 0, table, n16);
+            CK(hipEventRecord(b, 0));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            printf("calibrate seqwrite_mall bytes_per_dispatch %llu bytes_per_s %.4e\n", (unsigned long long)(n16 * 16),
+                   n16 * 16 / (ms / 10 * 1e-3));
             fflush(stdout);
         }
         return 0;

@@ -19,23 +19,30 @@ import json
 import re
 import sys
 
+REGIME = {0: "8 GiB table (HBM)", 1: "256 MiB table (Infinity Cache resident)"}
 
 def main():
-    rows, wrows, seq = {}, {}, None
+    rows, wrows, seqs = {}, {}, {}  # (G, regime) -> calibration; regime 0: 8 GiB table, 1: 256 MiB
     for line in open(sys.argv[1]):
-        m = re.match(r"calibrate (rows|writes)\s+(\d+) B G=\s*(\d+) rows_per_dispatch (\d+) rows_per_s (\S+)", line)
+        m = re.match(r"calibrate (rows|writes)(_mall)?\s+(\d+) B G=\s*(\d+) rows_per_dispatch (\d+) rows_per_s (\S+)", line)
         if m:
             d = rows if m.group(1) == "rows" else wrows
-            d[int(m.group(3))] = {"row_bytes": int(m.group(2)), "rows_per_dispatch": int(m.group(4)),
-                                  "rows_per_s": float(m.group(5))}
-        m = re.match(r"calibrate seqwrite bytes_per_dispatch (\d+) bytes_per_s (\S+)", line)
+            t = 1 if m.group(2) else 0
+            d[(int(m.group(4)), t)] = {"row_bytes": int(m.group(3)), "table": REGIME[t],
+                                       "rows_per_dispatch": int(m.group(5)), "rows_per_s": float(m.group(6))}
+        m = re.match(r"calibrate seqwrite(_mall)? bytes_per_dispatch (\d+) bytes_per_s (\S+)", line)
         if m:
-            seq = {"bytes_per_dispatch": int(m.group(1)), "bytes_per_s": float(m.group(2))}
-    req = collections.defaultdict(lambda: collections.defaultdict(float))  # (kernel, G) -> dispatch -> requests
+            t = 1 if m.group(1) else 0
+            seqs[t] = {"table": REGIME[t], "bytes_per_dispatch": int(m.group(2)), "bytes_per_s": float(m.group(3))}
+    req = collections.defaultdict(lambda: collections.defaultdict(float))  # (kernel, G, T) -> dispatch -> requests
     for r in csv.DictReader(open(sys.argv[2])):
         name = r["Kernel_Name"]
-        m = re.search(r"(gather|scatter)<(\d+),\s*(\d+)>", name)
-        key = (m.group(1), int(m.group(2))) if m else (("seqwrite", 0) if "seqwrite" in name else None)
+        m = re.search(r"(gather|scatter)<(\d+),\s*(\d+)(?:,\s*(\d+))?>", name)
+        if m:
+            key = (m.group(1), int(m.group(2)), int(m.group(4) or 0))
+        else:
+            m = re.search(r"seqwrite(?:<(\d+)>)?", name)
+            key = ("seqwrite", 0, int(m.group(1) or 0)) if m else None
         if key:
             req[key][(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
 
@@ -46,44 +53,44 @@ def main():
                 vals[disp] += v
         return sum(vals.values()) / len(vals) if vals else None
 
-    out = {"source": "tools/gather_bench.hip --calibrate (8 GiB table, uniformly random rows, K = 8, 4096 blocks; "
-                     "random-row stores scatter<G, 8>; a coalesced 2 GiB store sweep) timed with HIP events; "
-                     "requests per dispatch from rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum over the same "
-                     "command", "rows": [], "write_rows": []}
-    for g, r in sorted(rows.items()):
-        rq = per_dispatch(("gather", g), "TCC_EA0_RDREQ")
+    out = {"source": "tools/gather_bench.hip --calibrate (uniformly random rows, K = 8, 4096 blocks, on an 8 GiB "
+                     "table in HBM and on a 256 MiB table the Infinity Cache can hold; random-row stores "
+                     "scatter<G, 8, T>; coalesced store sweeps of 2 GiB and 256 MiB) timed with HIP events; requests "
+                     "per dispatch from rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum over the same command",
+           "rows": [], "write_rows": [], "write_sweeps": []}
+    for (g, t), r in sorted(rows.items(), key=lambda kv: (kv[0][1], kv[0][0])):
+        rq = per_dispatch(("gather", g, t), "TCC_EA0_RDREQ")
         if rq is None:
             continue
         per_row = rq / r["rows_per_dispatch"]
         out["rows"].append(dict(r, requests_per_row=per_row, requests_per_s=r["rows_per_s"] * per_row))
-    for g, r in sorted(wrows.items()):
-        rq = per_dispatch(("scatter", g), "TCC_EA0_WRREQ")
+    for (g, t), r in sorted(wrows.items(), key=lambda kv: (kv[0][1], kv[0][0])):
+        rq = per_dispatch(("scatter", g, t), "TCC_EA0_WRREQ")
         if rq is None:
             continue
         per_row = rq / r["rows_per_dispatch"]
         out["write_rows"].append(dict(r, requests_per_row=per_row, requests_per_s=r["rows_per_s"] * per_row))
-    if seq is not None:
-        rq = per_dispatch(("seqwrite", 0), "TCC_EA0_WRREQ")
+    for t, sq in sorted(seqs.items()):
+        rq = per_dispatch(("seqwrite", 0, t), "TCC_EA0_WRREQ")
         if rq is not None:
-            seq["requests_per_dispatch"] = rq
-            seq["requests_per_s"] = rq / (seq["bytes_per_dispatch"] / seq["bytes_per_s"])
-            out["write_sweep"] = seq
+            sq["requests_per_dispatch"] = rq
+            sq["requests_per_s"] = rq / (sq["bytes_per_dispatch"] / sq["bytes_per_s"])
+            out["write_sweeps"].append(sq)
     if not out["rows"]:
         raise SystemExit("no gather dispatches matched")
-    # the least flattering denominators: the highest rate of each direction
+    # the least flattering denominators: the highest rate of each direction, any table
     out["requests_per_s"] = max(x["requests_per_s"] for x in out["rows"])
-    w = [x["requests_per_s"] for x in out["write_rows"]] + ([seq["requests_per_s"]] if seq and "requests_per_s" in seq
-                                                             else [])
+    w = [x["requests_per_s"] for x in out["write_rows"] + out["write_sweeps"]]
     out["write_requests_per_s"] = max(w) if w else None
     json.dump(out, open(sys.argv[3] if len(sys.argv) > 3 else "profiles/request_ceiling.json", "w"), indent=1)
     for x in out["rows"]:
-        print(f'reads  {x["row_bytes"]:4d} B rows: {x["rows_per_s"] / 1e9:6.2f} G rows/s x {x["requests_per_row"]:.3f} '
-              f'requests/row = {x["requests_per_s"] / 1e9:6.2f} G requests/s')
+        print(f'reads  {x["row_bytes"]:4d} B rows, {x["table"]}: {x["rows_per_s"] / 1e9:6.2f} G rows/s x '
+              f'{x["requests_per_row"]:.3f} requests/row = {x["requests_per_s"] / 1e9:6.2f} G requests/s')
     for x in out["write_rows"]:
-        print(f'writes {x["row_bytes"]:4d} B rows: {x["rows_per_s"] / 1e9:6.2f} G rows/s x {x["requests_per_row"]:.3f} '
-              f'requests/row = {x["requests_per_s"] / 1e9:6.2f} G requests/s')
-    if seq and "requests_per_s" in seq:
-        print(f'writes sweep: {seq["bytes_per_s"] / 1e9:.0f} GB/s = {seq["requests_per_s"] / 1e9:.2f} G requests/s')
+        print(f'writes {x["row_bytes"]:4d} B rows, {x["table"]}: {x["rows_per_s"] / 1e9:6.2f} G rows/s x '
+              f'{x["requests_per_row"]:.3f} requests/row = {x["requests_per_s"] / 1e9:6.2f} G requests/s')
+    for x in out["write_sweeps"]:
+        print(f'writes sweep, {x["table"]}: {x["bytes_per_s"] / 1e9:.0f} GB/s = {x["requests_per_s"] / 1e9:.2f} G requests/s')
     print(f'ceilings: reads {out["requests_per_s"] / 1e9:.2f}, writes '
           f'{(out["write_requests_per_s"] or 0) / 1e9:.2f} G requests/s')
 
