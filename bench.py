@@ -191,11 +191,14 @@ def roofline(rounds_local: list[dict], nwp: int, n_own: int, E_own: int, shape: 
     traffic = traffic_ep / R if traffic_ep else None
     kind_s_ep = D["total_ms"] / max(1, episodes) * 1e-3  # the kind's device time per episode
     rd_ceil, wr_ceil, ceiling_src = request_ceiling()
-    line_frac = line_src = None
+    line_frac = line_src = line_rd = line_wr = None
     if reqs_ep and kind_s_ep > 0:
         rd, wr = reqs_ep
         # the time the kind's requests need at the ceilings, reads and writes each at its
-        # own rate (no write ceiling measured: writes at the read rate, an upper bound)
+        # own rate (no write ceiling measured: writes at the read rate, an upper bound);
+        # line_frac = line_read_frac + line_write_frac
+        line_rd = rd / rd_ceil / kind_s_ep
+        line_wr = wr / (wr_ceil or rd_ceil) / kind_s_ep
         need = rd / rd_ceil + wr / (wr_ceil or rd_ceil)
         line_frac = need / kind_s_ep
         line_src = (f"PMC: {rd:.4g} read + {wr:.4g} write memory-side requests per episode of this kind "
@@ -220,6 +223,8 @@ def roofline(rounds_local: list[dict], nwp: int, n_own: int, E_own: int, shape: 
         "launches": D["launches"],
         "dense_bytes_per_round": dense_bytes_per_round(n_own, E_own, nwp),
         "line_frac": line_frac,
+        "line_read_frac": line_rd,
+        "line_write_frac": line_wr,
         "line_source": line_src or "null: no request pass of this shape in profiles/",
         "read_requests_per_launch": reqs_ep[0] / R if reqs_ep else None,
         "write_requests_per_launch": reqs_ep[1] / R if reqs_ep else None,

@@ -81,6 +81,8 @@ def test_traffic_json_and_bench_normalisation(tmp_path, monkeypatch):
     monkeypatch.setattr(bench, "REQ_CEILING_JSON", str(ceil))
     roof = bench.roofline(rounds, 16, 1 << 20, 2 * (1 << 20), d["shape"], 3)
     assert roof["line_frac"] == pytest.approx((reqs[0] / 5e10 + reqs[1] / 8e10) / (4 * 0.4e-3))
+    assert roof["line_read_frac"] == pytest.approx(reqs[0] / 5e10 / (4 * 0.4e-3))
+    assert roof["line_write_frac"] == pytest.approx(reqs[1] / 8e10 / (4 * 0.4e-3))
     assert roof["traffic"] == pytest.approx(per_ep / 4)
     roof2 = bench.roofline(rounds, 16, 1 << 20, 2 * (1 << 20), other, 3)
     assert roof2["line_frac"] is None and "line_model" not in roof2
