@@ -462,6 +462,44 @@ void gg_engine::compute_round(Acc& total) {
                     if (act_p[u])
                         for (uint64_t j = 0; j < nw; j += 8) __builtin_prefetch(&Fp_all[u * nw + j]);
                 }
+            // A quiet node: nothing can reach it this round (no client broadcast, no
+            // in-neighbour with an F row or a push, no sync callback) and its rows
+            // did not change in r-1 or r-2, so both set buffers already hold its set
+            // and its F row of r-2 is zero: the rows are neither read nor written
+            // (the full path below would store the same bytes). Its counters are
+            // the read_oks arriving and its own timer.
+            bool quiet = !act_p[rep] && !act_c[rep] && !(f2 && fired_at(r - 2, rep)) &&
+                         !(any_inj && inj_by_node.count((uint32_t)g));
+            for (int64_t e = in_ptr[i]; quiet && e < in_ptr[i + 1]; ++e) {
+                const uint64_t urep = in_col[e];
+                if (act_p[urep] || (f3 && fired_at(r - 3, urep))) quiet = false;
+            }
+            if (quiet) {
+                if (f1)
+                    for (int64_t e = in_ptr[i]; e < in_ptr[i + 1]; ++e) {
+                        const uint64_t urep = in_col[e];
+                        const uint64_t u = any_w ? global_of(urep) : urep;
+                        if (fired_at(r - 1, urep) && !masked_in(wm1, u, g)) {  // read arrives
+                            a.read_oks++;                                      // HandleRead :131
+                            if (masked_in(w00, g, u)) a.node_dropped++;
+                        }
+                    }
+                if (sync && r == sync_next[i]) {  // (5) as below, with Tn = 0
+                    const uint64_t deg = (uint64_t)(out_ptr[i + 1] - out_ptr[i]);
+                    uint64_t mdrop = 0;
+                    if (w00 || wp1)
+                        for (int64_t e = out_ptr[i]; e < out_ptr[i + 1]; ++e)
+                            if (masked_in(w00, g, global_of(out_col[e]))) mdrop++;
+                    a.fired++;
+                    a.reads += deg;  // RPC read :120
+                    a.node_dropped += mdrop;
+                    firedw[t].push_back(rep);
+                    sync_k[i]++;
+                    sync_next[i] = r + gg_sync_interval(cfg.seed, g, sync_k[i], cfg.sync_base_ticks,
+                                                        cfg.sync_jitter_ticks);
+                }
+                continue;
+            }
             const uint64_t* spv = &sp_all[rep * nw];
             for (uint64_t j = 0; j < nw; ++j) sp[j] = S[j] = spv[j];
             // (1) client broadcasts
