@@ -342,8 +342,10 @@ def _ipc_connect(engines: list[Engine], group, rank: int, world: int, P: int) ->
         raise err
     B = IPC_BLOB_BYTES
     # the ranks map their peers' windows one rank at a time (a barrier between
-    # turns): with every rank opening at once, large windows (C4 2^24 on 2 ranks:
-    # 3.7 GiB) left both ranks blocked in hipIpcOpenMemHandle
+    # turns; GG_IPC_SERIAL_IMPORT=0: all at once), so a mapping that does not
+    # return names its rank. The stall this was first tried against (C4 2^24 on 2
+    # ranks) was the windows' size, not concurrency: the engine now allocates
+    # windows above 1 GiB in whole GiB
     serial = os.environ.get("GG_IPC_SERIAL_IMPORT", "1") != "0"
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
     ierr = None
