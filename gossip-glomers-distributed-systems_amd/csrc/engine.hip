@@ -3863,9 +3863,11 @@ int gg_dist_ipc_import(gg_engine* e, const uint8_t* blobs) {
     if (dbg) {
         size_t fr = 0, tot = 0;
         (void)hipMemGetInfo(&fr, &tot);
-        std::fprintf(stderr, "gg_dist_ipc_import part %u: HBM free %.2f of %.2f GiB, own window %.3f GiB\n",
+        std::fprintf(stderr,
+                     "gg_dist_ipc_import part %u: HBM free %.2f of %.2f GiB, own window %.3f GiB (allocated %.3f)\n",
                      e->part, fr / 1073741824.0, tot / 1073741824.0,
-                     (gg::kWinHdr + 2.0 * std::max<uint64_t>(e->win_rbuf, 256)) / 1073741824.0);
+                     (gg::kWinHdr + 2.0 * std::max<uint64_t>(e->win_rbuf, 256)) / 1073741824.0,
+                     win_size(e->d_win) / 1073741824.0);
     }
     double limit_s = 30.0;
     if (const char* s = test_knob("GG_IPC_OPEN_TIMEOUT_S")) limit_s = std::max(1.0, atof(s));
