@@ -55,7 +55,7 @@ struct Injection {
     uint32_t lane;
 };
 
-struct Acc {  // per-thread counters
+struct alignas(128) Acc {  // per-thread counters (a cache line pair each: no false sharing)
     uint64_t new_bits = 0, fwd_sent = 0, fwd_deliv = 0, pushes = 0, push_deliv = 0;
     uint64_t reads = 0, read_oks = 0, dropped = 0, fired = 0, hash = 0;
     uint64_t node_dropped = 0;  // dropped reads / read_oks (node-level, not per lane)
