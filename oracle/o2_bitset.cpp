@@ -449,11 +449,18 @@ void gg_engine::compute_round(Acc& total) {
     const bool any_w = wm3 || wm2 || wm1 || w00 || wp1;
     const bool f1 = sync && fired_any(r - 1), f2 = sync && fired_any(r - 2), f3 = sync && fired_any(r - 3);
     const bool any_inj = !inj_by_node.empty();
+    // nodes handed out in chunks (a sparse round's frontier sits in a few
+    // ranges of ids): the counters are sums, so the order of the chunks is free
+    std::atomic<uint64_t> next_chunk{0};
+    constexpr uint64_t kChunk = 4096;
     auto work = [&](int t) {
         Acc& a = accs[t];
         std::vector<uint64_t> S(nw), sp(nw);
-        const uint64_t b0 = n_own * t / T, b1 = n_own * (t + 1) / T;
         constexpr uint64_t kAhead = 8;  // sender rows prefetched this many nodes ahead
+        for (;;) {
+        const uint64_t b0 = next_chunk.fetch_add(kChunk, std::memory_order_relaxed);
+        if (b0 >= n_own) break;
+        const uint64_t b1 = std::min(n_own, b0 + kChunk);
         for (uint64_t i = b0; i < b1; ++i) {
             const uint64_t g = lo + i, rep = own0 + i;
             if (i + kAhead < b1)
@@ -619,6 +626,7 @@ void gg_engine::compute_round(Acc& total) {
                                                     cfg.sync_jitter_ticks);
             }
         }
+        }  // chunks
     };
     if (T == 1) {
         work(0);
