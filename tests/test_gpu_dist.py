@@ -1003,6 +1003,14 @@ def test_batched_refuses_lane_groups(hip_lib):
         Engine(10, 128, batch_ticks=2, world=2, rank=0, lane_groups=2, library=hip_lib)
 
 
+def test_ipc_rounded_windows_equal_oracle(hip_lib, cpu_lib, monkeypatch):
+    """Windows allocated larger than their exchange needs (GG_IPC_WINDOW_ALIGN_MB=64
+    rounds every new window up to 64 MiB, as the engine rounds windows above 1 GiB
+    to whole GiB): the same exchange, the same results against O2, at 3 ranks."""
+    monkeypatch.setenv("GG_IPC_WINDOW_ALIGN_MB", "64")  # inherited by the spawned ranks
+    test_ipc_exchange_equals_oracle(hip_lib, cpu_lib, 3, 1)
+
+
 def _episodes_worker(rank, world, port, lib, scenarios, q, lane_groups, episodes):
     import torch
     import torch.distributed as dist
