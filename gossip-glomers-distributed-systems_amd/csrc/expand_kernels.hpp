@@ -79,6 +79,11 @@ constexpr uint32_t kBllMax = 4096;  // block lists: nodes of a block's slice (kB
 #ifndef GG_STREAM1_ROWS
 #define GG_STREAM1_ROWS 8
 #endif
+// ... and the waves per SIMD it is compiled for (A/B knob; the lean W >= 128
+// kernels keep GG_STREAM_WAVES_PER_EU)
+#ifndef GG_STREAM1_WAVES_PER_EU
+#define GG_STREAM1_WAVES_PER_EU GG_STREAM_WAVES_PER_EU
+#endif
 
 // Sender (flag, row) pairs a lane keeps in flight in dense lean rounds.
 #ifndef GG_SPEC_BATCH
@@ -2338,7 +2343,7 @@ __device__ __forceinline__ uint32_t active_mask1(const uint64_t* abits, const ui
 // same three-stage pipeline (list entry k+3, row pointers k+2, columns k+1)
 // keeps each node to about one memory round trip. Same semantics and counters
 // as expand_stream.
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GG_STREAM_WAVES_PER_EU)))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GG_STREAM1_WAVES_PER_EU)))
 void expand_stream1(RoundArgs a) {
     constexpr int D = GG_STREAM1_ROWS;  // sender rows in flight per lane
     __shared__ unsigned long long s_red[kBlock / 64][C_NUM];
