@@ -5,6 +5,7 @@ goes, round by round (kernel ms, prep / stream split, new bits, active rows,
 gathers, the round's path bits).
 
 Usage: python tools/leg_rounds.py C5 [--side 32768] [--rounds 19]
+       python tools/leg_rounds.py C4 [--nodes 100000000] [--rounds 10]
 """
 import argparse
 import os
@@ -18,14 +19,21 @@ from ggamd.workload import BASE_SEED, inject, injection_arrays, uniform_injectio
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("leg", choices=["C5"])
+    ap.add_argument("leg", choices=["C4", "C5"])
     ap.add_argument("--side", type=int, default=32768)
-    ap.add_argument("--rounds", type=int, default=19)
+    ap.add_argument("--nodes", type=int, default=100_000_000)
+    ap.add_argument("--rounds", type=int, default=None)
     args = ap.parse_args()
-    side = args.side
-    V, K, seed = side * side, 64, BASE_SEED + 5  # bench.py's C5 leg
+    if args.leg == "C5":  # bench.py's legs
+        side = args.side
+        V, K, seed = side * side, 64, BASE_SEED + 5
+        gen = dict(kind="grid_links", n=side, seed=seed)
+    else:
+        V, K, seed = args.nodes, 4096, BASE_SEED + 4
+        gen = dict(kind="rmat", n=V, k=16, seed=seed, a=0.57, b=0.19, c=0.19)
+    args.rounds = args.rounds or (19 if args.leg == "C5" else 10)
     e = Engine(V, K, seed=seed, enable_sync=True, device=0)
-    e.generate(kind="grid_links", n=side, seed=seed)
+    e.generate(**gen)
     inj = injection_arrays(uniform_injections(V, K, seed))
     for _ in range(2):
         e.reset()
