@@ -1990,9 +1990,6 @@ __device__ __forceinline__ void stream_body(RoundArgs a) {
             // r-1 (ACT: the row in this round's set buffer is two rounds old)
             m.fl = (db ? a.flg_prev : a.flg_cur)[a.own0 + n];
             if (full) m.deg = 0;
-#ifdef GG_AB_PARENT_ONLY  // measurement only (wrong results): dense db rounds gather the first sender alone
-            if (DB && !MARK && dense && m.deg > 1) m.deg = 1;
-#endif
             if (a.hub_deg && m.deg > a.hub_deg) {  // a hub: hub_chunks/hub_finish take it
                 m.node |= kHubBit;
                 m.deg = 0;
