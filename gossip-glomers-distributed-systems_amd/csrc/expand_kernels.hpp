@@ -63,8 +63,11 @@ namespace gg {
 #ifndef GG_STREAM_ROWS
 #define GG_STREAM_ROWS 4
 #endif
+// 5 waves (round 6): expand_stream<32,2> (C4) fits 96 VGPRs + 12 B of scratch
+// instead of 4 waves: the C4 leg 824 -> 813 ms/step, C2 / C3 / C5 equal
+// (profiles/r6/ab_waves5/); 6 waves spill 76 B a lane and double C2's dense rounds
 #ifndef GG_STREAM_WAVES_PER_EU
-#define GG_STREAM_WAVES_PER_EU 4
+#define GG_STREAM_WAVES_PER_EU 5
 #endif
 constexpr int kStreamRows = GG_STREAM_ROWS;
 // ... in the marking kernel: three rows keep it at 95 VGPRs, 5 waves/SIMD (four:
