@@ -2300,8 +2300,11 @@ void expand_stream(RoundArgs a) {
 }
 
 // Partition-window rounds: the mask bookkeeping needs more registers (4 waves/SIMD).
+#ifndef GG_MASKED_WAVES_PER_EU
+#define GG_MASKED_WAVES_PER_EU 4
+#endif
 template <int G, int WPL>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GG_MASKED_WAVES_PER_EU)))
 void expand_stream_masked(RoundArgs a) {
     stream_body<G, WPL, true>(a);
 }
