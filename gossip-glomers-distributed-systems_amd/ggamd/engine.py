@@ -147,6 +147,14 @@ def load_library(path: str) -> C.CDLL:
         return _LIBS[path]
     if not os.path.exists(path):
         raise FileNotFoundError(f"engine library {path} is not built (run `make` in {PKG_DIR})")
+    # One HIP runtime per process: PyTorch ships its own libamdhip64 (soname
+    # libamdhip64.so.7, like /opt/rocm's, but loaded by file name). Loaded after the
+    # engine, torch brings a second runtime that finds no GPU; loaded first, the
+    # engine binds to torch's by soname. So torch, when installed, goes first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     P = C.POINTER
     lib.gg_abi_version.restype = C.c_int
